@@ -1,0 +1,264 @@
+"""Benchmark: GCNConv F=256 aggregation on the BASELINE config-2 graph.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...     (driver, N > 1)
+
+Workload (BASELINE.json configs[1]): RMAT scale 21 (N = 2,097,152),
+(a,b,c,d) = (.57,.19,.19,.05), 30M samples symmetrised (E = 60M), GCN
+add_remaining_self_loops (E' ~ 62M), x ~ N(0,1) [N, 256] fp32, seed 1.
+One step = one GCNConv propagate: the fused gather * norm -> segment-sum
++ bias HIP kernel (plus its split-row fix-up) over all E' edges.  The CSR /
+schedule / norm build (one-time, cached=True semantics) and the x @ W GEMM
+are timed separately and reported beside the metric.
+
+N > 1: the same graph is sharded by destination range (edge balanced); a
+step is halo all_to_all (RCCL) + local fused aggregation on every rank;
+value = E' / max-over-ranks step time (strong scaling).
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "pytorch_geometric-1_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+F_DIM = 256
+SCALE = 21
+SAMPLES = 30_000_000
+HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md chip table)
+BYTES_PER_EDGE = 4 * F_DIM + 4 + 4   # x_j row + col + norm   
+BYTES_PER_NODE = 4 * F_DIM + 4       # out row + rowptr
+PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-edges", type=int, default=16_000_000)
+    ap.add_argument("--chunk", type=int, default=256)
+    return ap.parse_args()
+
+
+def setup_dist(n):
+    if n <= 1 or "RANK" not in os.environ:
+        return 0, 1, 0
+    rank = int(os.environ["RANK"])
+    world = int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    torch.cuda.set_device(local)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return rank, world, local
+
+
+def barrier(world):
+    if world > 1:
+        dist.barrier()
+
+
+def cpu_baseline(ei_loops, norm, x, sample_edges):
+    """The reference algorithm on the host (oracle, kind 'port'): index_select
+    -> norm * x_j -> scatter_add_ (torch_scatter scatter_sum), timed on a
+    bounded sample of the same edges in their original order, in 4M-edge
+    chunks (the materialised x_j of all 62M edges is 64 GB)."""
+    from oracle import pyg_ref  # noqa: F401  (checker/baseline only)
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    E = min(sample_edges, ei_loops.shape[1])
+    ei = ei_loops[:, :E].cpu()
+    w = norm[:E].cpu()
+    xc = x.cpu()
+    N = xc.shape[0]
+    out = torch.zeros_like(xc)
+    chunk = 4_000_000
+    t0 = time.perf_counter()
+    for s in range(0, E, chunk):
+        e = min(E, s + chunk)
+        x_j = xc.index_select(0, ei[0, s:e])
+        msg = w[s:e].view(-1, 1) * x_j
+        out.scatter_add_(0, ei[1, s:e].view(-1, 1).expand_as(msg), msg)
+    dt = time.perf_counter() - t0
+    del out, xc
+    return {"value": E / dt, "unit": "edges/s", "cores": threads, "kind": "port",
+            "sample": "first %d of the %d edges (original order), F=%d, torch CPU index_select+mul+"
+                      "scatter_add_ in 4M-edge chunks, %.1f s" % (E, ei_loops.shape[1], N and F_DIM, dt)}
+
+
+def main():
+    args = parse()
+    rank, world, local = setup_dist(args.gpus)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    import mi355_mp
+    from mi355_mp import _lib, ops
+    from mi355_mp.graph import Graph
+    from mi355_mp.graphgen import rmat_edge_index
+    from torch_geometric.nn.conv.gcn_conv import GCNConv
+    mi355_mp.load_native()
+
+    N = 1 << SCALE
+    t0 = time.perf_counter()
+    ei = rmat_edge_index(scale=SCALE, n_samples=SAMPLES, seed=1, device=dev)
+    torch.cuda.synchronize()
+    t_gen = time.perf_counter() - t0
+
+    # one-time build: loops + norm (GCNConv.norm), CSR + schedule
+    t0 = time.perf_counter()
+    ei2, norm = GCNConv.norm(ei, N)
+    E2 = ei2.shape[1]
+    bias = torch.randn(F_DIM, device=dev, generator=torch.Generator(device=dev).manual_seed(7)) * 0.1
+    g = torch.Generator(device=dev).manual_seed(1)
+    if world == 1:
+        graph = Graph(ei2, N, N, chunk=args.chunk)
+        csr = graph.dst
+        w_csr = csr.to_csr_order(norm)
+        x = torch.randn(N, F_DIM, device=dev, generator=g)
+        n_rows = N
+        E_local = E2
+    else:
+        from mi355_mp import dist as mdist
+        plan = mdist.ShardPlan(ei2, N, rank, world).exchange_requests()
+        x_full = torch.randn(N, F_DIM, device=dev, generator=g)
+        x = x_full[plan.lo:plan.hi].contiguous()
+        del x_full
+        lei = plan.local_edge_index
+        graph = Graph(lei, plan.n_own, plan.n_local_src, chunk=args.chunk)
+        csr = graph.dst
+        w_csr = csr.to_csr_order(norm[plan.edge_pos])
+        n_rows = plan.n_own
+        E_local = lei.shape[1]
+    torch.cuda.synchronize()
+    t_build = time.perf_counter() - t0
+
+    lib = _lib.load()
+    st_main = csr.struct("other")
+
+    def aggregate(x_src, stages=_lib.MP_STAGE_ALL, out=None):
+        return ops._aggregate(csr, "other", x_src, w_csr, "sum", 0, bias, out=out, stages=stages)[0]
+
+    out_buf = torch.empty((n_rows, F_DIM), device=dev)
+
+    def step():
+        if world == 1:
+            aggregate(x, out=out_buf)
+        else:
+            xl = plan.halo_exchange(x, ops.gather_rows)
+            aggregate(xl, out=out_buf)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    ms_per_step = dt / args.steps * 1e3
+    value = E2 * args.steps / dt    # whole-job edges aggregated per second
+
+    # dominant kernel (main aggregation launch) timed with HIP events on the
+    # stream it runs on (torch's current stream), averaged over launches
+    x_src = x if world == 1 else plan.halo_exchange(x, ops.gather_rows)
+    reps = max(args.steps, 10)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    evf = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for k in range(reps):
+        ev[k][0].record()
+        aggregate(x_src, stages=_lib.MP_STAGE_MAIN, out=out_buf)
+        ev[k][1].record()
+        evf[k][0].record()
+        aggregate(x_src, stages=_lib.MP_STAGE_FIXUP, out=out_buf)
+        evf[k][1].record()
+    torch.cuda.synchronize()
+    main_ms = sorted(a.elapsed_time(b) for a, b in ev)
+    fix_ms = sorted(a.elapsed_time(b) for a, b in evf)
+    main_avg = sum(main_ms) / len(main_ms)
+    fix_avg = sum(fix_ms) / len(fix_ms)
+    alg_bytes = E_local * BYTES_PER_EDGE + n_rows * BYTES_PER_NODE
+    achieved = alg_bytes / (main_avg * 1e-3) / 1e9
+
+    # GEMM (reported separately, the only MFMA work)
+    W = torch.randn(F_DIM, F_DIM, device=dev) * 0.06
+    for _ in range(3):
+        torch.matmul(x, W)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        torch.matmul(x, W)
+    e1.record()
+    torch.cuda.synchronize()
+    gemm_ms = e0.elapsed_time(e1) / 10
+
+    traffic = None
+    if os.path.exists(PMC_FILE):
+        try:
+            with open(PMC_FILE) as f:
+                pmc = json.load(f)
+            if pmc.get("workload") == "rmat21_gcn_f256" and world == 1:
+                traffic = pmc.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(ei2, norm, x, args.cpu_sample_edges)
+
+    if rank == 0:
+        line = {
+            "metric": "edges aggregated/sec (GCNConv F=256 propagate, fused gather*norm->segment-sum+bias)",
+            "value": value,
+            "unit": "edges/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic RMAT (seeded, generated on device), random-init features",
+            "config": {"workload": "rmat21_gcn_f256", "graph": "RMAT scale 21 (.57,.19,.19,.05) "
+                       "30M samples symmetrised + add_remaining_self_loops", "num_nodes": N,
+                       "num_edges": E2, "features": F_DIM, "seed": 1,
+                       "parallelism": "dst-range shards x%d, RCCL halo all_to_all" % world if world > 1
+                       else "single GPU", "chunk": args.chunk},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_agg_main<SumRed<4,true,false>,4,8>",
+                         "algorithmic_bytes_per_launch": alg_bytes,
+                         "avg_launch_ms": main_avg, "median_launch_ms": main_ms[len(main_ms) // 2],
+                         "fixup_avg_ms": fix_avg},
+            "cpu_baseline": cpu,
+            "extra": {"gemm_xW_ms": gemm_ms, "layer_ms_est": gemm_ms + main_avg + fix_avg,
+                      "one_time_build_s": t_build, "graph_gen_s": t_gen,
+                      "edges_local_rank0": E_local, "n_split_rows": csr.n_split,
+                      "n_wave_tasks": csr.n_waves,
+                      "agg_only_GBps_incl_fixup": alg_bytes / ((main_avg + fix_avg) * 1e-3) / 1e9},
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,195 @@
+/*
+ * mi355_mp.h — C-ABI of the MI355X (gfx950) message-passing aggregation engine.
+ *
+ * This is the drop-in boundary for the hot path of PyG 1.4.3
+ * `MessagePassing.propagate()` (gather x_j / x_i -> message -> scatter-reduce)
+ * and of the torch_scatter 2.0.4 ops it calls.  Upstream those live in
+ * unvendored dependencies pinned at /root/reference/requirement.txt:1-7
+ * (torch_sparse 0.6.1, torch-scatter 2.0.4, torch-geometric 1.4.3); the
+ * reference tree itself only calls them (examples/gcn.py:18-27,
+ * ConvexPruning.py:180-224, examples/ppi.py:22-28, README.md:35-49,
+ * gmm_conv.py:131-144).  See SURVEY.md section 8b for the schema list.
+ *
+ * Conventions
+ *   - Plain pointers to DEVICE memory, int64 sizes, a hipStream_t passed as
+ *     `void* stream` (NULL = default stream).  No torch types.
+ *   - Every entry point only enqueues work on `stream`; none allocates, frees
+ *     or synchronises, so every call is hipGraph-capturable.  The caller owns
+ *     all outputs and workspaces (sizes from the *_bytes queries).
+ *   - Return value: MP_OK or an MP_ERR_* code; mp_last_error() gives the text
+ *     (thread-local).
+ *   - Graph structure is a destination-sorted CSR (stable: inside a row the
+ *     edges keep their original order), described by `mp_csr`.  All kernels
+ *     are deterministic: no float atomics on any forward output.
+ */
+#ifndef MI355_MP_H
+#define MI355_MP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MP_ABI_VERSION 1
+
+/* status codes */
+#define MP_OK 0
+#define MP_ERR_ARG 1   /* bad argument (shape, alignment, null pointer) */
+#define MP_ERR_HIP 2   /* a HIP runtime call failed */
+
+/* reductions (torch_scatter names: sum/add, mean, max, min) */
+#define MP_REDUCE_SUM 0
+#define MP_REDUCE_MEAN 1
+#define MP_REDUCE_MAX 2
+#define MP_REDUCE_MIN 3
+
+/* aggregate flags */
+#define MP_FLAG_INIT_FROM_OUT 1 /* torch_scatter `out=` given: reduce into out's values */
+#define MP_FLAG_PYG_MASK 2      /* torch_geometric.utils.scatter_: max -> out<-10000 := 0,
+                                   min -> out>10000 := 0 */
+
+/* aggregate stages (bench times the main kernel on its own) */
+#define MP_STAGE_MAIN 1
+#define MP_STAGE_FIXUP 2
+#define MP_STAGE_ALL 3
+
+/*
+ * Destination-sorted CSR plus its edge-balanced ("merge-path") schedule.
+ *   rowptr[n_rows+1]      row r owns CSR slots [rowptr[r], rowptr[r+1])
+ *   col[n_edges]          gather row for each slot (source node, or message row)
+ *   eid[n_edges]          original edge position of each slot (argmax output)
+ * Schedule (merge-path over the N+E work items "row r" and "slot k"; row r
+ * sits at merged position rowptr[r]+r, slot k of row r at k+r+1):
+ *   wave task w covers merged positions [w*chunk, (w+1)*chunk)
+ *   wave_row[n_waves+1]   first row whose marker lies in task w (owned rows)
+ *   wave_slot[n_waves+1]  first CSR slot processed by task w
+ *   split_waves[n_split]  for each row whose slots span several tasks, the
+ *                         last task touching it (fix-up list)
+ */
+typedef struct mp_csr {
+  const int32_t* rowptr;
+  const int32_t* col;
+  const int32_t* eid;
+  const int32_t* wave_row;
+  const int32_t* wave_slot;
+  const int32_t* split_waves;
+  int64_t n_rows;
+  int64_t n_edges;
+  int32_t chunk;
+  int32_t n_waves;
+  int32_t n_split;
+  int32_t reserved;
+} mp_csr;
+
+const char* mp_last_error(void);
+int mp_abi_version(void);
+
+/* ---- CSR build (replaces the sort/bucketing torch_scatter never did: upstream
+ *      scatter_add_ walks edges in original order) ---------------- */
+
+/* Workspace bytes for mp_csr_build. */
+size_t mp_csr_build_workspace(int64_t n_edges, int64_t n_rows);
+
+/* Stable sort of edges by key (edge_index[i], the aggregation index).
+ *   key[n_edges], other[n_edges]: int64 (rows of edge_index; any stride-1 view)
+ *   other may be NULL: then col[k] = eid[k] (aggregating materialised messages).
+ *   rowptr[n_rows+1], col[n_edges], eid[n_edges]: int32 outputs.
+ *   bad[1]: device int32, set to the number of key/other entries outside
+ *   [0,n_rows) / [0,n_other).  Replaces the index->CSR step of
+ *   torch_scatter segment_csr callers; PyG 1.4.3 scatter_ itself sorts nothing. */
+int mp_csr_build(const int64_t* key, const int64_t* other, int64_t n_edges,
+                 int64_t n_rows, int64_t n_other, int32_t* rowptr, int32_t* col,
+                 int32_t* eid, int32_t* bad, void* ws, size_t ws_bytes,
+                 void* stream);
+
+/* Number of wave tasks for `chunk` merged positions per task (chunk % 64 == 0). */
+int32_t mp_schedule_n_waves(int64_t n_rows, int64_t n_edges, int32_t chunk);
+size_t mp_schedule_workspace(int32_t n_waves);
+
+/* Builds wave_row[n_waves+1], wave_slot[n_waves+1] and split_waves[<=n_waves];
+ * writes the split count to n_split_dev[0] (device int32). */
+int mp_schedule_build(const int32_t* rowptr, int64_t n_rows, int64_t n_edges,
+                      int32_t chunk, int32_t* wave_row, int32_t* wave_slot,
+                      int32_t* split_waves, int32_t* n_split_dev, void* ws,
+                      size_t ws_bytes, void* stream);
+
+/* ---- fused gather -> (weight) -> segment reduce ---------------------------
+ * out[r, :] = REDUCE_{k in row r} ( w[k] * x[col[k], :] )     (w optional)
+ * Replaces: index_select(x, edge_index[j]) (PyG MessagePassing.__collect__),
+ * message() = norm.view(-1,1)*x_j (GCNConv) or x_j, and
+ * torch_scatter scatter_sum/scatter_mean/scatter_max/scatter_min [U8/U9],
+ * torch_geometric.utils.scatter_ [U2] (MP_FLAG_PYG_MASK), update() += bias.
+ *   w:      CSR-ordered per-slot weights or NULL
+ *   x:      [*, ldx] fp32 rows, F features used
+ *   bias:   [F] or NULL (added after the reduction, as GCNConv.update)
+ *   out:    [n_rows, ldo] fp32
+ *   arg_out:[n_rows, F] int64 (max/min only, else NULL): original edge
+ *           position of the first maximal element, n_edges for empty rows
+ *   slab:   workspace of mp_aggregate_slab_bytes() bytes
+ */
+size_t mp_aggregate_slab_bytes(const mp_csr* g, int32_t F, int32_t reduce);
+int mp_aggregate_f32(const mp_csr* g, const float* w, const float* x,
+                     int64_t ldx, int32_t F, int32_t reduce, int32_t flags,
+                     const float* bias, float* out, int64_t ldo,
+                     int64_t* arg_out, void* slab, size_t slab_bytes,
+                     int32_t stages, void* stream);
+
+/* ---- GATConv fused attention aggregation (call stack 3.2) ---
+ * a_dst[n,h] = <xw[n,h,:], att[h,0:C]>,  a_src[n,h] = <xw[n,h,:], att[h,C:2C]>
+ * (the split of (cat[x_i,x_j]*att).sum(-1) of GATConv.message [U6]). */
+int mp_gat_node_scores_f32(const float* xw, int64_t n_nodes, int32_t H,
+                           int32_t C, const float* att, float* a_src,
+                           float* a_dst, void* stream);
+
+/* out[i,h,:] = sum_k softmax_k(leaky_relu(a_src[col_k,h]+a_dst[i,h])) x[col_k,h,:]
+ * with torch_geometric.utils.softmax's +1e-16 denominator, single pass
+ * (online max/sum), optional bias [H*C], optional row_stats[n_rows,H,2] =
+ * (max, denominator) for mp_gat_alpha_f32. */
+size_t mp_gat_slab_bytes(const mp_csr* g, int32_t H, int32_t C);
+int mp_gat_aggregate_f32(const mp_csr* g, const float* xw, const float* a_src,
+                         const float* a_dst, int32_t H, int32_t C, float slope,
+                         const float* bias, float* out, int64_t ldo,
+                         float* row_stats, void* slab, size_t slab_bytes,
+                         int32_t stages, void* stream);
+
+/* alpha[e,h] for edges in ORIGINAL order (return_attention_weights, backward) */
+int mp_gat_alpha_f32(const int64_t* src_idx, const int64_t* dst_idx,
+                     int64_t n_edges, int32_t H, const float* a_src,
+                     const float* a_dst, float slope, const float* row_stats,
+                     float* alpha, void* stream);
+
+/* ---- helpers on the path -------------------------------------------------- */
+
+/* out[k,:] = x[idx[k],:]  (index_select of __collect__, scatter-sum backward,
+ * halo packing for the multi-GPU exchange) */
+int mp_gather_rows_f32(const float* x, int64_t ldx, const int64_t* idx,
+                       int64_t n, int32_t F, float* out, int64_t ldo,
+                       void* stream);
+
+/* dst[k] = src[perm[k]] (CSR-ordering of per-edge weights) */
+int mp_permute_f32(const float* src, const int32_t* perm, int64_t n,
+                   float* dst, void* stream);
+
+/* ScatterMax/ScatterMin backward [U8]: for every (r,f) with arg[r,f] != n_edges
+ *   src_map == NULL: grad[arg[r,f], f]            = grad_out[r,f]  (plain store)
+ *   src_map != NULL: grad[src_map[arg[r,f]], f]  += grad_out[r,f]  (atomic)
+ * grad must be zero-initialised by the caller. */
+int mp_scatter_arg_backward_f32(const float* grad_out, const int64_t* arg,
+                                int64_t n_rows, int32_t F, int64_t n_edges,
+                                const int64_t* src_map, float* grad,
+                                int64_t ldg, void* stream);
+
+/* GCNConv.norm [U5]: deg = scatter_add(w, row); dinv = deg^-1/2 (inf -> 0);
+ * norm[e] = dinv[row[e]] * w[e] * dinv[col[e]] (original edge order).
+ * w == NULL means all ones.  deg_ws: n_nodes floats of workspace. */
+int mp_gcn_norm_f32(const int64_t* row, const int64_t* col, const float* w,
+                    int64_t n_edges, int64_t n_nodes, float* deg_ws,
+                    float* norm, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MI355_MP_H */

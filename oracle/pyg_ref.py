@@ -1,0 +1,157 @@
+"""PyG 1.4.3 hot-path semantics on the CPU -- TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
+
+Plain torch CPU restatements of the torch_geometric 1.4.3 functions on the
+aggregation path (all [U]); callers in the reference tree:
+examples/gcn.py:18-27 (GCNConv cached), ConvexPruning.py:180-224 (GCN/GAT
+stacks), examples/ppi.py:22-28 (multi-head GAT), README.md:35-49 (custom
+MessagePassing with aggr='max').  Works in float32 (parity) or float64
+(ground truth for tolerance analysis).
+"""
+import torch
+import torch.nn.functional as F
+
+from . import scatter_ref as S
+
+
+# --- utils.loop [U4] --------------------------------------------------------
+
+def remove_self_loops(edge_index, edge_attr=None):
+    row, col = edge_index
+    mask = row != col
+    return edge_index[:, mask], (None if edge_attr is None else edge_attr[mask])
+
+
+def add_self_loops(edge_index, edge_weight=None, fill_value=1, num_nodes=None):
+    N = num_nodes
+    loops = torch.arange(N, dtype=torch.long).unsqueeze(0).repeat(2, 1)
+    if edge_weight is not None:
+        edge_weight = torch.cat([edge_weight, edge_weight.new_full((N,), fill_value)])
+    return torch.cat([edge_index, loops], dim=1), edge_weight
+
+
+def add_remaining_self_loops(edge_index, edge_weight=None, fill_value=1, num_nodes=None):
+    """kept non-loop edges (original order), then loops 0..N-1; a loop keeps the
+    weight of the node's last pre-existing loop, else fill_value."""
+    N = num_nodes
+    row, col = edge_index
+    mask = row != col
+    loop_weight = torch.full((N,), fill_value, dtype=None if edge_weight is None else edge_weight.dtype)
+    if edge_weight is not None:
+        rem = edge_weight[~mask]
+        rrows = row[~mask]
+        for k in range(rrows.numel()):  # sequential: last one wins (CPU index_put_)
+            loop_weight[rrows[k]] = rem[k]
+        edge_weight = torch.cat([edge_weight[mask], loop_weight])
+    loops = torch.arange(N, dtype=row.dtype).unsqueeze(0).repeat(2, 1)
+    return torch.cat([edge_index[:, mask], loops], dim=1), edge_weight
+
+
+# --- utils.scatter_ [U2] / utils.softmax [U3] ------------------------------
+
+def scatter_(name, src, index, dim_size):
+    if name == "add":
+        out = S.scatter_sum(src, index, dim_size)
+    elif name == "mean":
+        out = S.scatter_mean(src, index, dim_size)
+    elif name == "max":
+        out = S.scatter_max(src, index, dim_size)[0]
+        out[out < -10000] = 0
+    elif name == "min":
+        out = S.scatter_min(src, index, dim_size)[0]
+        out[out > 10000] = 0
+    else:
+        raise ValueError(name)
+    return out
+
+
+def _seg_max(src, index, N):
+    if src.dtype == torch.float32:
+        return S.scatter_max(src, index, N)[0]
+    out = torch.full((N,) + tuple(src.shape[1:]), float("-inf"), dtype=src.dtype)
+    out = out.scatter_reduce(0, index.view((-1,) + (1,) * (src.dim() - 1)).expand_as(src), src, "amax")
+    out[torch.isinf(out)] = 0
+    return out
+
+
+def softmax(src, index, num_nodes):
+    out = src - _seg_max(src, index, num_nodes)[index]
+    out = out.exp()
+    out = out / (S.scatter_sum(out, index, num_nodes)[index] + 1e-16)
+    return out
+
+
+# --- GCNConv [U5] -----------------------------------------------------------
+
+def gcn_norm(edge_index, num_nodes, edge_weight=None, improved=False, dtype=torch.float32):
+    if edge_weight is None:
+        edge_weight = torch.ones((edge_index.size(1),), dtype=dtype)
+    fill_value = 1 if not improved else 2
+    edge_index, edge_weight = add_remaining_self_loops(edge_index, edge_weight, fill_value, num_nodes)
+    row, col = edge_index
+    deg = S.scatter_sum(edge_weight, row, num_nodes)
+    deg_inv_sqrt = deg.pow(-0.5)
+    deg_inv_sqrt[deg_inv_sqrt == float("inf")] = 0
+    return edge_index, deg_inv_sqrt[row] * edge_weight * deg_inv_sqrt[col]
+
+
+def gcn_aggregate(x, edge_index, norm, num_nodes):
+    """propagate(edge_index, x=x, norm=norm): message norm*x_j, scatter add."""
+    x_j = x.index_select(0, edge_index[0])
+    msg = norm.view(-1, 1) * x_j
+    return S.scatter_sum(msg, edge_index[1], num_nodes)
+
+
+def gcn_conv(x, edge_index, weight, bias=None, edge_weight=None, improved=False):
+    N = x.size(0)
+    h = torch.matmul(x, weight)
+    ei, norm = gcn_norm(edge_index, N, edge_weight, improved, h.dtype)
+    out = gcn_aggregate(h, ei, norm, N)
+    return out + bias if bias is not None else out
+
+
+# --- GATConv [U6] -----------------------------------------------------------
+
+def gat_conv(x, edge_index, weight, att, bias, heads, out_channels, concat=True, negative_slope=0.2,
+             return_alpha=False):
+    N = x.size(0)
+    ei, _ = remove_self_loops(edge_index)
+    ei, _ = add_self_loops(ei, num_nodes=N)
+    h = torch.matmul(x, weight)
+    x_i = h.index_select(0, ei[1]).view(-1, heads, out_channels)
+    x_j = h.index_select(0, ei[0]).view(-1, heads, out_channels)
+    alpha = (torch.cat([x_i, x_j], dim=-1) * att).sum(dim=-1)
+    alpha = F.leaky_relu(alpha, negative_slope)
+    alpha = softmax(alpha, ei[1], N)
+    msg = x_j * alpha.view(-1, heads, 1)
+    out = S.scatter_sum(msg, ei[1], N)
+    out = out.view(-1, heads * out_channels) if concat else out.mean(dim=1)
+    if bias is not None:
+        out = out + bias
+    return (out, ei, alpha) if return_alpha else out
+
+
+# --- aggr='max' MessagePassing / GraphConv [U7] -----------------------------
+
+def max_aggregate(h, edge_index, num_nodes, pyg_mask=True):
+    """propagate with message h_j and aggr='max' -> (scatter_ output, arg)."""
+    msg = h.index_select(0, edge_index[0])
+    out, arg = S.scatter_max(msg, edge_index[1], num_nodes)
+    if pyg_mask:
+        out[out < -10000] = 0
+    return out, arg
+
+
+def graph_conv_max(x, edge_index, weight, lin_w, lin_b):
+    h = torch.matmul(x, weight)
+    out, _ = max_aggregate(h, edge_index, x.size(0))
+    return out + F.linear(x, lin_w, lin_b)
+
+
+def edge_conv_max(x, edge_index, mlp):
+    """README.md:35-49 EdgeConv: message mlp(cat[x_i, x_j - x_i]), aggr='max'."""
+    x_i = x.index_select(0, edge_index[1])
+    x_j = x.index_select(0, edge_index[0])
+    msg = mlp(torch.cat([x_i, x_j - x_i], dim=1))
+    out, _ = S.scatter_max(msg, edge_index[1], x.size(0))
+    out[out < -10000] = 0
+    return out

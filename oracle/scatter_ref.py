@@ -1,0 +1,120 @@
+"""torch_scatter 2.0.4 semantics on the CPU -- TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
+
+Restates, for 2-D src and a 1-D index along dim 0 (the only form PyG 1.4.3's
+MessagePassing produces):
+  scatter_sum  [U8] torch_scatter/scatter.py: broadcast(index) then
+               `src.new_zeros(size).scatter_add_(dim, index, src)`
+  scatter_mean [U8]: scatter_sum / scatter_sum(ones).clamp_(1) (true_divide)
+  scatter_max/min [U9] csrc/cpu/scatter_cpu.cpp: serial strict-compare loop,
+               first edge wins ties, empty row -> (0, E)   (scatter_loop.c)
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle_scatter.so")
+_lib = None
+
+R_SUM, R_MEAN, R_MAX, R_MIN = 0, 1, 2, 3
+
+
+def build():
+    """Compile scatter_loop.c with gcc (oracle/Makefile)."""
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def _c():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        lib = ctypes.CDLL(_LIB_PATH)
+        p = ctypes.c_void_p
+        i64 = ctypes.c_int64
+        lib.oracle_scatter_f32.argtypes = [p, p, i64, i64, i64, ctypes.c_int, ctypes.c_int, p, p]
+        lib.oracle_gather_sum_f32.argtypes = [p, p, p, p, i64, i64, i64, p]
+        lib.oracle_gather_max_f32.argtypes = [p, p, p, i64, i64, i64, p, p]
+        _lib = lib
+    return _lib
+
+
+def _np(t, dtype):
+    return np.ascontiguousarray(t.detach().cpu().numpy().astype(dtype, copy=False))
+
+
+def _addr(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+# --- torch-op forms (the literal upstream calls) ---------------------------
+
+def scatter_sum(src, index, dim_size):
+    """zeros(dim_size, F).scatter_add_(0, index broadcast, src) (edge order)."""
+    src2 = src.reshape(src.shape[0], -1)
+    out = torch.zeros((dim_size, src2.shape[1]), dtype=src.dtype)
+    if src2.numel():
+        out.scatter_add_(0, index.view(-1, 1).expand_as(src2), src2)
+    return out.reshape((dim_size,) + tuple(src.shape[1:]))
+
+
+def scatter_mean(src, index, dim_size):
+    out = scatter_sum(src, index, dim_size)
+    ones = torch.ones(index.size(), dtype=src.dtype)
+    count = torch.zeros(dim_size, dtype=src.dtype).scatter_add_(0, index, ones)
+    count.clamp_(1)
+    return out / count.view((-1,) + (1,) * (out.dim() - 1))
+
+
+# --- serial-loop forms (scatter_cpu.cpp) ---------------------------------
+
+def scatter_loop(src, index, dim_size, reduce, out=None):
+    """Serial loop in C; returns (out, arg or None).  fp32 only."""
+    red = {"sum": R_SUM, "add": R_SUM, "mean": R_MEAN, "max": R_MAX, "min": R_MIN}[reduce]
+    s = _np(src.reshape(src.shape[0], -1), np.float32)
+    E, F = s.shape
+    idx = _np(index, np.int64)
+    has_out = out is not None
+    o = _np(out, np.float32).copy() if has_out else np.empty((dim_size, F), np.float32)
+    a = np.empty((dim_size, F), np.int64) if red in (R_MAX, R_MIN) else None
+    _c().oracle_scatter_f32(_addr(s), _addr(idx), E, F, dim_size, red, int(has_out), _addr(o), _addr(a))
+    shape = (dim_size,) + tuple(src.shape[1:])
+    ot = torch.from_numpy(o).reshape(shape)
+    at = torch.from_numpy(a).reshape(shape) if a is not None else None
+    return ot, at
+
+
+def scatter_max(src, index, dim_size, out=None):
+    return scatter_loop(src, index, dim_size, "max", out)
+
+
+def scatter_min(src, index, dim_size, out=None):
+    return scatter_loop(src, index, dim_size, "min", out)
+
+
+def gather_sum(x, other, index, weight, dim_size):
+    """out[index[e]] += weight[e] * x[other[e]] in edge order (C loop)."""
+    xs = _np(x, np.float32)
+    F = xs.shape[1]
+    o = np.empty((dim_size, F), np.float32)
+    w = _np(weight, np.float32) if weight is not None else None
+    oth = _np(other, np.int64)
+    idx = _np(index, np.int64)
+    _c().oracle_gather_sum_f32(_addr(xs), _addr(oth), _addr(idx), _addr(w), idx.shape[0], F, dim_size,
+                               _addr(o))
+    return torch.from_numpy(o)
+
+
+def gather_max(x, other, index, dim_size):
+    xs = _np(x, np.float32)
+    F = xs.shape[1]
+    o = np.empty((dim_size, F), np.float32)
+    a = np.empty((dim_size, F), np.int64)
+    oth = _np(other, np.int64)
+    idx = _np(index, np.int64)
+    _c().oracle_gather_max_f32(_addr(xs), _addr(oth), _addr(idx), idx.shape[0], F, dim_size, _addr(o),
+                               _addr(a))
+    return torch.from_numpy(o), torch.from_numpy(a)

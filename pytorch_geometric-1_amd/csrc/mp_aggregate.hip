@@ -1,0 +1,629 @@
+// Fused gather -> message -> segment-reduce for gfx950 (MI355X).
+//
+// Replaces, for one MessagePassing.propagate() [U1]:
+//   x_j = x.index_select(0, edge_index[j])             (ATen index_select, [E',F] in HBM)
+//   msg = norm.view(-1,1) * x_j   (GCNConv.message)    (elementwise, [E',F] in HBM)
+//   out = torch_scatter.scatter_{sum,mean,max,min}(msg, edge_index[i], 0, dim_size=N)
+//   out = out + bias              (GCNConv.update)
+// with one pass that reads each x_j row once and writes each output row once.
+//
+// Mapping to CDNA4:
+//   * one wave (64 lanes) = one merge-path task: `chunk` work units where a unit
+//     is either "gather one CSR slot" or "finish one row" (mp_csr.hip).  Every
+//     wave therefore does the same amount of work whatever the in-degree
+//     distribution (RMAT hubs have ~1e4-1e5 in-edges, most rows < 10).
+//   * a lane owns VEC consecutive features (VEC=4: one dwordx4, a 256-feature
+//     row is one 1 KiB coalesced wave load); gridDim.y tiles wider rows.
+//   * the wave walks its slots in CSR order; col/weight/eid for 64 slots are
+//     loaded once per 64 slots (one coalesced dword per lane, next window
+//     prefetched) and broadcast with v_readlane -> the x-row address is a
+//     scalar base + lane offset.  U x-row loads are in flight per wave.
+//   * accumulation stays in VGPRs; a row is stored once (no atomics).  A row
+//     whose slots cross a task boundary leaves partials in a slab; a small
+//     fix-up kernel combines them in task order (deterministic).
+//   * sum uses separately-rounded mul and add (no FMA contraction) in original
+//     edge order, i.e. exactly the arithmetic of the reference's materialised
+//     `norm*x_j` followed by CPU scatter_add_: rows that fit in one task are
+//     bit-identical to the oracle.
+#include <float.h>
+
+#include "mp_common.h"
+
+namespace mp {
+
+constexpr int kWavesPerBlock = 4;
+constexpr int kBlock = 64 * kWavesPerBlock;
+
+struct AggArgs {
+  // graph + schedule
+  const int32_t* rowptr;
+  const int32_t* col;
+  const int32_t* eid;
+  const int32_t* wave_row;
+  const int32_t* wave_slot;
+  const int32_t* split_waves;
+  int64_t n_rows;
+  int64_t n_edges;
+  int32_t chunk;
+  int32_t n_waves;
+  int32_t n_split;
+  int32_t F;
+  // features
+  const float* w;
+  const float* x;
+  int64_t ldx;
+  int32_t flags;
+  const float* bias;
+  float* out;
+  int64_t ldo;
+  int64_t* arg_out;
+  // partial slabs: slot index s = 2*task + kind (kind 0 = continuation, 1 = head)
+  float* slab_v;
+  int32_t* slab_a;
+  int64_t slab_ld;
+  // GAT
+  const float* a_src;
+  const float* a_dst;
+  int32_t H;
+  int32_t C;
+  float slope;
+  float* row_stats;
+  float* slab_s;
+};
+
+// ---------------------------------------------------------------------------
+// Reducers: per-lane state for VEC features of one (partial) row.
+// ---------------------------------------------------------------------------
+
+template <int VEC, bool HAS_W, bool MEAN>
+struct SumRed {
+  static constexpr bool kW = HAS_W;
+  static constexpr bool kEid = false;
+  static constexpr bool kGat = false;
+  float acc[VEC];
+  int h = 0;  // unused (GAT only)
+
+  __device__ SumRed(const AggArgs&, int, bool) {}
+
+  __device__ __forceinline__ void begin(const AggArgs& p, int64_t row, bool owned, int f, bool act) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
+    if (owned && (p.flags & MP_FLAG_INIT_FROM_OUT) && act) {
+      Frag<VEC> o = load_frag<VEC>(p.out + row * p.ldo + f);
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) acc[k] = o.v[k];
+    }
+  }
+  __device__ __forceinline__ void consume(const Frag<VEC>& v, float wt, int, float) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = __fadd_rn(acc[k], HAS_W ? __fmul_rn(wt, v.v[k]) : v.v[k]);
+  }
+  __device__ __forceinline__ void store_partial(const AggArgs& p, int64_t s, int f, bool act) {
+    if (!act) return;
+    Frag<VEC> o;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) o.v[k] = acc[k];
+    store_frag<VEC>(p.slab_v + s * p.slab_ld + f, o);
+  }
+  __device__ __forceinline__ void load_partial(const AggArgs& p, int64_t s, int f) {
+    Frag<VEC> o = load_frag<VEC>(p.slab_v + s * p.slab_ld + f);
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = o.v[k];
+  }
+  __device__ __forceinline__ void merge_partial(const AggArgs& p, int64_t s, int f) {
+    Frag<VEC> o = load_frag<VEC>(p.slab_v + s * p.slab_ld + f);
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = __fadd_rn(acc[k], o.v[k]);
+  }
+  __device__ __forceinline__ void finish(const AggArgs& p, int64_t row, int64_t cnt, int f, bool act) {
+    if (!act) return;
+    Frag<VEC> o;
+    float c = (float)(cnt > 0 ? cnt : 1);
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) o.v[k] = MEAN ? __fdiv_rn(acc[k], c) : acc[k];
+    if (p.bias) {
+      Frag<VEC> b = load_frag<VEC>(p.bias + f);
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) o.v[k] = __fadd_rn(o.v[k], b.v[k]);
+    }
+    store_frag<VEC>(p.out + row * p.ldo + f, o);
+  }
+};
+
+// torch_scatter CPU scatter_max/min [U9]: out starts at lowest()/max(),
+// arg at src.size(0); strict compare so the FIRST edge (in original order)
+// wins ties; afterwards out==init -> 0 (only when out was not passed in).
+template <int VEC, bool HAS_W, bool IS_MAX>
+struct ArgRed {
+  static constexpr bool kW = HAS_W;
+  static constexpr bool kEid = true;
+  static constexpr bool kGat = false;
+  float m[VEC];
+  int a[VEC];
+  int h = 0;
+  int sentinel;
+
+  __device__ ArgRed(const AggArgs& p, int, bool) : sentinel((int)p.n_edges) {}
+
+  static __device__ __forceinline__ float init_val() { return IS_MAX ? -FLT_MAX : FLT_MAX; }
+  static __device__ __forceinline__ bool better(float v, float cur) { return IS_MAX ? (v > cur) : (v < cur); }
+
+  __device__ __forceinline__ void begin(const AggArgs& p, int64_t row, bool owned, int f, bool act) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      m[k] = init_val();
+      a[k] = sentinel;
+    }
+    if (owned && (p.flags & MP_FLAG_INIT_FROM_OUT) && act) {
+      Frag<VEC> o = load_frag<VEC>(p.out + row * p.ldo + f);
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) m[k] = o.v[k];
+    }
+  }
+  __device__ __forceinline__ void consume(const Frag<VEC>& v, float wt, int e, float) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      float val = HAS_W ? __fmul_rn(wt, v.v[k]) : v.v[k];
+      if (better(val, m[k])) {
+        m[k] = val;
+        a[k] = e;
+      }
+    }
+  }
+  __device__ __forceinline__ void store_partial(const AggArgs& p, int64_t s, int f, bool act) {
+    if (!act) return;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      p.slab_v[s * p.slab_ld + f + k] = m[k];
+      p.slab_a[s * p.slab_ld + f + k] = a[k];
+    }
+  }
+  __device__ __forceinline__ void load_partial(const AggArgs& p, int64_t s, int f) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      m[k] = p.slab_v[s * p.slab_ld + f + k];
+      a[k] = p.slab_a[s * p.slab_ld + f + k];
+    }
+  }
+  __device__ __forceinline__ void merge_partial(const AggArgs& p, int64_t s, int f) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      float v = p.slab_v[s * p.slab_ld + f + k];
+      int e = p.slab_a[s * p.slab_ld + f + k];
+      if (better(v, m[k])) {  // later tasks hold later edges: strict keeps the first
+        m[k] = v;
+        a[k] = e;
+      }
+    }
+  }
+  __device__ __forceinline__ void finish(const AggArgs& p, int64_t row, int64_t, int f, bool act) {
+    if (!act) return;
+    Frag<VEC> o;
+    const bool from_out = (p.flags & MP_FLAG_INIT_FROM_OUT) != 0;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      float v = m[k];
+      if (!from_out && v == init_val()) v = 0.f;
+      if (p.flags & MP_FLAG_PYG_MASK) {
+        if (IS_MAX ? (v < -10000.f) : (v > 10000.f)) v = 0.f;
+      }
+      if (p.bias) v = __fadd_rn(v, p.bias[f + k]);
+      o.v[k] = v;
+    }
+    store_frag<VEC>(p.out + row * p.ldo + f, o);
+    int64_t* ao = p.arg_out + row * (int64_t)p.F + f;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) ao[k] = (int64_t)a[k];
+  }
+};
+
+// GATConv [U6] + utils.softmax [U3], online: per (row, head) running max m,
+// denominator s and accumulator acc, rescaled when the max grows.  Every lane
+// of a head carries the same m/s (no cross-lane traffic).
+template <int VEC>
+struct GatRed {
+  static constexpr bool kW = false;
+  static constexpr bool kEid = false;
+  static constexpr bool kGat = true;
+  float acc[VEC];
+  float m, s, ad;
+  int h;
+
+  __device__ GatRed(const AggArgs& p, int f, bool act) : h(act ? f / p.C : 0) {}
+
+  __device__ __forceinline__ void begin(const AggArgs& p, int64_t row, bool, int, bool) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
+    m = -INFINITY;
+    s = 0.f;
+    ad = p.a_dst[row * p.H + h];
+  }
+  __device__ __forceinline__ void consume_gat(const AggArgs& p, const Frag<VEC>& v, float as) {
+    float a = as + ad;
+    a = a > 0.f ? a : a * p.slope;  // F.leaky_relu
+    float mn = fmaxf(m, a);
+    float sc = expf(m - mn);
+    float pe = expf(a - mn);
+    s = s * sc + pe;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = acc[k] * sc + pe * v.v[k];
+    m = mn;
+  }
+  __device__ __forceinline__ void consume(const Frag<VEC>&, float, int, float) {}
+  __device__ __forceinline__ int64_t stat_index(const AggArgs& p, int64_t s_) const { return (s_ * p.H + h) * 2; }
+  __device__ __forceinline__ void store_partial(const AggArgs& p, int64_t s_, int f, bool act) {
+    if (!act) return;
+    Frag<VEC> o;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) o.v[k] = acc[k];
+    store_frag<VEC>(p.slab_v + s_ * p.slab_ld + f, o);
+    if (f % p.C == 0) {
+      p.slab_s[stat_index(p, s_)] = m;
+      p.slab_s[stat_index(p, s_) + 1] = s;
+    }
+  }
+  __device__ __forceinline__ void load_partial(const AggArgs& p, int64_t s_, int f) {
+    Frag<VEC> o = load_frag<VEC>(p.slab_v + s_ * p.slab_ld + f);
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = o.v[k];
+    m = p.slab_s[stat_index(p, s_)];
+    s = p.slab_s[stat_index(p, s_) + 1];
+  }
+  __device__ __forceinline__ void merge_partial(const AggArgs& p, int64_t s_, int f) {
+    Frag<VEC> o = load_frag<VEC>(p.slab_v + s_ * p.slab_ld + f);
+    float pm = p.slab_s[stat_index(p, s_)];
+    float ps = p.slab_s[stat_index(p, s_) + 1];
+    float mn = fmaxf(m, pm);
+    float c0 = expf(m - mn), c1 = expf(pm - mn);
+    s = s * c0 + ps * c1;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = acc[k] * c0 + o.v[k] * c1;
+    m = mn;
+  }
+  __device__ __forceinline__ void finish(const AggArgs& p, int64_t row, int64_t, int f, bool act) {
+    if (!act) return;
+    Frag<VEC> o;
+    float den = s + 1e-16f;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) o.v[k] = acc[k] / den;
+    if (p.bias) {
+      Frag<VEC> b = load_frag<VEC>(p.bias + f);
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) o.v[k] = o.v[k] + b.v[k];
+    }
+    store_frag<VEC>(p.out + row * p.ldo + f, o);
+    if (p.row_stats && (f % p.C == 0)) {
+      p.row_stats[(row * p.H + h) * 2] = m;
+      p.row_stats[(row * p.H + h) * 2 + 1] = den;
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Per-wave slot window: col / weight / eid of 64 consecutive CSR slots held one
+// per lane, the next 64 prefetched.
+// ---------------------------------------------------------------------------
+template <bool W, bool EID>
+struct SlotWin {
+  int64_t base, limit;
+  int col, col_n, eid, eid_n;
+  float w, w_n;
+
+  __device__ __forceinline__ void fetch(const AggArgs& p, int64_t b, int lane, int& c, float& wt, int& e) {
+    int64_t k = b + lane;
+    bool ok = k < limit;
+    c = ok ? p.col[k] : 0;
+    if (W) wt = ok ? p.w[k] : 0.f;
+    if (EID) e = ok ? p.eid[k] : 0;
+  }
+  __device__ __forceinline__ void init(const AggArgs& p, int64_t b, int64_t lim, int lane) {
+    base = b;
+    limit = lim;
+    fetch(p, base, lane, col, w, eid);
+    fetch(p, base + 64, lane, col_n, w_n, eid_n);
+  }
+  __device__ __forceinline__ void ensure(const AggArgs& p, int64_t e, int lane) {
+    if (e >= base + 64) {  // slots are consumed in order, never skipping a window
+      base += 64;
+      col = col_n;
+      w = w_n;
+      eid = eid_n;
+      fetch(p, base + 64, lane, col_n, w_n, eid_n);
+    }
+  }
+};
+
+// Process CSR slots [s, t) of the current (partial) row.
+// All U row loads are issued unconditionally (indices past the segment are
+// clamped to its last slot, inactive lanes read feature 0) so no load sits
+// under an exec mask; only the wave-uniform consume loop is bounded by n.
+// Row address = uniform base (SGPR pair) + one shared 32-bit lane offset, so
+// the loads use the saddr form and U rows cost U*VEC data VGPRs only.
+template <class Red, int VEC, int U>
+__device__ __forceinline__ void run_slots(Red& red, const AggArgs& p, SlotWin<Red::kW, Red::kEid>& win,
+                                          int64_t s, int64_t t, uint32_t foff, int lane) {
+  const char* xb = reinterpret_cast<const char*>(p.x);
+  const int64_t ldxb = p.ldx * 4;
+  int64_t e = s;
+  while (e < t) {
+    win.ensure(p, e, lane);
+    const int off = (int)(e - win.base);
+    int64_t rem = t - e;
+    int n = 64 - off;
+    if (rem < n) n = (int)rem;
+    if (n > U) n = U;
+    n = uni(n);
+    Frag<VEC> v[U];
+    float as[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int uu = u < n ? u : n - 1;
+      const int c = readlane(win.col, off + uu);
+      const char* rowp = xb + (int64_t)c * ldxb;
+      v[u] = load_frag<VEC>(reinterpret_cast<const float*>(rowp + foff));
+      if constexpr (Red::kGat) as[u] = p.a_src[(int64_t)c * p.H + red.h];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u < n) {
+        if constexpr (Red::kGat) {
+          red.consume_gat(p, v[u], as[u]);
+        } else {
+          const float wt = Red::kW ? readlane(win.w, off + u) : 1.f;
+          const int ei = Red::kEid ? readlane(win.eid, off + u) : 0;
+          red.consume(v[u], wt, ei, 0.f);
+        }
+      }
+    }
+    e += n;
+  }
+}
+
+template <class Red, int VEC, int U>
+__global__ __launch_bounds__(kBlock) void k_agg_main(AggArgs p) {
+  const int lane = lane_id();
+  const int w = uni((int)blockIdx.x * kWavesPerBlock + (int)(threadIdx.x >> 6));
+  if (w >= p.n_waves) return;
+  const int f = (int)blockIdx.y * 64 * VEC + lane * VEC;
+  const bool act = f < p.F;
+  const uint32_t foff = (uint32_t)(act ? f : 0) * 4u;
+
+  const int r_first = uni(p.wave_row[w]);
+  const int r_last = uni(p.wave_row[w + 1]);
+  const int64_t e_begin = uni(p.wave_slot[w]);
+  const int64_t e_end = uni(p.wave_slot[w + 1]);
+
+  Red red(p, f, act);
+  SlotWin<Red::kW, Red::kEid> win;
+  win.init(p, e_begin, e_end, lane);
+
+  // rowptr window: rp = rowptr[rbase + lane]
+  int rbase = r_first;
+  int rp = (rbase + lane <= p.n_rows) ? p.rowptr[rbase + lane] : 0;
+
+  // continuation of the row owned by an earlier task
+  {
+    const int64_t ce = readlane(rp, 0);  // rowptr[r_first] (== n_edges when r_first == n_rows)
+    if (e_begin < ce) {
+      red.begin(p, r_first - 1, false, f, act);
+      run_slots<Red, VEC, U>(red, p, win, e_begin, ce < e_end ? ce : e_end, foff, lane);
+      red.store_partial(p, 2 * (int64_t)w, f, act);
+    }
+  }
+  // rows owned by this task
+  for (int r = r_first; r < r_last; ++r) {
+    if (r + 1 - rbase > 63) {
+      rbase = r;
+      rp = (rbase + lane <= p.n_rows) ? p.rowptr[rbase + lane] : 0;
+    }
+    const int64_t rs = readlane(rp, r - rbase);
+    const int64_t re = readlane(rp, r - rbase + 1);
+    red.begin(p, r, true, f, act);
+    if (re <= e_end) {
+      run_slots<Red, VEC, U>(red, p, win, rs, re, foff, lane);
+      red.finish(p, r, re - rs, f, act);
+    } else {
+      run_slots<Red, VEC, U>(red, p, win, rs, e_end, foff, lane);
+      red.store_partial(p, 2 * (int64_t)w + 1, f, act);
+    }
+  }
+}
+
+// One wave per split row: head partial of the owning task, then the
+// continuation partials of the following tasks, in task order.
+template <class Red, int VEC>
+__global__ __launch_bounds__(kBlock) void k_agg_fixup(AggArgs p) {
+  const int lane = lane_id();
+  const int i = uni((int)blockIdx.x * kWavesPerBlock + (int)(threadIdx.x >> 6));
+  if (i >= p.n_split) return;
+  const int f = (int)blockIdx.y * 64 * VEC + lane * VEC;
+  const bool act = f < p.F;
+  const int last = uni(p.split_waves[i]);
+  const int r = uni(p.wave_row[last]) - 1;
+  const int64_t rs = uni(p.rowptr[r]);
+  const int64_t re = uni(p.rowptr[r + 1]);
+  const int owner = (int)((rs + r) / p.chunk);
+  Red red(p, f, act);
+  if (act) {
+    red.load_partial(p, 2 * (int64_t)owner + 1, f);
+    for (int t = owner + 1; t <= last; ++t) red.merge_partial(p, 2 * (int64_t)t, f);
+  }
+  red.finish(p, r, re - rs, f, act);
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+
+static int pick_vec(int F, int64_t ldx, const void* x, int64_t ldo, const void* out) {
+  auto aligned = [](const void* ptr, int64_t ld, int v) {
+    return ((uintptr_t)ptr % (4 * v) == 0) && (ld % v == 0);
+  };
+  if (F % 4 == 0 && F > 128 && aligned(x, ldx, 4) && aligned(out, ldo, 4)) return 4;
+  if (F % 2 == 0 && F > 64 && aligned(x, ldx, 2) && aligned(out, ldo, 2)) return 2;
+  return 1;
+}
+
+template <class Red, int VEC>
+static int launch(const AggArgs& a, int stages, hipStream_t s) {
+  constexpr int U = VEC == 4 ? 8 : 16;
+  const int ftiles = (int)ceil_div(a.F, 64 * VEC);
+  if (stages & MP_STAGE_MAIN) {
+    dim3 grid((unsigned)ceil_div(a.n_waves, kWavesPerBlock), (unsigned)ftiles);
+    hipLaunchKernelGGL((k_agg_main<Red, VEC, U>), grid, dim3(kBlock), 0, s, a);
+    MP_CHECK_LAUNCH();
+  }
+  if ((stages & MP_STAGE_FIXUP) && a.n_split > 0) {
+    dim3 grid((unsigned)ceil_div(a.n_split, kWavesPerBlock), (unsigned)ftiles);
+    hipLaunchKernelGGL((k_agg_fixup<Red, VEC>), grid, dim3(kBlock), 0, s, a);
+    MP_CHECK_LAUNCH();
+  }
+  return MP_OK;
+}
+
+template <int VEC>
+static int dispatch_reduce(const AggArgs& a, int reduce, int stages, hipStream_t s) {
+  const bool hw = a.w != nullptr;
+  switch (reduce) {
+    case MP_REDUCE_SUM:
+      return hw ? launch<SumRed<VEC, true, false>, VEC>(a, stages, s)
+                : launch<SumRed<VEC, false, false>, VEC>(a, stages, s);
+    case MP_REDUCE_MEAN:
+      return hw ? launch<SumRed<VEC, true, true>, VEC>(a, stages, s)
+                : launch<SumRed<VEC, false, true>, VEC>(a, stages, s);
+    case MP_REDUCE_MAX:
+      return hw ? launch<ArgRed<VEC, true, true>, VEC>(a, stages, s)
+                : launch<ArgRed<VEC, false, true>, VEC>(a, stages, s);
+    case MP_REDUCE_MIN:
+      return hw ? launch<ArgRed<VEC, true, false>, VEC>(a, stages, s)
+                : launch<ArgRed<VEC, false, false>, VEC>(a, stages, s);
+  }
+  set_error("mp_aggregate_f32: unknown reduce %d", reduce);
+  return MP_ERR_ARG;
+}
+
+static int64_t slab_ld_for(int F) { return ceil_div(F, 256) * 256; }
+
+static int check_graph(const mp_csr* g, const char* who) {
+  MP_CHECK_ARG(g != nullptr, "%s: null graph", who);
+  MP_CHECK_ARG(g->rowptr && g->wave_row && g->wave_slot && (g->n_split == 0 || g->split_waves),
+               "%s: graph has null arrays", who);
+  MP_CHECK_ARG(g->n_edges == 0 || (g->col && g->eid), "%s: graph has null col/eid", who);
+  MP_CHECK_ARG(g->chunk > 0 && g->chunk % 64 == 0 && g->n_waves >= 1, "%s: bad schedule", who);
+  return MP_OK;
+}
+
+static void fill_graph(AggArgs& a, const mp_csr* g) {
+  a.rowptr = g->rowptr;
+  a.col = g->col;
+  a.eid = g->eid;
+  a.wave_row = g->wave_row;
+  a.wave_slot = g->wave_slot;
+  a.split_waves = g->split_waves;
+  a.n_rows = g->n_rows;
+  a.n_edges = g->n_edges;
+  a.chunk = g->chunk;
+  a.n_waves = g->n_waves;
+  a.n_split = g->n_split;
+}
+
+}  // namespace mp
+
+using namespace mp;
+
+extern "C" {
+
+size_t mp_aggregate_slab_bytes(const mp_csr* g, int32_t F, int32_t reduce) {
+  if (!g || F <= 0) return 256;
+  size_t slots = 2 * (size_t)g->n_waves;
+  size_t per = (size_t)slab_ld_for(F) * 4;
+  size_t v = align_up(slots * per, 256);
+  bool arg = reduce == MP_REDUCE_MAX || reduce == MP_REDUCE_MIN;
+  return v + (arg ? v : 0) + 256;
+}
+
+int mp_aggregate_f32(const mp_csr* g, const float* w, const float* x, int64_t ldx, int32_t F,
+                     int32_t reduce, int32_t flags, const float* bias, float* out, int64_t ldo,
+                     int64_t* arg_out, void* slab, size_t slab_bytes, int32_t stages, void* stream) {
+  int rc = check_graph(g, "mp_aggregate_f32");
+  if (rc) return rc;
+  MP_CHECK_ARG(F > 0, "mp_aggregate_f32: F must be positive");
+  MP_CHECK_ARG(out != nullptr && (g->n_edges == 0 || x != nullptr), "mp_aggregate_f32: null x/out");
+  MP_CHECK_ARG(ldx >= F && ldo >= F, "mp_aggregate_f32: leading dimension < F");
+  const bool is_arg = reduce == MP_REDUCE_MAX || reduce == MP_REDUCE_MIN;
+  MP_CHECK_ARG(!is_arg || arg_out != nullptr, "mp_aggregate_f32: max/min need arg_out");
+  MP_CHECK_ARG(slab != nullptr && slab_bytes >= mp_aggregate_slab_bytes(g, F, reduce),
+               "mp_aggregate_f32: slab workspace too small (%zu < %zu)", slab_bytes,
+               mp_aggregate_slab_bytes(g, F, reduce));
+  AggArgs a{};
+  fill_graph(a, g);
+  a.F = F;
+  a.w = w;
+  a.x = x;
+  a.ldx = ldx;
+  a.flags = flags;
+  a.bias = bias;
+  a.out = out;
+  a.ldo = ldo;
+  a.arg_out = arg_out;
+  a.slab_ld = slab_ld_for(F);
+  size_t v = align_up(2 * (size_t)g->n_waves * (size_t)a.slab_ld * 4, 256);
+  a.slab_v = (float*)slab;
+  a.slab_a = is_arg ? (int32_t*)((char*)slab + v) : nullptr;
+  hipStream_t s = as_stream(stream);
+  switch (pick_vec(F, ldx, x, ldo, out)) {
+    case 4: return dispatch_reduce<4>(a, reduce, stages, s);
+    case 2: return dispatch_reduce<2>(a, reduce, stages, s);
+    default: return dispatch_reduce<1>(a, reduce, stages, s);
+  }
+}
+
+size_t mp_gat_slab_bytes(const mp_csr* g, int32_t H, int32_t C) {
+  if (!g || H <= 0 || C <= 0) return 256;
+  size_t slots = 2 * (size_t)g->n_waves;
+  size_t v = align_up(slots * (size_t)slab_ld_for(H * C) * 4, 256);
+  size_t st = align_up(slots * (size_t)H * 2 * 4, 256);
+  return v + st + 256;
+}
+
+int mp_gat_aggregate_f32(const mp_csr* g, const float* xw, const float* a_src, const float* a_dst,
+                         int32_t H, int32_t C, float slope, const float* bias, float* out,
+                         int64_t ldo, float* row_stats, void* slab, size_t slab_bytes,
+                         int32_t stages, void* stream) {
+  int rc = check_graph(g, "mp_gat_aggregate_f32");
+  if (rc) return rc;
+  MP_CHECK_ARG(H > 0 && C > 0, "mp_gat_aggregate_f32: H, C must be positive");
+  MP_CHECK_ARG(xw && a_src && a_dst && out, "mp_gat_aggregate_f32: null input");
+  const int F = H * C;
+  MP_CHECK_ARG(ldo >= F, "mp_gat_aggregate_f32: ldo < H*C");
+  MP_CHECK_ARG(slab != nullptr && slab_bytes >= mp_gat_slab_bytes(g, H, C),
+               "mp_gat_aggregate_f32: slab workspace too small");
+  AggArgs a{};
+  fill_graph(a, g);
+  a.F = F;
+  a.x = xw;
+  a.ldx = F;
+  a.out = out;
+  a.ldo = ldo;
+  a.bias = bias;
+  a.a_src = a_src;
+  a.a_dst = a_dst;
+  a.H = H;
+  a.C = C;
+  a.slope = slope;
+  a.row_stats = row_stats;
+  a.slab_ld = slab_ld_for(F);
+  size_t v = align_up(2 * (size_t)g->n_waves * (size_t)a.slab_ld * 4, 256);
+  a.slab_v = (float*)slab;
+  a.slab_s = (float*)((char*)slab + v);
+  hipStream_t s = as_stream(stream);
+  int vec = pick_vec(F, F, xw, ldo, out);
+  while (vec > 1 && C % vec != 0) vec >>= 1;  // a lane's features must share a head
+  switch (vec) {
+    case 4: return launch<GatRed<4>, 4>(a, stages, s);
+    case 2: return launch<GatRed<2>, 2>(a, stages, s);
+    default: return launch<GatRed<1>, 1>(a, stages, s);
+  }
+}
+
+}  // extern "C"

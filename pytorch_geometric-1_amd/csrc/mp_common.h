@@ -1,0 +1,86 @@
+// Internal helpers shared by the mi355_mp HIP translation units (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "../../include/mi355_mp.h"
+
+namespace mp {
+
+void set_error(const char* fmt, ...);
+
+#define MP_CHECK_ARG(cond, ...)        \
+  do {                                 \
+    if (!(cond)) {                     \
+      ::mp::set_error(__VA_ARGS__);    \
+      return MP_ERR_ARG;               \
+    }                                  \
+  } while (0)
+
+#define MP_CHECK_HIP(expr)                                                   \
+  do {                                                                       \
+    hipError_t _e = (expr);                                                  \
+    if (_e != hipSuccess) {                                                  \
+      ::mp::set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), \
+                      __FILE__, __LINE__);                                   \
+      return MP_ERR_HIP;                                                     \
+    }                                                                        \
+  } while (0)
+
+#define MP_CHECK_LAUNCH() MP_CHECK_HIP(hipGetLastError())
+
+static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+static inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// wave-uniform value helpers
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+__device__ __forceinline__ int readlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ float readlane(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// Feature fragment: VEC consecutive fp32 owned by one lane.
+template <int VEC>
+struct Frag {
+  float v[VEC];
+};
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int VEC>
+__device__ __forceinline__ Frag<VEC> load_frag(const float* p) {
+  Frag<VEC> r;
+  if constexpr (VEC == 4) {
+    f32x4 t = *reinterpret_cast<const f32x4*>(p);
+    r.v[0] = t.x; r.v[1] = t.y; r.v[2] = t.z; r.v[3] = t.w;
+  } else if constexpr (VEC == 2) {
+    f32x2 t = *reinterpret_cast<const f32x2*>(p);
+    r.v[0] = t.x; r.v[1] = t.y;
+  } else {
+    r.v[0] = *p;
+  }
+  return r;
+}
+
+template <int VEC>
+__device__ __forceinline__ void store_frag(float* p, const Frag<VEC>& f) {
+  if constexpr (VEC == 4) {
+    f32x4 t = {f.v[0], f.v[1], f.v[2], f.v[3]};
+    *reinterpret_cast<f32x4*>(p) = t;
+  } else if constexpr (VEC == 2) {
+    f32x2 t = {f.v[0], f.v[1]};
+    *reinterpret_cast<f32x2*>(p) = t;
+  } else {
+    *p = f.v[0];
+  }
+}
+
+}  // namespace mp

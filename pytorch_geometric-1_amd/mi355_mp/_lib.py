@@ -1,0 +1,111 @@
+"""ctypes binding of the C-ABI in include/mi355_mp.h (libmi355_mp.so).
+
+The shared library is built in-tree by ``__graft_entry__.build()`` (or
+``make -C pytorch_geometric-1_amd/csrc``).  There is no fallback: if the
+library is missing, or a tensor is not on a ROCm device, every op raises.
+Only plain pointers, sizes and the HIP stream handle cross the boundary.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MI355_MP_LIB", os.path.join(_HERE, "libmi355_mp.so"))
+
+MP_OK = 0
+MP_REDUCE = {"sum": 0, "add": 0, "mean": 1, "max": 2, "min": 3}
+MP_FLAG_INIT_FROM_OUT = 1
+MP_FLAG_PYG_MASK = 2
+MP_STAGE_MAIN = 1
+MP_STAGE_FIXUP = 2
+MP_STAGE_ALL = 3
+
+c_p = ctypes.c_void_p
+i64 = ctypes.c_int64
+i32 = ctypes.c_int32
+f32 = ctypes.c_float
+sz = ctypes.c_size_t
+
+
+class MpCsr(ctypes.Structure):
+    _fields_ = [
+        ("rowptr", c_p), ("col", c_p), ("eid", c_p), ("wave_row", c_p),
+        ("wave_slot", c_p), ("split_waves", c_p), ("n_rows", i64),
+        ("n_edges", i64), ("chunk", i32), ("n_waves", i32), ("n_split", i32),
+        ("reserved", i32),
+    ]
+
+
+# name -> (restype, argtypes); mirrors include/mi355_mp.h one to one.
+SIGNATURES = {
+    "mp_last_error": (ctypes.c_char_p, []),
+    "mp_abi_version": (ctypes.c_int, []),
+    "mp_csr_build_workspace": (sz, [i64, i64]),
+    "mp_csr_build": (ctypes.c_int, [c_p, c_p, i64, i64, i64, c_p, c_p, c_p, c_p, c_p, sz, c_p]),
+    "mp_schedule_n_waves": (i32, [i64, i64, i32]),
+    "mp_schedule_workspace": (sz, [i32]),
+    "mp_schedule_build": (ctypes.c_int, [c_p, i64, i64, i32, c_p, c_p, c_p, c_p, c_p, sz, c_p]),
+    "mp_aggregate_slab_bytes": (sz, [ctypes.POINTER(MpCsr), i32, i32]),
+    "mp_aggregate_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, i64, i32, i32, i32, c_p,
+                                        c_p, i64, c_p, c_p, sz, i32, c_p]),
+    "mp_gat_node_scores_f32": (ctypes.c_int, [c_p, i64, i32, i32, c_p, c_p, c_p, c_p]),
+    "mp_gat_slab_bytes": (sz, [ctypes.POINTER(MpCsr), i32, i32]),
+    "mp_gat_aggregate_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, c_p, i32, i32, f32, c_p,
+                                            c_p, i64, c_p, c_p, sz, i32, c_p]),
+    "mp_gat_alpha_f32": (ctypes.c_int, [c_p, c_p, i64, i32, c_p, c_p, f32, c_p, c_p, c_p]),
+    "mp_gather_rows_f32": (ctypes.c_int, [c_p, i64, c_p, i64, i32, c_p, i64, c_p]),
+    "mp_permute_f32": (ctypes.c_int, [c_p, c_p, i64, c_p, c_p]),
+    "mp_scatter_arg_backward_f32": (ctypes.c_int, [c_p, c_p, i64, i32, i64, c_p, c_p, i64, c_p]),
+    "mp_gcn_norm_f32": (ctypes.c_int, [c_p, c_p, c_p, i64, i64, c_p, c_p, c_p]),
+}
+
+_lib = None
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def load(path=None):
+    """Load (once) and return the native library; raise if it is absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise NativeLibraryMissing(
+            "mi355_mp: native library %s not found; build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` "
+            "(there is no CPU fallback)" % p)
+    lib = ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != MP_OK:
+        msg = load().mp_last_error().decode(errors="replace")
+        raise RuntimeError("%s failed (code %d): %s" % (what, rc, msg))
+
+
+def stream_ptr(device=None):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def require_device(*tensors):
+    """Every hot-path op runs on the GPU only; there is no CPU fallback."""
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError(
+                "mi355_mp: tensors must be on a ROCm (cuda) device; got %s. "
+                "The MI355X engine has no CPU fallback." % t.device)

@@ -1,0 +1,106 @@
+"""Destination-range graph sharding with a halo exchange.
+
+The reference's only multi-GPU mechanism is torch_geometric.nn.DataParallel
+(replicas over a list of small graphs; /root/reference/ConvexPruning.py:530,
+examples/data_parallel.py:35-49).  One large graph is sharded here instead:
+
+  * rank p owns the destination rows [lo_p, hi_p); cut points come from the
+    in-degree prefix sum so every rank gets ~E/P edges (power-law safe);
+  * rank p also owns the node features of [lo_p, hi_p) (it computes its own
+    X W rows);
+  * halo plan (built once, cached like GCNConv(cached=True)): the sorted
+    unique remote source nodes of p's in-edges, grouped by owner; local
+    column ids are renumbered into [0, n_own + n_halo);
+  * per layer: every rank packs the rows its peers requested (native row
+    gather), one all_to_all_single moves them (RCCL over xGMI: each peer pair
+    on its own link), then the local fused aggregation runs on
+    [own rows ; halo rows].
+
+The plan logic is host/torch code (tested with gloo on CPU); the data path
+calls the native kernels through `local_aggregate`, which tests replace with
+the CPU oracle.
+"""
+import torch
+import torch.distributed as dist
+
+
+def edge_balanced_cuts(in_degree, parts):
+    """Row cut points [0=c_0 <= ... <= c_P = N] with ~equal edges per part."""
+    N = in_degree.numel()
+    csum = torch.cumsum(in_degree.to(torch.int64), 0)
+    E = int(csum[-1]) if N else 0
+    cuts = [0]
+    for p in range(1, parts):
+        target = (E * p) // parts
+        c = int(torch.searchsorted(csum, torch.tensor(target, device=csum.device), right=True))
+        cuts.append(max(c, cuts[-1]))
+    cuts.append(N)
+    return cuts
+
+
+class ShardPlan:
+    """Everything rank `rank` needs to aggregate its destination rows."""
+
+    def __init__(self, edge_index, num_nodes, rank, world, cuts=None, flow="source_to_target"):
+        i, j = (1, 0) if flow == "source_to_target" else (0, 1)
+        dst_all, src_all = edge_index[i], edge_index[j]
+        dev = edge_index.device
+        if cuts is None:
+            deg = torch.bincount(dst_all, minlength=num_nodes)
+            cuts = edge_balanced_cuts(deg, world)
+        self.cuts = cuts
+        self.rank, self.world = rank, world
+        lo, hi = cuts[rank], cuts[rank + 1]
+        self.lo, self.hi, self.n_own = lo, hi, hi - lo
+        mine = (dst_all >= lo) & (dst_all < hi)
+        self.edge_pos = torch.nonzero(mine).view(-1)          # positions in the global edge order
+        dst = dst_all[self.edge_pos] - lo
+        src = src_all[self.edge_pos]
+        owner = torch.searchsorted(torch.tensor(cuts[1:], device=dev), src, right=True)
+        remote = owner != rank
+        halo_nodes = torch.unique(src[remote])                 # sorted, hence grouped by owner
+        halo_owner = torch.searchsorted(torch.tensor(cuts[1:], device=dev), halo_nodes, right=True)
+        self.halo_nodes = halo_nodes
+        self.recv_counts = [int((halo_owner == q).sum()) for q in range(world)]
+        # local column ids: own rows first, then halo rows in sorted order
+        local_src = torch.empty_like(src)
+        local_src[~remote] = src[~remote] - lo
+        local_src[remote] = self.n_own + torch.searchsorted(halo_nodes, src[remote])
+        self.local_edge_index = torch.stack([local_src, dst]) if i == 1 else torch.stack([dst, local_src])
+        self.n_local_src = self.n_own + halo_nodes.numel()
+        self.send_idx = None
+        self.send_counts = None
+
+    def exchange_requests(self, group=None):
+        """All-to-all of the requested node ids (once per plan)."""
+        dev = self.halo_nodes.device
+        recv_counts = torch.tensor(self.recv_counts, dtype=torch.int64, device=dev)
+        send_counts = torch.empty_like(recv_counts)
+        dist.all_to_all_single(send_counts, recv_counts, group=group)
+        self.send_counts = send_counts.tolist()
+        requests = torch.empty(sum(self.send_counts), dtype=torch.int64, device=dev)
+        dist.all_to_all_single(requests, self.halo_nodes.contiguous(), output_split_sizes=self.send_counts,
+                               input_split_sizes=self.recv_counts, group=group)
+        self.send_idx = requests - self.lo     # rows of my own block that peers need
+        return self
+
+    def halo_exchange(self, x_own, gather_rows, group=None):
+        """[own rows ; halo rows] for this rank (one all_to_all_single)."""
+        F = x_own.shape[1]
+        send = gather_rows(x_own, self.send_idx) if self.send_idx.numel() else \
+            x_own.new_empty((0, F))
+        halo = x_own.new_empty((self.halo_nodes.numel(), F))
+        dist.all_to_all_single(halo, send.contiguous(), output_split_sizes=self.recv_counts,
+                               input_split_sizes=self.send_counts, group=group)
+        return torch.cat([x_own, halo], dim=0)
+
+
+def sharded_propagate(plan, x_own, local_aggregate, gather_rows, edge_weight=None, group=None):
+    """One sharded aggregation: halo exchange then local aggregation.
+
+    local_aggregate(x_local, local_edge_index, n_dst, n_src, edge_weight) -> [n_own, F]
+    edge_weight: per-edge weights in GLOBAL edge order (sliced by the plan).
+    """
+    x_local = plan.halo_exchange(x_own, gather_rows, group)
+    w = edge_weight[plan.edge_pos] if edge_weight is not None else None
+    return local_aggregate(x_local, plan.local_edge_index, plan.n_own, plan.n_local_src, w)

@@ -1,0 +1,190 @@
+"""Destination-sorted CSR graphs + merge-path schedules, built and cached on the GPU.
+
+PyG 1.4.3 keeps a graph as ``edge_index`` [2, E] int64 and, on every
+``propagate``, gathers ``x[edge_index[j]]`` and scatter-adds into
+``edge_index[i]``.  The engine instead sorts the edges by the
+aggregation index once (stable: each row keeps its edges in original order)
+and reuses that CSR for every aggregation over the same ``edge_index``
+tensor.  Caches are keyed on the tensor object (identity + version counter)
+and dropped when the tensor dies, mirroring GCNConv's ``cached=True`` idea
+without changing its semantics.
+"""
+import weakref
+
+import torch
+
+from . import _lib
+
+DEFAULT_CHUNK = 256
+
+
+class CSR:
+    """One stable CSR of ``key`` (int64 [E]) with gather column ``other``.
+
+    rowptr[n_rows+1], col[E] (= other[eid] or eid), eid[E] : int32 on device.
+    """
+
+    def __init__(self, key, other, n_rows, n_other, chunk=DEFAULT_CHUNK):
+        _lib.require_device(key)
+        lib = _lib.load()
+        dev = key.device
+        key = key.contiguous()
+        other = other.contiguous() if other is not None else None
+        E = key.numel()
+        self.n_rows = int(n_rows)
+        self.n_edges = int(E)
+        self.n_other = int(n_other)
+        self.device = dev
+        self.chunk = int(chunk)
+        self.rowptr = torch.empty(self.n_rows + 1, dtype=torch.int32, device=dev)
+        self.col = torch.empty(max(E, 1), dtype=torch.int32, device=dev)
+        self.eid = torch.empty(max(E, 1), dtype=torch.int32, device=dev)
+        bad = torch.zeros(1, dtype=torch.int32, device=dev)
+        st = _lib.stream_ptr(dev)
+        ws_bytes = lib.mp_csr_build_workspace(E, self.n_rows)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        _lib.check(lib.mp_csr_build(key.data_ptr(), _lib.ptr(other), E, self.n_rows, self.n_other,
+                                    self.rowptr.data_ptr(), self.col.data_ptr(), self.eid.data_ptr(),
+                                    bad.data_ptr(), ws.data_ptr(), ws_bytes, st), "mp_csr_build")
+        nbad = int(bad.item())
+        if nbad:
+            raise IndexError("mi355_mp: %d edge indices out of range (rows %d, columns %d)"
+                             % (nbad, self.n_rows, self.n_other))
+        del ws
+        # merge-path schedule
+        self.n_waves = int(lib.mp_schedule_n_waves(self.n_rows, E, self.chunk))
+        self.wave_row = torch.empty(self.n_waves + 1, dtype=torch.int32, device=dev)
+        self.wave_slot = torch.empty(self.n_waves + 1, dtype=torch.int32, device=dev)
+        self.split_waves = torch.empty(self.n_waves, dtype=torch.int32, device=dev)
+        n_split = torch.zeros(1, dtype=torch.int32, device=dev)
+        sws = lib.mp_schedule_workspace(self.n_waves)
+        ws = torch.empty(sws, dtype=torch.uint8, device=dev)
+        _lib.check(lib.mp_schedule_build(self.rowptr.data_ptr(), self.n_rows, E, self.chunk,
+                                         self.wave_row.data_ptr(), self.wave_slot.data_ptr(),
+                                         self.split_waves.data_ptr(), n_split.data_ptr(),
+                                         ws.data_ptr(), sws, st), "mp_schedule_build")
+        self.n_split = int(n_split.item())
+        self._structs = {}
+        self._deg = None
+
+    def struct(self, gather="other"):
+        """ctypes mp_csr; gather='other' reads x[other] rows, 'eid' reads message rows."""
+        s = self._structs.get(gather)
+        if s is None:
+            col = self.col if gather == "other" else self.eid
+            s = _lib.MpCsr(self.rowptr.data_ptr(), col.data_ptr(), self.eid.data_ptr(),
+                           self.wave_row.data_ptr(), self.wave_slot.data_ptr(),
+                           self.split_waves.data_ptr(), self.n_rows, self.n_edges, self.chunk,
+                           self.n_waves, self.n_split, 0)
+            self._structs[gather] = s
+        return s
+
+    def degree(self):
+        """In-degree per row (int64), from rowptr."""
+        if self._deg is None:
+            rp = self.rowptr.to(torch.int64)
+            self._deg = rp[1:] - rp[:-1]
+        return self._deg
+
+    def to_csr_order(self, edge_values):
+        """Permute a per-edge fp32 vector (original order) into CSR slot order."""
+        lib = _lib.load()
+        edge_values = edge_values.contiguous()
+        out = torch.empty_like(edge_values)
+        if self.n_edges:
+            _lib.check(lib.mp_permute_f32(edge_values.data_ptr(), self.eid.data_ptr(), self.n_edges,
+                                          out.data_ptr(), _lib.stream_ptr(self.device)),
+                       "mp_permute_f32")
+        return out
+
+
+class Graph:
+    """Both directions of one edge_index for a given flow.
+
+    ``dst`` : CSR keyed on the aggregation index edge_index[i] (gathers edge_index[j])
+    ``src`` : CSR keyed on edge_index[j] (transpose; used by backward passes)
+
+    Holds only a weak reference to ``edge_index`` (the caches must not keep
+    the user's tensor alive); callers keep it alive while a direction is
+    first built (autograd saves it for backward).
+    """
+
+    def __init__(self, edge_index, n_dst, n_src, flow="source_to_target", chunk=DEFAULT_CHUNK):
+        self.i, self.j = (1, 0) if flow == "source_to_target" else (0, 1)
+        self._ei = weakref.ref(edge_index)
+        self.n_dst, self.n_src = int(n_dst), int(n_src)
+        self.chunk = chunk
+        self._dst = None
+        self._src = None
+
+    def _edge_index(self):
+        ei = self._ei()
+        if ei is None:
+            raise RuntimeError("mi355_mp: edge_index was freed before its CSR was built")
+        return ei
+
+    @property
+    def dst(self):
+        if self._dst is None:
+            ei = self._edge_index()
+            self._dst = CSR(ei[self.i], ei[self.j], self.n_dst, self.n_src, self.chunk)
+        return self._dst
+
+    @property
+    def src(self):
+        if self._src is None:
+            ei = self._edge_index()
+            self._src = CSR(ei[self.j], ei[self.i], self.n_src, self.n_dst, self.chunk)
+        return self._src
+
+
+class _Cache:
+    """id(tensor) -> value, invalidated by the tensor's version counter or death."""
+
+    def __init__(self):
+        self._d = {}
+
+    def get(self, t, extra, factory):
+        if t._base is not None:  # a view (e.g. edge_index[1]): key on its base tensor
+            extra = (extra, t.storage_offset(), tuple(t.stride()), tuple(t.shape))
+            t = t._base
+        k = (id(t), extra)
+        hit = self._d.get(k)
+        if hit is not None and hit[0] == t._version:
+            return hit[1]
+        val = factory()
+        if hit is None:
+            try:
+                weakref.finalize(t, self._drop, id(t))
+            except TypeError:  # pragma: no cover - non-weakrefable input
+                return val
+        self._d[k] = (t._version, val)
+        return val
+
+    def _drop(self, tid):
+        for k in [k for k in self._d if k[0] == tid]:
+            del self._d[k]
+
+    def clear(self):
+        self._d.clear()
+
+
+_graph_cache = _Cache()
+_index_cache = _Cache()
+
+
+def graph_for(edge_index, n_dst, n_src, flow="source_to_target"):
+    """Cached Graph for an edge_index tensor (rebuilt if it is modified in place)."""
+    return _graph_cache.get(edge_index, (int(n_dst), int(n_src), flow),
+                            lambda: Graph(edge_index, n_dst, n_src, flow))
+
+
+def csr_for_index(index, n_rows):
+    """Cached CSR of a bare 1-D index (torch_scatter path: gathers message rows)."""
+    return _index_cache.get(index, int(n_rows),
+                            lambda: CSR(index.to(torch.int64), None, n_rows, index.numel()))
+
+
+def clear_caches():
+    _graph_cache.clear()
+    _index_cache.clear()

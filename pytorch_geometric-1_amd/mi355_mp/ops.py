@@ -1,0 +1,365 @@
+"""Torch-facing ops over the native engine (autograd included).
+
+Every function here launches HIP kernels from libmi355_mp.so on the current
+stream; inputs must already live on the GPU.  Backward passes reuse the same
+kernels on the transposed CSR.
+
+Reference semantics (all [U], restated from torch_scatter 2.0.4 /
+torch_geometric 1.4.3; see oracle/ for the CPU restatement used as checker):
+  * sum/add   : scatter_sum = zeros(...).scatter_add_(0, index, src)
+  * mean      : scatter_sum / count.clamp(1)
+  * max/min   : (out, arg); strict compare, first edge wins ties, empty row
+                -> (0, src.size(0)); scatter_(...) also masks <-10000 / >10000
+"""
+import torch
+
+from . import _lib
+from .graph import csr_for_index
+
+_REDUCES = ("sum", "add", "mean", "max", "min")
+
+
+def _f32_2d(x, what):
+    if x.dtype != torch.float32:
+        raise TypeError("mi355_mp: %s must be float32 (got %s)" % (what, x.dtype))
+    if x.dim() != 2:
+        raise ValueError("mi355_mp: %s must be 2-D [rows, features]" % what)
+    if x.stride(1) != 1:
+        x = x.contiguous()
+    return x
+
+
+def _aggregate(csr, gather, x, w_csr, reduce, flags, bias, out=None, stages=_lib.MP_STAGE_ALL):
+    """Launch mp_aggregate_f32; returns (out, arg_or_None)."""
+    lib = _lib.load()
+    F = x.shape[1]
+    dev = x.device
+    if out is None:
+        out = torch.empty((csr.n_rows, F), dtype=torch.float32, device=dev)
+    is_arg = reduce in ("max", "min")
+    arg = torch.empty((csr.n_rows, F), dtype=torch.int64, device=dev) if is_arg else None
+    if csr.n_rows == 0 or F == 0:
+        return out, arg
+    g = csr.struct(gather)
+    red = _lib.MP_REDUCE[reduce]
+    sb = lib.mp_aggregate_slab_bytes(g, F, red)
+    slab = torch.empty(sb, dtype=torch.uint8, device=dev)
+    _lib.check(lib.mp_aggregate_f32(g, _lib.ptr(w_csr), x.data_ptr(), x.stride(0), F, red, flags,
+                                    _lib.ptr(bias), out.data_ptr(), out.stride(0), _lib.ptr(arg),
+                                    slab.data_ptr(), sb, stages, _lib.stream_ptr(dev)),
+               "mp_aggregate_f32")
+    return out, arg
+
+
+def gather_rows(x, idx):
+    """out = x[idx] via the native row gather (no autograd; see GatherRows)."""
+    lib = _lib.load()
+    x = _f32_2d(x, "x")
+    idx = idx.to(torch.int64).contiguous()
+    out = torch.empty((idx.numel(), x.shape[1]), dtype=torch.float32, device=x.device)
+    if idx.numel() and x.shape[1]:
+        _lib.check(lib.mp_gather_rows_f32(x.data_ptr(), x.stride(0), idx.data_ptr(), idx.numel(),
+                                          x.shape[1], out.data_ptr(), out.stride(0),
+                                          _lib.stream_ptr(x.device)), "mp_gather_rows_f32")
+    return out
+
+
+# ---------------------------------------------------------------------------
+# fused gather -> weight -> reduce over a Graph (MessagePassing fast path)
+# ---------------------------------------------------------------------------
+
+class _FusedPropagate(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, edge_weight, bias, graph, edge_index, reduce, pyg_mask, weight_csr):
+        csr = graph.dst
+        w_csr = weight_csr
+        if w_csr is None and edge_weight is not None:
+            w_csr = csr.to_csr_order(edge_weight.to(torch.float32))
+        is_arg = reduce in ("max", "min")
+        need_mask_grad = is_arg and pyg_mask and ctx.needs_input_grad[0]
+        flags = _lib.MP_FLAG_PYG_MASK if (pyg_mask and not need_mask_grad) else 0
+        fuse_bias = bias if not need_mask_grad else None
+        out, arg = _aggregate(csr, "other", x, w_csr, reduce, flags, fuse_bias)
+        keep = None
+        if need_mask_grad:
+            keep = ~((out < -10000) if reduce == "max" else (out > 10000))
+            out = out.masked_fill(~keep, 0.0)
+            if bias is not None:
+                out = out + bias
+        ctx.graph = graph
+        ctx.reduce = reduce
+        ctx.n_src = x.shape[0]
+        ctx.save_for_backward(x, edge_weight, edge_index, arg, keep)
+        ctx.has_bias = bias is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        x, edge_weight, edge_index, arg, keep = ctx.saved_tensors
+        graph, reduce = ctx.graph, ctx.reduce
+        grad_out = grad_out.contiguous()
+        gx = gw = gb = None
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = grad_out.sum(0)
+        if reduce in ("max", "min"):
+            if ctx.needs_input_grad[1] and edge_weight is not None:
+                raise NotImplementedError("mi355_mp: gradient w.r.t. edge weights of a max/min "
+                                          "aggregation is not implemented")
+            if ctx.needs_input_grad[0]:
+                g = grad_out * keep if keep is not None else grad_out
+                gx = torch.zeros((ctx.n_src, x.shape[1]), dtype=torch.float32, device=x.device)
+                other = edge_index[graph.j].contiguous()
+                lib = _lib.load()
+                if edge_weight is not None:  # d(w*x)/dx = w: fold the weight into the scatter
+                    raise NotImplementedError("mi355_mp: weighted max/min backward not implemented")
+                _lib.check(lib.mp_scatter_arg_backward_f32(g.data_ptr(), arg.data_ptr(), g.shape[0],
+                                                           g.shape[1], graph.dst.n_edges,
+                                                           other.data_ptr(), gx.data_ptr(), gx.stride(0),
+                                                           _lib.stream_ptr(x.device)),
+                           "mp_scatter_arg_backward_f32")
+            return gx, None, gb, None, None, None, None, None
+        g = grad_out
+        if reduce == "mean":
+            deg = graph.dst.degree().clamp(min=1).to(torch.float32)
+            g = g / deg.view(-1, 1)
+        if ctx.needs_input_grad[0]:
+            src = graph.src  # transposed CSR: rows = source nodes, gathers destination rows
+            w_src = src.to_csr_order(edge_weight.to(torch.float32)) if edge_weight is not None else None
+            gx, _ = _aggregate(src, "other", g, w_src, "sum", 0, None)
+        if ctx.needs_input_grad[1] and edge_weight is not None:
+            xi = gather_rows(x, edge_index[graph.j])
+            gi = gather_rows(g, edge_index[graph.i])
+            gw = (xi * gi).sum(-1).to(edge_weight.dtype)
+        return gx, gw, gb, None, None, None, None, None
+
+
+def fused_propagate(graph, x, edge_index, edge_weight=None, reduce="sum", bias=None, pyg_mask=False,
+                    weight_csr=None):
+    """out[i] = REDUCE_{e : index[e] == i} (w[e] * x[other[e]]) (+ bias).
+
+    The fused form of ``propagate`` for message(x_j) / message(x_j, norm)
+    (PyG 1.4.3 MessagePassing [U1] + GCNConv.message [U5]).
+    """
+    if reduce not in _REDUCES:
+        raise ValueError("unknown reduce %r" % (reduce,))
+    reduce = "sum" if reduce == "add" else reduce
+    _lib.require_device(x, edge_index, edge_weight, bias)
+    x = _f32_2d(x, "x")
+    return _FusedPropagate.apply(x, edge_weight, bias, graph, edge_index, reduce, pyg_mask, weight_csr)
+
+
+# ---------------------------------------------------------------------------
+# materialised-message path (torch_scatter semantics)
+# ---------------------------------------------------------------------------
+
+class _SegmentReduce(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, src, index, dim_size, reduce, pyg_mask):
+        csr = csr_for_index(index, dim_size)
+        need_mask_grad = pyg_mask and reduce in ("max", "min") and ctx.needs_input_grad[0]
+        flags = _lib.MP_FLAG_PYG_MASK if (pyg_mask and not need_mask_grad) else 0
+        out, arg = _aggregate(csr, "eid", src, None, reduce, flags, None)
+        ctx.reduce = reduce
+        ctx.csr = csr
+        ctx.n_src = src.shape[0]
+        keep = None
+        if need_mask_grad:
+            keep = ~((out < -10000) if reduce == "max" else (out > 10000))
+            out = out.masked_fill(~keep, 0.0)
+        ctx.save_for_backward(index, arg, keep)
+        if arg is not None:
+            ctx.mark_non_differentiable(arg)
+        return out, arg
+
+    @staticmethod
+    def backward(ctx, grad_out, _grad_arg=None):
+        index, arg, keep = ctx.saved_tensors
+        grad_out = grad_out.contiguous()
+        reduce = ctx.reduce
+        if reduce in ("max", "min"):
+            lib = _lib.load()
+            g = grad_out * keep if keep is not None else grad_out
+            gs = torch.zeros((ctx.n_src, g.shape[1]), dtype=torch.float32, device=g.device)
+            _lib.check(lib.mp_scatter_arg_backward_f32(g.data_ptr(), arg.data_ptr(), g.shape[0], g.shape[1],
+                                                       ctx.n_src, None, gs.data_ptr(), gs.stride(0),
+                                                       _lib.stream_ptr(g.device)),
+                       "mp_scatter_arg_backward_f32")
+            return gs, None, None, None, None
+        g = grad_out
+        if reduce == "mean":
+            g = g / ctx.csr.degree().clamp(min=1).to(torch.float32).view(-1, 1)
+        return gather_rows(g, index), None, None, None, None
+
+
+def segment_reduce(src, index, dim_size, reduce="sum", pyg_mask=False):
+    """torch_scatter.scatter_{sum,mean,max,min}(src, index, 0, dim_size=...) on 2-D src.
+
+    Returns (out, arg) with arg None for sum/mean.
+    """
+    if reduce not in _REDUCES:
+        raise ValueError("unknown reduce %r" % (reduce,))
+    reduce = "sum" if reduce == "add" else reduce
+    _lib.require_device(src, index)
+    src = _f32_2d(src, "src")
+    if index.dim() != 1 or index.numel() != src.shape[0]:
+        raise ValueError("mi355_mp: index must be 1-D with src.size(0) entries")
+    return _SegmentReduce.apply(src, index, int(dim_size), reduce, pyg_mask)
+
+
+def segment_reduce_into(src, index, out, reduce="sum"):
+    """torch_scatter ``out=`` semantics: reduce into (and return) the given out tensor."""
+    reduce = "sum" if reduce == "add" else reduce
+    _lib.require_device(src, index, out)
+    src = _f32_2d(src, "src")
+    if out.dtype != torch.float32 or out.dim() != 2 or out.stride(1) != 1:
+        raise ValueError("mi355_mp: out must be a row-major float32 [dim_size, F] tensor")
+    if torch.is_grad_enabled() and (src.requires_grad or out.requires_grad):
+        raise NotImplementedError("mi355_mp: autograd through torch_scatter `out=` is not supported")
+    csr = csr_for_index(index, out.shape[0])
+    out, arg = _aggregate(csr, "eid", src, None, reduce, _lib.MP_FLAG_INIT_FROM_OUT, None, out=out)
+    return out, arg
+
+
+class GatherRows(torch.autograd.Function):
+    """x[idx] with backward = segment-sum of the row gradients by idx (native)."""
+
+    @staticmethod
+    def forward(ctx, x, idx):
+        ctx.n = x.shape[0]
+        ctx.save_for_backward(idx)
+        return gather_rows(x, idx)
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        csr = csr_for_index(idx, ctx.n)
+        gx, _ = _aggregate(csr, "eid", g.contiguous(), None, "sum", 0, None)
+        return gx, None
+
+
+def index_select_rows(x, idx):
+    """Differentiable native replacement of x.index_select(0, idx) for 2-D fp32 x."""
+    _lib.require_device(x, idx)
+    return GatherRows.apply(_f32_2d(x, "x"), idx)
+
+
+# ---------------------------------------------------------------------------
+# GCN normalisation (GCNConv.norm [U5])
+# ---------------------------------------------------------------------------
+
+def gcn_norm_weights(edge_index, num_nodes, edge_weight=None):
+    """norm[e] = deg^-1/2[row] * w[e] * deg^-1/2[col], deg = scatter_add(w, row).
+
+    edge_index must already carry the self loops (add_remaining_self_loops).
+    """
+    _lib.require_device(edge_index, edge_weight)
+    lib = _lib.load()
+    E = edge_index.shape[1]
+    dev = edge_index.device
+    row = edge_index[0].contiguous()
+    col = edge_index[1].contiguous()
+    w = edge_weight.to(torch.float32).contiguous() if edge_weight is not None else None
+    deg = torch.empty(max(int(num_nodes), 1), dtype=torch.float32, device=dev)
+    norm = torch.empty(E, dtype=torch.float32, device=dev)
+    _lib.check(lib.mp_gcn_norm_f32(row.data_ptr(), col.data_ptr(), _lib.ptr(w), E, int(num_nodes),
+                                   deg.data_ptr(), norm.data_ptr(), _lib.stream_ptr(dev)), "mp_gcn_norm_f32")
+    return norm
+
+
+# ---------------------------------------------------------------------------
+# GATConv fused attention aggregation (GATConv.message + utils.softmax [U3,U6])
+# ---------------------------------------------------------------------------
+
+def _gat_forward(graph, edge_index, xw, att, H, C, slope, bias, want_alpha):
+    lib = _lib.load()
+    dev = xw.device
+    N = xw.shape[0]
+    csr = graph.dst
+    st = _lib.stream_ptr(dev)
+    if graph.n_dst != N:
+        raise ValueError("mi355_mp: fused GAT needs a square graph (n_dst == x.size(0))")
+    att_c = att.reshape(H, 2 * C).contiguous().to(torch.float32)
+    a_src = torch.empty((N, H), dtype=torch.float32, device=dev)
+    a_dst = torch.empty((N, H), dtype=torch.float32, device=dev)
+    if N:
+        _lib.check(lib.mp_gat_node_scores_f32(xw.data_ptr(), N, H, C, att_c.data_ptr(), a_src.data_ptr(),
+                                              a_dst.data_ptr(), st), "mp_gat_node_scores_f32")
+    out = torch.empty((graph.n_dst, H * C), dtype=torch.float32, device=dev)
+    stats = torch.empty((graph.n_dst, H, 2), dtype=torch.float32, device=dev)
+    g = csr.struct("other")
+    sb = lib.mp_gat_slab_bytes(g, H, C)
+    slab = torch.empty(sb, dtype=torch.uint8, device=dev)
+    _lib.check(lib.mp_gat_aggregate_f32(g, xw.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(), H, C, float(slope),
+                                        _lib.ptr(bias), out.data_ptr(), out.stride(0), stats.data_ptr(),
+                                        slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st), "mp_gat_aggregate_f32")
+    alpha = None
+    if want_alpha:
+        E = edge_index.shape[1]
+        alpha = torch.empty((E, H), dtype=torch.float32, device=dev)
+        src = edge_index[graph.j].contiguous()
+        dst = edge_index[graph.i].contiguous()
+        _lib.check(lib.mp_gat_alpha_f32(src.data_ptr(), dst.data_ptr(), E, H, a_src.data_ptr(),
+                                        a_dst.data_ptr(), float(slope), stats.data_ptr(), alpha.data_ptr(), st),
+                   "mp_gat_alpha_f32")
+    return out, alpha, a_src, a_dst
+
+
+class _GatPropagate(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, xw, att, bias, graph, edge_index, H, C, slope, want_alpha):
+        need_grad = any(ctx.needs_input_grad[:3])
+        out, alpha, a_src, a_dst = _gat_forward(graph, edge_index, xw, att, H, C, slope, bias,
+                                                want_alpha or need_grad)
+        ctx.graph, ctx.H, ctx.C, ctx.slope = graph, H, C, slope
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(xw, att, edge_index, alpha, a_src, a_dst)
+        if alpha is not None:
+            ctx.mark_non_differentiable(alpha)
+        return out, alpha
+
+    @staticmethod
+    def backward(ctx, grad_out, _ga=None):
+        # Edge-level autograd of GATConv.message/softmax on [E,H] tensors; the
+        # [E,H*C] steps go through the native gather.  (Round-1 backward: the
+        # forward is the hot path.)
+        xw, att, edge_index, alpha, a_src, a_dst = ctx.saved_tensors
+        graph, H, C, slope = ctx.graph, ctx.H, ctx.C, ctx.slope
+        N = xw.shape[0]
+        src = edge_index[graph.j]
+        dst = edge_index[graph.i]
+        g = grad_out.contiguous()
+        gb = g.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        xj = gather_rows(xw, src).view(-1, H, C)
+        gi = gather_rows(g, dst).view(-1, H, C)
+        # message grad: d out_i / d x_j = alpha
+        gx = torch.zeros_like(xw).view(-1, H, C)
+        gx.index_add_(0, src, gi * alpha.unsqueeze(-1))
+        # attention grad
+        dalpha = (gi * xj).sum(-1)                                   # [E,H]
+        rs = torch.zeros((graph.n_dst, H), dtype=torch.float32, device=xw.device)
+        rs.index_add_(0, dst, alpha * dalpha)
+        ds = alpha * (dalpha - rs[dst])
+        s = a_src[src] + a_dst[dst]
+        de = ds * torch.where(s > 0, torch.ones_like(s), torch.full_like(s, slope))
+        ga_src = torch.zeros_like(a_src).index_add_(0, src, de)
+        ga_dst = torch.zeros((graph.n_dst, H), dtype=torch.float32, device=xw.device).index_add_(0, dst, de)
+        att3 = att.reshape(H, 2 * C)
+        x3 = xw.view(-1, H, C)
+        gx = gx + ga_src.unsqueeze(-1) * att3[:, C:].unsqueeze(0)
+        gx[:graph.n_dst] = gx[:graph.n_dst] + ga_dst.unsqueeze(-1) * att3[:, :C].unsqueeze(0)
+        gatt = None
+        if ctx.needs_input_grad[1]:
+            gd = (ga_dst.unsqueeze(-1) * x3[:graph.n_dst]).sum(0)
+            gs = (ga_src.unsqueeze(-1) * x3).sum(0)
+            gatt = torch.cat([gd, gs], dim=-1).view_as(att)
+        del N
+        return gx.view(-1, H * C), gatt, gb, None, None, None, None, None, None
+
+
+def gat_propagate(graph, edge_index, xw, att, heads, out_channels, negative_slope=0.2, bias=None,
+                  return_alpha=False):
+    """Fused GATConv aggregation: returns (out [N, H*C], alpha [E, H] or None)."""
+    _lib.require_device(xw, edge_index, att, bias)
+    xw = _f32_2d(xw, "x@W").contiguous()
+    return _GatPropagate.apply(xw, att, bias, graph, edge_index, int(heads), int(out_channels),
+                               float(negative_slope), bool(return_alpha))

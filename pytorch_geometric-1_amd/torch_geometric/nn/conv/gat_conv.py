@@ -1,0 +1,130 @@
+"""GATConv (PyG 1.4.3 [U6]; callers /root/reference/ConvexPruning.py:209-214,
+/root/reference/examples/ppi.py:22-28).
+
+    alpha_ij = softmax_i(leaky_relu(a^T [W x_i || W x_j]))
+    x'_i     = sum_j alpha_ij W x_j        (per head; concat or mean)
+
+forward: x W on hipBLASLt; per-node scores a_dst = <Wx, att[:C]>,
+a_src = <Wx, att[C:]> (a split of the reference's (cat[x_i,x_j]*att).sum(-1));
+then leaky_relu + segment softmax (+1e-16) + weighted aggregation + bias in
+ONE online-softmax HIP kernel (mp_gat_aggregate_f32).  Attention dropout in
+training mode (dropout > 0) needs torch's RNG on alpha, so that case runs the
+generic message path (still native gathers / scatters).
+"""
+import torch
+import torch.nn.functional as F
+from torch.nn import Parameter
+
+from mi355_mp import ops as _ops
+from mi355_mp.graph import graph_for
+
+from ...utils import softmax
+from ..inits import glorot, zeros
+from .message_passing import MessagePassing
+from ._structure import gat_loops
+
+
+class GATConv(MessagePassing):
+    r"""The graph attentional operator from the `"Graph Attention Networks"
+    <https://arxiv.org/abs/1710.10903>`_ paper.
+
+    Args:
+        in_channels (int), out_channels (int), heads (int, default 1),
+        concat (bool, default True), negative_slope (float, default 0.2),
+        dropout (float, default 0), bias (bool, default True).
+    """
+
+    def __init__(self, in_channels, out_channels, heads=1, concat=True, negative_slope=0.2, dropout=0,
+                 bias=True, **kwargs):
+        super(GATConv, self).__init__(aggr="add", **kwargs)
+        self.in_channels = in_channels
+        self.out_channels = out_channels
+        self.heads = heads
+        self.concat = concat
+        self.negative_slope = negative_slope
+        self.dropout = dropout
+        self.weight = Parameter(torch.Tensor(in_channels, heads * out_channels))
+        self.att = Parameter(torch.Tensor(1, heads, 2 * out_channels))
+        if bias and concat:
+            self.bias = Parameter(torch.Tensor(heads * out_channels))
+        elif bias and not concat:
+            self.bias = Parameter(torch.Tensor(out_channels))
+        else:
+            self.register_parameter("bias", None)
+        self.alpha = None
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        glorot(self.weight)
+        glorot(self.att)
+        zeros(self.bias)
+
+    def _can_fuse(self, x, size):
+        return (size is None and torch.is_tensor(x) and x.is_cuda and x.dtype == torch.float32
+                and type(self).message is GATConv.message and type(self).update is GATConv.update
+                and type(self).aggregate is MessagePassing.aggregate and self.node_dim == 0
+                and (self.dropout == 0 or not self.training))
+
+    def forward(self, x, edge_index, size=None, return_attention_weights=False):
+        """"""
+        if size is None and torch.is_tensor(x):
+            edge_index = gat_loops(edge_index, x.size(self.node_dim))
+
+        if self._can_fuse(x, size):
+            xw = torch.matmul(x, self.weight)
+            N = xw.size(0)
+            graph = graph_for(edge_index, N, N, self.flow)
+            fused_bias = self.bias if self.concat else None
+            out, alpha = _ops.gat_propagate(graph, edge_index, xw, self.att, self.heads, self.out_channels,
+                                            self.negative_slope, fused_bias, return_attention_weights)
+            if not self.concat:
+                out = out.view(-1, self.heads, self.out_channels).mean(dim=1)
+                if self.bias is not None:
+                    out = out + self.bias
+            if return_attention_weights:
+                return out, (edge_index, alpha)
+            return out
+
+        # generic path (bipartite inputs, attention dropout, overridden hooks)
+        if torch.is_tensor(x):
+            x = torch.matmul(x, self.weight)
+        else:
+            x = (None if x[0] is None else torch.matmul(x[0], self.weight),
+                 None if x[1] is None else torch.matmul(x[1], self.weight))
+        out = self.propagate(edge_index, size=size, x=x, return_attention_weights=return_attention_weights)
+        if return_attention_weights:
+            alpha, self.alpha = self.alpha, None
+            return out, (edge_index, alpha)
+        return out
+
+    def message(self, edge_index_i, x_i, x_j, size_i, return_attention_weights):
+        # Compute attention coefficients.
+        x_j = x_j.view(-1, self.heads, self.out_channels)
+        if x_i is None:
+            alpha = (x_j * self.att[:, :, self.out_channels:]).sum(dim=-1)
+        else:
+            x_i = x_i.view(-1, self.heads, self.out_channels)
+            alpha = (torch.cat([x_i, x_j], dim=-1) * self.att).sum(dim=-1)
+        alpha = F.leaky_relu(alpha, self.negative_slope)
+        alpha = softmax(alpha, edge_index_i, size_i)
+        if return_attention_weights:
+            self.alpha = alpha
+        # Sample attention coefficients stochastically.
+        alpha = F.dropout(alpha, p=self.dropout, training=self.training)
+        return x_j * alpha.view(-1, self.heads, 1)
+
+    def update(self, aggr_out):
+        if self.concat is True:
+            aggr_out = aggr_out.view(-1, self.heads * self.out_channels)
+        else:
+            aggr_out = aggr_out.mean(dim=1)
+        if self.bias is not None:
+            aggr_out = aggr_out + self.bias
+        return aggr_out
+
+    def _fused_message(self, kwargs):
+        return None  # the fused GAT path is taken in forward()
+
+    def __repr__(self):
+        return "{}({}, {}, heads={})".format(self.__class__.__name__, self.in_channels, self.out_channels,
+                                            self.heads)

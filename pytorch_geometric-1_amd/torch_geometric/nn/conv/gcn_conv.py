@@ -1,0 +1,115 @@
+"""GCNConv (PyG 1.4.3 [U5]; callers /root/reference/examples/gcn.py:18-19,
+/root/reference/ConvexPruning.py:180-185 with cached=True).
+
+    x' = D^-1/2 (A + I) D^-1/2 X W + b
+
+forward: X W on hipBLASLt (torch.matmul), then the normalised aggregation
++ bias as one fused HIP kernel (mi355_mp).  The normalisation (deg over
+edge_index[0] after add_remaining_self_loops, deg^-1/2 with inf -> 0,
+norm = dinv[row] * w * dinv[col]) is the native mp_gcn_norm_f32.
+"""
+import torch
+from torch.nn import Parameter
+
+from mi355_mp import ops as _ops
+
+from ..inits import glorot, zeros
+from .message_passing import MessagePassing
+from ._structure import remaining_loops_structure, remaining_loops_weight, cached_value
+
+
+class GCNConv(MessagePassing):
+    r"""The graph convolutional operator from the `"Semi-supervised
+    Classification with Graph Convolutional Networks"
+    <https://arxiv.org/abs/1609.02907>`_ paper.
+
+    Args:
+        in_channels (int): Size of each input sample.
+        out_channels (int): Size of each output sample.
+        improved (bool): use A + 2I. (default: False)
+        cached (bool): cache the normalised edge_index/norm of the first call.
+        bias (bool): learn an additive bias. (default: True)
+        normalize (bool): apply the symmetric normalisation. (default: True)
+    """
+
+    def __init__(self, in_channels, out_channels, improved=False, cached=False, bias=True,
+                 normalize=True, **kwargs):
+        super(GCNConv, self).__init__(aggr="add", **kwargs)
+        self.in_channels = in_channels
+        self.out_channels = out_channels
+        self.improved = improved
+        self.cached = cached
+        self.normalize = normalize
+        self.weight = Parameter(torch.Tensor(in_channels, out_channels))
+        if bias:
+            self.bias = Parameter(torch.Tensor(out_channels))
+        else:
+            self.register_parameter("bias", None)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        glorot(self.weight)
+        zeros(self.bias)
+        self.cached_result = None
+        self.cached_num_edges = None
+
+    @staticmethod
+    def norm(edge_index, num_nodes, edge_weight=None, improved=False, dtype=None):
+        fill_value = 1 if not improved else 2
+        ei, mask, inv_rows = remaining_loops_structure(edge_index, num_nodes)
+        if edge_weight is None:
+            # depends on the structure only: cache it with the structure
+            def build():
+                ones = torch.ones((edge_index.size(1),), dtype=torch.float32, device=edge_index.device)
+                w = remaining_loops_weight(ones, mask, inv_rows, num_nodes, fill_value)
+                return _ops.gcn_norm_weights(ei, num_nodes, w)
+            norm = cached_value(edge_index, ("gcn_norm", int(num_nodes), fill_value), build)
+            return ei, norm
+        w = remaining_loops_weight(edge_weight, mask, inv_rows, num_nodes, fill_value)
+        return ei, _ops.gcn_norm_weights(ei, num_nodes, w)
+
+    def forward(self, x, edge_index, edge_weight=None):
+        """"""
+        x = torch.matmul(x, self.weight)
+
+        if self.cached and self.cached_result is not None:
+            if edge_index.size(1) != self.cached_num_edges:
+                raise RuntimeError(
+                    "Cached {} number of edges, but found {}. Please disable the caching behavior "
+                    "of this layer by removing the `cached=True` argument in its constructor."
+                    .format(self.cached_num_edges, edge_index.size(1)))
+
+        if not self.cached or self.cached_result is None:
+            self.cached_num_edges = edge_index.size(1)
+            if self.normalize:
+                edge_index, norm = self.norm(edge_index, x.size(self.node_dim), edge_weight,
+                                             self.improved, x.dtype)
+            else:
+                norm = edge_weight
+            self.cached_result = edge_index, norm
+
+        edge_index, norm = self.cached_result
+        return self.propagate(edge_index, x=x, norm=norm)
+
+    def message(self, x_j, norm):
+        return norm.view(-1, 1) * x_j if norm is not None else x_j
+
+    def update(self, aggr_out):
+        if self.bias is not None:
+            aggr_out = aggr_out + self.bias
+        return aggr_out
+
+    # fused form: message = norm * x_j, update = + bias
+    def _fused_message(self, kwargs):
+        if type(self).message is GCNConv.message:
+            return "x", kwargs.get("norm", None)
+        return None
+
+    def _fused_bias(self):
+        if type(self).update is GCNConv.update:
+            return self.bias, True
+        return None, False
+
+    def __repr__(self):
+        return "{}({}, {})".format(self.__class__.__name__, self.in_channels, self.out_channels)
+

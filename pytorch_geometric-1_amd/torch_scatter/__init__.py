@@ -1,0 +1,138 @@
+"""torch_scatter 2.0.4-compatible front door over the MI355X engine.
+
+Same names, argument order and results as torch_scatter 2.0.4
+(pinned at /root/reference/requirement.txt:3; the package itself is not in
+the reference tree -- see SURVEY.md 2b U8/U9):
+
+    scatter_sum / scatter_add(src, index, dim=-1, out=None, dim_size=None)
+    scatter_mean(src, index, dim=-1, out=None, dim_size=None)
+    scatter_max / scatter_min(src, index, dim=-1, out=None, dim_size=None) -> (out, arg)
+    scatter(src, index, dim=-1, out=None, dim_size=None, reduce="sum")
+
+All reductions run as destination-sorted segmented reductions in HIP
+(mi355_mp.ops); fp32 on a ROCm device only -- there is no CPU path.
+"""
+import torch
+
+from mi355_mp import ops as _ops
+from mi355_mp import _lib
+
+__version__ = "2.0.4"
+
+__all__ = ["scatter", "scatter_sum", "scatter_add", "scatter_mean", "scatter_max", "scatter_min",
+           "segment_csr", "gather_csr"]
+
+
+def _index_1d(src, index, dim):
+    """Reduce torch_scatter's broadcast index to the 1-D index along `dim`."""
+    if index.dim() == 1:
+        if index.numel() != src.size(dim):
+            raise ValueError("index of size %d does not match src.size(%d) = %d"
+                             % (index.numel(), dim, src.size(dim)))
+        return index
+    if index.dim() != src.dim():
+        # torch_scatter.utils.broadcast: trailing singleton dims are appended
+        while index.dim() < src.dim():
+            index = index.unsqueeze(-1)
+    sl = [0] * index.dim()
+    sl[dim] = slice(None)
+    first = index[tuple(sl)]
+    if all(index.stride(d) == 0 or index.size(d) == 1 for d in range(index.dim()) if d != dim):
+        return first
+    view = [1] * index.dim()
+    view[dim] = -1
+    if bool((index == first.view(view)).all()):
+        return first
+    raise NotImplementedError("mi355_mp: element-wise (non-broadcast) scatter indices are not "
+                              "supported; pass a 1-D index along `dim`")
+
+
+def _prepare(src, index, dim, dim_size):
+    _lib.require_device(src, index)
+    if src.dtype != torch.float32:
+        raise TypeError("mi355_mp: scatter ops are implemented for float32 (got %s)" % src.dtype)
+    dim = dim % src.dim() if src.dim() else 0
+    idx = _index_1d(src, index, dim).to(torch.int64)
+    if dim_size is None:
+        dim_size = int(idx.max()) + 1 if idx.numel() > 0 else 0
+    moved = src.movedim(dim, 0)
+    rest = moved.shape[1:]
+    src2 = moved.reshape(moved.shape[0], -1)
+    return dim, idx, int(dim_size), src2, rest
+
+
+def _finish(out2, dim, rest):
+    out = out2.reshape((out2.shape[0],) + tuple(rest))
+    return out.movedim(0, dim)
+
+
+def _reduce(src, index, dim, out, dim_size, reduce):
+    if out is not None:
+        dim = dim % src.dim()
+        dim_size = out.size(dim)
+    dim, idx, dim_size, src2, rest = _prepare(src, index, dim, dim_size)
+    if out is not None:
+        _lib.require_device(out)
+        o2 = out.movedim(dim, 0).reshape(dim_size, -1)
+        contiguous_view = o2.data_ptr() == out.data_ptr() and o2.is_contiguous() and dim == 0
+        buf = o2 if contiguous_view else o2.contiguous()
+        res, arg = _ops.segment_reduce_into(src2, idx, buf, reduce)
+        if not contiguous_view:
+            out.copy_(_finish(res, dim, rest))
+        arg_full = _finish(arg, dim, rest) if arg is not None else None
+        return out, arg_full
+    res, arg = _ops.segment_reduce(src2, idx, dim_size, reduce)
+    return _finish(res, dim, rest), (_finish(arg, dim, rest) if arg is not None else None)
+
+
+def scatter_sum(src, index, dim=-1, out=None, dim_size=None):
+    return _reduce(src, index, dim, out, dim_size, "sum")[0]
+
+
+def scatter_add(src, index, dim=-1, out=None, dim_size=None):
+    return scatter_sum(src, index, dim, out, dim_size)
+
+
+def scatter_mean(src, index, dim=-1, out=None, dim_size=None):
+    return _reduce(src, index, dim, out, dim_size, "mean")[0]
+
+
+def scatter_max(src, index, dim=-1, out=None, dim_size=None):
+    return _reduce(src, index, dim, out, dim_size, "max")
+
+
+def scatter_min(src, index, dim=-1, out=None, dim_size=None):
+    return _reduce(src, index, dim, out, dim_size, "min")
+
+
+def scatter(src, index, dim=-1, out=None, dim_size=None, reduce="sum"):
+    if reduce in ("sum", "add"):
+        return scatter_sum(src, index, dim, out, dim_size)
+    if reduce == "mean":
+        return scatter_mean(src, index, dim, out, dim_size)
+    if reduce == "max":
+        return scatter_max(src, index, dim, out, dim_size)[0]
+    if reduce == "min":
+        return scatter_min(src, index, dim, out, dim_size)[0]
+    raise ValueError("unknown reduce %r" % (reduce,))
+
+
+def segment_csr(src, indptr, out=None, reduce="sum"):
+    """torch_scatter.segment_csr for 1-D indptr along dim 0 (sum/mean/max/min)."""
+    _lib.require_device(src, indptr)
+    counts = indptr[1:] - indptr[:-1]
+    index = torch.repeat_interleave(torch.arange(counts.numel(), device=src.device), counts)
+    res = _reduce(src, index, 0, out, counts.numel(), "sum" if reduce == "add" else reduce)
+    return res if reduce in ("max", "min") else res[0]
+
+
+def gather_csr(src, indptr, out=None):
+    """torch_scatter.gather_csr along dim 0: out[e] = src[segment(e)]."""
+    _lib.require_device(src, indptr)
+    counts = indptr[1:] - indptr[:-1]
+    index = torch.repeat_interleave(torch.arange(counts.numel(), device=src.device), counts)
+    res = _ops.index_select_rows(src.reshape(src.shape[0], -1), index).reshape((-1,) + tuple(src.shape[1:]))
+    if out is not None:
+        out.copy_(res)
+        return out
+    return res

@@ -1,0 +1,470 @@
+"""GPU parity tests: the HIP path (through the C-ABI) against the CPU oracle.
+
+Tolerances (north star: 1e-5 fp32, argmax bit-exact):
+  * max/min values and argmax/argmin indices: bit-exact.
+  * sum/mean: rows whose slots lie in one merge-path task are summed in
+    original edge order with unfused mul+add, i.e. the oracle's arithmetic:
+    bit-exact.  Rows split across tasks (hubs) are summed as ordered
+    partials: |got - want| <= 1e-5 * max(1, sum_e |w_e x_e|).
+  * GAT (online softmax, split dot products): same bound with alpha|x|.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import scatter_ref as S
+from oracle import pyg_ref as P
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _mods():
+    import mi355_mp
+    from mi355_mp import ops
+    from mi355_mp.graph import CSR, Graph
+    from mi355_mp.graphgen import powerlaw_edge_index
+    return mi355_mp, ops, CSR, Graph, powerlaw_edge_index
+
+
+def _bound_ok(got, want, terms, rel=1e-5):
+    tol = rel * torch.clamp(terms, min=1.0)
+    bad = (got - want).abs() > tol
+    assert not bool(bad.any()), "max excess %g" % float(((got - want).abs() - tol).max())
+
+
+def _split_rows(csr):
+    """Rows whose slots span more than one merge-path task (host mirror)."""
+    rp = csr.rowptr.cpu().numpy()
+    wr = csr.wave_row.cpu().numpy()
+    ws = csr.wave_slot.cpu().numpy()
+    rows = set()
+    for w in range(1, csr.n_waves):
+        r = wr[w]
+        if ws[w] < rp[r]:
+            rows.add(int(r) - 1)
+    return sorted(rows)
+
+
+# --------------------------------------------------------------------------
+# CSR + schedule
+# --------------------------------------------------------------------------
+
+def _merge_path_reference(rowptr, chunk):
+    """Brute-force merge path: walk the N+E items in order."""
+    N = len(rowptr) - 1
+    E = int(rowptr[-1])
+    items = []
+    for r in range(N):
+        items.append(("row", r))
+        for k in range(rowptr[r], rowptr[r + 1]):
+            items.append(("slot", k))
+    n_waves = max(1, -(-(N + E) // chunk))
+    wave_row, wave_slot = [], []
+    for w in range(n_waves):
+        seg = items[w * chunk:(w + 1) * chunk]
+        rows = [v for t, v in seg if t == "row"]
+        slots = [v for t, v in seg if t == "slot"]
+        # first owned row: first row marker at or after position w*chunk
+        later_rows = [v for t, v in items[w * chunk:] if t == "row"]
+        wave_row.append(later_rows[0] if later_rows else N)
+        later_slots = [v for t, v in items[w * chunk:] if t == "slot"]
+        wave_slot.append(later_slots[0] if later_slots else E)
+        del rows, slots
+    wave_row.append(N)
+    wave_slot.append(E)
+    return np.array(wave_row), np.array(wave_slot)
+
+
+@pytest.mark.parametrize("N,E,chunk", [(50, 400, 64), (300, 5000, 128), (7, 0, 64), (1000, 100, 64)])
+def test_csr_and_schedule_match_reference(N, E, chunk):
+    _, _, CSR, _, _ = _mods()
+    g = torch.Generator().manual_seed(N + E)
+    key = torch.randint(N, (E,), generator=g)
+    key[: E // 3] = key[0] if E else key[: E // 3]  # a hub row
+    other = torch.randint(N, (E,), generator=g)
+    csr = CSR(key.to(DEV), other.to(DEV), N, N, chunk=chunk)
+    perm = torch.sort(key, stable=True).indices
+    counts = torch.bincount(key, minlength=N)
+    rowptr = torch.cat([torch.zeros(1, dtype=torch.long), counts.cumsum(0)])
+    assert torch.equal(csr.rowptr.cpu().long(), rowptr)
+    if E:
+        assert torch.equal(csr.eid.cpu()[:E].long(), perm)
+        assert torch.equal(csr.col.cpu()[:E].long(), other[perm])
+    wr, ws = _merge_path_reference(rowptr.tolist(), chunk)
+    assert np.array_equal(csr.wave_row.cpu().numpy(), wr)
+    assert np.array_equal(csr.wave_slot.cpu().numpy(), ws)
+    # split list = last task of every row spanning tasks
+    n_split = csr.n_split
+    assert n_split == len(_split_rows(csr))
+
+
+def test_csr_rejects_out_of_range_index():
+    _, _, CSR, _, _ = _mods()
+    key = torch.tensor([0, 5, 1], device=DEV)
+    with pytest.raises(IndexError):
+        CSR(key, key, 3, 6)
+
+
+# --------------------------------------------------------------------------
+# fused gather -> reduce
+# --------------------------------------------------------------------------
+
+@pytest.mark.parametrize("F", [1, 3, 16, 64, 130, 256, 300])
+@pytest.mark.parametrize("chunk", [64, 256])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_fused_sum_mean(F, chunk, weighted):
+    _, ops, _, Graph, pl = _mods()
+    N, E = 700, 9000
+    ei = pl(N, E, seed=F + chunk)
+    g = torch.Generator().manual_seed(F)
+    x = torch.randn(N, F, generator=g)
+    w = torch.rand(E, generator=g) if weighted else None
+    graph = Graph(ei.to(DEV), N, N, chunk=chunk)
+    eid = ei.to(DEV)
+    out = ops.fused_propagate(graph, x.to(DEV), eid, w.to(DEV) if weighted else None, "sum").cpu()
+    want = S.gather_sum(x, ei[0], ei[1], w, N)
+    terms = S.gather_sum(x.abs(), ei[0], ei[1], w.abs() if weighted else None, N)
+    _bound_ok(out, want, terms)
+    split = set(_split_rows(graph.dst))
+    whole = torch.tensor([r for r in range(N) if r not in split], dtype=torch.long)
+    assert torch.equal(out[whole], want[whole]), "non-split rows must be bit-exact"
+    assert graph.dst.n_split > 0 or chunk == 256
+    # mean
+    outm = ops.fused_propagate(graph, x.to(DEV), eid, None, "mean").cpu()
+    wantm = S.scatter_mean(x[ei[0]], ei[1], N)
+    _bound_ok(outm, wantm, S.scatter_mean(x.abs()[ei[0]], ei[1], N))
+    assert torch.equal(outm[whole], wantm[whole])
+
+
+@pytest.mark.parametrize("F", [1, 5, 64, 256, 602])
+@pytest.mark.parametrize("reduce", ["max", "min"])
+def test_fused_max_min_bit_exact_with_ties(F, reduce):
+    _, ops, _, Graph, pl = _mods()
+    N, E = 600, 12000
+    ei = pl(N, E, seed=F)
+    g = torch.Generator().manual_seed(F)
+    # small integer values -> many exact ties across edges
+    x = torch.randint(-4, 5, (N, F), generator=g).to(torch.float32)
+    graph = Graph(ei.to(DEV), N, N, chunk=64)
+    out = ops.fused_propagate(graph, x.to(DEV), ei.to(DEV), None, reduce, pyg_mask=False)
+    out = out.cpu()
+    want, arg = S.scatter_loop(x[ei[0]], ei[1], N, reduce)
+    assert torch.equal(out, want)
+    # argmax via the segment op on materialised messages
+    msg = x.to(DEV)[ei[0].to(DEV)]
+    o2, a2 = ops.segment_reduce(msg, ei[1].to(DEV), N, reduce)
+    assert torch.equal(o2.cpu(), want)
+    assert torch.equal(a2.cpu(), arg)
+
+
+def test_max_special_values_and_pyg_mask():
+    _, ops, _, _, _ = _mods()
+    src = torch.tensor([[float("-inf")], [-20000.], [-5.], [float("nan")], [-30000.]])
+    idx = torch.tensor([0, 1, 1, 2, 4])
+    o, a = ops.segment_reduce(src.to(DEV), idx.to(DEV), 5, "max")
+    want, warg = S.scatter_max(src, idx, 5)
+    assert torch.equal(o.cpu(), want) and torch.equal(a.cpu(), warg)
+    from torch_geometric.utils import scatter_
+    m = scatter_("max", src.to(DEV), idx.to(DEV), 0, 5).cpu()
+    assert torch.equal(m, P.scatter_("max", src, idx, 5))
+
+
+def test_kat_through_torch_scatter_shim():
+    import torch_scatter
+    d = np.load("tests/golden/kat_scatter.npz")
+    src, idx = torch.from_numpy(d["src"]).to(DEV), torch.from_numpy(d["index"]).to(DEV)
+    n = int(d["dim_size"])
+    assert np.array_equal(torch_scatter.scatter_add(src, idx, 0, dim_size=n).cpu().numpy(), d["sum"])
+    assert np.array_equal(torch_scatter.scatter_mean(src, idx, 0, dim_size=n).cpu().numpy(), d["mean"])
+    o, a = torch_scatter.scatter_max(src, idx, 0, dim_size=n)
+    assert np.array_equal(o.cpu().numpy(), d["max"]) and np.array_equal(a.cpu().numpy(), d["argmax"])
+    o, a = torch_scatter.scatter_min(src, idx, 0, dim_size=n)
+    assert np.array_equal(o.cpu().numpy(), d["min"]) and np.array_equal(a.cpu().numpy(), d["argmin"])
+    # dim=-1 layout (torch_scatter's default dim) and a 3-D src
+    t = torch_scatter.scatter_sum(src.t().contiguous(), idx, dim=-1, dim_size=n)
+    assert np.array_equal(t.t().cpu().numpy(), d["sum"])
+    s3 = src.view(5, 2, 1).expand(5, 2, 3).contiguous()
+    r3 = torch_scatter.scatter_sum(s3, idx, 0, dim_size=n).cpu()
+    assert np.array_equal(r3[..., 2].numpy(), d["sum"])
+
+
+def test_out_argument_accumulates():
+    import torch_scatter
+    out0 = torch.tensor([[10., 10.], [-1., -1.]])
+    src = torch.tensor([[1., 2.], [3., 4.]])
+    idx = torch.tensor([0, 0])
+    out = out0.clone().to(DEV)
+    r = torch_scatter.scatter_add(src.to(DEV), idx.to(DEV), 0, out=out)
+    assert r.data_ptr() == out.data_ptr()
+    assert torch.equal(out.cpu(), S.scatter_loop(src, idx, 2, "sum", out=out0)[0])
+    out = out0.clone().to(DEV)
+    m, a = torch_scatter.scatter_max(src.to(DEV), idx.to(DEV), 0, out=out)
+    wm, wa = S.scatter_loop(src, idx, 2, "max", out=out0)
+    assert torch.equal(m.cpu(), wm) and torch.equal(a.cpu(), wa)
+
+
+def test_empty_graph_and_trailing_empty_rows():
+    _, ops, _, Graph, _ = _mods()
+    ei = torch.zeros((2, 0), dtype=torch.long, device=DEV)
+    x = torch.randn(5, 8, device=DEV)
+    out = ops.fused_propagate(Graph(ei, 9, 5), x, ei, None, "sum")
+    assert out.shape == (9, 8) and not bool(out.abs().sum())
+    o, a = ops.segment_reduce(torch.zeros((0, 4), device=DEV), torch.zeros(0, dtype=torch.long, device=DEV),
+                              3, "max")
+    assert not bool(o.abs().sum()) and bool((a == 0).all())
+    # many empty rows after the last edge (merge path bounds every task)
+    idx = torch.tensor([0, 0, 1], device=DEV)
+    src = torch.ones((3, 4), device=DEV)
+    o, _ = ops.segment_reduce(src, idx, 100_000, "sum")
+    assert o[0, 0].item() == 2.0 and o[1, 0].item() == 1.0 and o[2:].abs().sum().item() == 0.0
+
+
+def test_hub_row_split_over_many_tasks():
+    _, ops, _, Graph, _ = _mods()
+    g = torch.Generator().manual_seed(3)
+    N, E, F = 1000, 200_000, 64
+    dst = torch.randint(N, (E,), generator=g)
+    dst[: E // 2] = 7                       # node 7 has 100k in-edges
+    src = torch.randint(N, (E,), generator=g)
+    ei = torch.stack([src, dst])
+    x = torch.randn(N, F, generator=g)
+    graph = Graph(ei.to(DEV), N, N, chunk=64)
+    assert graph.dst.n_split > 100
+    out = ops.fused_propagate(graph, x.to(DEV), ei.to(DEV), None, "sum").cpu()
+    want = S.gather_sum(x, src, dst, None, N)
+    _bound_ok(out, want, S.gather_sum(x.abs(), src, dst, None, N))
+    o, a = ops.segment_reduce(x.to(DEV)[src.to(DEV)], dst.to(DEV), N, "max")
+    wo, wa = S.scatter_max(x[src], dst, N)
+    assert torch.equal(o.cpu(), wo) and torch.equal(a.cpu(), wa)
+
+
+def test_deterministic_bitwise():
+    _, ops, _, Graph, pl = _mods()
+    N, E, F = 4000, 100_000, 256
+    ei = pl(N, E, seed=9).to(DEV)
+    x = torch.randn(N, F, device=DEV)
+    graph = Graph(ei, N, N)
+    a = ops.fused_propagate(graph, x, ei, None, "sum")
+    b = ops.fused_propagate(graph, x, ei, None, "sum")
+    assert torch.equal(a, b)
+
+
+def test_no_cpu_fallback():
+    _, ops, _, Graph, _ = _mods()
+    ei = torch.tensor([[0, 1], [1, 0]])
+    with pytest.raises(RuntimeError):
+        ops.fused_propagate(Graph(ei, 2, 2), torch.randn(2, 3), ei)
+
+
+# --------------------------------------------------------------------------
+# layers vs the golden fixtures / oracle
+# --------------------------------------------------------------------------
+
+def _golden(name):
+    d = np.load("tests/golden/%s.npz" % name)
+    return {k: torch.from_numpy(d[k]) for k in d.files}
+
+
+def test_golden_powerlaw_aggregations():
+    _, ops, _, Graph, _ = _mods()
+    d = _golden("powerlaw_agg")
+    x, ei, w = d["x"], d["edge_index"], d["w"]
+    N = x.shape[0]
+    graph = Graph(ei.to(DEV), N, N, chunk=64)
+    out = ops.fused_propagate(graph, x.to(DEV), ei.to(DEV), w.to(DEV), "sum").cpu()
+    _bound_ok(out, d["gsum"], S.gather_sum(x.abs(), ei[0], ei[1], w, N))
+    outm = ops.fused_propagate(graph, x.to(DEV), ei.to(DEV), None, "mean").cpu()
+    _bound_ok(outm, d["gmean"], S.scatter_mean(x.abs()[ei[0]], ei[1], N))
+    mx = ops.fused_propagate(graph, x.to(DEV), ei.to(DEV), None, "max").cpu()
+    assert torch.equal(mx, d["gmax"])
+    _, am = ops.segment_reduce(x.to(DEV)[ei[0].to(DEV)], ei[1].to(DEV), N, "max")
+    assert torch.equal(am.cpu().to(torch.int32), d["gargmax"])
+
+
+def test_golden_gcn_and_gat_layers():
+    from torch_geometric.nn import GCNConv, GATConv
+    d = _golden("powerlaw_agg")
+    x, ei = d["x"], d["edge_index"]
+    F = x.shape[1]
+    conv = GCNConv(F, F).to(DEV)
+    with torch.no_grad():
+        conv.weight.copy_(d["gcn_w"])
+        conv.bias.copy_(d["gcn_b"])
+        out = conv(x.to(DEV), ei.to(DEV)).cpu()
+    assert (out - d["gcn"]).abs().max().item() < 1e-5 * max(1.0, d["gcn"].abs().max().item())
+    H, C = int(d["heads"]), int(d["out_channels"])
+    gat = GATConv(F, C, heads=H).to(DEV)
+    with torch.no_grad():
+        gat.weight.copy_(d["gat_w"])
+        gat.att.copy_(d["gat_att"])
+        gat.bias.copy_(d["gat_b"])
+        out, (ei2, alpha) = gat(x.to(DEV), ei.to(DEV), return_attention_weights=True)
+    assert (out.cpu() - d["gat"]).abs().max().item() < 1e-5 * max(1.0, d["gat"].abs().max().item())
+    assert (alpha.cpu() - d["gat_alpha"]).abs().max().item() < 1e-5
+
+
+def test_gat_aggregation_on_identical_inputs():
+    """Isolate the fused kernel from GEMM differences: same XW on both sides."""
+    _, ops, _, Graph, pl = _mods()
+    N, E, H, C = 900, 20000, 8, 32
+    ei = P.add_self_loops(P.remove_self_loops(pl(N, E, seed=4))[0], num_nodes=N)[0]
+    g = torch.Generator().manual_seed(4)
+    xw = torch.randn(N, H * C, generator=g)
+    att = torch.randn(1, H, 2 * C, generator=g) * 0.2
+    graph = Graph(ei.to(DEV), N, N, chunk=64)
+    out, alpha = ops.gat_propagate(graph, ei.to(DEV), xw.to(DEV), att.to(DEV), H, C, 0.2, None, True)
+    x_i = xw[ei[1]].view(-1, H, C)
+    x_j = xw[ei[0]].view(-1, H, C)
+    a = torch.nn.functional.leaky_relu((torch.cat([x_i, x_j], -1) * att).sum(-1), 0.2)
+    al = P.softmax(a, ei[1], N)
+    want = S.scatter_sum(x_j * al.view(-1, H, 1), ei[1], N).view(N, H * C)
+    terms = S.scatter_sum(x_j.abs() * al.view(-1, H, 1), ei[1], N).view(N, H * C)
+    _bound_ok(out.cpu(), want, terms)
+    assert (alpha.cpu() - al).abs().max().item() < 1e-6
+
+
+def test_cora_gcn_golden_forward():
+    from torch_geometric.nn import GCNConv
+    d = _golden("cora_gcn")
+    N, Fd = int(d["num_nodes"]), int(d["num_features"])
+    x = torch.zeros(N * Fd)
+    x[d["x_flat_idx"]] = d["x_val"]
+    x = x.view(N, Fd).to(DEV)
+    ei = d["edge_index"].to(DEV)
+    c1, c2 = GCNConv(Fd, 16, cached=True).to(DEV), GCNConv(16, 7, cached=True).to(DEV)
+    with torch.no_grad():
+        c1.weight.copy_(d["w1"]), c1.bias.copy_(d["b1"]), c2.weight.copy_(d["w2"]), c2.bias.copy_(d["b2"])
+        h = torch.relu(c1(x, ei))
+        logp = torch.log_softmax(c2(h, ei), dim=1).cpu()
+    assert (logp - d["logp"]).abs().max().item() < 1e-5
+
+
+def test_gcn_backward_matches_float64_autograd():
+    from torch_geometric.nn import GCNConv
+    _, _, _, _, pl = _mods()
+    N, E, Fi, Fo = 400, 6000, 12, 20
+    ei = pl(N, E, seed=2)
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(N, Fi, generator=g)
+    conv = GCNConv(Fi, Fo).to(DEV)
+    xd = x.to(DEV).requires_grad_(True)
+    gout = torch.randn(N, Fo, generator=g)
+    conv(xd, ei.to(DEV)).backward(gout.to(DEV))
+    W = conv.weight.detach().cpu().double().requires_grad_(True)
+    b = conv.bias.detach().cpu().double().requires_grad_(True)
+    x64 = x.double().requires_grad_(True)
+    P.gcn_conv(x64, ei, W, b).backward(gout.double())
+    assert torch.allclose(xd.grad.cpu().double(), x64.grad, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(conv.weight.grad.cpu().double(), W.grad, rtol=1e-4, atol=1e-4)
+    assert torch.allclose(conv.bias.grad.cpu().double(), b.grad, rtol=1e-5, atol=1e-4)
+
+
+def test_gat_backward_matches_float64_autograd():
+    from torch_geometric.nn import GATConv
+    _, _, _, _, pl = _mods()
+    N, E, Fi, H, C = 300, 4000, 10, 4, 8
+    ei = pl(N, E, seed=5)
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(N, Fi, generator=g)
+    conv = GATConv(Fi, C, heads=H).to(DEV)
+    with torch.no_grad():
+        conv.bias.normal_()
+    xd = x.to(DEV).requires_grad_(True)
+    gout = torch.randn(N, H * C, generator=g)
+    conv(xd, ei.to(DEV)).backward(gout.to(DEV))
+    W = conv.weight.detach().cpu().double().requires_grad_(True)
+    att = conv.att.detach().cpu().double().requires_grad_(True)
+    b = conv.bias.detach().cpu().double().requires_grad_(True)
+    x64 = x.double().requires_grad_(True)
+    P.gat_conv(x64, ei, W, att, b, H, C).backward(gout.double())
+    for got, want in ((xd.grad, x64.grad), (conv.weight.grad, W.grad), (conv.att.grad, att.grad),
+                      (conv.bias.grad, b.grad)):
+        assert torch.allclose(got.cpu().double(), want, rtol=1e-4, atol=1e-4)
+
+
+def test_graphconv_max_and_edgeconv_generic_path():
+    from torch_geometric.nn import GraphConv, MessagePassing
+    _, _, _, _, pl = _mods()
+    N, E, F = 500, 7000, 24
+    ei = pl(N, E, seed=8)
+    g = torch.Generator().manual_seed(8)
+    x = torch.randn(N, F, generator=g)
+    conv = GraphConv(F, 16, aggr="max").to(DEV)
+    with torch.no_grad():
+        out = conv(x.to(DEV), ei.to(DEV)).cpu()
+    want = P.graph_conv_max(x, ei, conv.weight.detach().cpu(), conv.lin.weight.detach().cpu(),
+                            conv.lin.bias.detach().cpu())
+    assert (out - want).abs().max().item() < 1e-4
+
+    class EdgeConv(MessagePassing):  # README.md:35-49
+        def __init__(self, F_in, F_out):
+            super(EdgeConv, self).__init__(aggr="max")
+            self.mlp = torch.nn.Sequential(torch.nn.Linear(2 * F_in, F_out), torch.nn.ReLU(),
+                                           torch.nn.Linear(F_out, F_out))
+
+        def forward(self, x, edge_index):
+            return self.propagate(edge_index, x=x)
+
+        def message(self, x_i, x_j):
+            return self.mlp(torch.cat([x_i, x_j - x_i], dim=1))
+
+    ec = EdgeConv(F, 8).to(DEV)
+    with torch.no_grad():
+        got = ec(x.to(DEV), ei.to(DEV)).cpu()
+    ec_cpu = EdgeConv(F, 8)
+    ec_cpu.load_state_dict({k: v.cpu() for k, v in ec.state_dict().items()})
+    with torch.no_grad():
+        want = P.edge_conv_max(x, ei, ec_cpu.mlp)
+    assert (got - want).abs().max().item() < 1e-4
+    # generic path backward runs (native gather backward + argmax scatter)
+    xd = x.to(DEV).requires_grad_(True)
+    ec(xd, ei.to(DEV)).sum().backward()
+    assert torch.isfinite(xd.grad).all()
+
+
+def test_sage_mean_layer():
+    from torch_geometric.nn import SAGEConv
+    _, _, _, _, pl = _mods()
+    N, E, F = 300, 3000, 16
+    ei = pl(N, E, seed=6)
+    x = torch.randn(N, F, generator=torch.Generator().manual_seed(6))
+    conv = SAGEConv(F, 8).to(DEV)
+    with torch.no_grad():
+        out = conv(x.to(DEV), ei.to(DEV)).cpu()
+    ei2, _ = P.add_remaining_self_loops(ei, None, 1, N)
+    agg = S.scatter_mean(x[ei2[0]], ei2[1], N)
+    want = agg @ conv.weight.detach().cpu() + conv.bias.detach().cpu()
+    assert (out - want).abs().max().item() < 1e-4
+
+
+# --------------------------------------------------------------------------
+# BASELINE config 2 at full size: size-independent properties
+# --------------------------------------------------------------------------
+
+def test_full_size_rmat_gcn_properties():
+    """RMAT scale 21, 30M samples symmetrised (E=60M), F=256: checksum of the
+    column sums, linearity, determinism (no oracle at this size)."""
+    _, ops, _, Graph, _ = _mods()
+    from mi355_mp.graphgen import rmat_edge_index
+    from torch_geometric.nn.conv.gcn_conv import GCNConv
+    ei = rmat_edge_index(scale=21, n_samples=30_000_000, seed=1, device=DEV)
+    N = 1 << 21
+    ei2, norm = GCNConv.norm(ei, N)
+    graph = Graph(ei2, N, N)
+    g = torch.Generator(device=DEV).manual_seed(1)
+    x1 = torch.randn(N, 256, device=DEV, generator=g)
+    x2 = torch.randn(N, 256, device=DEV, generator=g)
+    o1 = ops.fused_propagate(graph, x1, ei2, norm, "sum")
+    o1b = ops.fused_propagate(graph, x1, ei2, norm, "sum")
+    assert torch.equal(o1, o1b)
+    # checksum: sum_i out[i,:] = sum_j (sum_{e: src=j} norm_e) x[j,:]
+    ws = torch.zeros(N, dtype=torch.float64, device=DEV).index_add_(0, ei2[0], norm.double())
+    want = (ws.view(1, -1) @ x1.double()).view(-1)
+    got = o1.double().sum(0)
+    assert torch.allclose(got, want, rtol=1e-5, atol=1e-2)
+    # linearity
+    o2 = ops.fused_propagate(graph, x2, ei2, norm, "sum")
+    o12 = ops.fused_propagate(graph, 2 * x1 - x2, ei2, norm, "sum")
+    assert (o12 - (2 * o1 - o2)).abs().max().item() < 1e-4

@@ -1,0 +1,161 @@
+"""CPU tests of the oracle: hand-derived known-answer tests (KATs) of the
+torch_scatter 2.0.4 / PyG 1.4.3 semantics, agreement of the oracle's two
+independent forms (torch ops vs serial C loop), and the golden fixtures.
+
+Parity is UNPINNED by the reference (no tests / fixtures exist for this path
+in /root/reference, and torch_scatter / torch_geometric are not installable
+here): the KATs below are the pin, each value derived by hand from the
+published semantics quoted in oracle/scatter_ref.py and oracle/pyg_ref.py.
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import scatter_ref as S
+from oracle import pyg_ref as P
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+SRC = torch.tensor([[1., -2.], [3., 5.], [-1., 0.], [3., 7.], [2., -3.]])
+IDX = torch.tensor([0, 2, 0, 2, 3])
+
+
+def test_kat_sum_mean():
+    want_sum = torch.tensor([[0., -2.], [0., 0.], [6., 12.], [2., -3.], [0., 0.]])
+    want_mean = torch.tensor([[0., -1.], [0., 0.], [3., 6.], [2., -3.], [0., 0.]])
+    assert torch.equal(S.scatter_sum(SRC, IDX, 5), want_sum)
+    assert torch.equal(S.scatter_loop(SRC, IDX, 5, "sum")[0], want_sum)
+    assert torch.equal(S.scatter_mean(SRC, IDX, 5), want_mean)
+    assert torch.equal(S.scatter_loop(SRC, IDX, 5, "mean")[0], want_mean)
+
+
+def test_kat_max_min_first_index_ties_and_empty_rows():
+    out, arg = S.scatter_max(SRC, IDX, 5)
+    assert torch.equal(out, torch.tensor([[1., 0.], [0., 0.], [3., 7.], [2., -3.], [0., 0.]]))
+    # row 2 feature 0: 3 (edge 1) ties 3 (edge 3) -> first edge wins; empty -> E = 5
+    assert torch.equal(arg, torch.tensor([[0, 2], [5, 5], [1, 3], [4, 4], [5, 5]]))
+    out, arg = S.scatter_min(SRC, IDX, 5)
+    assert torch.equal(out, torch.tensor([[-1., -2.], [0., 0.], [3., 5.], [2., -3.], [0., 0.]]))
+    assert torch.equal(arg, torch.tensor([[2, 0], [5, 5], [1, 1], [4, 4], [5, 5]]))
+
+
+def test_kat_max_special_values():
+    src = torch.tensor([[float("-inf")], [-20000.], [-5.], [float("nan")]])
+    out, arg = S.scatter_max(src, torch.tensor([0, 1, 1, 2]), 4)
+    # -inf and nan never beat lowest(): the row stays at init -> 0, arg = E
+    assert torch.equal(out, torch.tensor([[0.], [-5.], [0.], [0.]]))
+    assert torch.equal(arg, torch.tensor([[4], [2], [4], [4]]))
+    # PyG scatter_ masks max < -10000 to 0
+    src = torch.tensor([[-20000.], [-30000.]])
+    assert S.scatter_max(src, torch.tensor([0, 0]), 1)[0].item() == -20000.
+    assert P.scatter_("max", src, torch.tensor([0, 0]), 1).item() == 0.
+    assert P.scatter_("min", torch.tensor([[20000.]]), torch.tensor([0]), 1).item() == 0.
+
+
+def test_kat_out_given():
+    out0 = torch.tensor([[10., 10.], [-1., -1.]])
+    src = torch.tensor([[1., 2.], [3., 4.]])
+    idx = torch.tensor([0, 0])
+    s, _ = S.scatter_loop(src, idx, 2, "sum", out=out0)
+    assert torch.equal(s, torch.tensor([[14., 16.], [-1., -1.]]))
+    m, a = S.scatter_loop(src, idx, 2, "max", out=out0)
+    assert torch.equal(m, out0)  # no element beats the given values; no lowest->0 masking
+    assert torch.equal(a, torch.tensor([[2, 2], [2, 2]]))
+
+
+def test_kat_add_remaining_self_loops_and_gcn_norm():
+    ei = torch.tensor([[0, 1, 1, 2], [1, 1, 2, 0]])
+    w = torch.tensor([1., 2., 3., 4.])
+    ei2, w2 = P.add_remaining_self_loops(ei, w, 1, 3)
+    assert ei2.tolist() == [[0, 1, 2, 0, 1, 2], [1, 2, 0, 0, 1, 2]]
+    assert w2.tolist() == [1., 3., 4., 1., 2., 1.]
+    _, norm = P.gcn_norm(ei, 3, w)
+    # deg over edge_index[0]: [2, 5, 5]
+    want = [1 / math.sqrt(2) / math.sqrt(5), 3 / 5, 4 / math.sqrt(5) / math.sqrt(2), 1 / 2, 2 / 5, 1 / 5]
+    assert np.allclose(norm.numpy(), want, rtol=1e-6, atol=0)
+    # improved=True: a node WITH a pre-existing loop keeps its weight, others get 2
+    ei3, w3 = P.add_remaining_self_loops(ei, torch.ones(4), 2, 3)
+    assert w3.tolist() == [1., 1., 1., 2., 1., 2.]
+
+
+def test_kat_gcn_norm_isolated_node_inf_to_zero():
+    # node 0's only edge is a zero-weight self loop, kept as its loop weight:
+    # deg(0) = 0 -> deg^-1/2 = inf -> 0, so its norm is 0 (not nan)
+    ei2, norm = P.gcn_norm(torch.tensor([[0], [0]]), 2, torch.tensor([0.]))
+    assert ei2.tolist() == [[0, 1], [0, 1]]
+    assert norm.tolist() == [0.0, 1.0]
+    _, n2 = P.gcn_norm(torch.tensor([[0, 1], [1, 0]]), 2, torch.tensor([1., 1.]))
+    assert torch.allclose(n2, torch.tensor([0.5, 0.5, 0.5, 0.5]))
+
+
+def test_kat_remove_add_self_loops_order():
+    ei = torch.tensor([[0, 1, 2, 2], [0, 0, 2, 1]])
+    e1, _ = P.remove_self_loops(ei)
+    assert e1.tolist() == [[1, 2], [0, 1]]
+    e2, _ = P.add_self_loops(e1, num_nodes=3)
+    assert e2.tolist() == [[1, 2, 0, 1, 2], [0, 1, 0, 1, 2]]
+
+
+def test_kat_softmax():
+    src = torch.tensor([1., 2., 3., 0.5])
+    idx = torch.tensor([0, 0, 1, 0])
+    out = P.softmax(src, idx, 3)
+    z = math.exp(-1) + 1 + math.exp(-1.5)
+    want = [math.exp(-1) / z, 1 / z, 1.0, math.exp(-1.5) / z]
+    assert np.allclose(out.numpy(), want, rtol=1e-6)
+
+
+def test_torch_and_loop_forms_agree_on_random_graph():
+    g = torch.Generator().manual_seed(5)
+    E, N, F = 3000, 300, 17
+    src = torch.randn(E, F, generator=g)
+    idx = torch.randint(N, (E,), generator=g)
+    assert torch.equal(S.scatter_sum(src, idx, N), S.scatter_loop(src, idx, N, "sum")[0])
+    assert torch.equal(S.scatter_mean(src, idx, N), S.scatter_loop(src, idx, N, "mean")[0])
+    # torch's amax reduction + first-index argmin over ties == the serial loop
+    out, arg = S.scatter_max(src, idx, N)
+    ref = torch.full((N, F), float("-inf")).scatter_reduce(0, idx.view(-1, 1).expand(E, F), src, "amax")
+    ref[torch.isinf(ref)] = 0
+    assert torch.equal(out, ref)
+    e = torch.arange(E).view(-1, 1).expand(E, F)
+    hit = src == ref[idx]
+    first = torch.full((N, F), E, dtype=torch.int64).scatter_reduce(
+        0, idx.view(-1, 1).expand(E, F), torch.where(hit, e, torch.full_like(e, E)), "amin")
+    assert torch.equal(arg, first)
+
+
+def test_gather_forms_match_materialised_messages():
+    g = torch.Generator().manual_seed(6)
+    N, E, F = 200, 2500, 9
+    x = torch.randn(N, F, generator=g)
+    ei = torch.randint(N, (2, E), generator=g)
+    w = torch.rand(E, generator=g)
+    msg = w.view(-1, 1) * x[ei[0]]
+    assert torch.equal(S.gather_sum(x, ei[0], ei[1], w, N), S.scatter_sum(msg, ei[1], N))
+    o1, a1 = S.gather_max(x, ei[0], ei[1], N)
+    o2, a2 = S.scatter_max(x[ei[0]], ei[1], N)
+    assert torch.equal(o1, o2) and torch.equal(a1, a2)
+
+
+def test_float64_twin_close():
+    g = torch.Generator().manual_seed(7)
+    N, E, F = 500, 6000, 8
+    x = torch.randn(N, F, generator=g)
+    ei = torch.randint(N, (2, E), generator=g)
+    W = torch.randn(F, F, generator=g)
+    o32 = P.gcn_conv(x, ei, W)
+    o64 = P.gcn_conv(x.double(), ei, W.double())
+    assert torch.allclose(o32.double(), o64, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("name", sorted(f for f in os.listdir(GOLDEN) if f.endswith(".npz"))
+                         if os.path.isdir(GOLDEN) else [])
+def test_golden_fixture_reproduces(name):
+    from tests.golden import make_golden
+    d = np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+    fresh = make_golden.compute(name[:-4], {k: d[k] for k in d.files})
+    for k, v in fresh.items():
+        assert np.array_equal(np.asarray(v), d[k]), (name, k)
