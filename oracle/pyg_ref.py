@@ -69,8 +69,7 @@ def _seg_max(src, index, N):
         return S.scatter_max(src, index, N)[0]
     out = torch.full((N,) + tuple(src.shape[1:]), float("-inf"), dtype=src.dtype)
     out = out.scatter_reduce(0, index.view((-1,) + (1,) * (src.dim() - 1)).expand_as(src), src, "amax")
-    out[torch.isinf(out)] = 0
-    return out
+    return torch.where(torch.isinf(out), torch.zeros_like(out), out)
 
 
 def softmax(src, index, num_nodes):

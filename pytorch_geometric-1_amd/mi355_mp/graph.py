@@ -104,14 +104,19 @@ class Graph:
     ``dst`` : CSR keyed on the aggregation index edge_index[i] (gathers edge_index[j])
     ``src`` : CSR keyed on edge_index[j] (transpose; used by backward passes)
 
-    Holds only a weak reference to ``edge_index`` (the caches must not keep
-    the user's tensor alive); callers keep it alive while a direction is
-    first built (autograd saves it for backward).
+    A Graph made by the cache (``graph_for``) holds only a weak reference to
+    ``edge_index`` (the cache must not keep the user's tensor alive; callers
+    keep it alive while a direction is first built -- autograd saves it for
+    backward); one constructed directly holds a strong reference.
     """
 
-    def __init__(self, edge_index, n_dst, n_src, flow="source_to_target", chunk=DEFAULT_CHUNK):
+    def __init__(self, edge_index, n_dst, n_src, flow="source_to_target", chunk=DEFAULT_CHUNK,
+                 weak=False):
         self.i, self.j = (1, 0) if flow == "source_to_target" else (0, 1)
-        self._ei = weakref.ref(edge_index)
+        if weak:
+            self._ei = weakref.ref(edge_index)
+        else:
+            self._ei = lambda ei=edge_index: ei
         self.n_dst, self.n_src = int(n_dst), int(n_src)
         self.chunk = chunk
         self._dst = None
@@ -176,7 +181,7 @@ _index_cache = _Cache()
 def graph_for(edge_index, n_dst, n_src, flow="source_to_target"):
     """Cached Graph for an edge_index tensor (rebuilt if it is modified in place)."""
     return _graph_cache.get(edge_index, (int(n_dst), int(n_src), flow),
-                            lambda: Graph(edge_index, n_dst, n_src, flow))
+                            lambda: Graph(edge_index, n_dst, n_src, flow, weak=True))
 
 
 def csr_for_index(index, n_rows):

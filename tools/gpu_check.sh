@@ -1,0 +1,17 @@
+#!/bin/bash
+# GPU-box run: parity tests, smoke, bench.  Stops at the first crash-type
+# exit (abort / segfault / timeout); plain test failures (rc 1) continue.
+set -u
+mkdir -p gpurun_out
+step() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name" ; date +%T
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"; tail -5 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+step pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout=600 ${PYTEST_ARGS:-}
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python bench.py --steps 20 --warmup 5
