@@ -144,8 +144,12 @@ def main():
     lib = _lib.load()
     st_main = csr.struct("other")
 
+    slab = torch.empty(lib.mp_aggregate_slab_bytes(st_main, F_DIM, _lib.MP_REDUCE["sum"]),
+                       dtype=torch.uint8, device=dev)
+
     def aggregate(x_src, stages=_lib.MP_STAGE_ALL, out=None):
-        return ops._aggregate(csr, "other", x_src, w_csr, "sum", 0, bias, out=out, stages=stages)[0]
+        return ops._aggregate(csr, "other", x_src, w_csr, "sum", 0, bias, out=out, stages=stages,
+                              slab=slab)[0]
 
     out_buf = torch.empty((n_rows, F_DIM), device=dev)
 
@@ -176,21 +180,25 @@ def main():
     value = E2 * args.steps / dt    # whole-job edges aggregated per second
 
     # dominant kernel (main aggregation launch) timed with HIP events on the
-    # stream it runs on (torch's current stream), averaged over launches
+    # stream it runs on (torch's current stream): `reps` back-to-back launches
+    # between two events (host launch latency amortised), averaged
     x_src = x if world == 1 else plan.halo_exchange(x, ops.gather_rows)
     reps = max(args.steps, 10)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
-    evf = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
-    for k in range(reps):
-        ev[k][0].record()
-        aggregate(x_src, stages=_lib.MP_STAGE_MAIN, out=out_buf)
-        ev[k][1].record()
-        evf[k][0].record()
-        aggregate(x_src, stages=_lib.MP_STAGE_FIXUP, out=out_buf)
-        evf[k][1].record()
-    torch.cuda.synchronize()
-    main_ms = sorted(a.elapsed_time(b) for a, b in ev)
-    fix_ms = sorted(a.elapsed_time(b) for a, b in evf)
+
+    def timed(stages, rounds=3):
+        per = []
+        for _ in range(rounds):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(reps):
+                aggregate(x_src, stages=stages, out=out_buf)
+            b.record()
+            torch.cuda.synchronize()
+            per.append(a.elapsed_time(b) / reps)
+        return sorted(per)
+
+    main_ms = timed(_lib.MP_STAGE_MAIN)
+    fix_ms = timed(_lib.MP_STAGE_FIXUP)
     main_avg = sum(main_ms) / len(main_ms)
     fix_avg = sum(fix_ms) / len(fix_ms)
     alg_bytes = E_local * BYTES_PER_EDGE + n_rows * BYTES_PER_NODE

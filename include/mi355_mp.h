@@ -109,9 +109,11 @@ int32_t mp_schedule_n_waves(int64_t n_rows, int64_t n_edges, int32_t chunk);
 size_t mp_schedule_workspace(int32_t n_waves);
 
 /* Builds wave_row[n_waves+1], wave_slot[n_waves+1] and split_waves[<=n_waves];
- * writes the split count to n_split_dev[0] (device int32). */
+ * writes the split count to n_split_dev[0] (device int32).  A task boundary
+ * that falls inside a row of <= snap slots is moved back to that row's start
+ * (0 <= snap < chunk-1), so only longer rows are ever split. */
 int mp_schedule_build(const int32_t* rowptr, int64_t n_rows, int64_t n_edges,
-                      int32_t chunk, int32_t* wave_row, int32_t* wave_slot,
+                      int32_t chunk, int32_t snap, int32_t* wave_row, int32_t* wave_slot,
                       int32_t* split_waves, int32_t* n_split_dev, void* ws,
                       size_t ws_bytes, void* stream);
 

@@ -73,13 +73,29 @@ struct AggArgs {
 
 // ---------------------------------------------------------------------------
 // Reducers: per-lane state for VEC features of one (partial) row.
+//
+// A partial (the state of a row cut at a task boundary) lives in a slab slot
+// in HBM between the main kernel and the fix-up, and in LDS between the
+// waves of one fix-up block.  PRef points at one lane's share of a partial:
+//   v  : VEC values,  a : VEC arg ids (max/min),  st : (m, s) pair (GAT).
+// Red::Part is the same state in registers, so a chain of partials can be
+// loaded U at a time (U loads in flight) and merged in order.
 // ---------------------------------------------------------------------------
+
+struct PRef {
+  float* v;
+  int32_t* a;
+  float* st;
+};
 
 template <int VEC, bool HAS_W, bool MEAN>
 struct SumRed {
   static constexpr bool kW = HAS_W;
   static constexpr bool kEid = false;
   static constexpr bool kGat = false;
+  struct Part {
+    float v[VEC];
+  };
   float acc[VEC];
   int h = 0;  // unused (GAT only)
 
@@ -98,22 +114,32 @@ struct SumRed {
 #pragma unroll
     for (int k = 0; k < VEC; ++k) acc[k] = __fadd_rn(acc[k], HAS_W ? __fmul_rn(wt, v.v[k]) : v.v[k]);
   }
-  __device__ __forceinline__ void store_partial(const AggArgs& p, int64_t s, int f, bool act) {
-    if (!act) return;
+  __device__ __forceinline__ void save(PRef r, bool) const {
     Frag<VEC> o;
 #pragma unroll
     for (int k = 0; k < VEC; ++k) o.v[k] = acc[k];
-    store_frag<VEC>(p.slab_v + s * p.slab_ld + f, o);
+    store_frag<VEC>(r.v, o);
   }
-  __device__ __forceinline__ void load_partial(const AggArgs& p, int64_t s, int f) {
-    Frag<VEC> o = load_frag<VEC>(p.slab_v + s * p.slab_ld + f);
+  static __device__ __forceinline__ Part load(PRef r) {
+    Frag<VEC> o = load_frag<VEC>(r.v);
+    Part q;
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) acc[k] = o.v[k];
+    for (int k = 0; k < VEC; ++k) q.v[k] = o.v[k];
+    return q;
   }
-  __device__ __forceinline__ void merge_partial(const AggArgs& p, int64_t s, int f) {
-    Frag<VEC> o = load_frag<VEC>(p.slab_v + s * p.slab_ld + f);
+  __device__ __forceinline__ void set(const Part& q) {
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) acc[k] = __fadd_rn(acc[k], o.v[k]);
+    for (int k = 0; k < VEC; ++k) acc[k] = q.v[k];
+  }
+  __device__ __forceinline__ void merge(const Part& q) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = __fadd_rn(acc[k], q.v[k]);
+  }
+  __device__ __forceinline__ Part part() const {
+    Part q;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) q.v[k] = acc[k];
+    return q;
   }
   __device__ __forceinline__ void finish(const AggArgs& p, int64_t row, int64_t cnt, int f, bool act) {
     if (!act) return;
@@ -133,11 +159,17 @@ struct SumRed {
 // torch_scatter CPU scatter_max/min [U9]: out starts at lowest()/max(),
 // arg at src.size(0); strict compare so the FIRST edge (in original order)
 // wins ties; afterwards out==init -> 0 (only when out was not passed in).
+// Partials are merged in task order with the same strict compare: a later
+// task only holds later edges of the row, so the first maximum survives.
 template <int VEC, bool HAS_W, bool IS_MAX>
 struct ArgRed {
   static constexpr bool kW = HAS_W;
   static constexpr bool kEid = true;
   static constexpr bool kGat = false;
+  struct Part {
+    float v[VEC];
+    int a[VEC];
+  };
   float m[VEC];
   int a[VEC];
   int h = 0;
@@ -170,31 +202,46 @@ struct ArgRed {
       }
     }
   }
-  __device__ __forceinline__ void store_partial(const AggArgs& p, int64_t s, int f, bool act) {
-    if (!act) return;
+  __device__ __forceinline__ void save(PRef r, bool) const {
 #pragma unroll
     for (int k = 0; k < VEC; ++k) {
-      p.slab_v[s * p.slab_ld + f + k] = m[k];
-      p.slab_a[s * p.slab_ld + f + k] = a[k];
+      r.v[k] = m[k];
+      r.a[k] = a[k];
     }
   }
-  __device__ __forceinline__ void load_partial(const AggArgs& p, int64_t s, int f) {
+  static __device__ __forceinline__ Part load(PRef r) {
+    Part q;
 #pragma unroll
     for (int k = 0; k < VEC; ++k) {
-      m[k] = p.slab_v[s * p.slab_ld + f + k];
-      a[k] = p.slab_a[s * p.slab_ld + f + k];
+      q.v[k] = r.v[k];
+      q.a[k] = r.a[k];
+    }
+    return q;
+  }
+  __device__ __forceinline__ void set(const Part& q) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      m[k] = q.v[k];
+      a[k] = q.a[k];
     }
   }
-  __device__ __forceinline__ void merge_partial(const AggArgs& p, int64_t s, int f) {
+  __device__ __forceinline__ void merge(const Part& q) {
 #pragma unroll
     for (int k = 0; k < VEC; ++k) {
-      float v = p.slab_v[s * p.slab_ld + f + k];
-      int e = p.slab_a[s * p.slab_ld + f + k];
-      if (better(v, m[k])) {  // later tasks hold later edges: strict keeps the first
-        m[k] = v;
-        a[k] = e;
+      if (better(q.v[k], m[k])) {
+        m[k] = q.v[k];
+        a[k] = q.a[k];
       }
     }
+  }
+  __device__ __forceinline__ Part part() const {
+    Part q;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      q.v[k] = m[k];
+      q.a[k] = a[k];
+    }
+    return q;
   }
   __device__ __forceinline__ void finish(const AggArgs& p, int64_t row, int64_t, int f, bool act) {
     if (!act) return;
@@ -225,6 +272,10 @@ struct GatRed {
   static constexpr bool kW = false;
   static constexpr bool kEid = false;
   static constexpr bool kGat = true;
+  struct Part {
+    float v[VEC];
+    float m, s;
+  };
   float acc[VEC];
   float m, s, ad;
   int h;
@@ -250,35 +301,46 @@ struct GatRed {
     m = mn;
   }
   __device__ __forceinline__ void consume(const Frag<VEC>&, float, int, float) {}
-  __device__ __forceinline__ int64_t stat_index(const AggArgs& p, int64_t s_) const { return (s_ * p.H + h) * 2; }
-  __device__ __forceinline__ void store_partial(const AggArgs& p, int64_t s_, int f, bool act) {
-    if (!act) return;
+  __device__ __forceinline__ void save(PRef r, bool stat_writer) const {
     Frag<VEC> o;
 #pragma unroll
     for (int k = 0; k < VEC; ++k) o.v[k] = acc[k];
-    store_frag<VEC>(p.slab_v + s_ * p.slab_ld + f, o);
-    if (f % p.C == 0) {
-      p.slab_s[stat_index(p, s_)] = m;
-      p.slab_s[stat_index(p, s_) + 1] = s;
+    store_frag<VEC>(r.v, o);
+    if (stat_writer) {
+      r.st[0] = m;
+      r.st[1] = s;
     }
   }
-  __device__ __forceinline__ void load_partial(const AggArgs& p, int64_t s_, int f) {
-    Frag<VEC> o = load_frag<VEC>(p.slab_v + s_ * p.slab_ld + f);
+  static __device__ __forceinline__ Part load(PRef r) {
+    Frag<VEC> o = load_frag<VEC>(r.v);
+    Part q;
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) acc[k] = o.v[k];
-    m = p.slab_s[stat_index(p, s_)];
-    s = p.slab_s[stat_index(p, s_) + 1];
+    for (int k = 0; k < VEC; ++k) q.v[k] = o.v[k];
+    q.m = r.st[0];
+    q.s = r.st[1];
+    return q;
   }
-  __device__ __forceinline__ void merge_partial(const AggArgs& p, int64_t s_, int f) {
-    Frag<VEC> o = load_frag<VEC>(p.slab_v + s_ * p.slab_ld + f);
-    float pm = p.slab_s[stat_index(p, s_)];
-    float ps = p.slab_s[stat_index(p, s_) + 1];
-    float mn = fmaxf(m, pm);
-    float c0 = expf(m - mn), c1 = expf(pm - mn);
-    s = s * c0 + ps * c1;
+  __device__ __forceinline__ void set(const Part& q) {
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) acc[k] = acc[k] * c0 + o.v[k] * c1;
+    for (int k = 0; k < VEC; ++k) acc[k] = q.v[k];
+    m = q.m;
+    s = q.s;
+  }
+  __device__ __forceinline__ void merge(const Part& q) {
+    float mn = fmaxf(m, q.m);
+    float c0 = expf(m - mn), c1 = expf(q.m - mn);
+    s = s * c0 + q.s * c1;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = acc[k] * c0 + q.v[k] * c1;
     m = mn;
+  }
+  __device__ __forceinline__ Part part() const {
+    Part q;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) q.v[k] = acc[k];
+    q.m = m;
+    q.s = s;
+    return q;
   }
   __device__ __forceinline__ void finish(const AggArgs& p, int64_t row, int64_t, int f, bool act) {
     if (!act) return;
@@ -298,6 +360,16 @@ struct GatRed {
     }
   }
 };
+
+// this lane's share of slab slot s (2*task + kind)
+template <class Red>
+__device__ __forceinline__ PRef slab_ref(const AggArgs& p, int64_t s, int f, const Red& red) {
+  PRef r;
+  r.v = p.slab_v + s * p.slab_ld + f;
+  r.a = p.slab_a ? p.slab_a + s * p.slab_ld + f : nullptr;
+  r.st = p.slab_s ? p.slab_s + (s * p.H + red.h) * 2 : nullptr;
+  return r;
+}
 
 // ---------------------------------------------------------------------------
 // Per-wave slot window: col / weight / eid of 64 consecutive CSR slots held one
@@ -407,7 +479,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_main(AggArgs p) {
     if (e_begin < ce) {
       red.begin(p, r_first - 1, false, f, act);
       run_slots<Red, VEC, U>(red, p, win, e_begin, ce < e_end ? ce : e_end, foff, lane);
-      red.store_partial(p, 2 * (int64_t)w, f, act);
+      if (act) red.save(slab_ref(p, 2 * (int64_t)w, f, red), Red::kGat && (f % p.C == 0));
     }
   }
   // rows owned by this task
@@ -424,30 +496,66 @@ __global__ __launch_bounds__(kBlock) void k_agg_main(AggArgs p) {
       red.finish(p, r, re - rs, f, act);
     } else {
       run_slots<Red, VEC, U>(red, p, win, rs, e_end, foff, lane);
-      red.store_partial(p, 2 * (int64_t)w + 1, f, act);
+      if (act) red.save(slab_ref(p, 2 * (int64_t)w + 1, f, red), Red::kGat && (f % p.C == 0));
     }
   }
 }
 
-// One wave per split row: head partial of the owning task, then the
-// continuation partials of the following tasks, in task order.
+// One 4-wave block per split row.  The row's partials form a chain in task
+// order: item 0 = head slab of the owning task, item k = continuation slab of
+// task owner+k.  Wave q reduces items [q*c, (q+1)*c) in order (U loads in
+// flight), waves 1..3 hand their result to wave 0 through LDS, wave 0 merges
+// them in wave order and finishes the row: a fixed order, so deterministic.
 template <class Red, int VEC>
 __global__ __launch_bounds__(kBlock) void k_agg_fixup(AggArgs p) {
+  constexpr int U = 4;
+  __shared__ typename Red::Part lds[kWavesPerBlock - 1][64];
+  __shared__ int has[kWavesPerBlock];
   const int lane = lane_id();
-  const int i = uni((int)blockIdx.x * kWavesPerBlock + (int)(threadIdx.x >> 6));
-  if (i >= p.n_split) return;
+  const int wid = uni((int)(threadIdx.x >> 6));
+  const int i = (int)blockIdx.x;
   const int f = (int)blockIdx.y * 64 * VEC + lane * VEC;
   const bool act = f < p.F;
+  const int fs = act ? f : 0;
   const int last = uni(p.split_waves[i]);
   const int r = uni(p.wave_row[last]) - 1;
   const int64_t rs = uni(p.rowptr[r]);
   const int64_t re = uni(p.rowptr[r + 1]);
-  const int owner = (int)((rs + r) / p.chunk);
-  Red red(p, f, act);
-  if (act) {
-    red.load_partial(p, 2 * (int64_t)owner + 1, f);
-    for (int t = owner + 1; t <= last; ++t) red.merge_partial(p, 2 * (int64_t)t, f);
+  // owner = last task whose first owned row is <= r
+  int lo = 0, hi = p.n_waves;  // wave_row[n_waves] = n_rows > r
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (p.wave_row[mid] <= r) lo = mid;
+    else hi = mid - 1;
   }
+  const int owner = uni(lo);
+  const int L = last - owner + 1;
+  const int c = (L + kWavesPerBlock - 1) / kWavesPerBlock;
+  const int b0 = wid * c;
+  const int b1 = min(L, b0 + c);
+  Red red(p, f, act);
+  auto item = [&](int k) {
+    int64_t slot = k == 0 ? 2 * (int64_t)owner + 1 : 2 * (int64_t)(owner + k);
+    return slab_ref(p, slot, fs, red);
+  };
+  const bool mine = b0 < b1;
+  if (mine) {
+    red.set(Red::load(item(b0)));
+    for (int k = b0 + 1; k < b1; k += U) {
+      typename Red::Part q[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) q[u] = Red::load(item(min(k + u, b1 - 1)));
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (k + u < b1) red.merge(q[u]);
+    }
+  }
+  if (lane == 0) has[wid] = mine ? 1 : 0;
+  if (wid > 0 && mine) lds[wid - 1][lane] = red.part();
+  __syncthreads();
+  if (wid != 0) return;
+  for (int q = 1; q < kWavesPerBlock; ++q)
+    if (has[q]) red.merge(lds[q - 1][lane]);
   red.finish(p, r, re - rs, f, act);
 }
 
@@ -474,7 +582,7 @@ static int launch(const AggArgs& a, int stages, hipStream_t s) {
     MP_CHECK_LAUNCH();
   }
   if ((stages & MP_STAGE_FIXUP) && a.n_split > 0) {
-    dim3 grid((unsigned)ceil_div(a.n_split, kWavesPerBlock), (unsigned)ftiles);
+    dim3 grid((unsigned)a.n_split, (unsigned)ftiles);
     hipLaunchKernelGGL((k_agg_fixup<Red, VEC>), grid, dim3(kBlock), 0, s, a);
     MP_CHECK_LAUNCH();
   }

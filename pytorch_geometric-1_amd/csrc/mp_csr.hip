@@ -98,8 +98,12 @@ static size_t sort_temp_bytes(int64_t n_edges, int64_t n_rows) {
 //   wave_slot[w] = min(w*chunk - wave_row[w], rowptr[wave_row[w]])
 // so every task does at most `chunk` units of (row store | edge gather) work,
 // whatever the degree distribution (power-law hubs, runs of empty rows).
+// Snap: when the boundary falls inside a row of at most `snap` slots, it is
+// moved back to that row's marker, so the row is not split (a task then does
+// at most chunk + snap units; snap < chunk keeps the starts increasing).
+// Only rows longer than `snap` (hubs) are ever cut and need a fix-up.
 __global__ void k_wave_row(const int32_t* __restrict__ rowptr, int64_t n_rows, int64_t n_edges,
-                           int32_t chunk, int32_t n_waves, int32_t* __restrict__ wave_row,
+                           int32_t chunk, int32_t snap, int32_t n_waves, int32_t* __restrict__ wave_row,
                            int32_t* __restrict__ wave_slot) {
   int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (w > n_waves) return;
@@ -122,6 +126,14 @@ __global__ void k_wave_row(const int32_t* __restrict__ rowptr, int64_t n_rows, i
   }
   int64_t slot = target - lo;
   int64_t rs = rowptr[lo];  // rowptr[n_rows] == n_edges
+  if (slot < rs && lo > 0) {  // the boundary cuts row lo-1
+    int64_t r0 = rowptr[lo - 1];
+    if (rs - r0 <= snap) {
+      wave_row[w] = (int32_t)(lo - 1);
+      wave_slot[w] = (int32_t)r0;
+      return;
+    }
+  }
   wave_row[w] = (int32_t)lo;
   wave_slot[w] = (int32_t)(slot < rs ? slot : rs);
 }
@@ -218,9 +230,10 @@ size_t mp_schedule_workspace(int32_t n_waves) {
 }
 
 int mp_schedule_build(const int32_t* rowptr, int64_t n_rows, int64_t n_edges, int32_t chunk,
-                      int32_t* wave_row, int32_t* wave_slot, int32_t* split_waves,
+                      int32_t snap, int32_t* wave_row, int32_t* wave_slot, int32_t* split_waves,
                       int32_t* n_split_dev, void* ws, size_t ws_bytes, void* stream) {
   MP_CHECK_ARG(chunk > 0 && chunk % 64 == 0, "mp_schedule_build: chunk must be a positive multiple of 64");
+  MP_CHECK_ARG(snap >= 0 && snap < chunk - 1, "mp_schedule_build: need 0 <= snap < chunk - 1");
   MP_CHECK_ARG(rowptr && wave_row && wave_slot && split_waves && n_split_dev,
                "mp_schedule_build: null pointer");
   MP_CHECK_ARG(n_rows + n_edges < (int64_t)INT32_MAX, "mp_schedule_build: N+E exceeds int32");
@@ -228,8 +241,8 @@ int mp_schedule_build(const int32_t* rowptr, int64_t n_rows, int64_t n_edges, in
   MP_CHECK_ARG(ws_bytes >= mp_schedule_workspace(n_waves), "mp_schedule_build: workspace too small");
   hipStream_t s = as_stream(stream);
   const int B = 256;
-  k_wave_row<<<ceil_div((int64_t)n_waves + 1, B), B, 0, s>>>(rowptr, n_rows, n_edges, chunk, n_waves,
-                                                             wave_row, wave_slot);
+  k_wave_row<<<ceil_div((int64_t)n_waves + 1, B), B, 0, s>>>(rowptr, n_rows, n_edges, chunk, snap,
+                                                             n_waves, wave_row, wave_slot);
   MP_CHECK_LAUNCH();
   uint8_t* flags = (uint8_t*)ws;
   void* tmp = (char*)ws + align_up((size_t)n_waves, 256);

@@ -45,7 +45,7 @@ SIGNATURES = {
     "mp_csr_build": (ctypes.c_int, [c_p, c_p, i64, i64, i64, c_p, c_p, c_p, c_p, c_p, sz, c_p]),
     "mp_schedule_n_waves": (i32, [i64, i64, i32]),
     "mp_schedule_workspace": (sz, [i32]),
-    "mp_schedule_build": (ctypes.c_int, [c_p, i64, i64, i32, c_p, c_p, c_p, c_p, c_p, sz, c_p]),
+    "mp_schedule_build": (ctypes.c_int, [c_p, i64, i64, i32, i32, c_p, c_p, c_p, c_p, c_p, sz, c_p]),
     "mp_aggregate_slab_bytes": (sz, [ctypes.POINTER(MpCsr), i32, i32]),
     "mp_aggregate_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, i64, i32, i32, i32, c_p,
                                         c_p, i64, c_p, c_p, sz, i32, c_p]),

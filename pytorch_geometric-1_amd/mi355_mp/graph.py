@@ -18,13 +18,18 @@ from . import _lib
 DEFAULT_CHUNK = 256
 
 
+def default_snap(chunk):
+    """Rows of up to chunk/2 slots are never split across tasks."""
+    return chunk // 2
+
+
 class CSR:
     """One stable CSR of ``key`` (int64 [E]) with gather column ``other``.
 
     rowptr[n_rows+1], col[E] (= other[eid] or eid), eid[E] : int32 on device.
     """
 
-    def __init__(self, key, other, n_rows, n_other, chunk=DEFAULT_CHUNK):
+    def __init__(self, key, other, n_rows, n_other, chunk=DEFAULT_CHUNK, snap=None):
         _lib.require_device(key)
         lib = _lib.load()
         dev = key.device
@@ -36,6 +41,7 @@ class CSR:
         self.n_other = int(n_other)
         self.device = dev
         self.chunk = int(chunk)
+        self.snap = default_snap(self.chunk) if snap is None else int(snap)
         self.rowptr = torch.empty(self.n_rows + 1, dtype=torch.int32, device=dev)
         self.col = torch.empty(max(E, 1), dtype=torch.int32, device=dev)
         self.eid = torch.empty(max(E, 1), dtype=torch.int32, device=dev)
@@ -59,7 +65,7 @@ class CSR:
         n_split = torch.zeros(1, dtype=torch.int32, device=dev)
         sws = lib.mp_schedule_workspace(self.n_waves)
         ws = torch.empty(sws, dtype=torch.uint8, device=dev)
-        _lib.check(lib.mp_schedule_build(self.rowptr.data_ptr(), self.n_rows, E, self.chunk,
+        _lib.check(lib.mp_schedule_build(self.rowptr.data_ptr(), self.n_rows, E, self.chunk, self.snap,
                                          self.wave_row.data_ptr(), self.wave_slot.data_ptr(),
                                          self.split_waves.data_ptr(), n_split.data_ptr(),
                                          ws.data_ptr(), sws, st), "mp_schedule_build")

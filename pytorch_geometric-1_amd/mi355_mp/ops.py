@@ -29,7 +29,8 @@ def _f32_2d(x, what):
     return x
 
 
-def _aggregate(csr, gather, x, w_csr, reduce, flags, bias, out=None, stages=_lib.MP_STAGE_ALL):
+def _aggregate(csr, gather, x, w_csr, reduce, flags, bias, out=None, stages=_lib.MP_STAGE_ALL, slab=None,
+               arg=None):
     """Launch mp_aggregate_f32; returns (out, arg_or_None)."""
     lib = _lib.load()
     F = x.shape[1]
@@ -37,13 +38,15 @@ def _aggregate(csr, gather, x, w_csr, reduce, flags, bias, out=None, stages=_lib
     if out is None:
         out = torch.empty((csr.n_rows, F), dtype=torch.float32, device=dev)
     is_arg = reduce in ("max", "min")
-    arg = torch.empty((csr.n_rows, F), dtype=torch.int64, device=dev) if is_arg else None
+    if is_arg and arg is None:
+        arg = torch.empty((csr.n_rows, F), dtype=torch.int64, device=dev)
     if csr.n_rows == 0 or F == 0:
         return out, arg
     g = csr.struct(gather)
     red = _lib.MP_REDUCE[reduce]
     sb = lib.mp_aggregate_slab_bytes(g, F, red)
-    slab = torch.empty(sb, dtype=torch.uint8, device=dev)
+    if slab is None or slab.numel() < sb:
+        slab = torch.empty(sb, dtype=torch.uint8, device=dev)
     _lib.check(lib.mp_aggregate_f32(g, _lib.ptr(w_csr), x.data_ptr(), x.stride(0), F, red, flags,
                                     _lib.ptr(bias), out.data_ptr(), out.stride(0), _lib.ptr(arg),
                                     slab.data_ptr(), sb, stages, _lib.stream_ptr(dev)),

@@ -51,8 +51,9 @@ def _split_rows(csr):
 # CSR + schedule
 # --------------------------------------------------------------------------
 
-def _merge_path_reference(rowptr, chunk):
-    """Brute-force merge path: walk the N+E items in order."""
+def _merge_path_reference(rowptr, chunk, snap):
+    """Brute-force merge path: walk the N+E items in order; a boundary inside
+    a row of <= snap slots moves back to that row's marker."""
     N = len(rowptr) - 1
     E = int(rowptr[-1])
     items = []
@@ -71,6 +72,10 @@ def _merge_path_reference(rowptr, chunk):
         wave_row.append(later_rows[0] if later_rows else N)
         later_slots = [v for t, v in items[w * chunk:] if t == "slot"]
         wave_slot.append(later_slots[0] if later_slots else E)
+        r0 = wave_row[-1]
+        if w > 0 and r0 > 0 and wave_slot[-1] < rowptr[r0] and rowptr[r0] - rowptr[r0 - 1] <= snap:
+            wave_row[-1] = r0 - 1
+            wave_slot[-1] = rowptr[r0 - 1]
         del rows, slots
     wave_row.append(N)
     wave_slot.append(E)
@@ -92,7 +97,7 @@ def test_csr_and_schedule_match_reference(N, E, chunk):
     if E:
         assert torch.equal(csr.eid.cpu()[:E].long(), perm)
         assert torch.equal(csr.col.cpu()[:E].long(), other[perm])
-    wr, ws = _merge_path_reference(rowptr.tolist(), chunk)
+    wr, ws = _merge_path_reference(rowptr.tolist(), chunk, csr.snap)
     assert np.array_equal(csr.wave_row.cpu().numpy(), wr)
     assert np.array_equal(csr.wave_slot.cpu().numpy(), ws)
     # split list = last task of every row spanning tasks

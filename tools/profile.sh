@@ -1,0 +1,22 @@
+#!/bin/bash
+# rocprofv3 on the GPU box: kernel-trace stats of bench.py, then separate PMC
+# passes (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950) restricted
+# to the dominant kernel.  Outputs under gpurun_out/prof/.
+set -u
+export TMPDIR=/tmp
+OUT=gpurun_out/prof
+mkdir -p $OUT
+run() {  # name timeout args...
+  local name=$1 t=$2; shift 2
+  echo "== $name"; date +%T
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"; tail -3 "$OUT/$name.log"
+  if [ $rc -ne 0 ]; then echo "STOP"; exit $rc; fi
+}
+B="bench.py --steps 20 --warmup 5 --no-cpu-baseline ${BENCH_ARGS:-}"
+run kt 600 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- python3 $B
+run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_agg_main -d $OUT/pmc_fetch -o pmc --output-format csv -- python3 $B
+run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_agg_main -d $OUT/pmc_write -o pmc --output-format csv -- python3 $B
+run pmc_l2 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex k_agg_main -d $OUT/pmc_l2 -o pmc --output-format csv -- python3 $B
+find $OUT -name "*.csv" | head -50
