@@ -29,7 +29,30 @@
 
 #include "mp_common.h"
 
+// Build-time tuning knobs (A/B-tested in one process by tools/ab_bench.py).
+#ifndef MP_U_VEC4
+#define MP_U_VEC4 8        // x-row loads in flight per wave (VEC=4)
+#endif
+#ifndef MP_NT_OUT
+#define MP_NT_OUT 0        // non-temporal output-row stores
+#endif
+#ifndef MP_NT_IDX
+#define MP_NT_IDX 0        // non-temporal col/weight/eid stream loads
+#endif
+
 namespace mp {
+
+template <int VEC>
+__device__ __forceinline__ void store_out(float* p, const Frag<VEC>& f) {
+  if constexpr (MP_NT_OUT) store_frag_nt<VEC>(p, f);
+  else store_frag<VEC>(p, f);
+}
+
+template <class T>
+__device__ __forceinline__ T ld_stream(const T* p) {
+  if constexpr (MP_NT_IDX) return __builtin_nontemporal_load(p);
+  else return *p;
+}
 
 constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = 64 * kWavesPerBlock;
@@ -152,7 +175,7 @@ struct SumRed {
 #pragma unroll
       for (int k = 0; k < VEC; ++k) o.v[k] = __fadd_rn(o.v[k], b.v[k]);
     }
-    store_frag<VEC>(p.out + row * p.ldo + f, o);
+    store_out<VEC>(p.out + row * p.ldo + f, o);
   }
 };
 
@@ -257,7 +280,7 @@ struct ArgRed {
       if (p.bias) v = __fadd_rn(v, p.bias[f + k]);
       o.v[k] = v;
     }
-    store_frag<VEC>(p.out + row * p.ldo + f, o);
+    store_out<VEC>(p.out + row * p.ldo + f, o);
     int64_t* ao = p.arg_out + row * (int64_t)p.F + f;
 #pragma unroll
     for (int k = 0; k < VEC; ++k) ao[k] = (int64_t)a[k];
@@ -353,7 +376,7 @@ struct GatRed {
 #pragma unroll
       for (int k = 0; k < VEC; ++k) o.v[k] = o.v[k] + b.v[k];
     }
-    store_frag<VEC>(p.out + row * p.ldo + f, o);
+    store_out<VEC>(p.out + row * p.ldo + f, o);
     if (p.row_stats && (f % p.C == 0)) {
       p.row_stats[(row * p.H + h) * 2] = m;
       p.row_stats[(row * p.H + h) * 2 + 1] = den;
@@ -384,9 +407,9 @@ struct SlotWin {
   __device__ __forceinline__ void fetch(const AggArgs& p, int64_t b, int lane, int& c, float& wt, int& e) {
     int64_t k = b + lane;
     bool ok = k < limit;
-    c = ok ? p.col[k] : 0;
-    if (W) wt = ok ? p.w[k] : 0.f;
-    if (EID) e = ok ? p.eid[k] : 0;
+    c = ok ? ld_stream(p.col + k) : 0;
+    if (W) wt = ok ? ld_stream(p.w + k) : 0.f;
+    if (EID) e = ok ? ld_stream(p.eid + k) : 0;
   }
   __device__ __forceinline__ void init(const AggArgs& p, int64_t b, int64_t lim, int lane) {
     base = b;
@@ -574,7 +597,7 @@ static int pick_vec(int F, int64_t ldx, const void* x, int64_t ldo, const void* 
 
 template <class Red, int VEC>
 static int launch(const AggArgs& a, int stages, hipStream_t s) {
-  constexpr int U = VEC == 4 ? 8 : 16;
+  constexpr int U = VEC == 4 ? MP_U_VEC4 : 16;
   const int ftiles = (int)ceil_div(a.F, 64 * VEC);
   if (stages & MP_STAGE_MAIN) {
     dim3 grid((unsigned)ceil_div(a.n_waves, kWavesPerBlock), (unsigned)ftiles);

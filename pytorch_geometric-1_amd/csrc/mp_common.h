@@ -83,4 +83,20 @@ __device__ __forceinline__ void store_frag(float* p, const Frag<VEC>& f) {
   }
 }
 
+// Non-temporal store of a fragment (output rows are written once and never
+// re-read by the kernel; keeping them out of L2/MALL leaves room for the
+// gathered x rows).
+template <int VEC>
+__device__ __forceinline__ void store_frag_nt(float* p, const Frag<VEC>& f) {
+  if constexpr (VEC == 4) {
+    f32x4 t = {f.v[0], f.v[1], f.v[2], f.v[3]};
+    __builtin_nontemporal_store(t, reinterpret_cast<f32x4*>(p));
+  } else if constexpr (VEC == 2) {
+    f32x2 t = {f.v[0], f.v[1]};
+    __builtin_nontemporal_store(t, reinterpret_cast<f32x2*>(p));
+  } else {
+    __builtin_nontemporal_store(f.v[0], p);
+  }
+}
+
 }  // namespace mp
