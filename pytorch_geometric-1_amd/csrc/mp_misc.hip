@@ -90,6 +90,43 @@ __global__ void k_gat_node_scores(const float* __restrict__ xw, int64_t n_nodes,
   a_src[i] = ss;
 }
 
+// Wave-per-node form (C % 4 == 0, G = C/4 lanes per head a power of two
+// <= 64): one coalesced 1 KiB pass per 256 features, per-lane partial dot
+// products, then a shuffle-xor reduction inside each G-lane head group.
+__global__ __launch_bounds__(256) void k_gat_node_scores_wave(const float* __restrict__ xw, int64_t n_nodes,
+                                                               int32_t H, int32_t C, int32_t G,
+                                                               const float* __restrict__ att,
+                                                               float* __restrict__ a_src,
+                                                               float* __restrict__ a_dst) {
+  const int lane = lane_id();
+  const int64_t HC = (int64_t)H * C;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t n = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); n < n_nodes; n += nw) {
+    for (int64_t base = 0; base < HC; base += 256) {
+      const int64_t f = base + lane * 4;
+      float sd = 0.f, ss = 0.f;
+      int h = 0;
+      if (f < HC) {
+        h = (int)(f / C);
+        const int c = (int)(f % C);
+        f32x4 v = *reinterpret_cast<const f32x4*>(xw + n * HC + f);
+        f32x4 ad = *reinterpret_cast<const f32x4*>(att + (int64_t)h * 2 * C + c);
+        f32x4 as = *reinterpret_cast<const f32x4*>(att + (int64_t)h * 2 * C + C + c);
+        sd = v.x * ad.x + v.y * ad.y + v.z * ad.z + v.w * ad.w;
+        ss = v.x * as.x + v.y * as.y + v.z * as.z + v.w * as.w;
+      }
+      for (int o = G >> 1; o > 0; o >>= 1) {
+        sd += __shfl_xor(sd, o);
+        ss += __shfl_xor(ss, o);
+      }
+      if (f < HC && (lane & (G - 1)) == 0) {
+        a_dst[n * H + h] = sd;
+        a_src[n * H + h] = ss;
+      }
+    }
+  }
+}
+
 // alpha[e,h] = exp(leaky(a_src[j,h]+a_dst[i,h]) - max_i,h) / (den_i,h)
 __global__ void k_gat_alpha(const int64_t* __restrict__ src_idx, const int64_t* __restrict__ dst_idx,
                             int64_t n_edges, int32_t H, const float* __restrict__ a_src,
@@ -175,9 +212,19 @@ int mp_gat_node_scores_f32(const float* xw, int64_t n_nodes, int32_t H, int32_t 
   MP_CHECK_ARG(H > 0 && C > 0 && n_nodes >= 0, "mp_gat_node_scores_f32: bad sizes");
   if (n_nodes == 0) return MP_OK;
   MP_CHECK_ARG(xw && att && a_src && a_dst, "mp_gat_node_scores_f32: null pointer");
-  int64_t total = n_nodes * (int64_t)H;
-  k_gat_node_scores<<<(unsigned)ceil_div(total, 256), 256, 0, as_stream(stream)>>>(xw, n_nodes, H, C, att,
-                                                                                   a_src, a_dst);
+  const int G = C / 4;
+  const bool wave_form = C % 4 == 0 && G <= 64 && (G & (G - 1)) == 0 && (uintptr_t)xw % 16 == 0 &&
+                         (uintptr_t)att % 16 == 0;
+  if (wave_form) {
+    int64_t blocks = ceil_div(n_nodes, 4);
+    if (blocks > 16384) blocks = 16384;
+    k_gat_node_scores_wave<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(xw, n_nodes, H, C, G, att, a_src,
+                                                                            a_dst);
+  } else {
+    int64_t total = n_nodes * (int64_t)H;
+    k_gat_node_scores<<<(unsigned)ceil_div(total, 256), 256, 0, as_stream(stream)>>>(xw, n_nodes, H, C, att,
+                                                                                     a_src, a_dst);
+  }
   MP_CHECK_LAUNCH();
   return MP_OK;
 }

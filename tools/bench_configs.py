@@ -1,0 +1,165 @@
+"""Measures the BASELINE.md configs other than the bench.py headline:
+
+  c3  same RMAT graph, GATConv heads=8 C=32 (fused online-softmax aggregation)
+  c4  Reddit-scale power-law N=232,965 E=114,615,892, F=256, aggr='max'
+      (segmented max + int64 first-index argmax)
+  c5  ogbn-products-scale N=2,449,029 E=123,718,280 GCNConv F=256 (1 GPU)
+
+For each: dominant-kernel time (HIP events over back-to-back launches),
+edges/s, algorithmic GB/s with BASELINE.md's byte formulas, fraction of the
+8 TB/s spec.  One JSON line per config.
+    python tools/bench_configs.py [--configs c3,c4,c5]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "pytorch_geometric-1_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import torch  # noqa: E402
+
+PEAK = 8000.0
+
+
+def timed(fn, reps=10, rounds=3):
+    fn()
+    torch.cuda.synchronize()
+    per = []
+    for _ in range(rounds):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(reps):
+            fn()
+        b.record()
+        torch.cuda.synchronize()
+        per.append(a.elapsed_time(b) / reps)
+    return sorted(per)[len(per) // 2]
+
+
+def report(name, desc, E, N, bpe, bpn, ms_main, ms_total, extra=None):
+    alg = E * bpe + N * bpn
+    gbs = alg / (ms_main * 1e-3) / 1e9
+    line = {"config": name, "desc": desc, "num_nodes": N, "num_edges": E,
+            "edges_per_s": E / (ms_total * 1e-3), "main_kernel_ms": ms_main, "aggregate_ms": ms_total,
+            "algorithmic_bytes": alg, "achieved_GBps": gbs, "frac_of_8TBps": gbs / PEAK}
+    if extra:
+        line.update(extra)
+    print(json.dumps(line), flush=True)
+
+
+def c3(dev):
+    from mi355_mp import _lib, ops
+    from mi355_mp.graph import Graph
+    from mi355_mp.graphgen import rmat_edge_index
+    from torch_geometric.nn.conv._structure import gat_loops
+    N, H, C = 1 << 21, 8, 32
+    ei = gat_loops(rmat_edge_index(scale=21, n_samples=30_000_000, seed=1, device=dev), N)
+    graph = Graph(ei, N, N)
+    csr = graph.dst
+    g = torch.Generator(device=dev).manual_seed(2)
+    xw = torch.randn(N, H * C, device=dev, generator=g)
+    att = torch.randn(1, H, 2 * C, device=dev, generator=g) * 0.1
+    bias = torch.randn(H * C, device=dev, generator=g) * 0.1
+    lib = _lib.load()
+    a_src = torch.empty(N, H, device=dev)
+    a_dst = torch.empty(N, H, device=dev)
+    att_c = att.reshape(H, 2 * C).contiguous()
+    out = torch.empty(N, H * C, device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    s = csr.struct("other")
+    sb = lib.mp_gat_slab_bytes(s, H, C)
+    slab = torch.empty(sb, dtype=torch.uint8, device=dev)
+
+    def scores():
+        _lib.check(lib.mp_gat_node_scores_f32(xw.data_ptr(), N, H, C, att_c.data_ptr(), a_src.data_ptr(),
+                                              a_dst.data_ptr(), st), "scores")
+
+    def agg(stages):
+        _lib.check(lib.mp_gat_aggregate_f32(s, xw.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(), H, C, 0.2,
+                                            bias.data_ptr(), out.data_ptr(), H * C, None, slab.data_ptr(), sb,
+                                            stages, st), "gat")
+    scores()
+    ms_main = timed(lambda: agg(_lib.MP_STAGE_MAIN))
+    ms_fix = timed(lambda: agg(_lib.MP_STAGE_FIXUP))
+    ms_scores = timed(scores)
+    E = csr.n_edges
+    report("c3", "RMAT21 GATConv heads=8 C=32, fused leaky_relu+softmax(+1e-16)+aggregate+bias",
+           E, N, 4 * H * C + 4 + 4 * H, 4 * H * C + 4 * H + 4, ms_main, ms_main + ms_fix + ms_scores,
+           {"fixup_ms": ms_fix, "node_scores_ms": ms_scores, "n_split": csr.n_split})
+    # parity spot check against the generic PyG formula on identical inputs (one row block)
+    del graph
+
+
+def c4(dev):
+    from mi355_mp import _lib, ops
+    from mi355_mp.graph import Graph
+    from mi355_mp.graphgen import powerlaw_edge_index
+    N, E, F = 232_965, 114_615_892, 256
+    ei = powerlaw_edge_index(N, E, seed=3, device=dev)
+    graph = Graph(ei, N, N)
+    csr = graph.dst
+    x = torch.randn(N, F, device=dev, generator=torch.Generator(device=dev).manual_seed(3))
+    out = torch.empty(N, F, device=dev)
+    arg = torch.empty(N, F, dtype=torch.int64, device=dev)
+    lib = _lib.load()
+    s = csr.struct("other")
+    red = _lib.MP_REDUCE["max"]
+    sb = lib.mp_aggregate_slab_bytes(s, F, red)
+    slab = torch.empty(sb, dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+
+    def agg(stages):
+        _lib.check(lib.mp_aggregate_f32(s, None, x.data_ptr(), F, F, red, _lib.MP_FLAG_PYG_MASK, None,
+                                        out.data_ptr(), F, arg.data_ptr(), slab.data_ptr(), sb, stages, st),
+                   "max")
+    ms_main = timed(lambda: agg(_lib.MP_STAGE_MAIN))
+    ms_fix = timed(lambda: agg(_lib.MP_STAGE_FIXUP))
+    report("c4", "Reddit-scale power-law, aggr='max' + int64 first-index argmax, PyG -10000 mask",
+           csr.n_edges, N, 4 * F + 4, 4 * F + 8 * F + 4, ms_main, ms_main + ms_fix,
+           {"fixup_ms": ms_fix, "n_split": csr.n_split,
+            "note": "x is 238 MB: it fits the 256 MB Infinity Cache, so gathers are mostly on-die"})
+
+
+def c5(dev):
+    from mi355_mp import _lib, ops
+    from mi355_mp.graph import Graph
+    from mi355_mp.graphgen import powerlaw_edge_index
+    from torch_geometric.nn.conv.gcn_conv import GCNConv
+    N, E, F = 2_449_029, 123_718_280, 256
+    ei = powerlaw_edge_index(N, E, seed=4, device=dev)
+    ei2, norm = GCNConv.norm(ei, N)
+    graph = Graph(ei2, N, N)
+    csr = graph.dst
+    w = csr.to_csr_order(norm)
+    x = torch.randn(N, F, device=dev, generator=torch.Generator(device=dev).manual_seed(4))
+    bias = torch.zeros(F, device=dev)
+    out = torch.empty(N, F, device=dev)
+    slab = torch.empty(_lib.load().mp_aggregate_slab_bytes(csr.struct("other"), F, 0), dtype=torch.uint8,
+                       device=dev)
+
+    def agg(stages):
+        ops._aggregate(csr, "other", x, w, "sum", 0, bias, out=out, stages=stages, slab=slab)
+    ms_main = timed(lambda: agg(_lib.MP_STAGE_MAIN))
+    ms_fix = timed(lambda: agg(_lib.MP_STAGE_FIXUP))
+    report("c5", "ogbn-products-scale power-law GCNConv F=256 on ONE GPU", csr.n_edges, N,
+           4 * F + 8, 4 * F + 4, ms_main, ms_main + ms_fix, {"fixup_ms": ms_fix, "n_split": csr.n_split})
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="c3,c4,c5")
+    args = ap.parse_args()
+    import mi355_mp
+    mi355_mp.load_native()
+    dev = torch.device("cuda", 0)
+    for c in args.configs.split(","):
+        globals()[c](dev)
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -12,6 +12,10 @@ step() {  # name timeout cmd...
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
-step pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout=600 ${PYTEST_ARGS:-}
+if [ -n "${PYTEST_K:-}" ]; then
+  step pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout=600 -k "$PYTEST_K"
+else
+  step pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout=600
+fi
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --steps 20 --warmup 5
