@@ -57,8 +57,16 @@ def setup_dist(n):
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", rank))
-    torch.cuda.set_device(local)
-    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    backend = os.environ.get("MP_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        # rehearsal of the multi-GPU path on a box with fewer GPUs than ranks:
+        # ranks share devices, halo rows are staged through the host
+        local = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local)
+        dist.init_process_group("gloo")
+    else:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return rank, world, local
 
 
@@ -130,7 +138,9 @@ def main():
         from mi355_mp import dist as mdist
         plan = mdist.ShardPlan(ei2, N, rank, world).exchange_requests()
         x_full = torch.randn(N, F_DIM, device=dev, generator=g)
-        x = x_full[plan.lo:plan.hi].contiguous()
+        x_local = plan.local_buffer(F_DIM)
+        x_local[:plan.n_own].copy_(x_full[plan.lo:plan.hi])
+        x = x_local[:plan.n_own]
         del x_full
         lei = plan.local_edge_index
         graph = Graph(lei, plan.n_own, plan.n_local_src, chunk=args.chunk)
@@ -157,8 +167,7 @@ def main():
         if world == 1:
             aggregate(x, out=out_buf)
         else:
-            xl = plan.halo_exchange(x, ops.gather_rows)
-            aggregate(xl, out=out_buf)
+            aggregate(plan.exchange_into(x_local, ops.gather_rows), out=out_buf)
 
     for _ in range(args.warmup):
         step()
@@ -173,7 +182,8 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+        tt = torch.tensor([dt], dtype=torch.float64)
+        tt = tt.to(dev) if dist.get_backend() == "nccl" else tt
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     ms_per_step = dt / args.steps * 1e3
@@ -182,7 +192,7 @@ def main():
     # dominant kernel (main aggregation launch) timed with HIP events on the
     # stream it runs on (torch's current stream): `reps` back-to-back launches
     # between two events (host launch latency amortised), averaged
-    x_src = x if world == 1 else plan.halo_exchange(x, ops.gather_rows)
+    x_src = x if world == 1 else plan.exchange_into(x_local, ops.gather_rows)
     reps = max(args.steps, 10)
 
     def timed(stages, rounds=3):

@@ -24,6 +24,20 @@ import torch
 import torch.distributed as dist
 
 
+def _a2a(out, inp, out_splits=None, in_splits=None, group=None):
+    """all_to_all_single; with the gloo backend (CPU-only collectives: the
+    multi-process rehearsal of the RCCL path) device tensors are staged
+    through host memory."""
+    if out.is_cuda and dist.get_backend(group) == "gloo":
+        o = out.cpu()
+        dist.all_to_all_single(o, inp.cpu(), output_split_sizes=out_splits, input_split_sizes=in_splits,
+                               group=group)
+        out.copy_(o)
+        return out
+    dist.all_to_all_single(out, inp, output_split_sizes=out_splits, input_split_sizes=in_splits, group=group)
+    return out
+
+
 def edge_balanced_cuts(in_degree, parts):
     """Row cut points [0=c_0 <= ... <= c_P = N] with ~equal edges per part."""
     N = in_degree.numel()
@@ -76,23 +90,33 @@ class ShardPlan:
         dev = self.halo_nodes.device
         recv_counts = torch.tensor(self.recv_counts, dtype=torch.int64, device=dev)
         send_counts = torch.empty_like(recv_counts)
-        dist.all_to_all_single(send_counts, recv_counts, group=group)
+        _a2a(send_counts, recv_counts, group=group)
         self.send_counts = send_counts.tolist()
         requests = torch.empty(sum(self.send_counts), dtype=torch.int64, device=dev)
-        dist.all_to_all_single(requests, self.halo_nodes.contiguous(), output_split_sizes=self.send_counts,
-                               input_split_sizes=self.recv_counts, group=group)
+        _a2a(requests, self.halo_nodes.contiguous(), self.send_counts, self.recv_counts, group)
         self.send_idx = requests - self.lo     # rows of my own block that peers need
         return self
 
+    def local_buffer(self, F, dtype=torch.float32, device=None):
+        """[n_own + n_halo, F] buffer: the owner writes rows [:n_own] (e.g. its
+        X W GEMM output), exchange_into() fills the halo rows [n_own:]."""
+        return torch.empty((self.n_local_src, F), dtype=dtype, device=device or self.halo_nodes.device)
+
+    def exchange_into(self, x_local, gather_rows, group=None):
+        """Pack the rows peers requested from x_local[:n_own] (native row
+        gather) and receive this rank's halo rows straight into
+        x_local[n_own:] (one all_to_all_single, no concatenation)."""
+        F = x_local.shape[1]
+        own = x_local[:self.n_own]
+        send = gather_rows(own, self.send_idx) if self.send_idx.numel() else x_local.new_empty((0, F))
+        _a2a(x_local[self.n_own:], send.contiguous(), self.recv_counts, self.send_counts, group)
+        return x_local
+
     def halo_exchange(self, x_own, gather_rows, group=None):
-        """[own rows ; halo rows] for this rank (one all_to_all_single)."""
-        F = x_own.shape[1]
-        send = gather_rows(x_own, self.send_idx) if self.send_idx.numel() else \
-            x_own.new_empty((0, F))
-        halo = x_own.new_empty((self.halo_nodes.numel(), F))
-        dist.all_to_all_single(halo, send.contiguous(), output_split_sizes=self.recv_counts,
-                               input_split_sizes=self.send_counts, group=group)
-        return torch.cat([x_own, halo], dim=0)
+        """[own rows ; halo rows] for this rank (allocating form)."""
+        x_local = self.local_buffer(x_own.shape[1], x_own.dtype, x_own.device)
+        x_local[:self.n_own].copy_(x_own)
+        return self.exchange_into(x_local, gather_rows, group)
 
 
 def sharded_propagate(plan, x_own, local_aggregate, gather_rows, edge_weight=None, group=None):
