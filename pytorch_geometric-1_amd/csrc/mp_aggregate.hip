@@ -31,13 +31,25 @@
 
 // Build-time tuning knobs (A/B-tested in one process by tools/ab_bench.py).
 #ifndef MP_U_VEC4
-#define MP_U_VEC4 8        // x-row loads in flight per wave (VEC=4)
+#define MP_U_VEC4 8        // x-row loads in flight per task (VEC=4, 64-lane tasks)
+#endif
+#ifndef MP_U_NARROW
+#define MP_U_NARROW 12     // x-row loads in flight per task (VEC=4, tasks of < 64 lanes)
 #endif
 #ifndef MP_NT_OUT
 #define MP_NT_OUT 0        // non-temporal output-row stores
 #endif
 #ifndef MP_NT_IDX
 #define MP_NT_IDX 0        // non-temporal col/weight/eid stream loads
+#endif
+#ifndef MP_NT_X
+#define MP_NT_X 0          // non-temporal x-row loads (all rows)
+#endif
+#ifndef MP_FORCE_VEC
+#define MP_FORCE_VEC 0     // 1/2/4: force the lane width (feature tiles of 64*VEC run in turn)
+#endif
+#ifndef MP_COLD_FLAG
+#define MP_COLD_FLAG 0     // col < 0 marks a cold source row: ~col is the row, loaded non-temporal
 #endif
 
 namespace mp {
@@ -395,35 +407,60 @@ __device__ __forceinline__ PRef slab_ref(const AggArgs& p, int64_t s, int f, con
 }
 
 // ---------------------------------------------------------------------------
-// Per-wave slot window: col / weight / eid of 64 consecutive CSR slots held one
-// per lane, the next 64 prefetched.
+// Lane groups.  A wave runs G = 64/L independent merge-path tasks, one per
+// group of L lanes (L = 64: one task per wave, every per-task value is
+// wave-uniform and lives in SGPRs).  A group covers L*VEC features of a row;
+// gridDim.y walks the feature tiles, which the dispatcher runs roughly one
+// after another, so the gathered working set of a pass is L*VEC*4 bytes per
+// row -- narrow tiles keep more hub rows resident in L2.
 // ---------------------------------------------------------------------------
-template <bool W, bool EID>
+template <int L>
+struct Grp {
+  static constexpr int G = 64 / L;
+  static __device__ __forceinline__ int bc(int v, int idx) {
+    if constexpr (L == 64) return readlane(v, idx);
+    else return __shfl(v, idx, L);
+  }
+  static __device__ __forceinline__ float bc(float v, int idx) {
+    if constexpr (L == 64) return readlane(v, idx);
+    else return __shfl(v, idx, L);
+  }
+  static __device__ __forceinline__ int un(int v) {
+    if constexpr (L == 64) return uni(v);
+    else return v;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Per-group slot window: col / weight / eid of L consecutive CSR slots held one
+// per lane, the next L prefetched.
+// ---------------------------------------------------------------------------
+template <bool W, bool EID, int L>
 struct SlotWin {
   int64_t base, limit;
   int col, col_n, eid, eid_n;
   float w, w_n;
 
-  __device__ __forceinline__ void fetch(const AggArgs& p, int64_t b, int lane, int& c, float& wt, int& e) {
-    int64_t k = b + lane;
+  __device__ __forceinline__ void fetch(const AggArgs& p, int64_t b, int gl, int& c, float& wt, int& e) {
+    int64_t k = b + gl;
     bool ok = k < limit;
     c = ok ? ld_stream(p.col + k) : 0;
     if (W) wt = ok ? ld_stream(p.w + k) : 0.f;
     if (EID) e = ok ? ld_stream(p.eid + k) : 0;
   }
-  __device__ __forceinline__ void init(const AggArgs& p, int64_t b, int64_t lim, int lane) {
+  __device__ __forceinline__ void init(const AggArgs& p, int64_t b, int64_t lim, int gl) {
     base = b;
     limit = lim;
-    fetch(p, base, lane, col, w, eid);
-    fetch(p, base + 64, lane, col_n, w_n, eid_n);
+    fetch(p, base, gl, col, w, eid);
+    fetch(p, base + L, gl, col_n, w_n, eid_n);
   }
-  __device__ __forceinline__ void ensure(const AggArgs& p, int64_t e, int lane) {
-    if (e >= base + 64) {  // slots are consumed in order, never skipping a window
-      base += 64;
+  __device__ __forceinline__ void ensure(const AggArgs& p, int64_t e, int gl) {
+    if (e >= base + L) {  // slots are consumed in order, never skipping a window
+      base += L;
       col = col_n;
       w = w_n;
       eid = eid_n;
-      fetch(p, base + 64, lane, col_n, w_n, eid_n);
+      fetch(p, base + L, gl, col_n, w_n, eid_n);
     }
   }
 };
@@ -431,31 +468,39 @@ struct SlotWin {
 // Process CSR slots [s, t) of the current (partial) row.
 // All U row loads are issued unconditionally (indices past the segment are
 // clamped to its last slot, inactive lanes read feature 0) so no load sits
-// under an exec mask; only the wave-uniform consume loop is bounded by n.
-// Row address = uniform base (SGPR pair) + one shared 32-bit lane offset, so
-// the loads use the saddr form and U rows cost U*VEC data VGPRs only.
-template <class Red, int VEC, int U>
-__device__ __forceinline__ void run_slots(Red& red, const AggArgs& p, SlotWin<Red::kW, Red::kEid>& win,
-                                          int64_t s, int64_t t, uint32_t foff, int lane) {
+// under an exec mask; only the group-uniform consume loop is bounded by n.
+// For L = 64 the row address is a uniform base (SGPR pair) + one shared
+// 32-bit lane offset, so U rows cost U*VEC data VGPRs only.
+template <class Red, int VEC, int U, int L>
+__device__ __forceinline__ void run_slots(Red& red, const AggArgs& p, SlotWin<Red::kW, Red::kEid, L>& win,
+                                          int64_t s, int64_t t, uint32_t foff, int gl) {
+  using GR = Grp<L>;
   const char* xb = reinterpret_cast<const char*>(p.x);
   const int64_t ldxb = p.ldx * 4;
   int64_t e = s;
   while (e < t) {
-    win.ensure(p, e, lane);
+    win.ensure(p, e, gl);
     const int off = (int)(e - win.base);
     int64_t rem = t - e;
-    int n = 64 - off;
+    int n = L - off;
     if (rem < n) n = (int)rem;
     if (n > U) n = U;
-    n = uni(n);
+    n = GR::un(n);
     Frag<VEC> v[U];
     float as[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int uu = u < n ? u : n - 1;
-      const int c = readlane(win.col, off + uu);
-      const char* rowp = xb + (int64_t)c * ldxb;
-      v[u] = load_frag<VEC>(reinterpret_cast<const float*>(rowp + foff));
+      int c = GR::bc(win.col, off + uu);
+      if constexpr (MP_COLD_FLAG) {
+        const bool cold = c < 0;
+        c = c & 0x7fffffff;
+        const float* src = reinterpret_cast<const float*>(xb + (int64_t)c * ldxb + foff);
+        v[u] = cold ? load_frag_nt<VEC>(src) : load_frag<VEC>(src);
+      } else {
+        const float* src = reinterpret_cast<const float*>(xb + (int64_t)c * ldxb + foff);
+        v[u] = MP_NT_X ? load_frag_nt<VEC>(src) : load_frag<VEC>(src);
+      }
       if constexpr (Red::kGat) as[u] = p.a_src[(int64_t)c * p.H + red.h];
     }
 #pragma unroll
@@ -464,8 +509,8 @@ __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p, SlotWin<Re
         if constexpr (Red::kGat) {
           red.consume_gat(p, v[u], as[u]);
         } else {
-          const float wt = Red::kW ? readlane(win.w, off + u) : 1.f;
-          const int ei = Red::kEid ? readlane(win.eid, off + u) : 0;
+          const float wt = Red::kW ? GR::bc(win.w, off + u) : 1.f;
+          const int ei = Red::kEid ? GR::bc(win.eid, off + u) : 0;
           red.consume(v[u], wt, ei, 0.f);
         }
       }
@@ -474,51 +519,54 @@ __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p, SlotWin<Re
   }
 }
 
-template <class Red, int VEC, int U>
+template <class Red, int VEC, int U, int L>
 __global__ __launch_bounds__(kBlock) void k_agg_main(AggArgs p) {
+  using GR = Grp<L>;
   const int lane = lane_id();
-  const int w = uni((int)blockIdx.x * kWavesPerBlock + (int)(threadIdx.x >> 6));
+  const int gl = lane & (L - 1);
+  const int wave = (int)blockIdx.x * kWavesPerBlock + (int)(threadIdx.x >> 6);
+  const int w = GR::un(wave * GR::G + lane / L);  // this group's task
   if (w >= p.n_waves) return;
-  const int f = (int)blockIdx.y * 64 * VEC + lane * VEC;
+  const int f = (int)blockIdx.y * L * VEC + gl * VEC;
   const bool act = f < p.F;
   const uint32_t foff = (uint32_t)(act ? f : 0) * 4u;
 
-  const int r_first = uni(p.wave_row[w]);
-  const int r_last = uni(p.wave_row[w + 1]);
-  const int64_t e_begin = uni(p.wave_slot[w]);
-  const int64_t e_end = uni(p.wave_slot[w + 1]);
+  const int r_first = GR::un(p.wave_row[w]);
+  const int r_last = GR::un(p.wave_row[w + 1]);
+  const int64_t e_begin = GR::un(p.wave_slot[w]);
+  const int64_t e_end = GR::un(p.wave_slot[w + 1]);
 
   Red red(p, f, act);
-  SlotWin<Red::kW, Red::kEid> win;
-  win.init(p, e_begin, e_end, lane);
+  SlotWin<Red::kW, Red::kEid, L> win;
+  win.init(p, e_begin, e_end, gl);
 
-  // rowptr window: rp = rowptr[rbase + lane]
+  // rowptr window: rp = rowptr[rbase + gl]
   int rbase = r_first;
-  int rp = (rbase + lane <= p.n_rows) ? p.rowptr[rbase + lane] : 0;
+  int rp = (rbase + gl <= p.n_rows) ? p.rowptr[rbase + gl] : 0;
 
   // continuation of the row owned by an earlier task
   {
-    const int64_t ce = readlane(rp, 0);  // rowptr[r_first] (== n_edges when r_first == n_rows)
+    const int64_t ce = GR::bc(rp, 0);  // rowptr[r_first] (== n_edges when r_first == n_rows)
     if (e_begin < ce) {
       red.begin(p, r_first - 1, false, f, act);
-      run_slots<Red, VEC, U>(red, p, win, e_begin, ce < e_end ? ce : e_end, foff, lane);
+      run_slots<Red, VEC, U, L>(red, p, win, e_begin, ce < e_end ? ce : e_end, foff, gl);
       if (act) red.save(slab_ref(p, 2 * (int64_t)w, f, red), Red::kGat && (f % p.C == 0));
     }
   }
   // rows owned by this task
   for (int r = r_first; r < r_last; ++r) {
-    if (r + 1 - rbase > 63) {
+    if (r + 1 - rbase > L - 1) {
       rbase = r;
-      rp = (rbase + lane <= p.n_rows) ? p.rowptr[rbase + lane] : 0;
+      rp = (rbase + gl <= p.n_rows) ? p.rowptr[rbase + gl] : 0;
     }
-    const int64_t rs = readlane(rp, r - rbase);
-    const int64_t re = readlane(rp, r - rbase + 1);
+    const int64_t rs = GR::bc(rp, r - rbase);
+    const int64_t re = GR::bc(rp, r - rbase + 1);
     red.begin(p, r, true, f, act);
     if (re <= e_end) {
-      run_slots<Red, VEC, U>(red, p, win, rs, re, foff, lane);
+      run_slots<Red, VEC, U, L>(red, p, win, rs, re, foff, gl);
       red.finish(p, r, re - rs, f, act);
     } else {
-      run_slots<Red, VEC, U>(red, p, win, rs, e_end, foff, lane);
+      run_slots<Red, VEC, U, L>(red, p, win, rs, e_end, foff, gl);
       if (act) red.save(slab_ref(p, 2 * (int64_t)w + 1, f, red), Red::kGat && (f % p.C == 0));
     }
   }
@@ -586,48 +634,87 @@ __global__ __launch_bounds__(kBlock) void k_agg_fixup(AggArgs p) {
 // host side
 // ---------------------------------------------------------------------------
 
-static int pick_vec(int F, int64_t ldx, const void* x, int64_t ldo, const void* out) {
+struct Shape {
+  int vec, lanes;
+};
+
+#ifndef MP_WIDE_LANES
+#define MP_WIDE_LANES 32   // lanes per task for rows of >= 256 features (A/B: 32 beats 64 by ~9%)
+#endif
+
+static int next_pow2(int v) {
+  int r = 1;
+  while (r < v) r <<= 1;
+  return r;
+}
+
+// VEC = widest aligned per-lane vector; L = lanes per task: enough to cover
+// the row (small F packs several tasks per wave), at most 64.
+static Shape pick_shape(int F, int64_t ldx, const void* x, int64_t ldo, const void* out) {
   auto aligned = [](const void* ptr, int64_t ld, int v) {
     return ((uintptr_t)ptr % (4 * v) == 0) && (ld % v == 0);
   };
-  if (F % 4 == 0 && F > 128 && aligned(x, ldx, 4) && aligned(out, ldo, 4)) return 4;
-  if (F % 2 == 0 && F > 64 && aligned(x, ldx, 2) && aligned(out, ldo, 2)) return 2;
-  return 1;
+  int vec = 1;
+  if (MP_FORCE_VEC && F % MP_FORCE_VEC == 0 && aligned(x, ldx, MP_FORCE_VEC) && aligned(out, ldo, MP_FORCE_VEC))
+    vec = MP_FORCE_VEC;
+  else if (F % 4 == 0 && aligned(x, ldx, 4) && aligned(out, ldo, 4)) vec = 4;
+  else if (F % 2 == 0 && F > 64 && aligned(x, ldx, 2) && aligned(out, ldo, 2)) vec = 2;
+  int lanes = 64;
+  if (vec == 4) {
+    int need = next_pow2((F + 3) / 4);
+    lanes = need < 4 ? 4 : (need > 64 ? 64 : need);
+    if (F >= 256) lanes = MP_WIDE_LANES;
+  }
+  return {vec, lanes};
 }
 
-template <class Red, int VEC>
-static int launch(const AggArgs& a, int stages, hipStream_t s) {
-  constexpr int U = VEC == 4 ? MP_U_VEC4 : 16;
-  const int ftiles = (int)ceil_div(a.F, 64 * VEC);
+template <class Red, int VEC, int L>
+static int launch_l(const AggArgs& a, int stages, hipStream_t s) {
+  constexpr int U = VEC == 4 ? (L == 64 ? MP_U_VEC4 : MP_U_NARROW) : 16;
+  const int ftiles = (int)ceil_div(a.F, L * VEC);
   if (stages & MP_STAGE_MAIN) {
-    dim3 grid((unsigned)ceil_div(a.n_waves, kWavesPerBlock), (unsigned)ftiles);
-    hipLaunchKernelGGL((k_agg_main<Red, VEC, U>), grid, dim3(kBlock), 0, s, a);
+    dim3 grid((unsigned)ceil_div(a.n_waves, kWavesPerBlock * (64 / L)), (unsigned)ftiles);
+    hipLaunchKernelGGL((k_agg_main<Red, VEC, U, L>), grid, dim3(kBlock), 0, s, a);
     MP_CHECK_LAUNCH();
   }
   if ((stages & MP_STAGE_FIXUP) && a.n_split > 0) {
-    dim3 grid((unsigned)a.n_split, (unsigned)ftiles);
+    dim3 grid((unsigned)a.n_split, (unsigned)ceil_div(a.F, 64 * VEC));
     hipLaunchKernelGGL((k_agg_fixup<Red, VEC>), grid, dim3(kBlock), 0, s, a);
     MP_CHECK_LAUNCH();
   }
   return MP_OK;
 }
 
+template <class Red, int VEC>
+static int launch(const AggArgs& a, int stages, hipStream_t s, int lanes = 64) {
+  if constexpr (VEC == 4) {
+    switch (lanes) {
+      case 4: return launch_l<Red, 4, 4>(a, stages, s);
+      case 8: return launch_l<Red, 4, 8>(a, stages, s);
+      case 16: return launch_l<Red, 4, 16>(a, stages, s);
+      case 32: return launch_l<Red, 4, 32>(a, stages, s);
+      default: break;
+    }
+  }
+  return launch_l<Red, VEC, 64>(a, stages, s);
+}
+
 template <int VEC>
-static int dispatch_reduce(const AggArgs& a, int reduce, int stages, hipStream_t s) {
+static int dispatch_reduce(const AggArgs& a, int reduce, int stages, hipStream_t s, int L) {
   const bool hw = a.w != nullptr;
   switch (reduce) {
     case MP_REDUCE_SUM:
-      return hw ? launch<SumRed<VEC, true, false>, VEC>(a, stages, s)
-                : launch<SumRed<VEC, false, false>, VEC>(a, stages, s);
+      return hw ? launch<SumRed<VEC, true, false>, VEC>(a, stages, s, L)
+                : launch<SumRed<VEC, false, false>, VEC>(a, stages, s, L);
     case MP_REDUCE_MEAN:
-      return hw ? launch<SumRed<VEC, true, true>, VEC>(a, stages, s)
-                : launch<SumRed<VEC, false, true>, VEC>(a, stages, s);
+      return hw ? launch<SumRed<VEC, true, true>, VEC>(a, stages, s, L)
+                : launch<SumRed<VEC, false, true>, VEC>(a, stages, s, L);
     case MP_REDUCE_MAX:
-      return hw ? launch<ArgRed<VEC, true, true>, VEC>(a, stages, s)
-                : launch<ArgRed<VEC, false, true>, VEC>(a, stages, s);
+      return hw ? launch<ArgRed<VEC, true, true>, VEC>(a, stages, s, L)
+                : launch<ArgRed<VEC, false, true>, VEC>(a, stages, s, L);
     case MP_REDUCE_MIN:
-      return hw ? launch<ArgRed<VEC, true, false>, VEC>(a, stages, s)
-                : launch<ArgRed<VEC, false, false>, VEC>(a, stages, s);
+      return hw ? launch<ArgRed<VEC, true, false>, VEC>(a, stages, s, L)
+                : launch<ArgRed<VEC, false, false>, VEC>(a, stages, s, L);
   }
   set_error("mp_aggregate_f32: unknown reduce %d", reduce);
   return MP_ERR_ARG;
@@ -702,10 +789,11 @@ int mp_aggregate_f32(const mp_csr* g, const float* w, const float* x, int64_t ld
   a.slab_v = (float*)slab;
   a.slab_a = is_arg ? (int32_t*)((char*)slab + v) : nullptr;
   hipStream_t s = as_stream(stream);
-  switch (pick_vec(F, ldx, x, ldo, out)) {
-    case 4: return dispatch_reduce<4>(a, reduce, stages, s);
-    case 2: return dispatch_reduce<2>(a, reduce, stages, s);
-    default: return dispatch_reduce<1>(a, reduce, stages, s);
+  const Shape sh = pick_shape(F, ldx, x, ldo, out);
+  switch (sh.vec) {
+    case 4: return dispatch_reduce<4>(a, reduce, stages, s, sh.lanes);
+    case 2: return dispatch_reduce<2>(a, reduce, stages, s, 64);
+    default: return dispatch_reduce<1>(a, reduce, stages, s, 64);
   }
 }
 
@@ -748,7 +836,8 @@ int mp_gat_aggregate_f32(const mp_csr* g, const float* xw, const float* a_src, c
   a.slab_v = (float*)slab;
   a.slab_s = (float*)((char*)slab + v);
   hipStream_t s = as_stream(stream);
-  int vec = pick_vec(F, F, xw, ldo, out);
+  int vec = pick_shape(F, F, xw, ldo, out).vec;
+  if (vec == 2 && F <= 64) vec = 1;
   while (vec > 1 && C % vec != 0) vec >>= 1;  // a lane's features must share a head
   switch (vec) {
     case 4: return launch<GatRed<4>, 4>(a, stages, s);

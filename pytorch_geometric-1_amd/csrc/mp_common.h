@@ -83,6 +83,21 @@ __device__ __forceinline__ void store_frag(float* p, const Frag<VEC>& f) {
   }
 }
 
+template <int VEC>
+__device__ __forceinline__ Frag<VEC> load_frag_nt(const float* p) {
+  Frag<VEC> r;
+  if constexpr (VEC == 4) {
+    f32x4 t = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+    r.v[0] = t.x; r.v[1] = t.y; r.v[2] = t.z; r.v[3] = t.w;
+  } else if constexpr (VEC == 2) {
+    f32x2 t = __builtin_nontemporal_load(reinterpret_cast<const f32x2*>(p));
+    r.v[0] = t.x; r.v[1] = t.y;
+  } else {
+    r.v[0] = __builtin_nontemporal_load(p);
+  }
+  return r;
+}
+
 // Non-temporal store of a fragment (output rows are written once and never
 // re-read by the kernel; keeping them out of L2/MALL leaves room for the
 // gathered x rows).
