@@ -45,6 +45,18 @@
 #ifndef MP_NT_X
 #define MP_NT_X 0          // non-temporal x-row loads (all rows)
 #endif
+#ifndef MP_GAT_FAST_EXP
+#define MP_GAT_FAST_EXP 0  // 1: softmax exponentials via __expf (v_exp_f32)
+#endif
+
+__device__ __forceinline__ float gat_exp(float v) {
+  if constexpr (MP_GAT_FAST_EXP) return __expf(v);
+  else return expf(v);
+}
+
+#ifndef MP_GAT_LANES
+#define MP_GAT_LANES 64    // lanes per GAT task for H*C >= 256
+#endif
 #ifndef MP_FORCE_VEC
 #define MP_FORCE_VEC 0     // 1/2/4: force the lane width (feature tiles of 64*VEC run in turn)
 #endif
@@ -328,8 +340,8 @@ struct GatRed {
     float a = as + ad;
     a = a > 0.f ? a : a * p.slope;  // F.leaky_relu
     float mn = fmaxf(m, a);
-    float sc = expf(m - mn);
-    float pe = expf(a - mn);
+    float sc = gat_exp(m - mn);
+    float pe = gat_exp(a - mn);
     s = s * sc + pe;
 #pragma unroll
     for (int k = 0; k < VEC; ++k) acc[k] = acc[k] * sc + pe * v.v[k];
@@ -840,7 +852,7 @@ int mp_gat_aggregate_f32(const mp_csr* g, const float* xw, const float* a_src, c
   if (vec == 2 && F <= 64) vec = 1;
   while (vec > 1 && C % vec != 0) vec >>= 1;  // a lane's features must share a head
   switch (vec) {
-    case 4: return launch<GatRed<4>, 4>(a, stages, s);
+    case 4: return launch<GatRed<4>, 4>(a, stages, s, F >= 256 ? MP_GAT_LANES : 64);
     case 2: return launch<GatRed<2>, 2>(a, stages, s);
     default: return launch<GatRed<1>, 1>(a, stages, s);
   }

@@ -473,3 +473,83 @@ def test_full_size_rmat_gcn_properties():
     o2 = ops.fused_propagate(graph, x2, ei2, norm, "sum")
     o12 = ops.fused_propagate(graph, 2 * x1 - x2, ei2, norm, "sum")
     assert (o12 - (2 * o1 - o2)).abs().max().item() < 1e-4
+
+
+# --------------------------------------------------------------------------
+# examples/gcn.py flow end to end (training through the drop-in API)
+# --------------------------------------------------------------------------
+
+def _cora_training(model_fn, epochs=60):
+    from mi355_mp.graphgen import cora_like
+    torch.manual_seed(0)
+    d = cora_like(seed=0)
+    x, ei, y = d["x"].to(DEV), d["edge_index"].to(DEV), d["y"].to(DEV)
+    tm = d["train_mask"].to(DEV)
+    model = model_fn(x.shape[1], d["num_classes"]).to(DEV)
+    opt = torch.optim.Adam(model.parameters(), lr=0.01, weight_decay=5e-4)
+    losses = []
+    for _ in range(epochs):
+        model.train()
+        opt.zero_grad()
+        out = model(x, ei)
+        loss = torch.nn.functional.nll_loss(out[tm], y[tm])
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    return losses
+
+
+def test_examples_gcn_training_flow():
+    from torch_geometric.nn import GCNConv
+
+    class Net(torch.nn.Module):  # examples/gcn.py:15-28
+        def __init__(self, f, k):
+            super(Net, self).__init__()
+            self.conv1 = GCNConv(f, 16, cached=True)
+            self.conv2 = GCNConv(16, k, cached=True)
+
+        def forward(self, x, ei):
+            x = torch.relu(self.conv1(x, ei))
+            x = torch.nn.functional.dropout(x, training=self.training)
+            return torch.log_softmax(self.conv2(x, ei), dim=1)
+
+    losses = _cora_training(Net)
+    assert all(np.isfinite(losses)) and losses[-1] < 0.5 * losses[0]
+
+
+def test_gat_training_flow():
+    from torch_geometric.nn import GATConv
+
+    class Net(torch.nn.Module):  # ConvexPruning.py:209-224 style
+        def __init__(self, f, k):
+            super(Net, self).__init__()
+            self.conv1 = GATConv(f, 8, heads=4)
+            self.conv2 = GATConv(32, k, heads=1, concat=False)
+
+        def forward(self, x, ei):
+            x = torch.nn.functional.elu(self.conv1(x, ei))
+            return torch.log_softmax(self.conv2(x, ei), dim=1)
+
+    losses = _cora_training(Net, epochs=40)
+    assert all(np.isfinite(losses)) and losses[-1] < 0.7 * losses[0]
+
+
+@pytest.mark.parametrize("F", [4, 8, 16, 32, 64, 100, 128])
+def test_small_feature_widths_lane_groups(F):
+    """F <= 128 packs several merge-path tasks per wave (L = F/4 lanes)."""
+    _, ops, _, Graph, pl = _mods()
+    N, E = 800, 15000
+    ei = pl(N, E, seed=F + 100)
+    g = torch.Generator().manual_seed(F)
+    x = torch.randn(N, F, generator=g)
+    w = torch.rand(E, generator=g)
+    graph = Graph(ei.to(DEV), N, N, chunk=64)
+    out = ops.fused_propagate(graph, x.to(DEV), ei.to(DEV), w.to(DEV), "sum").cpu()
+    want = S.gather_sum(x, ei[0], ei[1], w, N)
+    _bound_ok(out, want, S.gather_sum(x.abs(), ei[0], ei[1], w, N))
+    split = set(_split_rows(graph.dst))
+    whole = torch.tensor([r for r in range(N) if r not in split], dtype=torch.long)
+    assert torch.equal(out[whole], want[whole])
+    mx, am = ops.segment_reduce(x.to(DEV)[ei[0].to(DEV)], ei[1].to(DEV), N, "max")
+    wm, wa = S.scatter_max(x[ei[0]], ei[1], N)
+    assert torch.equal(mx.cpu(), wm) and torch.equal(am.cpu(), wa)
