@@ -262,7 +262,7 @@ def main():
                        else "single GPU", "chunk": args.chunk},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_agg_main<SumRed<4,true,false>,4,8>",
+                         "kernel": "k_agg_main<SumRed<4,true,false>,VEC=4,U=12,L=32>",
                          "algorithmic_bytes_per_launch": alg_bytes,
                          "avg_launch_ms": main_avg, "median_launch_ms": main_ms[len(main_ms) // 2],
                          "fixup_avg_ms": fix_avg},

@@ -483,7 +483,10 @@ def _cora_training(model_fn, epochs=60):
     from mi355_mp.graphgen import cora_like
     torch.manual_seed(0)
     d = cora_like(seed=0)
-    x, ei, y = d["x"].to(DEV), d["edge_index"].to(DEV), d["y"].to(DEV)
+    x, ei = d["x"].to(DEV), d["edge_index"].to(DEV)
+    # learnable labels: a random linear function of the features
+    R = torch.randn(x.shape[1], d["num_classes"], generator=torch.Generator().manual_seed(1)).to(DEV)
+    y = (x @ R).argmax(1)
     tm = d["train_mask"].to(DEV)
     model = model_fn(x.shape[1], d["num_classes"]).to(DEV)
     opt = torch.optim.Adam(model.parameters(), lr=0.01, weight_decay=5e-4)
@@ -500,21 +503,42 @@ def _cora_training(model_fn, epochs=60):
 
 
 def test_examples_gcn_training_flow():
+    """examples/gcn.py:15-40 (2-layer GCNConv(cached=True), Adam lr 0.01 wd 5e-4,
+    nll_loss) trained on the engine and, from the same initial weights, on the
+    float64 CPU oracle: the loss curves must agree."""
     from torch_geometric.nn import GCNConv
-
-    class Net(torch.nn.Module):  # examples/gcn.py:15-28
-        def __init__(self, f, k):
-            super(Net, self).__init__()
-            self.conv1 = GCNConv(f, 16, cached=True)
-            self.conv2 = GCNConv(16, k, cached=True)
-
-        def forward(self, x, ei):
-            x = torch.relu(self.conv1(x, ei))
-            x = torch.nn.functional.dropout(x, training=self.training)
-            return torch.log_softmax(self.conv2(x, ei), dim=1)
-
-    losses = _cora_training(Net)
-    assert all(np.isfinite(losses)) and losses[-1] < 0.5 * losses[0]
+    from mi355_mp.graphgen import cora_like
+    d = cora_like(seed=0)
+    x, ei, y, tm = d["x"], d["edge_index"], d["y"], d["train_mask"]
+    K = d["num_classes"]
+    torch.manual_seed(0)
+    c1, c2 = GCNConv(x.shape[1], 16, cached=True), GCNConv(16, K, cached=True)
+    with torch.no_grad():
+        c1.bias.normal_(0, 0.1), c2.bias.normal_(0, 0.1)
+    ref = [p.detach().double().clone().requires_grad_(True) for p in (c1.weight, c1.bias, c2.weight, c2.bias)]
+    c1, c2 = c1.to(DEV), c2.to(DEV)
+    params = list(c1.parameters()) + list(c2.parameters())
+    opt = torch.optim.Adam(params, lr=0.01, weight_decay=5e-4)
+    opt_ref = torch.optim.Adam(ref, lr=0.01, weight_decay=5e-4)
+    xd, eid, yd, tmd = x.to(DEV), ei.to(DEV), y.to(DEV), tm.to(DEV)
+    x64 = x.double()
+    gpu, cpu = [], []
+    for _ in range(30):
+        opt.zero_grad()
+        out = torch.log_softmax(c2(torch.relu(c1(xd, eid)), eid), dim=1)
+        loss = torch.nn.functional.nll_loss(out[tmd], yd[tmd])
+        loss.backward()
+        opt.step()
+        gpu.append(loss.item())
+        opt_ref.zero_grad()
+        h = torch.relu(P.gcn_conv(x64, ei, ref[0], ref[1]))
+        o = torch.log_softmax(P.gcn_conv(h, ei, ref[2], ref[3]), dim=1)
+        lr_ = torch.nn.functional.nll_loss(o[tm], y[tm])
+        lr_.backward()
+        opt_ref.step()
+        cpu.append(lr_.item())
+    assert np.allclose(gpu, cpu, rtol=1e-4, atol=1e-5), (gpu[-3:], cpu[-3:])
+    assert gpu[-1] < gpu[0]
 
 
 def test_gat_training_flow():

@@ -15,7 +15,7 @@ import os
 import shutil
 import sys
 
-KERNEL = "k_agg_main<mp::SumRed<4, true, false>, 4, 8>"
+KERNEL = "k_agg_main<mp::SumRed<4, true, false>, 4, 12, 32>"
 
 
 def per_launch(path, counter):
