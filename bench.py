@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-edges", type=int, default=16_000_000)
     ap.add_argument("--chunk", type=int, default=256)
+    ap.add_argument("--no-overlap", action="store_true", help="N>1: exchange, then aggregate (no overlap)")
     return ap.parse_args()
 
 
@@ -146,6 +147,7 @@ def main():
         graph = Graph(lei, plan.n_own, plan.n_local_src, chunk=args.chunk)
         csr = graph.dst
         w_csr = csr.to_csr_order(norm[plan.edge_pos])
+        overlap = mdist.OverlappedAggregation(plan, norm, chunk=args.chunk)
         n_rows = plan.n_own
         E_local = lei.shape[1]
     torch.cuda.synchronize()
@@ -166,8 +168,10 @@ def main():
     def step():
         if world == 1:
             aggregate(x, out=out_buf)
-        else:
+        elif args.no_overlap:
             aggregate(plan.exchange_into(x_local, ops.gather_rows), out=out_buf)
+        else:
+            overlap.step(x_local, out_buf, bias)
 
     for _ in range(args.warmup):
         step()
@@ -270,6 +274,9 @@ def main():
             "extra": {"gemm_xW_ms": gemm_ms, "layer_ms_est": gemm_ms + main_avg + fix_avg,
                       "one_time_build_s": t_build, "graph_gen_s": t_gen,
                       "edges_local_rank0": E_local, "n_split_rows": csr.n_split,
+                      "halo_rows_rank0": (plan.n_local_src - plan.n_own) if world > 1 else 0,
+                      "interior_edges_rank0": overlap.n_interior if world > 1 else E_local,
+                      "overlap": world > 1 and not args.no_overlap,
                       "n_wave_tasks": csr.n_waves,
                       "agg_only_GBps_incl_fixup": alg_bytes / ((main_avg + fix_avg) * 1e-3) / 1e9},
         }

@@ -67,6 +67,8 @@ extern "C" {
  *   wave_slot[n_waves+1]  first CSR slot processed by task w
  *   split_waves[n_split]  for each row whose slots span several tasks, the
  *                         last task touching it (fix-up list)
+ *   n_cols                number of rows of the gathered tensor (x, or the
+ *                         messages when col == eid)
  */
 typedef struct mp_csr {
   const int32_t* rowptr;
@@ -80,7 +82,7 @@ typedef struct mp_csr {
   int32_t chunk;
   int32_t n_waves;
   int32_t n_split;
-  int32_t reserved;
+  int32_t n_cols;   /* rows of the gathered x (bounds the 32-bit buffer offsets) */
 } mp_csr;
 
 const char* mp_last_error(void);

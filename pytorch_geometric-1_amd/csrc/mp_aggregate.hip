@@ -45,6 +45,9 @@
 #ifndef MP_NT_X
 #define MP_NT_X 0          // non-temporal x-row loads (all rows)
 #endif
+#ifndef MP_BUF_X
+#define MP_BUF_X 0         // x rows through one buffer resource (32-bit offsets) when x < 4 GB
+#endif
 #ifndef MP_GAT_FAST_EXP
 #define MP_GAT_FAST_EXP 0  // 1: softmax exponentials via __expf (v_exp_f32)
 #endif
@@ -95,6 +98,8 @@ struct AggArgs {
   int32_t n_waves;
   int32_t n_split;
   int32_t F;
+  int32_t n_cols;
+  uint32_t x_bytes;  // extent of x for the buffer path (0: not used)
   // features
   const float* w;
   const float* x;
@@ -483,12 +488,14 @@ struct SlotWin {
 // under an exec mask; only the group-uniform consume loop is bounded by n.
 // For L = 64 the row address is a uniform base (SGPR pair) + one shared
 // 32-bit lane offset, so U rows cost U*VEC data VGPRs only.
-template <class Red, int VEC, int U, int L>
+template <class Red, int VEC, int U, int L, bool BUF>
 __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p, SlotWin<Red::kW, Red::kEid, L>& win,
                                           int64_t s, int64_t t, uint32_t foff, int gl) {
   using GR = Grp<L>;
   const char* xb = reinterpret_cast<const char*>(p.x);
   const int64_t ldxb = p.ldx * 4;
+  [[maybe_unused]] __amdgpu_buffer_rsrc_t xr;
+  if constexpr (BUF) xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
   int64_t e = s;
   while (e < t) {
     win.ensure(p, e, gl);
@@ -509,6 +516,8 @@ __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p, SlotWin<Re
         c = c & 0x7fffffff;
         const float* src = reinterpret_cast<const float*>(xb + (int64_t)c * ldxb + foff);
         v[u] = cold ? load_frag_nt<VEC>(src) : load_frag<VEC>(src);
+      } else if constexpr (BUF) {
+        v[u] = load_frag_buf<VEC>(xr, (uint32_t)c * (uint32_t)ldxb + foff);
       } else {
         const float* src = reinterpret_cast<const float*>(xb + (int64_t)c * ldxb + foff);
         v[u] = MP_NT_X ? load_frag_nt<VEC>(src) : load_frag<VEC>(src);
@@ -531,7 +540,7 @@ __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p, SlotWin<Re
   }
 }
 
-template <class Red, int VEC, int U, int L>
+template <class Red, int VEC, int U, int L, bool BUF>
 __global__ __launch_bounds__(kBlock) void k_agg_main(AggArgs p) {
   using GR = Grp<L>;
   const int lane = lane_id();
@@ -561,7 +570,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_main(AggArgs p) {
     const int64_t ce = GR::bc(rp, 0);  // rowptr[r_first] (== n_edges when r_first == n_rows)
     if (e_begin < ce) {
       red.begin(p, r_first - 1, false, f, act);
-      run_slots<Red, VEC, U, L>(red, p, win, e_begin, ce < e_end ? ce : e_end, foff, gl);
+      run_slots<Red, VEC, U, L, BUF>(red, p, win, e_begin, ce < e_end ? ce : e_end, foff, gl);
       if (act) red.save(slab_ref(p, 2 * (int64_t)w, f, red), Red::kGat && (f % p.C == 0));
     }
   }
@@ -575,10 +584,10 @@ __global__ __launch_bounds__(kBlock) void k_agg_main(AggArgs p) {
     const int64_t re = GR::bc(rp, r - rbase + 1);
     red.begin(p, r, true, f, act);
     if (re <= e_end) {
-      run_slots<Red, VEC, U, L>(red, p, win, rs, re, foff, gl);
+      run_slots<Red, VEC, U, L, BUF>(red, p, win, rs, re, foff, gl);
       red.finish(p, r, re - rs, f, act);
     } else {
-      run_slots<Red, VEC, U, L>(red, p, win, rs, e_end, foff, gl);
+      run_slots<Red, VEC, U, L, BUF>(red, p, win, rs, e_end, foff, gl);
       if (act) red.save(slab_ref(p, 2 * (int64_t)w + 1, f, red), Red::kGat && (f % p.C == 0));
     }
   }
@@ -686,7 +695,15 @@ static int launch_l(const AggArgs& a, int stages, hipStream_t s) {
   const int ftiles = (int)ceil_div(a.F, L * VEC);
   if (stages & MP_STAGE_MAIN) {
     dim3 grid((unsigned)ceil_div(a.n_waves, kWavesPerBlock * (64 / L)), (unsigned)ftiles);
-    hipLaunchKernelGGL((k_agg_main<Red, VEC, U, L>), grid, dim3(kBlock), 0, s, a);
+    // 32-bit buffer offsets when every gathered byte lies below 4 GiB
+    const int64_t xb = (int64_t)a.n_cols * a.ldx * 4;
+    if (MP_BUF_X && a.n_cols > 0 && xb <= (int64_t)0xFFFFFFF0) {
+      AggArgs b = a;
+      b.x_bytes = (uint32_t)xb;
+      hipLaunchKernelGGL((k_agg_main<Red, VEC, U, L, MP_BUF_X != 0>), grid, dim3(kBlock), 0, s, b);
+    } else {
+      hipLaunchKernelGGL((k_agg_main<Red, VEC, U, L, false>), grid, dim3(kBlock), 0, s, a);
+    }
     MP_CHECK_LAUNCH();
   }
   if ((stages & MP_STAGE_FIXUP) && a.n_split > 0) {
@@ -755,6 +772,7 @@ static void fill_graph(AggArgs& a, const mp_csr* g) {
   a.chunk = g->chunk;
   a.n_waves = g->n_waves;
   a.n_split = g->n_split;
+  a.n_cols = g->n_cols;
 }
 
 }  // namespace mp

@@ -128,3 +128,56 @@ def sharded_propagate(plan, x_own, local_aggregate, gather_rows, edge_weight=Non
     x_local = plan.halo_exchange(x_own, gather_rows, group)
     w = edge_weight[plan.edge_pos] if edge_weight is not None else None
     return local_aggregate(x_local, plan.local_edge_index, plan.n_own, plan.n_local_src, w)
+
+
+class OverlappedAggregation:
+    """GCN-style sharded aggregation with the halo exchange hidden behind the
+    interior edges.
+
+    The rank's in-edges split into interior edges (source owned by this rank)
+    and boundary edges (source in the halo), each a cached CSR in global edge
+    order.  One step:
+      1. pack the rows peers asked for (native row gather),
+      2. start the all_to_all (RCCL runs on its own stream),
+      3. aggregate the interior edges into `out` meanwhile,
+      4. wait for the halo, then aggregate the boundary edges on top of `out`
+         (MP_FLAG_INIT_FROM_OUT) and add the bias once.
+    A row's sum is (interior part) + (boundary part, in order): within the
+    1e-5 bound of the single-GPU order, not bit-identical to it.
+    """
+
+    def __init__(self, plan, edge_weight=None, chunk=256):
+        from .graph import Graph
+        self.plan = plan
+        lei = plan.local_edge_index
+        src_local = lei[0]
+        interior = src_local < plan.n_own
+        w = edge_weight[plan.edge_pos] if edge_weight is not None else None
+        ei_int = lei[:, interior]
+        ei_bnd = lei[:, ~interior]
+        self.g_int = Graph(ei_int, plan.n_own, plan.n_own, chunk=chunk)
+        self.g_bnd = Graph(ei_bnd, plan.n_own, plan.n_local_src, chunk=chunk)
+        self.w_int = self.g_int.dst.to_csr_order(w[interior].contiguous()) if w is not None else None
+        self.w_bnd = self.g_bnd.dst.to_csr_order(w[~interior].contiguous()) if w is not None else None
+        self.n_interior = int(ei_int.shape[1])
+        self.n_boundary = int(ei_bnd.shape[1])
+
+    def step(self, x_local, out, bias=None, group=None):
+        from . import _lib, ops
+        plan = self.plan
+        F = x_local.shape[1]
+        own = x_local[:plan.n_own]
+        send = ops.gather_rows(own, plan.send_idx) if plan.send_idx.numel() else x_local.new_empty((0, F))
+        halo = x_local[plan.n_own:]
+        work = None
+        if x_local.is_cuda and dist.get_backend(group) == "gloo":
+            _a2a(halo, send, plan.recv_counts, plan.send_counts, group)
+        else:
+            work = dist.all_to_all_single(halo, send, output_split_sizes=plan.recv_counts,
+                                          input_split_sizes=plan.send_counts, group=group, async_op=True)
+        ops._aggregate(self.g_int.dst, "other", own, self.w_int, "sum", 0, None, out=out)
+        if work is not None:
+            work.wait()
+        ops._aggregate(self.g_bnd.dst, "other", x_local, self.w_bnd, "sum", _lib.MP_FLAG_INIT_FROM_OUT, bias,
+                       out=out)
+        return out

@@ -78,10 +78,11 @@ class CSR:
         s = self._structs.get(gather)
         if s is None:
             col = self.col if gather == "other" else self.eid
+            n_cols = self.n_other if gather == "other" else self.n_edges
             s = _lib.MpCsr(self.rowptr.data_ptr(), col.data_ptr(), self.eid.data_ptr(),
                            self.wave_row.data_ptr(), self.wave_slot.data_ptr(),
                            self.split_waves.data_ptr(), self.n_rows, self.n_edges, self.chunk,
-                           self.n_waves, self.n_split, 0)
+                           self.n_waves, self.n_split, n_cols)
             self._structs[gather] = s
         return s
 
