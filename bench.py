@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-edges", type=int, default=16_000_000)
+    ap.add_argument("--cpu-sample-edges", type=int, default=48_000_000)
     ap.add_argument("--chunk", type=int, default=256)
     ap.add_argument("--no-overlap", action="store_true", help="N>1: exchange, then aggregate (no overlap)")
     return ap.parse_args()

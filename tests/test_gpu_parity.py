@@ -577,3 +577,15 @@ def test_small_feature_widths_lane_groups(F):
     mx, am = ops.segment_reduce(x.to(DEV)[ei[0].to(DEV)], ei[1].to(DEV), N, "max")
     wm, wa = S.scatter_max(x[ei[0]], ei[1], N)
     assert torch.equal(mx.cpu(), wm) and torch.equal(am.cpu(), wa)
+
+
+def test_global_pooling():
+    from torch_geometric.nn import global_add_pool, global_mean_pool, global_max_pool
+    g = torch.Generator().manual_seed(40)
+    sizes = torch.randint(1, 60, (37,), generator=g)
+    batch = torch.repeat_interleave(torch.arange(37), sizes)
+    x = torch.randn(batch.numel(), 48, generator=g)
+    xd, bd = x.to(DEV), batch.to(DEV)
+    assert torch.equal(global_add_pool(xd, bd).cpu(), S.scatter_sum(x, batch, 37))
+    assert torch.equal(global_mean_pool(xd, bd).cpu(), S.scatter_mean(x, batch, 37))
+    assert torch.equal(global_max_pool(xd, bd, size=40).cpu(), P.scatter_("max", x, batch, 40))
