@@ -45,6 +45,9 @@
 #ifndef MP_NT_X
 #define MP_NT_X 0          // non-temporal x-row loads (all rows)
 #endif
+#ifndef MP_XCD_TILES
+#define MP_XCD_TILES 0     // 1: feature tile = (blockIdx % 8) % tiles (XCD-affine tiles, needs 8 % tiles == 0)
+#endif
 #ifndef MP_BUF_X
 #define MP_BUF_X 0         // x rows through one buffer resource (32-bit offsets) when x < 4 GB
 #endif
@@ -545,10 +548,21 @@ __global__ __launch_bounds__(kBlock) void k_agg_main(AggArgs p) {
   using GR = Grp<L>;
   const int lane = lane_id();
   const int gl = lane & (L - 1);
-  const int wave = (int)blockIdx.x * kWavesPerBlock + (int)(threadIdx.x >> 6);
+  int bx = (int)blockIdx.x, tile = (int)blockIdx.y;
+  if constexpr (MP_XCD_TILES) {
+    // blocks b and b+8 share an XCD (dispatch is round-robin over the 8 XCDs;
+    // speed only): give every XCD one feature tile so its L2 holds only that
+    // tile of the hot rows.  tiles = gridDim.y divides 8 (checked on the host).
+    const int T = (int)gridDim.y;
+    const int b = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+    const int xcd = b & 7;
+    tile = xcd % T;
+    bx = (b >> 3) * (8 / T) + xcd / T;
+  }
+  const int wave = bx * kWavesPerBlock + (int)(threadIdx.x >> 6);
   const int w = GR::un(wave * GR::G + lane / L);  // this group's task
   if (w >= p.n_waves) return;
-  const int f = (int)blockIdx.y * L * VEC + gl * VEC;
+  const int f = tile * L * VEC + gl * VEC;
   const bool act = f < p.F;
   const uint32_t foff = (uint32_t)(act ? f : 0) * 4u;
 
@@ -694,7 +708,9 @@ static int launch_l(const AggArgs& a, int stages, hipStream_t s) {
   constexpr int U = VEC == 4 ? (L == 64 ? MP_U_VEC4 : MP_U_NARROW) : 16;
   const int ftiles = (int)ceil_div(a.F, L * VEC);
   if (stages & MP_STAGE_MAIN) {
-    dim3 grid((unsigned)ceil_div(a.n_waves, kWavesPerBlock * (64 / L)), (unsigned)ftiles);
+    int64_t nb = ceil_div(a.n_waves, kWavesPerBlock * (64 / L));
+    if (MP_XCD_TILES && 8 % ftiles == 0) nb = ceil_div(nb, 8 / ftiles) * (8 / ftiles);
+    dim3 grid((unsigned)nb, (unsigned)ftiles);
     // 32-bit buffer offsets when every gathered byte lies below 4 GiB
     const int64_t xb = (int64_t)a.n_cols * a.ldx * 4;
     if (MP_BUF_X && a.n_cols > 0 && xb <= (int64_t)0xFFFFFFF0) {

@@ -589,3 +589,123 @@ def test_global_pooling():
     assert torch.equal(global_add_pool(xd, bd).cpu(), S.scatter_sum(x, batch, 37))
     assert torch.equal(global_mean_pool(xd, bd).cpu(), S.scatter_mean(x, batch, 37))
     assert torch.equal(global_max_pool(xd, bd, size=40).cpu(), P.scatter_("max", x, batch, 40))
+
+
+# --------------------------------------------------------------------------
+# API-surface parity: strides, bipartite, flow, layer options, weight grads
+# --------------------------------------------------------------------------
+
+def test_strided_and_offset_x():
+    _, ops, _, Graph, pl = _mods()
+    N, E = 500, 6000
+    ei = pl(N, E, seed=50)
+    base = torch.randn(N, 300, generator=torch.Generator().manual_seed(50))
+    for sl in (slice(0, 256), slice(4, 260), slice(3, 67)):  # ldx 300; offset rows; odd offset
+        x = base[:, sl]
+        out = ops.fused_propagate(Graph(ei.to(DEV), N, N), base.to(DEV)[:, sl], ei.to(DEV), None, "sum").cpu()
+        want = S.gather_sum(x.contiguous(), ei[0], ei[1], None, N)
+        _bound_ok(out, want, S.gather_sum(x.abs().contiguous(), ei[0], ei[1], None, N))
+
+
+def test_bipartite_and_flow():
+    from torch_geometric.nn import MessagePassing
+    g = torch.Generator().manual_seed(51)
+    Ns, Nd, E, F = 300, 120, 4000, 20
+    ei = torch.stack([torch.randint(Ns, (E,), generator=g), torch.randint(Nd, (E,), generator=g)])
+    xs = torch.randn(Ns, F, generator=g)
+    xd = torch.randn(Nd, F, generator=g)
+    mp_ = MessagePassing(aggr="add").to(DEV)
+    out = mp_.propagate(ei.to(DEV), size=(Ns, Nd), x=(xs.to(DEV), xd.to(DEV))).cpu()
+    assert out.shape == (Nd, F)
+    assert torch.equal(out, S.gather_sum(xs, ei[0], ei[1], None, Nd))
+    # target_to_source: aggregate at edge_index[0] from edge_index[1]
+    mp2 = MessagePassing(aggr="mean", flow="target_to_source").to(DEV)
+    ei2 = torch.randint(200, (2, 3000), generator=g)
+    x2 = torch.randn(200, F, generator=g)
+    out2 = mp2.propagate(ei2.to(DEV), x=x2.to(DEV)).cpu()
+    want2 = S.scatter_mean(x2[ei2[1]], ei2[0], 200)
+    _bound_ok(out2, want2, S.scatter_mean(x2.abs()[ei2[1]], ei2[0], 200))
+    with pytest.raises(ValueError):
+        mp_.propagate(ei.to(DEV), size=(Ns + 1, Nd), x=(xs.to(DEV), xd.to(DEV)))
+
+
+@pytest.mark.parametrize("improved,normalize,weighted", [(True, True, False), (False, False, True),
+                                                         (False, True, True)])
+def test_gcn_options(improved, normalize, weighted):
+    from torch_geometric.nn import GCNConv
+    _, _, _, _, pl = _mods()
+    N, E, F = 400, 5000, 32
+    ei = pl(N, E, seed=52)
+    # a few explicit self loops with their own weights (add_remaining keeps them)
+    ei[:, :20] = torch.arange(20).repeat(2, 1)
+    g = torch.Generator().manual_seed(52)
+    x = torch.randn(N, F, generator=g)
+    w = torch.rand(E, generator=g) + 0.1 if weighted else None
+    conv = GCNConv(F, F, improved=improved, normalize=normalize).to(DEV)
+    with torch.no_grad():
+        conv.bias.normal_()
+        out = conv(x.to(DEV), ei.to(DEV), w.to(DEV) if weighted else None).cpu()
+    W, b = conv.weight.detach().cpu(), conv.bias.detach().cpu()
+    h = x @ W
+    if normalize:
+        want = P.gcn_conv(x, ei, W, b, edge_weight=w, improved=improved)
+    else:
+        want = S.gather_sum(h, ei[0], ei[1], w, N) + b
+    assert (out - want).abs().max().item() < 1e-4
+
+
+def test_edge_weight_gradient():
+    _, ops, _, Graph, pl = _mods()
+    N, E, F = 300, 4000, 16
+    ei = pl(N, E, seed=53)
+    g = torch.Generator().manual_seed(53)
+    x = torch.randn(N, F, generator=g)
+    w = torch.rand(E, generator=g)
+    xd = x.to(DEV).requires_grad_(True)
+    wd = w.to(DEV).requires_grad_(True)
+    gout = torch.randn(N, F, generator=g)
+    ops.fused_propagate(Graph(ei.to(DEV), N, N), xd, ei.to(DEV), wd, "sum").backward(gout.to(DEV))
+    x64 = x.double().requires_grad_(True)
+    w64 = w.double().requires_grad_(True)
+    (w64.view(-1, 1) * x64[ei[0]]).new_zeros(N, F).index_add(0, ei[1], w64.view(-1, 1) * x64[ei[0]]) \
+        .backward(gout.double())
+    assert torch.allclose(xd.grad.cpu().double(), x64.grad, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(wd.grad.cpu().double(), w64.grad, rtol=1e-5, atol=1e-4)
+
+
+def test_sage_concat_and_gat_mean_heads():
+    from torch_geometric.nn import SAGEConv, GATConv
+    _, _, _, _, pl = _mods()
+    N, E, F = 300, 3000, 12
+    ei = pl(N, E, seed=54)
+    x = torch.randn(N, F, generator=torch.Generator().manual_seed(54))
+    conv = SAGEConv(F, 8, concat=True, normalize=True).to(DEV)
+    with torch.no_grad():
+        out = conv(x.to(DEV), ei.to(DEV)).cpu()
+    agg = S.scatter_mean(x[ei[0]], ei[1], N)
+    want = torch.nn.functional.normalize(torch.cat([x, agg], -1) @ conv.weight.detach().cpu()
+                                         + conv.bias.detach().cpu(), p=2, dim=-1)
+    assert (out - want).abs().max().item() < 1e-5
+    gat = GATConv(F, 6, heads=3, concat=False).to(DEV)
+    with torch.no_grad():
+        gat.bias.normal_()
+        out = gat(x.to(DEV), ei.to(DEV)).cpu()
+    want = P.gat_conv(x, ei, gat.weight.detach().cpu(), gat.att.detach().cpu(), gat.bias.detach().cpu(), 3, 6,
+                      concat=False)
+    assert (out - want).abs().max().item() < 1e-5
+
+
+def test_gat_dropout_training_uses_generic_path():
+    from torch_geometric.nn import GATConv
+    _, _, _, _, pl = _mods()
+    N, E, F = 200, 2000, 8
+    ei = pl(N, E, seed=55)
+    x = torch.randn(N, F, generator=torch.Generator().manual_seed(55)).to(DEV)
+    gat = GATConv(F, 4, heads=2, dropout=0.5).to(DEV)
+    gat.train()
+    out = gat(x, ei.to(DEV))
+    assert out.shape == (N, 8) and torch.isfinite(out).all()
+    gat.eval()
+    a = gat(x, ei.to(DEV))
+    b = gat(x, ei.to(DEV))
+    assert torch.equal(a, b)
