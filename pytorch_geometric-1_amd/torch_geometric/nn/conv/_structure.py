@@ -15,28 +15,41 @@ from ...utils.loop import add_self_loops, remove_self_loops
 _cache = _Cache()
 
 
+def last_loop_edge(edge_index, mask, num_nodes):
+    """For every node with a pre-existing self loop: (nodes, position of its
+    LAST loop edge).  Upstream's `loop_weight[row[inv_mask]] = w[inv_mask]`
+    is a sequential index_put_ on the CPU, so with duplicate loops the last
+    one wins; a device index_put_ with duplicates would pick any of them."""
+    row = edge_index[0]
+    pos = torch.nonzero(~mask).view(-1)
+    last = torch.full((num_nodes,), -1, dtype=torch.long, device=row.device)
+    if pos.numel():
+        last.scatter_reduce_(0, row[pos], pos, "amax", include_self=True)
+    nodes = torch.nonzero(last >= 0).view(-1)
+    return nodes, last[nodes]
+
+
 def remaining_loops_structure(edge_index, num_nodes):
-    """(edge_index with remaining self loops, kept-edge mask, loop rows of the
-    removed loops) -- the structure half of add_remaining_self_loops."""
+    """(edge_index with remaining self loops, kept-edge mask, (loop nodes,
+    their last loop edge)) -- the structure half of add_remaining_self_loops."""
 
     def build():
         row, col = edge_index
         mask = row != col
-        inv_rows = row[~mask]
         loop_index = torch.arange(0, num_nodes, dtype=row.dtype, device=row.device)
         loop_index = loop_index.unsqueeze(0).repeat(2, 1)
         ei = torch.cat([edge_index[:, mask], loop_index], dim=1)
-        return ei, mask, inv_rows
+        return ei, mask, last_loop_edge(edge_index, mask, num_nodes)
 
     return _cache.get(edge_index, ("remaining", int(num_nodes)), build)
 
 
-def remaining_loops_weight(edge_weight, mask, inv_rows, num_nodes, fill_value):
+def remaining_loops_weight(edge_weight, mask, loops, num_nodes, fill_value):
     """The weight half of add_remaining_self_loops (same order and values)."""
     loop_weight = torch.full((num_nodes,), fill_value, dtype=edge_weight.dtype, device=edge_weight.device)
-    remaining = edge_weight[~mask]
-    if remaining.numel() > 0:
-        loop_weight[inv_rows] = remaining
+    nodes, last = loops
+    if nodes.numel() > 0:
+        loop_weight[nodes] = edge_weight[last]
     return torch.cat([edge_weight[mask], loop_weight], dim=0)
 
 

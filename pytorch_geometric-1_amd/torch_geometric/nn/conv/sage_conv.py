@@ -9,9 +9,9 @@ import torch
 import torch.nn.functional as F
 from torch.nn import Parameter
 
-from ...utils import add_remaining_self_loops
 from ..inits import uniform
 from .message_passing import MessagePassing
+from ._structure import remaining_loops_structure, remaining_loops_weight
 
 
 class SAGEConv(MessagePassing):
@@ -36,8 +36,12 @@ class SAGEConv(MessagePassing):
     def forward(self, x, edge_index, edge_weight=None, size=None, res_n_id=None):
         """"""
         if not self.concat and torch.is_tensor(x):
-            edge_index, edge_weight = add_remaining_self_loops(edge_index, edge_weight, 1,
-                                                               x.size(self.node_dim))
+            # add_remaining_self_loops(edge_index, edge_weight, 1, N), structure cached on edge_index
+            N = x.size(self.node_dim)
+            ei, mask, loops = remaining_loops_structure(edge_index, N)
+            if edge_weight is not None:
+                edge_weight = remaining_loops_weight(edge_weight, mask, loops, N, 1)
+            edge_index = ei
         return self.propagate(edge_index, size=size, x=x, edge_weight=edge_weight, res_n_id=res_n_id)
 
     def message(self, x_j, edge_weight):

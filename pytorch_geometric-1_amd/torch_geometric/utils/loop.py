@@ -46,9 +46,14 @@ def add_remaining_self_loops(edge_index, edge_weight=None, fill_value=1, num_nod
                              device=edge_index.device)
     if edge_weight is not None:
         assert edge_weight.numel() == edge_index.size(1)
-        remaining_edge_weight = edge_weight[inv_mask]
-        if remaining_edge_weight.numel() > 0:
-            loop_weight[row[inv_mask]] = remaining_edge_weight
+        # sequential semantics of the CPU index_put_: with duplicate self
+        # loops the LAST one's weight wins (deterministic on the device too)
+        pos = torch.nonzero(inv_mask).view(-1)
+        if pos.numel() > 0:
+            last = torch.full((num_nodes,), -1, dtype=torch.long, device=row.device)
+            last.scatter_reduce_(0, row[pos], pos, "amax", include_self=True)
+            has = last >= 0
+            loop_weight[has] = edge_weight[last[has]]
         edge_weight = torch.cat([edge_weight[mask], loop_weight], dim=0)
     loop_index = torch.arange(0, num_nodes, dtype=row.dtype, device=row.device)
     loop_index = loop_index.unsqueeze(0).repeat(2, 1)

@@ -147,10 +147,15 @@ def test_graph_generators_deterministic_and_shaped():
 def test_gcn_structure_cache_matches_reference_loops():
     from oracle import pyg_ref as P
     from torch_geometric.nn.conv._structure import remaining_loops_structure, remaining_loops_weight
-    ei = torch.tensor([[0, 1, 1, 2, 2], [1, 1, 2, 0, 2]])
-    w = torch.tensor([1., 2., 3., 4., 5.])
-    ei2, mask, inv = remaining_loops_structure(ei, 4)
-    w2 = remaining_loops_weight(w, mask, inv, 4, 2)
+    # node 1 has two self loops (weights 2 and 6): the last one wins, as on the CPU
+    ei = torch.tensor([[0, 1, 1, 2, 2, 1], [1, 1, 2, 0, 2, 1]])
+    w = torch.tensor([1., 2., 3., 4., 5., 6.])
+    ei2, mask, loops = remaining_loops_structure(ei, 4)
+    w2 = remaining_loops_weight(w, mask, loops, 4, 2)
     r_ei, r_w = P.add_remaining_self_loops(ei, w, 2, 4)
     assert torch.equal(ei2, r_ei) and torch.equal(w2, r_w)
+    assert r_w.tolist()[-4:] == [2., 6., 5., 2.]
     assert remaining_loops_structure(ei, 4)[0] is ei2    # cached on the tensor
+    from torch_geometric.utils import add_remaining_self_loops
+    u_ei, u_w = add_remaining_self_loops(ei, w, 2, 4)
+    assert torch.equal(u_ei, r_ei) and torch.equal(u_w, r_w)
