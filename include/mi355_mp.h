@@ -158,6 +158,31 @@ int mp_gat_aggregate_f32(const mp_csr* g, const float* xw, const float* a_src,
                          float* row_stats, void* slab, size_t slab_bytes,
                          int32_t stages, void* stream);
 
+/* ---- GATConv backward pieces ------------------------------ */
+
+/* slot_row[k] = the row owning CSR slot k (one-time per graph). */
+int mp_csr_slot_rows(const mp_csr* g, int32_t* slot_row, void* stream);
+
+/* alpha_csr[k,h] = exp(leaky(a_src[col_k,h]+a_dst[r,h]) - m[r,h]) / den[r,h]
+ * and (if score != NULL) score[k,h] = a_src[col_k,h] + a_dst[r,h] (the
+ * pre-activation), both in CSR slot order, r = slot_row[k]. */
+int mp_gat_alpha_csr_f32(const mp_csr* g, const int32_t* slot_row, const float* a_src,
+                         const float* a_dst, int32_t H, float slope, const float* row_stats,
+                         float* alpha_csr, float* score, void* stream);
+
+/* Per-head weighted aggregation: with C = F / H,
+ * out[r, h*C + c] = sum_k w[k*H + h] * x[col[k], h*C + c]   (w in CSR slot order)
+ * (GATConv's d out / d x_j = alpha, applied over the transposed CSR). */
+int mp_aggregate_heads_f32(const mp_csr* g, const float* w, int32_t H, const float* x,
+                           int64_t ldx, int32_t F, float* out, int64_t ldo, void* slab,
+                           size_t slab_bytes, int32_t stages, void* stream);
+
+/* Sampled dense-dense product over CSR slots (GAT d alpha):
+ * out[k*H + h] = sum_c grow[r, h*C + c] * x[col[k], h*C + c], r = slot_row[k]. */
+int mp_gat_sddmm_f32(const mp_csr* g, const int32_t* slot_row, const float* grow, int64_t ldg,
+                     const float* x, int64_t ldx, int32_t H, int32_t C, float* out,
+                     void* stream);
+
 /* alpha[e,h] for edges in ORIGINAL order (return_attention_weights, backward) */
 int mp_gat_alpha_f32(const int64_t* src_idx, const int64_t* dst_idx,
                      int64_t n_edges, int32_t H, const float* a_src,

@@ -148,6 +148,7 @@ struct SumRed {
   static constexpr bool kW = HAS_W;
   static constexpr bool kEid = false;
   static constexpr bool kGat = false;
+  static constexpr bool kHW = false;
   struct Part {
     float v[VEC];
   };
@@ -221,6 +222,7 @@ struct ArgRed {
   static constexpr bool kW = HAS_W;
   static constexpr bool kEid = true;
   static constexpr bool kGat = false;
+  static constexpr bool kHW = false;
   struct Part {
     float v[VEC];
     int a[VEC];
@@ -327,6 +329,7 @@ struct GatRed {
   static constexpr bool kW = false;
   static constexpr bool kEid = false;
   static constexpr bool kGat = true;
+  static constexpr bool kHW = false;
   struct Part {
     float v[VEC];
     float m, s;
@@ -414,6 +417,17 @@ struct GatRed {
       p.row_stats[(row * p.H + h) * 2 + 1] = den;
     }
   }
+};
+
+// Per-head weighted sum (GAT backward: d out / d x_j = alpha[e,h]): the weight
+// of slot k for this lane's head h = f / C is w[k*H + h].
+template <int VEC>
+struct HeadSumRed : SumRed<VEC, true, false> {
+  static constexpr bool kW = false;
+  static constexpr bool kHW = true;
+  int h;
+  __device__ HeadSumRed(const AggArgs& p, int f, bool act) : SumRed<VEC, true, false>(p, f, act),
+                                                              h(act ? f / p.C : 0) {}
 };
 
 // this lane's share of slab slot s (2*task + kind)
@@ -510,9 +524,11 @@ __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p, SlotWin<Re
     n = GR::un(n);
     Frag<VEC> v[U];
     float as[U];
+    [[maybe_unused]] float hw[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int uu = u < n ? u : n - 1;
+      if constexpr (Red::kHW) hw[u] = p.w[(e + uu) * p.H + red.h];
       int c = GR::bc(win.col, off + uu);
       if constexpr (MP_COLD_FLAG) {
         const bool cold = c < 0;
@@ -533,7 +549,7 @@ __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p, SlotWin<Re
         if constexpr (Red::kGat) {
           red.consume_gat(p, v[u], as[u]);
         } else {
-          const float wt = Red::kW ? GR::bc(win.w, off + u) : 1.f;
+          const float wt = Red::kHW ? hw[u] : (Red::kW ? GR::bc(win.w, off + u) : 1.f);
           const int ei = Red::kEid ? GR::bc(win.eid, off + u) : 0;
           red.consume(v[u], wt, ei, 0.f);
         }
@@ -841,6 +857,36 @@ int mp_aggregate_f32(const mp_csr* g, const float* w, const float* x, int64_t ld
     case 2: return dispatch_reduce<2>(a, reduce, stages, s, 64);
     default: return dispatch_reduce<1>(a, reduce, stages, s, 64);
   }
+}
+
+int mp_aggregate_heads_f32(const mp_csr* g, const float* w, int32_t H, const float* x, int64_t ldx, int32_t F,
+                           float* out, int64_t ldo, void* slab, size_t slab_bytes, int32_t stages, void* stream) {
+  int rc = check_graph(g, "mp_aggregate_heads_f32");
+  if (rc) return rc;
+  MP_CHECK_ARG(F > 0 && H > 0 && F % H == 0, "mp_aggregate_heads_f32: F must be a positive multiple of H");
+  MP_CHECK_ARG(out && (g->n_edges == 0 || (x && w)), "mp_aggregate_heads_f32: null pointer");
+  MP_CHECK_ARG(ldx >= F && ldo >= F, "mp_aggregate_heads_f32: leading dimension < F");
+  MP_CHECK_ARG(slab && slab_bytes >= mp_aggregate_slab_bytes(g, F, MP_REDUCE_SUM),
+               "mp_aggregate_heads_f32: slab workspace too small");
+  AggArgs a{};
+  fill_graph(a, g);
+  a.F = F;
+  a.w = w;
+  a.x = x;
+  a.ldx = ldx;
+  a.out = out;
+  a.ldo = ldo;
+  a.H = H;
+  a.C = F / H;
+  a.slab_ld = slab_ld_for(F);
+  a.slab_v = (float*)slab;
+  hipStream_t s = as_stream(stream);
+  Shape sh = pick_shape(F, ldx, x, ldo, out);
+  int vec = sh.vec;
+  while (vec > 1 && a.C % vec != 0) vec >>= 1;  // a lane's features must share a head
+  if (vec == 4) return launch<HeadSumRed<4>, 4>(a, stages, s, sh.lanes);
+  if (vec == 2) return launch<HeadSumRed<2>, 2>(a, stages, s, 64);
+  return launch<HeadSumRed<1>, 1>(a, stages, s, 64);
 }
 
 size_t mp_gat_slab_bytes(const mp_csr* g, int32_t H, int32_t C) {

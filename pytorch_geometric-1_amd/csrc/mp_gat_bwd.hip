@@ -1,0 +1,156 @@
+// GATConv backward pieces on the destination-sorted CSR (gfx950):
+//   slot -> row map, alpha / pre-activation score in CSR slot order, and the
+//   sampled dense-dense product d alpha[k,h] = <grad_out[row_k,h,:], xw[col_k,h,:]>.
+// The alpha-weighted transposed aggregation is mp_aggregate_heads_f32 (the
+// main kernel template with a per-head weight).  Reference: GATConv.message
+// + utils.softmax autograd (PyG 1.4.3 [U3,U6]).
+#include "mp_common.h"
+
+namespace mp {
+
+__global__ void k_slot_rows(const int32_t* __restrict__ rowptr, int64_t n_rows, int64_t n_edges,
+                            int32_t* __restrict__ slot_row) {
+  int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_edges) return;
+  int64_t lo = 0, hi = n_rows;  // last r with rowptr[r] <= k
+  while (lo < hi) {
+    int64_t mid = (lo + hi + 1) >> 1;
+    if ((int64_t)rowptr[mid] <= k) lo = mid;
+    else hi = mid - 1;
+  }
+  slot_row[k] = (int32_t)lo;
+}
+
+__global__ void k_gat_alpha_csr(const int32_t* __restrict__ col, const int32_t* __restrict__ slot_row,
+                                int64_t n_edges, int32_t H, const float* __restrict__ a_src,
+                                const float* __restrict__ a_dst, float slope, const float* __restrict__ stats,
+                                float* __restrict__ alpha, float* __restrict__ score) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_edges * (int64_t)H) return;
+  const int64_t k = i / H;
+  const int h = (int)(i % H);
+  const int64_t r = slot_row[k], j = col[k];
+  const float sc = a_src[j * H + h] + a_dst[r * H + h];
+  const float a = sc > 0.f ? sc : sc * slope;
+  alpha[i] = expf(a - stats[(r * H + h) * 2]) / stats[(r * H + h) * 2 + 1];
+  if (score) score[i] = sc;
+}
+
+// One wave per 256 consecutive slots; lane l owns VEC features f of a
+// 64*VEC-feature tile; a head spans G = C/VEC lanes (power of two <= 64) and
+// its dot product is reduced with shuffle-xor inside the group.
+template <int VEC>
+__global__ __launch_bounds__(256) void k_gat_sddmm(const int32_t* __restrict__ col,
+                                                    const int32_t* __restrict__ slot_row, int64_t n_edges,
+                                                    const float* __restrict__ grow, int64_t ldg,
+                                                    const float* __restrict__ x, int64_t ldx, int32_t H,
+                                                    int32_t C, int32_t G, float* __restrict__ out) {
+  constexpr int U = 8;
+  const int lane = lane_id();
+  const int64_t k0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 256;
+  if (k0 >= n_edges) return;
+  const int64_t k1 = k0 + 256 < n_edges ? k0 + 256 : n_edges;
+  const int F = H * C;
+  const int f = (int)blockIdx.y * 64 * VEC + lane * VEC;
+  const bool act = f < F;
+  const int fs = act ? f : 0;
+  const int h = fs / C;
+  for (int64_t kb = k0; kb < k1; kb += 64) {
+    const int64_t kk = kb + lane;
+    const int rwin = kk < k1 ? slot_row[kk] : 0;
+    const int cwin = kk < k1 ? col[kk] : 0;
+    const int nb = (int)((k1 - kb) < 64 ? (k1 - kb) : 64);
+    for (int b = 0; b < nb; b += U) {
+      float d[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int uu = b + u < nb ? b + u : nb - 1;
+        const int r = readlane(rwin, uu);
+        const int j = readlane(cwin, uu);
+        Frag<VEC> gv = load_frag<VEC>(grow + (int64_t)r * ldg + fs);
+        Frag<VEC> xv = load_frag<VEC>(x + (int64_t)j * ldx + fs);
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) t += gv.v[q] * xv.v[q];
+        d[u] = act ? t : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        for (int o = G >> 1; o > 0; o >>= 1) d[u] += __shfl_xor(d[u], o);
+        if (b + u < nb && act && (lane & (G - 1)) == 0) out[(kb + b + u) * H + h] = d[u];
+      }
+    }
+  }
+}
+
+// general C: one thread per (slot, head)
+__global__ void k_gat_sddmm_scalar(const int32_t* __restrict__ col, const int32_t* __restrict__ slot_row,
+                                   int64_t n_edges, const float* __restrict__ grow, int64_t ldg,
+                                   const float* __restrict__ x, int64_t ldx, int32_t H, int32_t C,
+                                   float* __restrict__ out) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_edges * (int64_t)H) return;
+  const int64_t k = i / H;
+  const int h = (int)(i % H);
+  const float* gr = grow + (int64_t)slot_row[k] * ldg + (int64_t)h * C;
+  const float* xr = x + (int64_t)col[k] * ldx + (int64_t)h * C;
+  float t = 0.f;
+  for (int c = 0; c < C; ++c) t += gr[c] * xr[c];
+  out[i] = t;
+}
+
+}  // namespace mp
+
+using namespace mp;
+
+extern "C" {
+
+int mp_csr_slot_rows(const mp_csr* g, int32_t* slot_row, void* stream) {
+  MP_CHECK_ARG(g && g->rowptr && slot_row, "mp_csr_slot_rows: null pointer");
+  if (g->n_edges == 0) return MP_OK;
+  k_slot_rows<<<(unsigned)ceil_div(g->n_edges, 256), 256, 0, as_stream(stream)>>>(g->rowptr, g->n_rows,
+                                                                                  g->n_edges, slot_row);
+  MP_CHECK_LAUNCH();
+  return MP_OK;
+}
+
+int mp_gat_alpha_csr_f32(const mp_csr* g, const int32_t* slot_row, const float* a_src, const float* a_dst,
+                         int32_t H, float slope, const float* row_stats, float* alpha_csr, float* score,
+                         void* stream) {
+  MP_CHECK_ARG(g && H > 0, "mp_gat_alpha_csr_f32: bad argument");
+  if (g->n_edges == 0) return MP_OK;
+  MP_CHECK_ARG(g->col && slot_row && a_src && a_dst && row_stats && alpha_csr,
+               "mp_gat_alpha_csr_f32: null pointer");
+  int64_t total = g->n_edges * (int64_t)H;
+  k_gat_alpha_csr<<<(unsigned)ceil_div(total, 256), 256, 0, as_stream(stream)>>>(
+      g->col, slot_row, g->n_edges, H, a_src, a_dst, slope, row_stats, alpha_csr, score);
+  MP_CHECK_LAUNCH();
+  return MP_OK;
+}
+
+int mp_gat_sddmm_f32(const mp_csr* g, const int32_t* slot_row, const float* grow, int64_t ldg, const float* x,
+                     int64_t ldx, int32_t H, int32_t C, float* out, void* stream) {
+  MP_CHECK_ARG(g && H > 0 && C > 0, "mp_gat_sddmm_f32: bad argument");
+  if (g->n_edges == 0) return MP_OK;
+  MP_CHECK_ARG(g->col && slot_row && grow && x && out, "mp_gat_sddmm_f32: null pointer");
+  const int64_t F = (int64_t)H * C;
+  MP_CHECK_ARG(ldg >= F && ldx >= F, "mp_gat_sddmm_f32: leading dimension < H*C");
+  hipStream_t s = as_stream(stream);
+  auto aligned4 = [](const void* p, int64_t ld) { return (uintptr_t)p % 16 == 0 && ld % 4 == 0; };
+  const bool v4 = C % 4 == 0 && aligned4(grow, ldg) && aligned4(x, ldx);
+  const int vec = v4 ? 4 : 1;
+  const int G = C / vec;
+  if (G >= 1 && G <= 64 && (G & (G - 1)) == 0) {
+    dim3 grid((unsigned)ceil_div(ceil_div(g->n_edges, 256), 4), (unsigned)ceil_div(F, 64 * vec));
+    if (v4) k_gat_sddmm<4><<<grid, 256, 0, s>>>(g->col, slot_row, g->n_edges, grow, ldg, x, ldx, H, C, G, out);
+    else k_gat_sddmm<1><<<grid, 256, 0, s>>>(g->col, slot_row, g->n_edges, grow, ldg, x, ldx, H, C, G, out);
+  } else {
+    int64_t total = g->n_edges * (int64_t)H;
+    k_gat_sddmm_scalar<<<(unsigned)ceil_div(total, 256), 256, 0, s>>>(g->col, slot_row, g->n_edges, grow, ldg,
+                                                                      x, ldx, H, C, out);
+  }
+  MP_CHECK_LAUNCH();
+  return MP_OK;
+}
+
+}  // extern "C"

@@ -54,6 +54,12 @@ SIGNATURES = {
     "mp_gat_aggregate_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, c_p, i32, i32, f32, c_p,
                                             c_p, i64, c_p, c_p, sz, i32, c_p]),
     "mp_gat_alpha_f32": (ctypes.c_int, [c_p, c_p, i64, i32, c_p, c_p, f32, c_p, c_p, c_p]),
+    "mp_csr_slot_rows": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p]),
+    "mp_gat_alpha_csr_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, c_p, i32, f32, c_p, c_p, c_p,
+                                            c_p]),
+    "mp_aggregate_heads_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, i32, c_p, i64, i32, c_p, i64, c_p,
+                                              sz, i32, c_p]),
+    "mp_gat_sddmm_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, i64, c_p, i64, i32, i32, c_p, c_p]),
     "mp_gather_rows_f32": (ctypes.c_int, [c_p, i64, c_p, i64, i32, c_p, i64, c_p]),
     "mp_permute_f32": (ctypes.c_int, [c_p, c_p, i64, c_p, c_p]),
     "mp_scatter_arg_backward_f32": (ctypes.c_int, [c_p, c_p, i64, i32, i64, c_p, c_p, i64, c_p]),

@@ -74,10 +74,16 @@ class CSR:
         self._deg = None
 
     def struct(self, gather="other"):
-        """ctypes mp_csr; gather='other' reads x[other] rows, 'eid' reads message rows."""
+        """ctypes mp_csr; gather='other' reads x[other] rows, 'eid' reads message
+        rows (original edge order), 'slot' reads rows already in CSR slot order."""
         s = self._structs.get(gather)
         if s is None:
-            col = self.col if gather == "other" else self.eid
+            if gather == "slot":
+                if getattr(self, "_ident", None) is None:
+                    self._ident = torch.arange(max(self.n_edges, 1), dtype=torch.int32, device=self.device)
+                col = self._ident
+            else:
+                col = self.col if gather == "other" else self.eid
             n_cols = self.n_other if gather == "other" else self.n_edges
             s = _lib.MpCsr(self.rowptr.data_ptr(), col.data_ptr(), self.eid.data_ptr(),
                            self.wave_row.data_ptr(), self.wave_slot.data_ptr(),
@@ -85,6 +91,15 @@ class CSR:
                            self.n_waves, self.n_split, n_cols)
             self._structs[gather] = s
         return s
+
+    def slot_rows(self):
+        """int32 [E]: the row owning each CSR slot (cached)."""
+        if getattr(self, "_slot_rows", None) is None:
+            sr = torch.empty(max(self.n_edges, 1), dtype=torch.int32, device=self.device)
+            _lib.check(_lib.load().mp_csr_slot_rows(self.struct("other"), sr.data_ptr(),
+                                                    _lib.stream_ptr(self.device)), "mp_csr_slot_rows")
+            self._slot_rows = sr
+        return self._slot_rows
 
     def degree(self):
         """In-degree per row (int64), from rowptr."""

@@ -304,59 +304,89 @@ def _gat_forward(graph, edge_index, xw, att, H, C, slope, bias, want_alpha):
         _lib.check(lib.mp_gat_alpha_f32(src.data_ptr(), dst.data_ptr(), E, H, a_src.data_ptr(),
                                         a_dst.data_ptr(), float(slope), stats.data_ptr(), alpha.data_ptr(), st),
                    "mp_gat_alpha_f32")
-    return out, alpha, a_src, a_dst
+    return out, alpha, a_src, a_dst, stats
+
+
+def _heads_aggregate(csr, gather, w_slot, H, x):
+    """out[r, h*C+c] = sum_k w_slot[k, h] * x[col_k, h*C+c] (mp_aggregate_heads_f32)."""
+    lib = _lib.load()
+    F = x.shape[1]
+    out = torch.empty((csr.n_rows, F), dtype=torch.float32, device=x.device)
+    if csr.n_rows == 0:
+        return out
+    g = csr.struct(gather)
+    sb = lib.mp_aggregate_slab_bytes(g, F, 0)
+    slab = torch.empty(sb, dtype=torch.uint8, device=x.device)
+    _lib.check(lib.mp_aggregate_heads_f32(g, w_slot.data_ptr(), H, x.data_ptr(), x.stride(0), F, out.data_ptr(),
+                                          out.stride(0), slab.data_ptr(), sb, _lib.MP_STAGE_ALL,
+                                          _lib.stream_ptr(x.device)), "mp_aggregate_heads_f32")
+    return out
 
 
 class _GatPropagate(torch.autograd.Function):
     @staticmethod
     def forward(ctx, xw, att, bias, graph, edge_index, H, C, slope, want_alpha):
-        need_grad = any(ctx.needs_input_grad[:3])
-        out, alpha, a_src, a_dst = _gat_forward(graph, edge_index, xw, att, H, C, slope, bias,
-                                                want_alpha or need_grad)
+        out, alpha, a_src, a_dst, stats = _gat_forward(graph, edge_index, xw, att, H, C, slope, bias, want_alpha)
         ctx.graph, ctx.H, ctx.C, ctx.slope = graph, H, C, slope
         ctx.has_bias = bias is not None
-        ctx.save_for_backward(xw, att, edge_index, alpha, a_src, a_dst)
+        ctx.save_for_backward(xw, att, edge_index, a_src, a_dst, stats)
         if alpha is not None:
             ctx.mark_non_differentiable(alpha)
         return out, alpha
 
     @staticmethod
     def backward(ctx, grad_out, _ga=None):
-        # Edge-level autograd of GATConv.message/softmax on [E,H] tensors; the
-        # [E,H*C] steps go through the native gather.  (Round-1 backward: the
-        # forward is the hot path.)
-        xw, att, edge_index, alpha, a_src, a_dst = ctx.saved_tensors
+        """Native GAT backward over the two CSRs of the graph:
+          dx_j   = sum_i alpha_ij g_i          (per-head weighted transposed aggregation)
+          dalpha = <g_i, xw_j> per head        (CSR SDDMM)
+          ds     = alpha (dalpha - sum_row alpha dalpha)   (softmax backward)
+          de     = ds * leaky'(s);  d a_dst = row sums, d a_src = column sums of de
+          dxw   += d a_src (x) att_src + d a_dst (x) att_dst;  d att = sum_n d a (x) xw
+        Only [E, H]-sized arrays are materialised, never [E, H*C]."""
+        lib = _lib.load()
+        xw, att, edge_index, a_src, a_dst, stats = ctx.saved_tensors
         graph, H, C, slope = ctx.graph, ctx.H, ctx.C, ctx.slope
-        N = xw.shape[0]
-        src = edge_index[graph.j]
-        dst = edge_index[graph.i]
+        dev = xw.device
+        st = _lib.stream_ptr(dev)
         g = grad_out.contiguous()
+        N = xw.shape[0]
         gb = g.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
-        xj = gather_rows(xw, src).view(-1, H, C)
-        gi = gather_rows(g, dst).view(-1, H, C)
-        # message grad: d out_i / d x_j = alpha
-        gx = torch.zeros_like(xw).view(-1, H, C)
-        gx.index_add_(0, src, gi * alpha.unsqueeze(-1))
-        # attention grad
-        dalpha = (gi * xj).sum(-1)                                   # [E,H]
-        rs = torch.zeros((graph.n_dst, H), dtype=torch.float32, device=xw.device)
-        rs.index_add_(0, dst, alpha * dalpha)
-        ds = alpha * (dalpha - rs[dst])
-        s = a_src[src] + a_dst[dst]
-        de = ds * torch.where(s > 0, torch.ones_like(s), torch.full_like(s, slope))
-        ga_src = torch.zeros_like(a_src).index_add_(0, src, de)
-        ga_dst = torch.zeros((graph.n_dst, H), dtype=torch.float32, device=xw.device).index_add_(0, dst, de)
+        dst, src = graph.dst, graph.src
+        E = dst.n_edges
+        sr = dst.slot_rows()
+        alpha = torch.empty((max(E, 1), H), dtype=torch.float32, device=dev)
+        score = torch.empty_like(alpha)
+        _lib.check(lib.mp_gat_alpha_csr_f32(dst.struct("other"), sr.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(),
+                                            H, float(slope), stats.data_ptr(), alpha.data_ptr(), score.data_ptr(),
+                                            st), "mp_gat_alpha_csr_f32")
+        eid_d = dst.eid[:E].long()
+        # message part of d xw: alpha in the transposed CSR's slot order
+        alpha_orig = torch.empty_like(alpha)
+        alpha_orig[eid_d] = alpha
+        alpha_src = alpha_orig[src.eid[:E].long()].contiguous()
+        gx = _heads_aggregate(src, "other", alpha_src, H, g)
+        # d alpha (CSR order) and the softmax backward
+        dalpha = torch.empty_like(alpha)
+        _lib.check(lib.mp_gat_sddmm_f32(dst.struct("other"), sr.data_ptr(), g.data_ptr(), g.stride(0), xw.data_ptr(),
+                                        xw.stride(0), H, C, dalpha.data_ptr(), st), "mp_gat_sddmm_f32")
+        t = (alpha * dalpha)[:E].contiguous()
+        rs, _ = _aggregate(dst, "slot", t, None, "sum", 0, None)             # sum over each row's slots
+        ds = alpha[:E] * (dalpha[:E] - rs[sr[:E].long()])
+        de = (ds * torch.where(score[:E] > 0, torch.ones_like(ds), torch.full_like(ds, slope))).contiguous()
+        ga_dst, _ = _aggregate(dst, "slot", de, None, "sum", 0, None)
+        de_orig = torch.empty_like(de)
+        de_orig[eid_d] = de
+        ga_src, _ = _aggregate(src, "eid", de_orig, None, "sum", 0, None)
         att3 = att.reshape(H, 2 * C)
-        x3 = xw.view(-1, H, C)
-        gx = gx + ga_src.unsqueeze(-1) * att3[:, C:].unsqueeze(0)
-        gx[:graph.n_dst] = gx[:graph.n_dst] + ga_dst.unsqueeze(-1) * att3[:, :C].unsqueeze(0)
+        x3 = xw.view(N, H, C)
+        gx = gx.view(N, H, C) + ga_src.unsqueeze(-1) * att3[:, C:].unsqueeze(0) \
+            + ga_dst.unsqueeze(-1) * att3[:, :C].unsqueeze(0)
         gatt = None
         if ctx.needs_input_grad[1]:
-            gd = (ga_dst.unsqueeze(-1) * x3[:graph.n_dst]).sum(0)
-            gs = (ga_src.unsqueeze(-1) * x3).sum(0)
+            gd = torch.einsum("nh,nhc->hc", ga_dst, x3)
+            gs = torch.einsum("nh,nhc->hc", ga_src, x3)
             gatt = torch.cat([gd, gs], dim=-1).view_as(att)
-        del N
-        return gx.view(-1, H * C), gatt, gb, None, None, None, None, None, None
+        return gx.reshape(N, H * C), gatt, gb, None, None, None, None, None, None
 
 
 def gat_propagate(graph, edge_index, xw, att, heads, out_channels, negative_slope=0.2, bias=None,
