@@ -124,6 +124,13 @@ struct AggArgs {
   float slope;
   float* row_stats;
   float* slab_s;
+  // GAT backward (transposed CSR: rows = source nodes j, col = destination i)
+  const float* y;     // xw, the row's own features (d alpha = <g_i, xw_j>)
+  int64_t ldy;
+  const float* rs;    // [n_cols, H]  sum_j alpha_ij d alpha_ij = <g_i, agg_i>
+  float* de;          // [n_edges, H] d score per slot (this CSR's slot order)
+  float* ga;          // [n_rows, H]  d a_src = row sums of d score
+  const float* att;   // [H, 2C]      (att_dst | att_src)
 };
 
 // ---------------------------------------------------------------------------
@@ -149,6 +156,8 @@ struct SumRed {
   static constexpr bool kEid = false;
   static constexpr bool kGat = false;
   static constexpr bool kHW = false;
+  static constexpr bool kGatB = false;
+  static constexpr bool kStat = false;
   struct Part {
     float v[VEC];
   };
@@ -223,6 +232,8 @@ struct ArgRed {
   static constexpr bool kEid = true;
   static constexpr bool kGat = false;
   static constexpr bool kHW = false;
+  static constexpr bool kGatB = false;
+  static constexpr bool kStat = false;
   struct Part {
     float v[VEC];
     int a[VEC];
@@ -330,6 +341,8 @@ struct GatRed {
   static constexpr bool kEid = false;
   static constexpr bool kGat = true;
   static constexpr bool kHW = false;
+  static constexpr bool kGatB = false;
+  static constexpr bool kStat = true;
   struct Part {
     float v[VEC];
     float m, s;
@@ -430,6 +443,110 @@ struct HeadSumRed : SumRed<VEC, true, false> {
                                                               h(act ? f / p.C : 0) {}
 };
 
+// GATConv backward in one pass over the TRANSPOSED CSR (row j = source node,
+// slots = its out-edges j->i in original edge order).  Per slot the gathered
+// row is g_i = d out_i, and with alpha_ij rebuilt from the forward's row
+// statistics (m_i, s_i + 1e-16):
+//   d xw_j    += alpha_ij g_i                               (message part)
+//   dalpha_ij  = <g_i, xw_j>_h                              (the row's own xw)
+//   de_ij      = alpha_ij (dalpha_ij - rs_i) leaky'(score)  (softmax + leaky_relu backward)
+//   d a_src_j += de_ij,  and at the row end d xw_j += d a_src_j (x) att_src.
+// rs_i = <g_i, agg_i>_h replaces the per-edge sum_j alpha_ij dalpha_ij, so no
+// [E, H*C] product is ever formed.  A head spans HL = C/VEC lanes (power of
+// two); its dot product is reduced with shuffle-xor inside the head group.
+template <int VEC>
+struct GatBwdRed {
+  static constexpr bool kW = false;
+  static constexpr bool kEid = false;
+  static constexpr bool kGat = false;
+  static constexpr bool kHW = false;
+  static constexpr bool kGatB = true;
+  static constexpr bool kStat = true;
+  struct Part {
+    float v[VEC];
+    float d;
+  };
+  float acc[VEC];
+  float y[VEC];
+  float dacc, as;
+  int h, hl;
+  bool leader;
+
+  __device__ GatBwdRed(const AggArgs& p, int f, bool act)
+      : h(act ? f / p.C : 0), hl(p.C / VEC), leader(act && ((f / VEC) & (p.C / VEC - 1)) == 0) {}
+
+  __device__ __forceinline__ void begin(const AggArgs& p, int64_t row, bool, int f, bool act) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
+    dacc = 0.f;
+    Frag<VEC> o = load_frag<VEC>(p.y + row * p.ldy + (act ? f : 0));
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) y[k] = act ? o.v[k] : 0.f;
+    as = p.a_src[row * p.H + h];
+  }
+  // head-group dot product <v, y> (all lanes of the head get the sum)
+  __device__ __forceinline__ float dot(const Frag<VEC>& v) const {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) t = __fadd_rn(t, __fmul_rn(v.v[k], y[k]));
+    for (int o = 1; o < hl; o <<= 1) t = __fadd_rn(t, __shfl_xor(t, o));
+    return t;
+  }
+  __device__ __forceinline__ void consume_gatb(const AggArgs& p, const Frag<VEC>& v, float dal, float ad,
+                                               float m, float den, float r, int64_t slot) {
+    const float sc = as + ad;
+    const float a = sc > 0.f ? sc : sc * p.slope;
+    const float alpha = expf(a - m) / den;
+    const float de = __fmul_rn(__fmul_rn(alpha, __fsub_rn(dal, r)), sc > 0.f ? 1.f : p.slope);
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = __fadd_rn(acc[k], __fmul_rn(alpha, v.v[k]));
+    dacc = __fadd_rn(dacc, de);
+    if (leader) p.de[slot * p.H + h] = de;
+  }
+  __device__ __forceinline__ void consume(const Frag<VEC>&, float, int, float) {}
+  __device__ __forceinline__ void save(PRef r, bool stat_writer) const {
+    Frag<VEC> o;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) o.v[k] = acc[k];
+    store_frag<VEC>(r.v, o);
+    if (stat_writer) r.st[0] = dacc;
+  }
+  static __device__ __forceinline__ Part load(PRef r) {
+    Frag<VEC> o = load_frag<VEC>(r.v);
+    Part q;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) q.v[k] = o.v[k];
+    q.d = r.st[0];
+    return q;
+  }
+  __device__ __forceinline__ void set(const Part& q) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = q.v[k];
+    dacc = q.d;
+  }
+  __device__ __forceinline__ void merge(const Part& q) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = __fadd_rn(acc[k], q.v[k]);
+    dacc = __fadd_rn(dacc, q.d);
+  }
+  __device__ __forceinline__ Part part() const {
+    Part q;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) q.v[k] = acc[k];
+    q.d = dacc;
+    return q;
+  }
+  __device__ __forceinline__ void finish(const AggArgs& p, int64_t row, int64_t, int f, bool act) {
+    if (!act) return;
+    const float* at = p.att + (int64_t)h * 2 * p.C + p.C + (f % p.C);
+    Frag<VEC> o;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) o.v[k] = __fadd_rn(acc[k], __fmul_rn(dacc, at[k]));
+    store_out<VEC>(p.out + row * p.ldo + f, o);
+    if (leader) p.ga[row * p.H + h] = dacc;
+  }
+};
+
 // this lane's share of slab slot s (2*task + kind)
 template <class Red>
 __device__ __forceinline__ PRef slab_ref(const AggArgs& p, int64_t s, int f, const Red& red) {
@@ -525,6 +642,7 @@ __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p, SlotWin<Re
     Frag<VEC> v[U];
     float as[U];
     [[maybe_unused]] float hw[U];
+    [[maybe_unused]] float ad[U], mm[U], dd[U], rr[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int uu = u < n ? u : n - 1;
@@ -542,12 +660,25 @@ __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p, SlotWin<Re
         v[u] = MP_NT_X ? load_frag_nt<VEC>(src) : load_frag<VEC>(src);
       }
       if constexpr (Red::kGat) as[u] = p.a_src[(int64_t)c * p.H + red.h];
+      if constexpr (Red::kGatB) {
+        const int64_t q = (int64_t)c * p.H + red.h;
+        ad[u] = p.a_dst[q];
+        mm[u] = p.row_stats[2 * q];
+        dd[u] = p.row_stats[2 * q + 1];
+        rr[u] = p.rs[q];
+      }
+    }
+    if constexpr (Red::kGatB) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) as[u] = red.dot(v[u]);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (u < n) {
         if constexpr (Red::kGat) {
           red.consume_gat(p, v[u], as[u]);
+        } else if constexpr (Red::kGatB) {
+          red.consume_gatb(p, v[u], as[u], ad[u], mm[u], dd[u], rr[u], e + u);
         } else {
           const float wt = Red::kHW ? hw[u] : (Red::kW ? GR::bc(win.w, off + u) : 1.f);
           const int ei = Red::kEid ? GR::bc(win.eid, off + u) : 0;
@@ -601,7 +732,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_main(AggArgs p) {
     if (e_begin < ce) {
       red.begin(p, r_first - 1, false, f, act);
       run_slots<Red, VEC, U, L, BUF>(red, p, win, e_begin, ce < e_end ? ce : e_end, foff, gl);
-      if (act) red.save(slab_ref(p, 2 * (int64_t)w, f, red), Red::kGat && (f % p.C == 0));
+      if (act) red.save(slab_ref(p, 2 * (int64_t)w, f, red), Red::kStat && (f % p.C == 0));
     }
   }
   // rows owned by this task
@@ -618,7 +749,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_main(AggArgs p) {
       red.finish(p, r, re - rs, f, act);
     } else {
       run_slots<Red, VEC, U, L, BUF>(red, p, win, rs, e_end, foff, gl);
-      if (act) red.save(slab_ref(p, 2 * (int64_t)w + 1, f, red), Red::kGat && (f % p.C == 0));
+      if (act) red.save(slab_ref(p, 2 * (int64_t)w + 1, f, red), Red::kStat && (f % p.C == 0));
     }
   }
 }
@@ -936,6 +1067,55 @@ int mp_gat_aggregate_f32(const mp_csr* g, const float* xw, const float* a_src, c
     case 2: return launch<GatRed<2>, 2>(a, stages, s);
     default: return launch<GatRed<1>, 1>(a, stages, s);
   }
+}
+
+int mp_gat_backward_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, const float* xw, const float* a_src,
+                        const float* a_dst, const float* row_stats, const float* rs, const float* att, int32_t H,
+                        int32_t C, float slope, float* grad_xw, float* grad_a_src, float* de, void* slab,
+                        size_t slab_bytes, int32_t stages, void* stream) {
+  int rc = check_graph(gt, "mp_gat_backward_f32");
+  if (rc) return rc;
+  MP_CHECK_ARG(H > 0 && C > 0, "mp_gat_backward_f32: H, C must be positive");
+  MP_CHECK_ARG(grad_out && xw && a_src && a_dst && row_stats && rs && att && grad_xw && grad_a_src &&
+                   (gt->n_edges == 0 || de),
+               "mp_gat_backward_f32: null pointer");
+  const int F = H * C;
+  MP_CHECK_ARG(ldg >= F, "mp_gat_backward_f32: ldg < H*C");
+  MP_CHECK_ARG(slab && slab_bytes >= mp_gat_slab_bytes(gt, H, C), "mp_gat_backward_f32: slab workspace too small");
+  AggArgs a{};
+  fill_graph(a, gt);
+  a.F = F;
+  a.x = grad_out;
+  a.ldx = ldg;
+  a.out = grad_xw;
+  a.ldo = F;
+  a.y = xw;
+  a.ldy = F;
+  a.a_src = a_src;
+  a.a_dst = a_dst;
+  a.row_stats = const_cast<float*>(row_stats);
+  a.rs = rs;
+  a.att = att;
+  a.de = de;
+  a.ga = grad_a_src;
+  a.H = H;
+  a.C = C;
+  a.slope = slope;
+  a.slab_ld = slab_ld_for(F);
+  size_t v = align_up(2 * (size_t)gt->n_waves * (size_t)a.slab_ld * 4, 256);
+  a.slab_v = (float*)slab;
+  a.slab_s = (float*)((char*)slab + v);
+  hipStream_t s = as_stream(stream);
+  auto pow2 = [](int q) { return q >= 1 && q <= 64 && (q & (q - 1)) == 0; };
+  const bool v4 = C % 4 == 0 && pow2(C / 4) && (uintptr_t)grad_out % 16 == 0 && ldg % 4 == 0 &&
+                  (uintptr_t)xw % 16 == 0 && (uintptr_t)grad_xw % 16 == 0;
+  if (v4) {
+    int lanes = F >= 256 ? MP_GAT_LANES : pick_shape(F, ldg, grad_out, F, grad_xw).lanes;
+    if (lanes < C / 4) lanes = C / 4;
+    return launch<GatBwdRed<4>, 4>(a, stages, s, lanes);
+  }
+  MP_CHECK_ARG(pow2(C), "mp_gat_backward_f32: C=%d needs C/4 or C to be a power of two <= 64", C);
+  return launch<GatBwdRed<1>, 1>(a, stages, s);
 }
 
 }  // extern "C"

@@ -99,6 +99,57 @@ __global__ void k_gat_sddmm_scalar(const int32_t* __restrict__ col, const int32_
   out[i] = t;
 }
 
+// out[n,h] = <a[n, hC:(h+1)C], b[n, hC:(h+1)C]>: one wave per node, lane l owns
+// 4 features, a head spans G = C/4 lanes (power of two) -> shuffle-xor sum.
+__global__ __launch_bounds__(256) void k_heads_rowdot_wave(const float* __restrict__ a, int64_t lda,
+                                                           const float* __restrict__ b, int64_t ldb, int64_t n,
+                                                           int32_t H, int32_t C, int32_t G,
+                                                           float* __restrict__ out) {
+  const int lane = lane_id();
+  const int64_t HC = (int64_t)H * C;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n; r += nw) {
+    for (int64_t base = 0; base < HC; base += 256) {
+      const int64_t f = base + lane * 4;
+      const bool act = f < HC;
+      const int64_t fs = act ? f : 0;
+      Frag<4> x = load_frag<4>(a + r * lda + fs);
+      Frag<4> y = load_frag<4>(b + r * ldb + fs);
+      float t = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) t = __fadd_rn(t, __fmul_rn(x.v[k], y.v[k]));
+      for (int o = 1; o < G; o <<= 1) t = __fadd_rn(t, __shfl_xor(t, o));
+      if (act && (lane & (G - 1)) == 0) out[r * H + fs / C] = t;
+    }
+  }
+}
+
+__global__ void k_heads_rowdot_scalar(const float* __restrict__ a, int64_t lda, const float* __restrict__ b,
+                                      int64_t ldb, int64_t n, int32_t H, int32_t C, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * (int64_t)H) return;
+  const int64_t r = i / H;
+  const int h = (int)(i % H);
+  const float* x = a + r * lda + (int64_t)h * C;
+  const float* y = b + r * ldb + (int64_t)h * C;
+  float t = 0.f;
+  for (int c = 0; c < C; ++c) t = __fadd_rn(t, __fmul_rn(x[c], y[c]));
+  out[i] = t;
+}
+
+// y[n, h*C + c] += s[n, h] * att[h*att_ld + c]
+__global__ void k_heads_outer_add(float* __restrict__ y, int64_t ldy, const float* __restrict__ s, int64_t n,
+                                  int32_t H, int32_t C, const float* __restrict__ att, int64_t att_ld) {
+  const int64_t F = (int64_t)H * C;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * F) return;
+  const int64_t r = i / F;
+  const int f = (int)(i % F);
+  const int h = f / C;
+  float* d = y + r * ldy + f;
+  *d = __fadd_rn(*d, __fmul_rn(s[r * H + h], att[(int64_t)h * att_ld + (f % C)]));
+}
+
 }  // namespace mp
 
 using namespace mp;
@@ -149,6 +200,40 @@ int mp_gat_sddmm_f32(const mp_csr* g, const int32_t* slot_row, const float* grow
     k_gat_sddmm_scalar<<<(unsigned)ceil_div(total, 256), 256, 0, s>>>(g->col, slot_row, g->n_edges, grow, ldg,
                                                                       x, ldx, H, C, out);
   }
+  MP_CHECK_LAUNCH();
+  return MP_OK;
+}
+
+int mp_heads_rowdot_f32(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t n, int32_t H, int32_t C,
+                        float* out, void* stream) {
+  MP_CHECK_ARG(H > 0 && C > 0 && n >= 0, "mp_heads_rowdot_f32: bad sizes");
+  if (n == 0) return MP_OK;
+  MP_CHECK_ARG(a && b && out, "mp_heads_rowdot_f32: null pointer");
+  const int64_t F = (int64_t)H * C;
+  MP_CHECK_ARG(lda >= F && ldb >= F, "mp_heads_rowdot_f32: leading dimension < H*C");
+  hipStream_t s = as_stream(stream);
+  const int G = C / 4;
+  const bool v4 = C % 4 == 0 && G <= 64 && (G & (G - 1)) == 0 && (uintptr_t)a % 16 == 0 &&
+                  (uintptr_t)b % 16 == 0 && lda % 4 == 0 && ldb % 4 == 0;
+  if (v4) {
+    int64_t blocks = ceil_div(n, 4);
+    if (blocks > 65536) blocks = 65536;
+    k_heads_rowdot_wave<<<(unsigned)blocks, 256, 0, s>>>(a, lda, b, ldb, n, H, C, G, out);
+  } else {
+    k_heads_rowdot_scalar<<<(unsigned)ceil_div(n * H, 256), 256, 0, s>>>(a, lda, b, ldb, n, H, C, out);
+  }
+  MP_CHECK_LAUNCH();
+  return MP_OK;
+}
+
+int mp_heads_outer_add_f32(float* y, int64_t ldy, const float* s, int64_t n, int32_t H, int32_t C, const float* att,
+                           int64_t att_ld, void* stream) {
+  MP_CHECK_ARG(H > 0 && C > 0 && n >= 0, "mp_heads_outer_add_f32: bad sizes");
+  if (n == 0) return MP_OK;
+  MP_CHECK_ARG(y && s && att && ldy >= (int64_t)H * C && att_ld >= C, "mp_heads_outer_add_f32: bad argument");
+  const int64_t total = n * H * C;
+  k_heads_outer_add<<<(unsigned)ceil_div(total, 256), 256, 0, as_stream(stream)>>>(y, ldy, s, n, H, C, att,
+                                                                                   att_ld);
   MP_CHECK_LAUNCH();
   return MP_OK;
 }

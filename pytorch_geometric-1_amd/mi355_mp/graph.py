@@ -73,10 +73,25 @@ class CSR:
         self._structs = {}
         self._deg = None
 
+    def add_gather(self, name, col, n_cols):
+        """Register a custom gather column (int32 [E]) under ``name`` for struct()."""
+        self._extra = getattr(self, "_extra", {})
+        self._extra[name] = (col.contiguous(), int(n_cols))
+        self._structs.pop(name, None)
+
     def struct(self, gather="other"):
         """ctypes mp_csr; gather='other' reads x[other] rows, 'eid' reads message
-        rows (original edge order), 'slot' reads rows already in CSR slot order."""
+        rows (original edge order), 'slot' reads rows already in CSR slot order;
+        other names are columns registered with add_gather()."""
         s = self._structs.get(gather)
+        extra = getattr(self, "_extra", {})
+        if s is None and gather in extra:
+            col, n_cols = extra[gather]
+            s = _lib.MpCsr(self.rowptr.data_ptr(), col.data_ptr(), self.eid.data_ptr(),
+                           self.wave_row.data_ptr(), self.wave_slot.data_ptr(),
+                           self.split_waves.data_ptr(), self.n_rows, self.n_edges, self.chunk,
+                           self.n_waves, self.n_split, n_cols)
+            self._structs[gather] = s
         if s is None:
             if gather == "slot":
                 if getattr(self, "_ident", None) is None:
@@ -163,6 +178,21 @@ class Graph:
             ei = self._edge_index()
             self._src = CSR(ei[self.j], ei[self.i], self.n_src, self.n_dst, self.chunk)
         return self._src
+
+    def dst_gather_src_slots(self):
+        """Registers on the dst CSR the gather 'src_slot': for each dst slot, the
+        slot of the same edge in the src CSR, so per-edge values produced in
+        src-CSR order are reduced over dst rows without a permutation pass."""
+        dst = self.dst
+        if "src_slot" not in getattr(dst, "_extra", {}):
+            src = self.src
+            E = dst.n_edges
+            inv = torch.empty(max(E, 1), dtype=torch.int32, device=dst.device)
+            if E:
+                inv[src.eid[:E].long()] = torch.arange(E, dtype=torch.int32, device=dst.device)
+            m = dst.to_csr_order(inv.view(torch.float32)).view(torch.int32)  # bit copy: m[k] = inv[eid[k]]
+            dst.add_gather("src_slot", m, E)
+        return dst
 
 
 class _Cache:

@@ -323,13 +323,66 @@ def _heads_aggregate(csr, gather, w_slot, H, x):
     return out
 
 
+def _gat_bwd_fused_ok(C):
+    """mp_gat_backward_f32 reduces a head's dot product over C/4 (or C) lanes."""
+    def pow2(q):
+        return 1 <= q <= 64 and (q & (q - 1)) == 0
+    return (C % 4 == 0 and pow2(C // 4)) or pow2(C)
+
+
+def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope, want_att):
+    """GATConv backward in one gather pass over the transposed CSR
+    (mp_gat_backward_f32), then the d a_dst row sums over the dst CSR (reading
+    the per-edge d score through the src-slot map) and the att_dst term."""
+    lib = _lib.load()
+    dev = xw.device
+    st = _lib.stream_ptr(dev)
+    N = xw.shape[0]
+    F = H * C
+    att_c = att.reshape(H, 2 * C).contiguous()
+    rs = torch.empty((N, H), dtype=torch.float32, device=dev)
+    _lib.check(lib.mp_heads_rowdot_f32(g.data_ptr(), g.stride(0), agg.data_ptr(), agg.stride(0), N, H, C,
+                                       rs.data_ptr(), st), "mp_heads_rowdot_f32")
+    src = graph.src
+    E = src.n_edges
+    gx = torch.empty((N, F), dtype=torch.float32, device=dev)
+    ga_src = torch.empty((N, H), dtype=torch.float32, device=dev)
+    de = torch.empty((max(E, 1), H), dtype=torch.float32, device=dev)
+    gs = src.struct("other")
+    sb = lib.mp_gat_slab_bytes(gs, H, C)
+    slab = torch.empty(sb, dtype=torch.uint8, device=dev)
+    _lib.check(lib.mp_gat_backward_f32(gs, g.data_ptr(), g.stride(0), xw.data_ptr(), a_src.data_ptr(),
+                                       a_dst.data_ptr(), stats.data_ptr(), rs.data_ptr(), att_c.data_ptr(), H, C,
+                                       float(slope), gx.data_ptr(), ga_src.data_ptr(), de.data_ptr(),
+                                       slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st), "mp_gat_backward_f32")
+    del slab
+    dst = graph.dst_gather_src_slots()
+    ga_dst, _ = _aggregate(dst, "src_slot", de, None, "sum", 0, None)
+    _lib.check(lib.mp_heads_outer_add_f32(gx.data_ptr(), gx.stride(0), ga_dst.data_ptr(), N, H, C,
+                                          att_c.data_ptr(), 2 * C, st), "mp_heads_outer_add_f32")
+    gatt = None
+    if want_att:
+        x3 = xw.view(N, H, C)
+        gatt = torch.cat([torch.einsum("nh,nhc->hc", ga_dst, x3), torch.einsum("nh,nhc->hc", ga_src, x3)],
+                         dim=-1).view_as(att)
+    return gx, gatt
+
+
 class _GatPropagate(torch.autograd.Function):
     @staticmethod
     def forward(ctx, xw, att, bias, graph, edge_index, H, C, slope, want_alpha):
-        out, alpha, a_src, a_dst, stats = _gat_forward(graph, edge_index, xw, att, H, C, slope, bias, want_alpha)
+        fused = any(ctx.needs_input_grad[:3]) and _gat_bwd_fused_ok(C)
+        # the fused backward needs the pre-bias aggregate (rs_i = <g_i, agg_i>)
+        out, alpha, a_src, a_dst, stats = _gat_forward(graph, edge_index, xw, att, H, C, slope,
+                                                       None if fused else bias, want_alpha)
+        agg = None
+        if fused:
+            agg = out
+            out = agg + bias if bias is not None else agg.clone()
         ctx.graph, ctx.H, ctx.C, ctx.slope = graph, H, C, slope
         ctx.has_bias = bias is not None
-        ctx.save_for_backward(xw, att, edge_index, a_src, a_dst, stats)
+        ctx.fused = fused
+        ctx.save_for_backward(xw, att, edge_index, a_src, a_dst, stats, agg)
         if alpha is not None:
             ctx.mark_non_differentiable(alpha)
         return out, alpha
@@ -344,13 +397,17 @@ class _GatPropagate(torch.autograd.Function):
           dxw   += d a_src (x) att_src + d a_dst (x) att_dst;  d att = sum_n d a (x) xw
         Only [E, H]-sized arrays are materialised, never [E, H*C]."""
         lib = _lib.load()
-        xw, att, edge_index, a_src, a_dst, stats = ctx.saved_tensors
+        xw, att, edge_index, a_src, a_dst, stats, agg = ctx.saved_tensors
         graph, H, C, slope = ctx.graph, ctx.H, ctx.C, ctx.slope
         dev = xw.device
         st = _lib.stream_ptr(dev)
         g = grad_out.contiguous()
         N = xw.shape[0]
         gb = g.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        if ctx.fused:
+            gx, gatt = _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope,
+                                           ctx.needs_input_grad[1])
+            return gx, gatt, gb, None, None, None, None, None, None
         dst, src = graph.dst, graph.src
         E = dst.n_edges
         sr = dst.slot_rows()

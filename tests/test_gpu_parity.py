@@ -711,10 +711,12 @@ def test_gat_dropout_training_uses_generic_path():
     assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("H,C", [(8, 32), (3, 5), (1, 64), (4, 100)])
+@pytest.mark.parametrize("H,C", [(8, 32), (3, 5), (1, 64), (4, 100), (2, 16), (4, 8), (1, 256), (2, 2)])
 def test_gat_native_backward_pieces(H, C):
     """GAT backward vs float64 autograd of the reference formula, several
-    head shapes (power-of-two and odd C: vector and scalar SDDMM paths)."""
+    head shapes: C/4 a power of two (fused transposed-CSR pass, head groups of
+    1..64 lanes), C a power of two (fused, one feature per lane), and other C
+    (alpha + heads aggregation + SDDMM pieces)."""
     from torch_geometric.nn import GATConv
     _, _, _, _, pl = _mods()
     N, E, Fi = 350, 5000, 12
@@ -752,3 +754,48 @@ def test_aggregate_heads_direct():
     want = S.scatter_sum(msg, ei[1], N)
     terms = S.scatter_sum(msg.abs(), ei[1], N)
     _bound_ok(out, want, terms)
+
+
+def test_gat_fused_backward_hub_rows_split_across_tasks():
+    """A star whose centre has thousands of out- and in-edges: its rows in both
+    CSRs span many merge-path tasks (fix-up partials carry the d a_src sums)."""
+    from torch_geometric.nn import GATConv
+    from mi355_mp import ops
+    N, Fi, H, C = 3000, 8, 4, 16
+    leaves = torch.arange(1, N)
+    g = torch.Generator().manual_seed(31)
+    extra = torch.randint(0, N, (2, 4000), generator=g)
+    ei = torch.cat([torch.stack([torch.zeros(N - 1, dtype=torch.long), leaves]),
+                    torch.stack([leaves, torch.zeros(N - 1, dtype=torch.long)]), extra], 1)
+    x = torch.randn(N, Fi, generator=g)
+    conv = GATConv(Fi, C, heads=H).to(DEV)
+    with torch.no_grad():
+        conv.bias.normal_()
+    xd = x.to(DEV).requires_grad_(True)
+    gout = torch.randn(N, H * C, generator=g)
+    assert ops._gat_bwd_fused_ok(C)
+    conv(xd, ei.to(DEV)).backward(gout.to(DEV))
+    W = conv.weight.detach().cpu().double().requires_grad_(True)
+    att = conv.att.detach().cpu().double().requires_grad_(True)
+    b = conv.bias.detach().cpu().double().requires_grad_(True)
+    x64 = x.double().requires_grad_(True)
+    P.gat_conv(x64, ei, W, att, b, H, C).backward(gout.double())
+    for got, want in ((xd.grad, x64.grad), (conv.weight.grad, W.grad), (conv.att.grad, att.grad),
+                      (conv.bias.grad, b.grad)):
+        assert torch.allclose(got.cpu().double(), want, rtol=1e-4, atol=1e-4)
+
+
+def test_gat_forward_identical_with_and_without_grad():
+    """Training mode adds the bias outside the kernel (the backward keeps the
+    pre-bias aggregate): the same fp32 add, so the output is bit-identical."""
+    from torch_geometric.nn import GATConv
+    _, _, _, _, pl = _mods()
+    N, E, Fi, H, C = 500, 6000, 16, 4, 32
+    ei = pl(N, E, seed=12).to(DEV)
+    x = torch.randn(N, Fi, generator=torch.Generator().manual_seed(12)).to(DEV)
+    conv = GATConv(Fi, C, heads=H).to(DEV)
+    with torch.no_grad():
+        conv.bias.normal_()
+        a = conv(x, ei)
+    b = conv(x.requires_grad_(True), ei)
+    assert torch.equal(a, b.detach())

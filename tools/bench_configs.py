@@ -149,9 +149,59 @@ def c5(dev):
            4 * F + 8, 4 * F + 4, ms_main, ms_main + ms_fix, {"fixup_ms": ms_fix, "n_split": csr.n_split})
 
 
+def _train_step_ms(conv, x, ei):
+    def step():
+        out = conv(x, ei)
+        out.backward(torch.ones_like(out))
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(5):
+        step()
+    b.record()
+    torch.cuda.synchronize()
+    fwd_a, fwd_b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.no_grad():
+        conv(x, ei)
+        fwd_a.record()
+        for _ in range(5):
+            conv(x, ei)
+        fwd_b.record()
+    torch.cuda.synchronize()
+    return fwd_a.elapsed_time(fwd_b) / 5, a.elapsed_time(b) / 5
+
+
+def c2train(dev):
+    """Full GCNConv(256, 256) layer on config 2: x@W + fused aggregation (+ backward:
+    transposed-CSR aggregation, GEMM grads)."""
+    from mi355_mp.graphgen import rmat_edge_index
+    from torch_geometric.nn import GCNConv
+    N = 1 << 21
+    ei = rmat_edge_index(scale=21, n_samples=30_000_000, seed=1, device=dev)
+    x = torch.randn(N, 256, device=dev).requires_grad_(True)
+    conv = GCNConv(256, 256, cached=True).to(dev)
+    fwd, step = _train_step_ms(conv, x, ei)
+    print(json.dumps({"config": "c2train", "desc": "GCNConv(256,256) layer on RMAT21, cached=True",
+                      "forward_ms": fwd, "forward_backward_ms": step}), flush=True)
+
+
+def c3train(dev):
+    from mi355_mp.graphgen import rmat_edge_index
+    from torch_geometric.nn import GATConv
+    N = 1 << 21
+    ei = rmat_edge_index(scale=21, n_samples=30_000_000, seed=1, device=dev)
+    x = torch.randn(N, 256, device=dev).requires_grad_(True)
+    conv = GATConv(256, 32, heads=8).to(dev)
+    fwd, step = _train_step_ms(conv, x, ei)
+    print(json.dumps({"config": "c3train", "desc": "GATConv(256, 32, heads=8) layer on RMAT21",
+                      "forward_ms": fwd, "forward_backward_ms": step}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="c3,c4,c5")
+    ap.add_argument("--configs", default="c3,c4,c5,c2train,c3train")
     args = ap.parse_args()
     import mi355_mp
     mi355_mp.load_native()
