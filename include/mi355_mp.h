@@ -187,22 +187,24 @@ int mp_gat_sddmm_f32(const mp_csr* g, const int32_t* slot_row, const float* grow
  * col = destination i, slots in original edge order).  Replaces the autograd
  * of GATConv.message + utils.softmax + scatter_add (PyG 1.4.3 [U3,U6];
  * /root/reference/ConvexPruning.py:209-214) with one gather of grad_out rows:
- *   grad_xw[j]     = sum_i alpha_ij g_i + grad_a_src[j,h] * att[h, C:]
- *   de[k, h]       = alpha_ij (<g_i, xw_j>_h - rs[i,h]) leaky'(a_src[j,h]+a_dst[i,h])
- *   grad_a_src[j,h]= sum over the row of de
+ *   grad_xw[j]      = sum_i alpha_ij g_i + grad_a_src[j,h] * att[h, C:]
+ *   de[k, h]        = alpha_ij (<g_i, xw_j>_h - rs[i,h]) leaky'(a_src[j,h]+a_dst[i,h])
+ *   grad_a_src[j,h] = sum over the row of de
  * alpha_ij = exp(leaky(score) - m_i) / den_i from the forward's row_stats.
- * rs[i,h] = <g_i, agg_i>_h (mp_heads_rowdot_f32 of grad_out and the pre-bias
- * aggregate).  de is written in gt's slot order.  Needs C/4 or C to be a power
- * of two <= 64.  Slab: mp_gat_slab_bytes(gt, H, C). */
+ * pack [n_dst, H, 4] = mp_gat_backward_prep_f32 output.  de is written in gt's
+ * slot order.  Needs C/4 or C to be a power of two <= 64.
+ * Slab: mp_gat_slab_bytes(gt, H, C). */
 int mp_gat_backward_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, const float* xw,
-                        const float* a_src, const float* a_dst, const float* row_stats,
-                        const float* rs, const float* att, int32_t H, int32_t C, float slope,
-                        float* grad_xw, float* grad_a_src, float* de, void* slab,
-                        size_t slab_bytes, int32_t stages, void* stream);
+                        const float* a_src, const float* pack, const float* att, int32_t H,
+                        int32_t C, float slope, float* grad_xw, float* grad_a_src, float* de,
+                        void* slab, size_t slab_bytes, int32_t stages, void* stream);
 
-/* out[n,h] = sum_c a[n, h*C+c] * b[n, h*C+c] */
-int mp_heads_rowdot_f32(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t n,
-                        int32_t H, int32_t C, float* out, void* stream);
+/* pack[n,h,:] = (a_dst[n,h], m[n,h], 1/den[n,h], rs[n,h]) with
+ * rs[n,h] = sum_c grad_out[n, h*C+c] * agg[n, h*C+c]  (agg = pre-bias GAT output;
+ * rs = sum_j alpha_nj <g_n, xw_j>_h, the softmax-backward row term). */
+int mp_gat_backward_prep_f32(const float* grad_out, int64_t ldg, const float* agg, int64_t lda,
+                             const float* a_dst, const float* row_stats, int64_t n, int32_t H,
+                             int32_t C, float* pack, void* stream);
 
 /* y[n, h*C+c] += s[n,h] * att[h*att_ld + c]  (per-head outer-product update) */
 int mp_heads_outer_add_f32(float* y, int64_t ldy, const float* s, int64_t n, int32_t H,

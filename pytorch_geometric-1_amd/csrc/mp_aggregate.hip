@@ -127,7 +127,7 @@ struct AggArgs {
   // GAT backward (transposed CSR: rows = source nodes j, col = destination i)
   const float* y;     // xw, the row's own features (d alpha = <g_i, xw_j>)
   int64_t ldy;
-  const float* rs;    // [n_cols, H]  sum_j alpha_ij d alpha_ij = <g_i, agg_i>
+  const f32x4* pack;  // [n_cols, H]  (a_dst, m, 1/den, rs) of the destination, rs = <g_i, agg_i>_h
   float* de;          // [n_edges, H] d score per slot (this CSR's slot order)
   float* ga;          // [n_rows, H]  d a_src = row sums of d score
   const float* att;   // [H, 2C]      (att_dst | att_src)
@@ -164,6 +164,7 @@ struct SumRed {
   float acc[VEC];
   int h = 0;  // unused (GAT only)
 
+  __device__ SumRed() {}
   __device__ SumRed(const AggArgs&, int, bool) {}
 
   __device__ __forceinline__ void begin(const AggArgs& p, int64_t row, bool owned, int f, bool act) {
@@ -243,6 +244,7 @@ struct ArgRed {
   int h = 0;
   int sentinel;
 
+  __device__ ArgRed() {}
   __device__ ArgRed(const AggArgs& p, int, bool) : sentinel((int)p.n_edges) {}
 
   static __device__ __forceinline__ float init_val() { return IS_MAX ? -FLT_MAX : FLT_MAX; }
@@ -446,14 +448,17 @@ struct HeadSumRed : SumRed<VEC, true, false> {
 // GATConv backward in one pass over the TRANSPOSED CSR (row j = source node,
 // slots = its out-edges j->i in original edge order).  Per slot the gathered
 // row is g_i = d out_i, and with alpha_ij rebuilt from the forward's row
-// statistics (m_i, s_i + 1e-16):
+// statistics (m_i, 1/(s_i + 1e-16)):
 //   d xw_j    += alpha_ij g_i                               (message part)
 //   dalpha_ij  = <g_i, xw_j>_h                              (the row's own xw)
 //   de_ij      = alpha_ij (dalpha_ij - rs_i) leaky'(score)  (softmax + leaky_relu backward)
 //   d a_src_j += de_ij,  and at the row end d xw_j += d a_src_j (x) att_src.
 // rs_i = <g_i, agg_i>_h replaces the per-edge sum_j alpha_ij dalpha_ij, so no
-// [E, H*C] product is ever formed.  A head spans HL = C/VEC lanes (power of
-// two); its dot product is reduced with shuffle-xor inside the head group.
+// [E, H*C] product is ever formed.  The destination's (a_dst, m, 1/den, rs)
+// come packed in one float4 per (node, head): one 16-byte gather per slot.
+// A head spans HL = C/VEC lanes (power of two); its dot product is reduced
+// with DPP adds inside the head group.  Gradients are checked to a
+// tolerance, so this pass uses FMA and the hardware exp.
 template <int VEC>
 struct GatBwdRed {
   static constexpr bool kW = false;
@@ -486,21 +491,20 @@ struct GatBwdRed {
   }
   // head-group dot product <v, y> (all lanes of the head get the sum)
   __device__ __forceinline__ float dot(const Frag<VEC>& v) const {
-    float t = 0.f;
+    float t = v.v[0] * y[0];
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) t = __fadd_rn(t, __fmul_rn(v.v[k], y[k]));
-    for (int o = 1; o < hl; o <<= 1) t = __fadd_rn(t, __shfl_xor(t, o));
-    return t;
+    for (int k = 1; k < VEC; ++k) t = __builtin_fmaf(v.v[k], y[k], t);
+    return group_sum(t, hl);
   }
-  __device__ __forceinline__ void consume_gatb(const AggArgs& p, const Frag<VEC>& v, float dal, float ad,
-                                               float m, float den, float r, int64_t slot) {
-    const float sc = as + ad;
-    const float a = sc > 0.f ? sc : sc * p.slope;
-    const float alpha = expf(a - m) / den;
-    const float de = __fmul_rn(__fmul_rn(alpha, __fsub_rn(dal, r)), sc > 0.f ? 1.f : p.slope);
+  __device__ __forceinline__ void consume_gatb(const AggArgs& p, const Frag<VEC>& v, float dal, f32x4 q,
+                                               int64_t slot) {
+    const float sc = as + q.x;
+    const float lk = sc > 0.f ? 1.f : p.slope;
+    const float alpha = __expf(sc * lk - q.y) * q.z;
+    const float de = alpha * (dal - q.w) * lk;
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) acc[k] = __fadd_rn(acc[k], __fmul_rn(alpha, v.v[k]));
-    dacc = __fadd_rn(dacc, de);
+    for (int k = 0; k < VEC; ++k) acc[k] = __builtin_fmaf(alpha, v.v[k], acc[k]);
+    dacc += de;
     if (leader) p.de[slot * p.H + h] = de;
   }
   __device__ __forceinline__ void consume(const Frag<VEC>&, float, int, float) {}
@@ -526,8 +530,8 @@ struct GatBwdRed {
   }
   __device__ __forceinline__ void merge(const Part& q) {
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) acc[k] = __fadd_rn(acc[k], q.v[k]);
-    dacc = __fadd_rn(dacc, q.d);
+    for (int k = 0; k < VEC; ++k) acc[k] += q.v[k];
+    dacc += q.d;
   }
   __device__ __forceinline__ Part part() const {
     Part q;
@@ -541,7 +545,7 @@ struct GatBwdRed {
     const float* at = p.att + (int64_t)h * 2 * p.C + p.C + (f % p.C);
     Frag<VEC> o;
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) o.v[k] = __fadd_rn(acc[k], __fmul_rn(dacc, at[k]));
+    for (int k = 0; k < VEC; ++k) o.v[k] = __builtin_fmaf(dacc, at[k], acc[k]);
     store_out<VEC>(p.out + row * p.ldo + f, o);
     if (leader) p.ga[row * p.H + h] = dacc;
   }
@@ -642,7 +646,7 @@ __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p, SlotWin<Re
     Frag<VEC> v[U];
     float as[U];
     [[maybe_unused]] float hw[U];
-    [[maybe_unused]] float ad[U], mm[U], dd[U], rr[U];
+    [[maybe_unused]] f32x4 pk[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int uu = u < n ? u : n - 1;
@@ -660,13 +664,7 @@ __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p, SlotWin<Re
         v[u] = MP_NT_X ? load_frag_nt<VEC>(src) : load_frag<VEC>(src);
       }
       if constexpr (Red::kGat) as[u] = p.a_src[(int64_t)c * p.H + red.h];
-      if constexpr (Red::kGatB) {
-        const int64_t q = (int64_t)c * p.H + red.h;
-        ad[u] = p.a_dst[q];
-        mm[u] = p.row_stats[2 * q];
-        dd[u] = p.row_stats[2 * q + 1];
-        rr[u] = p.rs[q];
-      }
+      if constexpr (Red::kGatB) pk[u] = p.pack[(int64_t)c * p.H + red.h];
     }
     if constexpr (Red::kGatB) {
 #pragma unroll
@@ -678,7 +676,7 @@ __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p, SlotWin<Re
         if constexpr (Red::kGat) {
           red.consume_gat(p, v[u], as[u]);
         } else if constexpr (Red::kGatB) {
-          red.consume_gatb(p, v[u], as[u], ad[u], mm[u], dd[u], rr[u], e + u);
+          red.consume_gatb(p, v[u], as[u], pk[u], e + u);
         } else {
           const float wt = Red::kHW ? hw[u] : (Red::kW ? GR::bc(win.w, off + u) : 1.f);
           const int ei = Red::kEid ? GR::bc(win.eid, off + u) : 0;
@@ -751,6 +749,84 @@ __global__ __launch_bounds__(kBlock) void k_agg_main(AggArgs p) {
       run_slots<Red, VEC, U, L, BUF>(red, p, win, rs, e_end, foff, gl);
       if (act) red.save(slab_ref(p, 2 * (int64_t)w + 1, f, red), Red::kStat && (f % p.C == 0));
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Narrow rows (F <= 16): one merge-path task per LANE.  A lane holds the whole
+// row (NV fragments of VEC features, one reducer each) and walks its task's
+// slots in CSR order with U slots' loads in flight, so a wave keeps 64*U row
+// gathers outstanding instead of 64/L*L.  Same schedule, slab layout and
+// fix-up as k_agg_main; rows stay sequential, so results are identical.
+// ---------------------------------------------------------------------------
+template <class Red, int VEC, int NV, int U>
+__device__ __forceinline__ void lane_slots(Red (&red)[NV], const AggArgs& p, int64_t s, int64_t t) {
+  for (int64_t e = s; e < t; e += U) {
+    const int64_t n = t - e < U ? t - e : U;
+    int c[U];
+    [[maybe_unused]] float wt[U];
+    [[maybe_unused]] int ei[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t k = e + (u < n ? u : n - 1);
+      c[u] = p.col[k];
+      if constexpr (Red::kW) wt[u] = p.w[k];
+      if constexpr (Red::kEid) ei[u] = p.eid[k];
+    }
+    Frag<VEC> v[U][NV];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float* row = p.x + (int64_t)c[u] * p.ldx;
+#pragma unroll
+      for (int q = 0; q < NV; ++q) v[u][q] = load_frag<VEC>(row + (q * VEC < p.F ? q * VEC : 0));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u < n) {
+#pragma unroll
+        for (int q = 0; q < NV; ++q)
+          red[q].consume(v[u][q], Red::kW ? wt[u] : 1.f, Red::kEid ? ei[u] : 0, 0.f);
+      }
+    }
+  }
+}
+
+template <class Red, int VEC, int NV, int U>
+__global__ __launch_bounds__(kBlock) void k_agg_lane(AggArgs p) {
+  const int w = (int)(blockIdx.x * kBlock + threadIdx.x);
+  if (w >= p.n_waves) return;
+  const int r_first = p.wave_row[w];
+  const int r_last = p.wave_row[w + 1];
+  const int64_t e_begin = p.wave_slot[w];
+  const int64_t e_end = p.wave_slot[w + 1];
+  Red red[NV];
+#pragma unroll
+  for (int q = 0; q < NV; ++q) red[q] = Red(p, q * VEC, q * VEC < p.F);
+  const int64_t ce = p.rowptr[r_first];
+  if (e_begin < ce) {
+#pragma unroll
+    for (int q = 0; q < NV; ++q) red[q].begin(p, r_first - 1, false, q * VEC, q * VEC < p.F);
+    lane_slots<Red, VEC, NV, U>(red, p, e_begin, ce < e_end ? ce : e_end);
+#pragma unroll
+    for (int q = 0; q < NV; ++q)
+      if (q * VEC < p.F) red[q].save(slab_ref(p, 2 * (int64_t)w, q * VEC, red[q]), false);
+  }
+  int64_t rs = ce;
+  for (int r = r_first; r < r_last; ++r) {
+    const int64_t re = p.rowptr[r + 1];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) red[q].begin(p, r, true, q * VEC, q * VEC < p.F);
+    if (re <= e_end) {
+      lane_slots<Red, VEC, NV, U>(red, p, rs, re);
+#pragma unroll
+      for (int q = 0; q < NV; ++q) red[q].finish(p, r, re - rs, q * VEC, q * VEC < p.F);
+    } else {
+      lane_slots<Red, VEC, NV, U>(red, p, rs, e_end);
+#pragma unroll
+      for (int q = 0; q < NV; ++q)
+        if (q * VEC < p.F) red[q].save(slab_ref(p, 2 * (int64_t)w + 1, q * VEC, red[q]), false);
+    }
+    rs = re;
   }
 }
 
@@ -877,6 +953,46 @@ static int launch_l(const AggArgs& a, int stages, hipStream_t s) {
   return MP_OK;
 }
 
+#ifndef MP_LANE_MAX_F
+#define MP_LANE_MAX_F 8    // rows of 2..this many features: one task per lane (0: off; A/B: wins at F=4,8, loses at 1,16)
+#endif
+#ifndef MP_U_LANE
+#define MP_U_LANE 8        // slots in flight per lane task
+#endif
+
+template <class Red, int VEC, int NV>
+static int launch_lane(const AggArgs& a, int stages, hipStream_t s) {
+  if (stages & MP_STAGE_MAIN) {
+    dim3 grid((unsigned)ceil_div(a.n_waves, kBlock));
+    constexpr int U = VEC * NV >= 16 ? (MP_U_LANE + 1) / 2 : MP_U_LANE;  // 16-float rows: keep VGPRs < 128
+    hipLaunchKernelGGL((k_agg_lane<Red, VEC, NV, U>), grid, dim3(kBlock), 0, s, a);
+    MP_CHECK_LAUNCH();
+  }
+  if ((stages & MP_STAGE_FIXUP) && a.n_split > 0) {
+    dim3 grid((unsigned)a.n_split, (unsigned)ceil_div(a.F, 64 * VEC));
+    hipLaunchKernelGGL((k_agg_fixup<Red, VEC>), grid, dim3(kBlock), 0, s, a);
+    MP_CHECK_LAUNCH();
+  }
+  return MP_OK;
+}
+
+// lane-task shape for F <= MP_LANE_MAX_F: VEC=4 with NV in {1,2,4} or VEC=1
+// with NV in {4,8,16}; -1 when the row is too wide
+template <class Red, int VEC>
+static int try_lane(const AggArgs& a, int stages, hipStream_t s) {
+  if (a.F > MP_LANE_MAX_F || a.F > 16 || a.F < 2) return -1;
+  if constexpr (VEC == 4) {
+    if (a.F <= 4) return launch_lane<Red, 4, 1>(a, stages, s);
+    if (a.F <= 8) return launch_lane<Red, 4, 2>(a, stages, s);
+    return launch_lane<Red, 4, 4>(a, stages, s);
+  } else if constexpr (VEC == 1) {
+    if (a.F <= 4) return launch_lane<Red, 1, 4>(a, stages, s);
+    if (a.F <= 8) return launch_lane<Red, 1, 8>(a, stages, s);
+    return launch_lane<Red, 1, 16>(a, stages, s);
+  }
+  return -1;
+}
+
 template <class Red, int VEC>
 static int launch(const AggArgs& a, int stages, hipStream_t s, int lanes = 64) {
   if constexpr (VEC == 4) {
@@ -891,22 +1007,31 @@ static int launch(const AggArgs& a, int stages, hipStream_t s, int lanes = 64) {
   return launch_l<Red, VEC, 64>(a, stages, s);
 }
 
+template <class Red, int VEC>
+static int launch_any(const AggArgs& a, int stages, hipStream_t s, int L) {
+  if constexpr (VEC != 2) {
+    int rc = try_lane<Red, VEC>(a, stages, s);
+    if (rc >= 0) return rc;
+  }
+  return launch<Red, VEC>(a, stages, s, L);
+}
+
 template <int VEC>
 static int dispatch_reduce(const AggArgs& a, int reduce, int stages, hipStream_t s, int L) {
   const bool hw = a.w != nullptr;
   switch (reduce) {
     case MP_REDUCE_SUM:
-      return hw ? launch<SumRed<VEC, true, false>, VEC>(a, stages, s, L)
-                : launch<SumRed<VEC, false, false>, VEC>(a, stages, s, L);
+      return hw ? launch_any<SumRed<VEC, true, false>, VEC>(a, stages, s, L)
+                : launch_any<SumRed<VEC, false, false>, VEC>(a, stages, s, L);
     case MP_REDUCE_MEAN:
-      return hw ? launch<SumRed<VEC, true, true>, VEC>(a, stages, s, L)
-                : launch<SumRed<VEC, false, true>, VEC>(a, stages, s, L);
+      return hw ? launch_any<SumRed<VEC, true, true>, VEC>(a, stages, s, L)
+                : launch_any<SumRed<VEC, false, true>, VEC>(a, stages, s, L);
     case MP_REDUCE_MAX:
-      return hw ? launch<ArgRed<VEC, true, true>, VEC>(a, stages, s, L)
-                : launch<ArgRed<VEC, false, true>, VEC>(a, stages, s, L);
+      return hw ? launch_any<ArgRed<VEC, true, true>, VEC>(a, stages, s, L)
+                : launch_any<ArgRed<VEC, false, true>, VEC>(a, stages, s, L);
     case MP_REDUCE_MIN:
-      return hw ? launch<ArgRed<VEC, true, false>, VEC>(a, stages, s, L)
-                : launch<ArgRed<VEC, false, false>, VEC>(a, stages, s, L);
+      return hw ? launch_any<ArgRed<VEC, true, false>, VEC>(a, stages, s, L)
+                : launch_any<ArgRed<VEC, false, false>, VEC>(a, stages, s, L);
   }
   set_error("mp_aggregate_f32: unknown reduce %d", reduce);
   return MP_ERR_ARG;
@@ -1070,15 +1195,14 @@ int mp_gat_aggregate_f32(const mp_csr* g, const float* xw, const float* a_src, c
 }
 
 int mp_gat_backward_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, const float* xw, const float* a_src,
-                        const float* a_dst, const float* row_stats, const float* rs, const float* att, int32_t H,
-                        int32_t C, float slope, float* grad_xw, float* grad_a_src, float* de, void* slab,
-                        size_t slab_bytes, int32_t stages, void* stream) {
+                        const float* pack, const float* att, int32_t H, int32_t C, float slope, float* grad_xw,
+                        float* grad_a_src, float* de, void* slab, size_t slab_bytes, int32_t stages, void* stream) {
   int rc = check_graph(gt, "mp_gat_backward_f32");
   if (rc) return rc;
   MP_CHECK_ARG(H > 0 && C > 0, "mp_gat_backward_f32: H, C must be positive");
-  MP_CHECK_ARG(grad_out && xw && a_src && a_dst && row_stats && rs && att && grad_xw && grad_a_src &&
-                   (gt->n_edges == 0 || de),
+  MP_CHECK_ARG(grad_out && xw && a_src && pack && att && grad_xw && grad_a_src && (gt->n_edges == 0 || de),
                "mp_gat_backward_f32: null pointer");
+  MP_CHECK_ARG((uintptr_t)pack % 16 == 0, "mp_gat_backward_f32: pack must be 16-byte aligned");
   const int F = H * C;
   MP_CHECK_ARG(ldg >= F, "mp_gat_backward_f32: ldg < H*C");
   MP_CHECK_ARG(slab && slab_bytes >= mp_gat_slab_bytes(gt, H, C), "mp_gat_backward_f32: slab workspace too small");
@@ -1092,9 +1216,7 @@ int mp_gat_backward_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, co
   a.y = xw;
   a.ldy = F;
   a.a_src = a_src;
-  a.a_dst = a_dst;
-  a.row_stats = const_cast<float*>(row_stats);
-  a.rs = rs;
+  a.pack = reinterpret_cast<const f32x4*>(pack);
   a.att = att;
   a.de = de;
   a.ga = grad_a_src;

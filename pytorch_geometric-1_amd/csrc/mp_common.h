@@ -37,6 +37,24 @@ static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; 
 
 static inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// Sum over aligned groups of `g` lanes (g a power of two <= 64, wave-uniform)
+// with DPP lane permutes (quad_perm, row_half_mirror, row_mirror) fused into
+// the adds; every lane of a group ends with the same value (each step adds a
+// lane pair in both orders, and fp addition is commutative).
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float group_sum(float t, int g) {
+  if (g >= 2) t += dpp<0xB1>(t);   // quad_perm(1,0,3,2)
+  if (g >= 4) t += dpp<0x4E>(t);   // quad_perm(2,3,0,1)
+  if (g >= 8) t += dpp<0x141>(t);  // row_half_mirror
+  if (g >= 16) t += dpp<0x140>(t); // row_mirror
+  if (g >= 32) t += __shfl_xor(t, 16);
+  if (g >= 64) t += __shfl_xor(t, 32);
+  return t;
+}
+
 // wave-uniform value helpers
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }

@@ -99,12 +99,20 @@ __global__ void k_gat_sddmm_scalar(const int32_t* __restrict__ col, const int32_
   out[i] = t;
 }
 
-// out[n,h] = <a[n, hC:(h+1)C], b[n, hC:(h+1)C]>: one wave per node, lane l owns
-// 4 features, a head spans G = C/4 lanes (power of two) -> shuffle-xor sum.
-__global__ __launch_bounds__(256) void k_heads_rowdot_wave(const float* __restrict__ a, int64_t lda,
-                                                           const float* __restrict__ b, int64_t ldb, int64_t n,
-                                                           int32_t H, int32_t C, int32_t G,
-                                                           float* __restrict__ out) {
+// Backward prologue of the fused GAT pass, per (node n, head h):
+//   pack[n,h] = (a_dst[n,h], m[n,h], 1/den[n,h], rs[n,h]),  rs = <g[n,h,:], agg[n,h,:]>
+// (rs = sum_j alpha_nj <g_n, xw_j>_h since agg_n = sum_j alpha_nj xw_j).
+// One wave per node, lane l owns 4 features, a head spans G = C/4 lanes.
+__device__ __forceinline__ void write_pack(float* pack, const float* a_dst, const float* stats, int64_t q, float rs) {
+  f32x4 v = {a_dst[q], stats[2 * q], 1.f / stats[2 * q + 1], rs};
+  *reinterpret_cast<f32x4*>(pack + 4 * q) = v;
+}
+
+__global__ __launch_bounds__(256) void k_gat_bwd_prep_wave(const float* __restrict__ g, int64_t ldg,
+                                                           const float* __restrict__ agg, int64_t lda,
+                                                           const float* __restrict__ a_dst,
+                                                           const float* __restrict__ stats, int64_t n, int32_t H,
+                                                           int32_t C, int32_t G, float* __restrict__ pack) {
   const int lane = lane_id();
   const int64_t HC = (int64_t)H * C;
   const int64_t nw = (int64_t)gridDim.x * 4;
@@ -113,41 +121,49 @@ __global__ __launch_bounds__(256) void k_heads_rowdot_wave(const float* __restri
       const int64_t f = base + lane * 4;
       const bool act = f < HC;
       const int64_t fs = act ? f : 0;
-      Frag<4> x = load_frag<4>(a + r * lda + fs);
-      Frag<4> y = load_frag<4>(b + r * ldb + fs);
+      Frag<4> x = load_frag<4>(g + r * ldg + fs);
+      Frag<4> y = load_frag<4>(agg + r * lda + fs);
       float t = 0.f;
 #pragma unroll
       for (int k = 0; k < 4; ++k) t = __fadd_rn(t, __fmul_rn(x.v[k], y.v[k]));
       for (int o = 1; o < G; o <<= 1) t = __fadd_rn(t, __shfl_xor(t, o));
-      if (act && (lane & (G - 1)) == 0) out[r * H + fs / C] = t;
+      if (act && (lane & (G - 1)) == 0) write_pack(pack, a_dst, stats, r * H + fs / C, t);
     }
   }
 }
 
-__global__ void k_heads_rowdot_scalar(const float* __restrict__ a, int64_t lda, const float* __restrict__ b,
-                                      int64_t ldb, int64_t n, int32_t H, int32_t C, float* __restrict__ out) {
+__global__ void k_gat_bwd_prep_scalar(const float* __restrict__ g, int64_t ldg, const float* __restrict__ agg,
+                                      int64_t lda, const float* __restrict__ a_dst, const float* __restrict__ stats,
+                                      int64_t n, int32_t H, int32_t C, float* __restrict__ pack) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n * (int64_t)H) return;
   const int64_t r = i / H;
   const int h = (int)(i % H);
-  const float* x = a + r * lda + (int64_t)h * C;
-  const float* y = b + r * ldb + (int64_t)h * C;
+  const float* x = g + r * ldg + (int64_t)h * C;
+  const float* y = agg + r * lda + (int64_t)h * C;
   float t = 0.f;
   for (int c = 0; c < C; ++c) t = __fadd_rn(t, __fmul_rn(x[c], y[c]));
-  out[i] = t;
+  write_pack(pack, a_dst, stats, i, t);
 }
 
-// y[n, h*C + c] += s[n, h] * att[h*att_ld + c]
+// y[n, h*C + c] += s[n, h] * att[h*att_ld + c]; VEC consecutive features per thread
+template <int VEC>
 __global__ void k_heads_outer_add(float* __restrict__ y, int64_t ldy, const float* __restrict__ s, int64_t n,
                                   int32_t H, int32_t C, const float* __restrict__ att, int64_t att_ld) {
-  const int64_t F = (int64_t)H * C;
+  const int F = H * C;
+  const int per_row = F / VEC;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n * F) return;
-  const int64_t r = i / F;
-  const int f = (int)(i % F);
+  if (i >= n * per_row) return;
+  const int64_t r = i / per_row;
+  const int f = (int)(i - r * per_row) * VEC;
   const int h = f / C;
+  const float sv = s[r * H + h];
+  const float* a = att + (int64_t)h * att_ld + (f - h * C);
   float* d = y + r * ldy + f;
-  *d = __fadd_rn(*d, __fmul_rn(s[r * H + h], att[(int64_t)h * att_ld + (f % C)]));
+  Frag<VEC> v = load_frag<VEC>(d);
+#pragma unroll
+  for (int k = 0; k < VEC; ++k) v.v[k] = __fadd_rn(v.v[k], __fmul_rn(sv, a[k]));
+  store_frag<VEC>(d, v);
 }
 
 }  // namespace mp
@@ -204,23 +220,26 @@ int mp_gat_sddmm_f32(const mp_csr* g, const int32_t* slot_row, const float* grow
   return MP_OK;
 }
 
-int mp_heads_rowdot_f32(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t n, int32_t H, int32_t C,
-                        float* out, void* stream) {
-  MP_CHECK_ARG(H > 0 && C > 0 && n >= 0, "mp_heads_rowdot_f32: bad sizes");
+int mp_gat_backward_prep_f32(const float* grad_out, int64_t ldg, const float* agg, int64_t lda, const float* a_dst,
+                             const float* row_stats, int64_t n, int32_t H, int32_t C, float* pack, void* stream) {
+  MP_CHECK_ARG(H > 0 && C > 0 && n >= 0, "mp_gat_backward_prep_f32: bad sizes");
   if (n == 0) return MP_OK;
-  MP_CHECK_ARG(a && b && out, "mp_heads_rowdot_f32: null pointer");
+  MP_CHECK_ARG(grad_out && agg && a_dst && row_stats && pack, "mp_gat_backward_prep_f32: null pointer");
+  MP_CHECK_ARG((uintptr_t)pack % 16 == 0, "mp_gat_backward_prep_f32: pack must be 16-byte aligned");
   const int64_t F = (int64_t)H * C;
-  MP_CHECK_ARG(lda >= F && ldb >= F, "mp_heads_rowdot_f32: leading dimension < H*C");
+  MP_CHECK_ARG(ldg >= F && lda >= F, "mp_gat_backward_prep_f32: leading dimension < H*C");
   hipStream_t s = as_stream(stream);
   const int G = C / 4;
-  const bool v4 = C % 4 == 0 && G <= 64 && (G & (G - 1)) == 0 && (uintptr_t)a % 16 == 0 &&
-                  (uintptr_t)b % 16 == 0 && lda % 4 == 0 && ldb % 4 == 0;
+  const bool v4 = C % 4 == 0 && G <= 64 && (G & (G - 1)) == 0 && (uintptr_t)grad_out % 16 == 0 &&
+                  (uintptr_t)agg % 16 == 0 && ldg % 4 == 0 && lda % 4 == 0;
   if (v4) {
     int64_t blocks = ceil_div(n, 4);
     if (blocks > 65536) blocks = 65536;
-    k_heads_rowdot_wave<<<(unsigned)blocks, 256, 0, s>>>(a, lda, b, ldb, n, H, C, G, out);
+    k_gat_bwd_prep_wave<<<(unsigned)blocks, 256, 0, s>>>(grad_out, ldg, agg, lda, a_dst, row_stats, n, H, C, G,
+                                                          pack);
   } else {
-    k_heads_rowdot_scalar<<<(unsigned)ceil_div(n * H, 256), 256, 0, s>>>(a, lda, b, ldb, n, H, C, out);
+    k_gat_bwd_prep_scalar<<<(unsigned)ceil_div(n * H, 256), 256, 0, s>>>(grad_out, ldg, agg, lda, a_dst, row_stats,
+                                                                         n, H, C, pack);
   }
   MP_CHECK_LAUNCH();
   return MP_OK;
@@ -231,9 +250,15 @@ int mp_heads_outer_add_f32(float* y, int64_t ldy, const float* s, int64_t n, int
   MP_CHECK_ARG(H > 0 && C > 0 && n >= 0, "mp_heads_outer_add_f32: bad sizes");
   if (n == 0) return MP_OK;
   MP_CHECK_ARG(y && s && att && ldy >= (int64_t)H * C && att_ld >= C, "mp_heads_outer_add_f32: bad argument");
-  const int64_t total = n * H * C;
-  k_heads_outer_add<<<(unsigned)ceil_div(total, 256), 256, 0, as_stream(stream)>>>(y, ldy, s, n, H, C, att,
-                                                                                   att_ld);
+  hipStream_t st = as_stream(stream);
+  const bool v4 = C % 4 == 0 && (uintptr_t)y % 16 == 0 && ldy % 4 == 0 && (uintptr_t)att % 16 == 0 && att_ld % 4 == 0;
+  if (v4) {
+    const int64_t total = n * H * C / 4;
+    k_heads_outer_add<4><<<(unsigned)ceil_div(total, 256), 256, 0, st>>>(y, ldy, s, n, H, C, att, att_ld);
+  } else {
+    const int64_t total = n * H * C;
+    k_heads_outer_add<1><<<(unsigned)ceil_div(total, 256), 256, 0, st>>>(y, ldy, s, n, H, C, att, att_ld);
+  }
   MP_CHECK_LAUNCH();
   return MP_OK;
 }

@@ -201,13 +201,13 @@ class _Cache:
     def __init__(self):
         self._d = {}
 
-    def get(self, t, extra, factory):
+    def get(self, t, extra, factory, valid=None):
         if t._base is not None:  # a view (e.g. edge_index[1]): key on its base tensor
             extra = (extra, t.storage_offset(), tuple(t.stride()), tuple(t.shape))
             t = t._base
         k = (id(t), extra)
         hit = self._d.get(k)
-        if hit is not None and hit[0] == t._version:
+        if hit is not None and hit[0] == t._version and (valid is None or valid(hit[1])):
             return hit[1]
         val = factory()
         if hit is None:
@@ -242,6 +242,23 @@ def csr_for_index(index, n_rows):
                             lambda: CSR(index.to(torch.int64), None, n_rows, index.numel()))
 
 
+_order_cache = _Cache()
+
+
+def in_csr_order(csr, edge_values):
+    """Per-edge fp32 values permuted into ``csr``'s slot order, cached on the
+    value tensor (identity + version) for this CSR: a cached GCN norm is
+    permuted once, not on every forward and backward."""
+    v = edge_values.to(torch.float32)
+    if v is not edge_values or v.requires_grad:
+        return csr.to_csr_order(v.detach())
+    ref = weakref.ref(csr)
+    val = _order_cache.get(v, (id(csr), csr.n_edges), lambda: (ref, csr.to_csr_order(v.detach())),
+                           valid=lambda h: h[0]() is csr)
+    return val[1]
+
+
 def clear_caches():
     _graph_cache.clear()
     _index_cache.clear()
+    _order_cache.clear()

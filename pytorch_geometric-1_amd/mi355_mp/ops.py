@@ -14,7 +14,7 @@ torch_geometric 1.4.3; see oracle/ for the CPU restatement used as checker):
 import torch
 
 from . import _lib
-from .graph import csr_for_index
+from .graph import csr_for_index, in_csr_order
 
 _REDUCES = ("sum", "add", "mean", "max", "min")
 
@@ -77,7 +77,7 @@ class _FusedPropagate(torch.autograd.Function):
         csr = graph.dst
         w_csr = weight_csr
         if w_csr is None and edge_weight is not None:
-            w_csr = csr.to_csr_order(edge_weight.to(torch.float32))
+            w_csr = in_csr_order(csr, edge_weight)
         is_arg = reduce in ("max", "min")
         need_mask_grad = is_arg and pyg_mask and ctx.needs_input_grad[0]
         flags = _lib.MP_FLAG_PYG_MASK if (pyg_mask and not need_mask_grad) else 0
@@ -127,7 +127,7 @@ class _FusedPropagate(torch.autograd.Function):
             g = g / deg.view(-1, 1)
         if ctx.needs_input_grad[0]:
             src = graph.src  # transposed CSR: rows = source nodes, gathers destination rows
-            w_src = src.to_csr_order(edge_weight.to(torch.float32)) if edge_weight is not None else None
+            w_src = in_csr_order(src, edge_weight) if edge_weight is not None else None
             gx, _ = _aggregate(src, "other", g, w_src, "sum", 0, None)
         if ctx.needs_input_grad[1] and edge_weight is not None:
             xi = gather_rows(x, edge_index[graph.j])
@@ -340,9 +340,10 @@ def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope
     N = xw.shape[0]
     F = H * C
     att_c = att.reshape(H, 2 * C).contiguous()
-    rs = torch.empty((N, H), dtype=torch.float32, device=dev)
-    _lib.check(lib.mp_heads_rowdot_f32(g.data_ptr(), g.stride(0), agg.data_ptr(), agg.stride(0), N, H, C,
-                                       rs.data_ptr(), st), "mp_heads_rowdot_f32")
+    pack = torch.empty((N, H, 4), dtype=torch.float32, device=dev)
+    _lib.check(lib.mp_gat_backward_prep_f32(g.data_ptr(), g.stride(0), agg.data_ptr(), agg.stride(0),
+                                            a_dst.data_ptr(), stats.data_ptr(), N, H, C, pack.data_ptr(), st),
+               "mp_gat_backward_prep_f32")
     src = graph.src
     E = src.n_edges
     gx = torch.empty((N, F), dtype=torch.float32, device=dev)
@@ -352,9 +353,9 @@ def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope
     sb = lib.mp_gat_slab_bytes(gs, H, C)
     slab = torch.empty(sb, dtype=torch.uint8, device=dev)
     _lib.check(lib.mp_gat_backward_f32(gs, g.data_ptr(), g.stride(0), xw.data_ptr(), a_src.data_ptr(),
-                                       a_dst.data_ptr(), stats.data_ptr(), rs.data_ptr(), att_c.data_ptr(), H, C,
-                                       float(slope), gx.data_ptr(), ga_src.data_ptr(), de.data_ptr(),
-                                       slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st), "mp_gat_backward_f32")
+                                       pack.data_ptr(), att_c.data_ptr(), H, C, float(slope), gx.data_ptr(),
+                                       ga_src.data_ptr(), de.data_ptr(), slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
+               "mp_gat_backward_f32")
     del slab
     dst = graph.dst_gather_src_slots()
     ga_dst, _ = _aggregate(dst, "src_slot", de, None, "sum", 0, None)

@@ -558,7 +558,7 @@ def test_gat_training_flow():
     assert all(np.isfinite(losses)) and losses[-1] < 0.7 * losses[0]
 
 
-@pytest.mark.parametrize("F", [4, 8, 16, 32, 64, 100, 128])
+@pytest.mark.parametrize("F", [2, 4, 7, 8, 12, 16, 32, 64, 100, 128])
 def test_small_feature_widths_lane_groups(F):
     """F <= 128 packs several merge-path tasks per wave (L = F/4 lanes)."""
     _, ops, _, Graph, pl = _mods()
