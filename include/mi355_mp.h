@@ -201,10 +201,24 @@ int mp_gat_backward_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, co
 
 /* pack[n,h,:] = (a_dst[n,h], m[n,h], 1/den[n,h], rs[n,h]) with
  * rs[n,h] = sum_c grad_out[n, h*C+c] * agg[n, h*C+c]  (agg = pre-bias GAT output;
- * rs = sum_j alpha_nj <g_n, xw_j>_h, the softmax-backward row term). */
+ * rs = sum_j alpha_nj <g_n, xw_j>_h, the softmax-backward row term).
+ * gsum_part (optional, [mp_gat_bwd_blocks(n), H*C], needs C%4==0, H*C<=256):
+ * per-block column sums of grad_out (the bias gradient is their sum over blocks). */
 int mp_gat_backward_prep_f32(const float* grad_out, int64_t ldg, const float* agg, int64_t lda,
                              const float* a_dst, const float* row_stats, int64_t n, int32_t H,
-                             int32_t C, float* pack, void* stream);
+                             int32_t C, float* pack, float* gsum_part, void* stream);
+
+/* Rows of the per-block partial arrays of the prep/finish kernels for n nodes. */
+int mp_gat_bwd_blocks(int64_t n);
+
+/* Backward epilogue (C%4==0, H*C<=256), one pass over the nodes:
+ *   grad_xw[n, h*C+c] += ga_dst[n,h] * att[h, c]        (att = [H, 2C]: dst half first)
+ *   att_part[b, 0, :]  = sum over block b's nodes of ga_dst[n,h] * xw[n, h*C+c]
+ *   att_part[b, 1, :]  = ... ga_src[n,h] * xw[n, h*C+c]
+ * att_part is [mp_gat_bwd_blocks(n), 2, H*C]; d att = its sum over blocks. */
+int mp_gat_backward_finish_f32(float* grad_xw, const float* xw, const float* ga_dst,
+                               const float* ga_src, const float* att, int64_t n, int32_t H,
+                               int32_t C, float* att_part, void* stream);
 
 /* y[n, h*C+c] += s[n,h] * att[h*att_ld + c]  (per-head outer-product update) */
 int mp_heads_outer_add_f32(float* y, int64_t ldy, const float* s, int64_t n, int32_t H,

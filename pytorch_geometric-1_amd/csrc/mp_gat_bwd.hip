@@ -99,6 +99,73 @@ __global__ void k_gat_sddmm_scalar(const int32_t* __restrict__ col, const int32_
   out[i] = t;
 }
 
+// Deterministic block partial: the 4 waves' per-lane sums of one 256-feature
+// tile (lane l holds features 4l..4l+3) are added in wave order through LDS
+// and stored as one row of the [gridDim.x, F] partial array.
+__device__ __forceinline__ void block_partial_store(const float (&v)[4], float* __restrict__ dst, int64_t F) {
+  __shared__ float red[3][256];
+  const int lane = lane_id();
+  const int wid = (int)(threadIdx.x >> 6);
+  if (wid > 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) red[wid - 1][lane * 4 + k] = v[k];
+  }
+  __syncthreads();
+  if (wid == 0) {
+    float t[4] = {v[0], v[1], v[2], v[3]};
+    for (int q = 0; q < 3; ++q) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) t[k] += red[q][lane * 4 + k];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (lane * 4 + k < F) dst[lane * 4 + k] = t[k];
+  }
+}
+
+// Backward epilogue, one wave per node n (H*C <= 256, C % 4 == 0):
+//   gx[n, h*C+c] += ga_dst[n,h] * att[h, c]                (the x_i use of xw in the score)
+//   att_part[blk, 0, :] += ga_dst[n,h] * xw[n, :]          (d att_dst, per-block partial)
+//   att_part[blk, 1, :] += ga_src[n,h] * xw[n, :]          (d att_src)
+__global__ __launch_bounds__(256) void k_gat_bwd_finish(float* __restrict__ gx, const float* __restrict__ xw,
+                                                        const float* __restrict__ ga_dst,
+                                                        const float* __restrict__ ga_src,
+                                                        const float* __restrict__ att, int64_t n, int32_t H,
+                                                        int32_t C, float* __restrict__ att_part) {
+  const int lane = lane_id();
+  const int HC = H * C;
+  const int f = lane * 4;
+  const bool act = f < HC;
+  const int fs = act ? f : 0;
+  const int h = fs / C;
+  const int c = fs - h * C;
+  f32x4 ad = *reinterpret_cast<const f32x4*>(att + (int64_t)h * 2 * C + c);
+  float pd[4] = {0.f, 0.f, 0.f, 0.f}, ps[4] = {0.f, 0.f, 0.f, 0.f};
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n; r += nw) {
+    const float gd = ga_dst[r * H + h];
+    const float gs = ga_src[r * H + h];
+    Frag<4> x = load_frag<4>(xw + r * HC + fs);
+    if (act) {
+      float* d = gx + r * HC + f;
+      Frag<4> o = load_frag<4>(d);
+      o.v[0] = __builtin_fmaf(gd, ad.x, o.v[0]);
+      o.v[1] = __builtin_fmaf(gd, ad.y, o.v[1]);
+      o.v[2] = __builtin_fmaf(gd, ad.z, o.v[2]);
+      o.v[3] = __builtin_fmaf(gd, ad.w, o.v[3]);
+      store_frag<4>(d, o);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        pd[k] = __builtin_fmaf(gd, x.v[k], pd[k]);
+        ps[k] = __builtin_fmaf(gs, x.v[k], ps[k]);
+      }
+    }
+  }
+  block_partial_store(pd, att_part + (int64_t)blockIdx.x * 2 * HC, HC);
+  __syncthreads();
+  block_partial_store(ps, att_part + (int64_t)blockIdx.x * 2 * HC + HC, HC);
+}
+
 // Backward prologue of the fused GAT pass, per (node n, head h):
 //   pack[n,h] = (a_dst[n,h], m[n,h], 1/den[n,h], rs[n,h]),  rs = <g[n,h,:], agg[n,h,:]>
 // (rs = sum_j alpha_nj <g_n, xw_j>_h since agg_n = sum_j alpha_nj xw_j).
@@ -112,11 +179,16 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep_wave(const float* __restri
                                                            const float* __restrict__ agg, int64_t lda,
                                                            const float* __restrict__ a_dst,
                                                            const float* __restrict__ stats, int64_t n, int32_t H,
-                                                           int32_t C, int32_t G, float* __restrict__ pack) {
+                                                           int32_t C, int32_t G, float* __restrict__ pack,
+                                                           float* __restrict__ gsum_part) {
   const int lane = lane_id();
+  const int wid = (int)(threadIdx.x >> 6);
   const int64_t HC = (int64_t)H * C;
   const int64_t nw = (int64_t)gridDim.x * 4;
-  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n; r += nw) {
+  // bias-gradient partial (column sums of g) for rows of one 256-feature tile
+  // (HC <= 256 when gsum_part != nullptr)
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t r = (int64_t)blockIdx.x * 4 + wid; r < n; r += nw) {
     for (int64_t base = 0; base < HC; base += 256) {
       const int64_t f = base + lane * 4;
       const bool act = f < HC;
@@ -128,8 +200,13 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep_wave(const float* __restri
       for (int k = 0; k < 4; ++k) t = __fadd_rn(t, __fmul_rn(x.v[k], y.v[k]));
       for (int o = 1; o < G; o <<= 1) t = __fadd_rn(t, __shfl_xor(t, o));
       if (act && (lane & (G - 1)) == 0) write_pack(pack, a_dst, stats, r * H + fs / C, t);
+      if (gsum_part && act) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cs[k] += x.v[k];
+      }
     }
   }
+  if (gsum_part) block_partial_store(cs, gsum_part + (int64_t)blockIdx.x * HC, HC);
 }
 
 __global__ void k_gat_bwd_prep_scalar(const float* __restrict__ g, int64_t ldg, const float* __restrict__ agg,
@@ -220,8 +297,15 @@ int mp_gat_sddmm_f32(const mp_csr* g, const int32_t* slot_row, const float* grow
   return MP_OK;
 }
 
+int mp_gat_bwd_blocks(int64_t n) {
+  int64_t b = ceil_div(n, 4);
+  if (b > 8192) b = 8192;
+  return (int)(b < 1 ? 1 : b);
+}
+
 int mp_gat_backward_prep_f32(const float* grad_out, int64_t ldg, const float* agg, int64_t lda, const float* a_dst,
-                             const float* row_stats, int64_t n, int32_t H, int32_t C, float* pack, void* stream) {
+                             const float* row_stats, int64_t n, int32_t H, int32_t C, float* pack,
+                             float* gsum_part, void* stream) {
   MP_CHECK_ARG(H > 0 && C > 0 && n >= 0, "mp_gat_backward_prep_f32: bad sizes");
   if (n == 0) return MP_OK;
   MP_CHECK_ARG(grad_out && agg && a_dst && row_stats && pack, "mp_gat_backward_prep_f32: null pointer");
@@ -232,15 +316,27 @@ int mp_gat_backward_prep_f32(const float* grad_out, int64_t ldg, const float* ag
   const int G = C / 4;
   const bool v4 = C % 4 == 0 && G <= 64 && (G & (G - 1)) == 0 && (uintptr_t)grad_out % 16 == 0 &&
                   (uintptr_t)agg % 16 == 0 && ldg % 4 == 0 && lda % 4 == 0;
+  MP_CHECK_ARG(!gsum_part || (v4 && F <= 256), "mp_gat_backward_prep_f32: gsum_part needs C%%4==0 and H*C<=256");
   if (v4) {
-    int64_t blocks = ceil_div(n, 4);
-    if (blocks > 65536) blocks = 65536;
-    k_gat_bwd_prep_wave<<<(unsigned)blocks, 256, 0, s>>>(grad_out, ldg, agg, lda, a_dst, row_stats, n, H, C, G,
-                                                          pack);
+    k_gat_bwd_prep_wave<<<(unsigned)mp_gat_bwd_blocks(n), 256, 0, s>>>(grad_out, ldg, agg, lda, a_dst, row_stats, n,
+                                                                      H, C, G, pack, gsum_part);
   } else {
     k_gat_bwd_prep_scalar<<<(unsigned)ceil_div(n * H, 256), 256, 0, s>>>(grad_out, ldg, agg, lda, a_dst, row_stats,
                                                                          n, H, C, pack);
   }
+  MP_CHECK_LAUNCH();
+  return MP_OK;
+}
+
+int mp_gat_backward_finish_f32(float* grad_xw, const float* xw, const float* ga_dst, const float* ga_src,
+                                const float* att, int64_t n, int32_t H, int32_t C, float* att_part, void* stream) {
+  MP_CHECK_ARG(H > 0 && C > 0 && n >= 0, "mp_gat_backward_finish_f32: bad sizes");
+  MP_CHECK_ARG(C % 4 == 0 && H * C <= 256, "mp_gat_backward_finish_f32: needs C %% 4 == 0 and H*C <= 256");
+  MP_CHECK_ARG(grad_xw && xw && ga_dst && ga_src && att && att_part, "mp_gat_backward_finish_f32: null pointer");
+  MP_CHECK_ARG((uintptr_t)grad_xw % 16 == 0 && (uintptr_t)xw % 16 == 0 && (uintptr_t)att % 16 == 0,
+               "mp_gat_backward_finish_f32: 16-byte alignment required");
+  k_gat_bwd_finish<<<(unsigned)mp_gat_bwd_blocks(n), 256, 0, as_stream(stream)>>>(grad_xw, xw, ga_dst, ga_src, att, n,
+                                                                                 H, C, att_part);
   MP_CHECK_LAUNCH();
   return MP_OK;
 }

@@ -62,7 +62,9 @@ SIGNATURES = {
     "mp_gat_sddmm_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, i64, c_p, i64, i32, i32, c_p, c_p]),
     "mp_gat_backward_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, i64, c_p, c_p, c_p, c_p, i32, i32,
                                            ctypes.c_float, c_p, c_p, c_p, c_p, sz, i32, c_p]),
-    "mp_gat_backward_prep_f32": (ctypes.c_int, [c_p, i64, c_p, i64, c_p, c_p, i64, i32, i32, c_p, c_p]),
+    "mp_gat_backward_prep_f32": (ctypes.c_int, [c_p, i64, c_p, i64, c_p, c_p, i64, i32, i32, c_p, c_p, c_p]),
+    "mp_gat_bwd_blocks": (ctypes.c_int, [i64]),
+    "mp_gat_backward_finish_f32": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, i64, i32, i32, c_p, c_p]),
     "mp_heads_outer_add_f32": (ctypes.c_int, [c_p, i64, c_p, i64, i32, i32, c_p, i64, c_p]),
     "mp_gather_rows_f32": (ctypes.c_int, [c_p, i64, c_p, i64, i32, c_p, i64, c_p]),
     "mp_permute_f32": (ctypes.c_int, [c_p, c_p, i64, c_p, c_p]),

@@ -330,20 +330,31 @@ def _gat_bwd_fused_ok(C):
     return (C % 4 == 0 and pow2(C // 4)) or pow2(C)
 
 
-def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope, want_att):
-    """GATConv backward in one gather pass over the transposed CSR
-    (mp_gat_backward_f32), then the d a_dst row sums over the dst CSR (reading
-    the per-edge d score through the src-slot map) and the att_dst term."""
+def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope, want_att, want_bias):
+    """GATConv backward: prep (packed destination terms + bias-grad partials),
+    one gather pass over the transposed CSR (mp_gat_backward_f32), the d a_dst
+    row sums over the dst CSR (reading the per-edge d score through the
+    src-slot map), and the epilogue (att_dst term + att-grad partials).
+    Returns (d xw, d att or None, d bias or None)."""
     lib = _lib.load()
     dev = xw.device
     st = _lib.stream_ptr(dev)
     N = xw.shape[0]
     F = H * C
     att_c = att.reshape(H, 2 * C).contiguous()
+    if N == 0:
+        return (torch.zeros_like(xw), torch.zeros_like(att) if want_att else None,
+                g.new_zeros(F) if want_bias else None)
+    epi = C % 4 == 0 and F <= 256
+    nb = int(lib.mp_gat_bwd_blocks(N))
     pack = torch.empty((N, H, 4), dtype=torch.float32, device=dev)
+    gpart = torch.empty((nb, F), dtype=torch.float32, device=dev) if (want_bias and epi) else None
     _lib.check(lib.mp_gat_backward_prep_f32(g.data_ptr(), g.stride(0), agg.data_ptr(), agg.stride(0),
-                                            a_dst.data_ptr(), stats.data_ptr(), N, H, C, pack.data_ptr(), st),
-               "mp_gat_backward_prep_f32")
+                                            a_dst.data_ptr(), stats.data_ptr(), N, H, C, pack.data_ptr(),
+                                            _lib.ptr(gpart), st), "mp_gat_backward_prep_f32")
+    gb = None
+    if want_bias:
+        gb = gpart.sum(0) if gpart is not None else g.sum(0)
     src = graph.src
     E = src.n_edges
     gx = torch.empty((N, F), dtype=torch.float32, device=dev)
@@ -356,23 +367,33 @@ def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope
                                        pack.data_ptr(), att_c.data_ptr(), H, C, float(slope), gx.data_ptr(),
                                        ga_src.data_ptr(), de.data_ptr(), slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
                "mp_gat_backward_f32")
-    del slab
+    del slab, pack
     dst = graph.dst_gather_src_slots()
     ga_dst, _ = _aggregate(dst, "src_slot", de, None, "sum", 0, None)
-    _lib.check(lib.mp_heads_outer_add_f32(gx.data_ptr(), gx.stride(0), ga_dst.data_ptr(), N, H, C,
-                                          att_c.data_ptr(), 2 * C, st), "mp_heads_outer_add_f32")
+    del de
     gatt = None
-    if want_att:
-        x3 = xw.view(N, H, C)
-        gatt = torch.cat([torch.einsum("nh,nhc->hc", ga_dst, x3), torch.einsum("nh,nhc->hc", ga_src, x3)],
-                         dim=-1).view_as(att)
-    return gx, gatt
+    if epi:
+        apart = torch.empty((nb, 2, F), dtype=torch.float32, device=dev)
+        _lib.check(lib.mp_gat_backward_finish_f32(gx.data_ptr(), xw.data_ptr(), ga_dst.data_ptr(), ga_src.data_ptr(),
+                                                  att_c.data_ptr(), N, H, C, apart.data_ptr(), st),
+                   "mp_gat_backward_finish_f32")
+        if want_att:
+            p = apart.sum(0).view(2, H, C)
+            gatt = torch.cat([p[0], p[1]], dim=-1).view_as(att)
+    else:
+        _lib.check(lib.mp_heads_outer_add_f32(gx.data_ptr(), gx.stride(0), ga_dst.data_ptr(), N, H, C,
+                                              att_c.data_ptr(), 2 * C, st), "mp_heads_outer_add_f32")
+        if want_att:
+            x3 = xw.view(N, H, C)
+            gatt = torch.cat([torch.einsum("nh,nhc->hc", ga_dst, x3), torch.einsum("nh,nhc->hc", ga_src, x3)],
+                             dim=-1).view_as(att)
+    return gx, gatt, gb
 
 
 class _GatPropagate(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, xw, att, bias, graph, edge_index, H, C, slope, want_alpha):
-        fused = any(ctx.needs_input_grad[:3]) and _gat_bwd_fused_ok(C)
+    def forward(ctx, xw, att, bias, graph, edge_index, H, C, slope, want_alpha, train):
+        fused = train and _gat_bwd_fused_ok(C)
         # the fused backward needs the pre-bias aggregate (rs_i = <g_i, agg_i>)
         out, alpha, a_src, a_dst, stats = _gat_forward(graph, edge_index, xw, att, H, C, slope,
                                                        None if fused else bias, want_alpha)
@@ -404,11 +425,11 @@ class _GatPropagate(torch.autograd.Function):
         st = _lib.stream_ptr(dev)
         g = grad_out.contiguous()
         N = xw.shape[0]
-        gb = g.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
         if ctx.fused:
-            gx, gatt = _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope,
-                                           ctx.needs_input_grad[1])
-            return gx, gatt, gb, None, None, None, None, None, None
+            gx, gatt, gb = _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope,
+                                               ctx.needs_input_grad[1], ctx.has_bias and ctx.needs_input_grad[2])
+            return gx, gatt, gb, None, None, None, None, None, None, None
+        gb = g.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
         dst, src = graph.dst, graph.src
         E = dst.n_edges
         sr = dst.slot_rows()
@@ -444,7 +465,7 @@ class _GatPropagate(torch.autograd.Function):
             gd = torch.einsum("nh,nhc->hc", ga_dst, x3)
             gs = torch.einsum("nh,nhc->hc", ga_src, x3)
             gatt = torch.cat([gd, gs], dim=-1).view_as(att)
-        return gx.reshape(N, H * C), gatt, gb, None, None, None, None, None, None
+        return gx.reshape(N, H * C), gatt, gb, None, None, None, None, None, None, None
 
 
 def gat_propagate(graph, edge_index, xw, att, heads, out_channels, negative_slope=0.2, bias=None,
@@ -452,5 +473,54 @@ def gat_propagate(graph, edge_index, xw, att, heads, out_channels, negative_slop
     """Fused GATConv aggregation: returns (out [N, H*C], alpha [E, H] or None)."""
     _lib.require_device(xw, edge_index, att, bias)
     xw = _f32_2d(xw, "x@W").contiguous()
+    # autograd.Function.forward always runs with grad disabled: decide here whether
+    # a backward can follow (then the forward keeps the pre-bias aggregate)
+    train = torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in (xw, att, bias))
     return _GatPropagate.apply(xw, att, bias, graph, edge_index, int(heads), int(out_channels),
-                               float(negative_slope), bool(return_alpha))
+                               float(negative_slope), bool(return_alpha), train)
+
+
+class _FeatureTransform(torch.autograd.Function):
+    """x @ W with a split-K weight gradient.
+
+    Forward is torch.matmul (hipBLASLt), identical to the reference's
+    ``torch.matmul(x, self.weight)`` (GCNConv/GATConv [U5, U6]).  The weight
+    gradient x^T g reduces over all N rows into a small [F_in, F_out] matrix:
+    as one GEMM it has a handful of output tiles (a few dozen workgroups on
+    256 CUs), so it is computed as a batched GEMM over row chunks of
+    SPLIT_ROWS (one output tile set per chunk) plus a sum over chunks."""
+    SPLIT_ROWS = 8192
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return torch.matmul(x, w)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        gx = gw = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.matmul(g, w.t())
+        if ctx.needs_input_grad[1]:
+            n = x.shape[0]
+            k = _FeatureTransform.SPLIT_ROWS
+            s = n // k
+            if s >= 8:
+                m = s * k
+                xs = x[:m].view(s, k, x.shape[1]).transpose(1, 2)
+                gs = g[:m].view(s, k, g.shape[1])
+                gw = torch.bmm(xs, gs).sum(0)
+                if m < n:
+                    gw = gw + torch.matmul(x[m:].t(), g[m:])
+            else:
+                gw = torch.matmul(x.t(), g)
+        return gx, gw
+
+
+def feature_transform(x, w):
+    """``torch.matmul(x, w)`` for a 2-D fp32 device x (split-K weight gradient)."""
+    if not (torch.is_tensor(x) and x.dim() == 2 and x.is_cuda and x.dtype == torch.float32 and w.dim() == 2
+            and torch.is_grad_enabled() and w.requires_grad):
+        return torch.matmul(x, w)
+    return _FeatureTransform.apply(x, w)

@@ -71,7 +71,7 @@ class GATConv(MessagePassing):
             edge_index = gat_loops(edge_index, x.size(self.node_dim))
 
         if self._can_fuse(x, size):
-            xw = torch.matmul(x, self.weight)
+            xw = _ops.feature_transform(x, self.weight)
             N = xw.size(0)
             graph = graph_for(edge_index, N, N, self.flow)
             fused_bias = self.bias if self.concat else None

@@ -70,7 +70,7 @@ class GCNConv(MessagePassing):
 
     def forward(self, x, edge_index, edge_weight=None):
         """"""
-        x = torch.matmul(x, self.weight)
+        x = _ops.feature_transform(x, self.weight)
 
         if self.cached and self.cached_result is not None:
             if edge_index.size(1) != self.cached_num_edges:

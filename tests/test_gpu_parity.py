@@ -711,7 +711,7 @@ def test_gat_dropout_training_uses_generic_path():
     assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("H,C", [(8, 32), (3, 5), (1, 64), (4, 100), (2, 16), (4, 8), (1, 256), (2, 2)])
+@pytest.mark.parametrize("H,C", [(8, 32), (3, 5), (1, 64), (4, 100), (2, 16), (4, 8), (1, 256), (2, 2), (8, 64)])
 def test_gat_native_backward_pieces(H, C):
     """GAT backward vs float64 autograd of the reference formula, several
     head shapes: C/4 a power of two (fused transposed-CSR pass, head groups of
@@ -799,3 +799,23 @@ def test_gat_forward_identical_with_and_without_grad():
         a = conv(x, ei)
     b = conv(x.requires_grad_(True), ei)
     assert torch.equal(a, b.detach())
+
+
+def test_feature_transform_split_k_weight_grad():
+    """x @ W with the split-K weight gradient (>= 8 row chunks + a remainder):
+    forward identical to torch.matmul, gradients vs float64."""
+    from mi355_mp import ops
+    g = torch.Generator().manual_seed(21)
+    N, Fi, Fo = 8 * 8192 + 777, 24, 40
+    x = torch.randn(N, Fi, generator=g)
+    w = torch.randn(Fi, Fo, generator=g)
+    gout = torch.randn(N, Fo, generator=g)
+    xd = x.to(DEV).requires_grad_(True)
+    wd = w.to(DEV).requires_grad_(True)
+    y = ops.feature_transform(xd, wd)
+    assert torch.equal(y.detach(), torch.matmul(x.to(DEV), w.to(DEV)))
+    y.backward(gout.to(DEV))
+    want_w = x.double().t() @ gout.double()
+    want_x = gout.double() @ w.double().t()
+    assert torch.allclose(wd.grad.cpu().double(), want_w, rtol=1e-5, atol=1e-3)
+    assert torch.allclose(xd.grad.cpu().double(), want_x, rtol=1e-5, atol=1e-4)
