@@ -58,7 +58,9 @@ extern "C" {
 /*
  * Destination-sorted CSR plus its edge-balanced ("merge-path") schedule.
  *   rowptr[n_rows+1]      row r owns CSR slots [rowptr[r], rowptr[r+1])
- *   col[n_edges]          gather row for each slot (source node, or message row)
+ *   col[n_edges]          gather row for each slot (source node, or message row);
+ *                         NULL = identity (row k of x for slot k: values already
+ *                         in CSR slot order)
  *   eid[n_edges]          original edge position of each slot (argmax output)
  * Schedule (merge-path over the N+E work items "row r" and "slot k"; row r
  * sits at merged position rowptr[r]+r, slot k of row r at k+r+1):
@@ -191,8 +193,11 @@ int mp_gat_sddmm_f32(const mp_csr* g, const int32_t* slot_row, const float* grow
  *   de[k, h]        = alpha_ij (<g_i, xw_j>_h - rs[i,h]) leaky'(a_src[j,h]+a_dst[i,h])
  *   grad_a_src[j,h] = sum over the row of de
  * alpha_ij = exp(leaky(score) - m_i) / den_i from the forward's row_stats.
- * pack [n_dst, H, 4] = mp_gat_backward_prep_f32 output.  de is written in gt's
- * slot order.  Needs C/4 or C to be a power of two <= 64.
+ * pack [n_dst, H, 4] = mp_gat_backward_prep_f32 output.  de[gt.eid[k], h]
+ * receives slot k's value: pass the destination-CSR slot of each edge in
+ * gt.eid to get de in destination-CSR order (then d a_dst is a contiguous
+ * segmented sum: mp_aggregate_f32 with col = NULL).  Needs C/4 or C to be a
+ * power of two <= 64.
  * Slab: mp_gat_slab_bytes(gt, H, C). */
 int mp_gat_backward_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, const float* xw,
                         const float* a_src, const float* pack, const float* att, int32_t H,

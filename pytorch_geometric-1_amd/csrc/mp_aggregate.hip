@@ -462,7 +462,7 @@ struct HeadSumRed : SumRed<VEC, true, false> {
 template <int VEC>
 struct GatBwdRed {
   static constexpr bool kW = false;
-  static constexpr bool kEid = false;
+  static constexpr bool kEid = true;
   static constexpr bool kGat = false;
   static constexpr bool kHW = false;
   static constexpr bool kGatB = true;
@@ -599,7 +599,7 @@ struct SlotWin {
   __device__ __forceinline__ void fetch(const AggArgs& p, int64_t b, int gl, int& c, float& wt, int& e) {
     int64_t k = b + gl;
     bool ok = k < limit;
-    c = ok ? ld_stream(p.col + k) : 0;
+    c = ok ? (p.col ? ld_stream(p.col + k) : (int)k) : 0;  // col == nullptr: identity (rows in slot order)
     if (W) wt = ok ? ld_stream(p.w + k) : 0.f;
     if (EID) e = ok ? ld_stream(p.eid + k) : 0;
   }
@@ -676,7 +676,7 @@ __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p, SlotWin<Re
         if constexpr (Red::kGat) {
           red.consume_gat(p, v[u], as[u]);
         } else if constexpr (Red::kGatB) {
-          red.consume_gatb(p, v[u], as[u], pk[u], e + u);
+          red.consume_gatb(p, v[u], as[u], pk[u], GR::bc(win.eid, off + u));
         } else {
           const float wt = Red::kHW ? hw[u] : (Red::kW ? GR::bc(win.w, off + u) : 1.f);
           const int ei = Red::kEid ? GR::bc(win.eid, off + u) : 0;
@@ -769,7 +769,7 @@ __device__ __forceinline__ void lane_slots(Red (&red)[NV], const AggArgs& p, int
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t k = e + (u < n ? u : n - 1);
-      c[u] = p.col[k];
+      c[u] = p.col ? p.col[k] : (int)k;
       if constexpr (Red::kW) wt[u] = p.w[k];
       if constexpr (Red::kEid) ei[u] = p.eid[k];
     }
@@ -1043,7 +1043,7 @@ static int check_graph(const mp_csr* g, const char* who) {
   MP_CHECK_ARG(g != nullptr, "%s: null graph", who);
   MP_CHECK_ARG(g->rowptr && g->wave_row && g->wave_slot && (g->n_split == 0 || g->split_waves),
                "%s: graph has null arrays", who);
-  MP_CHECK_ARG(g->n_edges == 0 || (g->col && g->eid), "%s: graph has null col/eid", who);
+  MP_CHECK_ARG(g->n_edges == 0 || g->eid, "%s: graph has null eid", who);
   MP_CHECK_ARG(g->chunk > 0 && g->chunk % 64 == 0 && g->n_waves >= 1, "%s: bad schedule", who);
   return MP_OK;
 }

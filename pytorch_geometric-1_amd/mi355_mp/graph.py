@@ -73,34 +73,34 @@ class CSR:
         self._structs = {}
         self._deg = None
 
-    def add_gather(self, name, col, n_cols):
-        """Register a custom gather column (int32 [E]) under ``name`` for struct()."""
+    def add_gather(self, name, col, n_cols, eid=None):
+        """Register a struct variant under ``name`` for struct(): a custom gather
+        column (int32 [E]; None = identity, rows in slot order) and optionally a
+        custom per-slot id array in place of eid."""
         self._extra = getattr(self, "_extra", {})
-        self._extra[name] = (col.contiguous(), int(n_cols))
+        self._extra[name] = (None if col is None else col.contiguous(), int(n_cols),
+                             None if eid is None else eid.contiguous())
         self._structs.pop(name, None)
 
     def struct(self, gather="other"):
         """ctypes mp_csr; gather='other' reads x[other] rows, 'eid' reads message
-        rows (original edge order), 'slot' reads rows already in CSR slot order;
-        other names are columns registered with add_gather()."""
+        rows (original edge order), 'slot' reads rows already in CSR slot order
+        (identity column: col = NULL); other names are variants registered with
+        add_gather()."""
         s = self._structs.get(gather)
-        extra = getattr(self, "_extra", {})
-        if s is None and gather in extra:
-            col, n_cols = extra[gather]
-            s = _lib.MpCsr(self.rowptr.data_ptr(), col.data_ptr(), self.eid.data_ptr(),
-                           self.wave_row.data_ptr(), self.wave_slot.data_ptr(),
-                           self.split_waves.data_ptr(), self.n_rows, self.n_edges, self.chunk,
-                           self.n_waves, self.n_split, n_cols)
-            self._structs[gather] = s
         if s is None:
-            if gather == "slot":
-                if getattr(self, "_ident", None) is None:
-                    self._ident = torch.arange(max(self.n_edges, 1), dtype=torch.int32, device=self.device)
-                col = self._ident
+            extra = getattr(self, "_extra", {})
+            eid = self.eid
+            if gather in extra:
+                col, n_cols, e2 = extra[gather]
+                if e2 is not None:
+                    eid = e2
+            elif gather == "slot":
+                col, n_cols = None, self.n_edges
             else:
                 col = self.col if gather == "other" else self.eid
-            n_cols = self.n_other if gather == "other" else self.n_edges
-            s = _lib.MpCsr(self.rowptr.data_ptr(), col.data_ptr(), self.eid.data_ptr(),
+                n_cols = self.n_other if gather == "other" else self.n_edges
+            s = _lib.MpCsr(self.rowptr.data_ptr(), _lib.ptr(col), eid.data_ptr(),
                            self.wave_row.data_ptr(), self.wave_slot.data_ptr(),
                            self.split_waves.data_ptr(), self.n_rows, self.n_edges, self.chunk,
                            self.n_waves, self.n_split, n_cols)
@@ -179,20 +179,21 @@ class Graph:
             self._src = CSR(ei[self.j], ei[self.i], self.n_src, self.n_dst, self.chunk)
         return self._src
 
-    def dst_gather_src_slots(self):
-        """Registers on the dst CSR the gather 'src_slot': for each dst slot, the
-        slot of the same edge in the src CSR, so per-edge values produced in
-        src-CSR order are reduced over dst rows without a permutation pass."""
-        dst = self.dst
-        if "src_slot" not in getattr(dst, "_extra", {}):
-            src = self.src
+    def src_with_dst_slots(self):
+        """The src CSR with the struct variant 'dst_slot': its per-slot id array
+        holds, for each src slot, the slot of the same edge in the dst CSR, so a
+        pass over the src CSR can write per-edge values straight into dst-CSR
+        order (mp_gat_backward_f32's de)."""
+        src = self.src
+        if "dst_slot" not in getattr(src, "_extra", {}):
+            dst = self.dst
             E = dst.n_edges
             inv = torch.empty(max(E, 1), dtype=torch.int32, device=dst.device)
             if E:
-                inv[src.eid[:E].long()] = torch.arange(E, dtype=torch.int32, device=dst.device)
-            m = dst.to_csr_order(inv.view(torch.float32)).view(torch.int32)  # bit copy: m[k] = inv[eid[k]]
-            dst.add_gather("src_slot", m, E)
-        return dst
+                inv[dst.eid[:E].long()] = torch.arange(E, dtype=torch.int32, device=dst.device)
+            pos = src.to_csr_order(inv.view(torch.float32)).view(torch.int32)  # bit copy: pos[k] = inv[eid[k]]
+            src.add_gather("dst_slot", src.col, src.n_other, eid=pos)
+        return src
 
 
 class _Cache:

@@ -355,12 +355,12 @@ def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope
     gb = None
     if want_bias:
         gb = gpart.sum(0) if gpart is not None else g.sum(0)
-    src = graph.src
+    src = graph.src_with_dst_slots()
     E = src.n_edges
     gx = torch.empty((N, F), dtype=torch.float32, device=dev)
     ga_src = torch.empty((N, H), dtype=torch.float32, device=dev)
-    de = torch.empty((max(E, 1), H), dtype=torch.float32, device=dev)
-    gs = src.struct("other")
+    de = torch.empty((max(E, 1), H), dtype=torch.float32, device=dev)   # in dst-CSR slot order
+    gs = src.struct("dst_slot")
     sb = lib.mp_gat_slab_bytes(gs, H, C)
     slab = torch.empty(sb, dtype=torch.uint8, device=dev)
     _lib.check(lib.mp_gat_backward_f32(gs, g.data_ptr(), g.stride(0), xw.data_ptr(), a_src.data_ptr(),
@@ -368,8 +368,7 @@ def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope
                                        ga_src.data_ptr(), de.data_ptr(), slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
                "mp_gat_backward_f32")
     del slab, pack
-    dst = graph.dst_gather_src_slots()
-    ga_dst, _ = _aggregate(dst, "src_slot", de, None, "sum", 0, None)
+    ga_dst, _ = _aggregate(graph.dst, "slot", de, None, "sum", 0, None)
     del de
     gatt = None
     if epi:
