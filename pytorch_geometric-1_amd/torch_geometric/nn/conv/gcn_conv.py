@@ -7,11 +7,18 @@ forward: X W on hipBLASLt (torch.matmul), then the normalised aggregation
 + bias as one fused HIP kernel (mi355_mp).  The normalisation (deg over
 edge_index[0] after add_remaining_self_loops, deg^-1/2 with inf -> 0,
 norm = dinv[row] * w * dinv[col]) is the native mp_gcn_norm_f32.
+
+``aggregate_first=True`` (an extension; default False keeps the reference's
+order and results): when in_channels < out_channels the layer computes
+(Â X) W + b instead of Â (X W) + b -- the aggregation then moves
+in_channels-wide rows instead of out_channels-wide ones.  The
+two orders agree to rounding, not bit for bit.
 """
 import torch
 from torch.nn import Parameter
 
 from mi355_mp import ops as _ops
+from mi355_mp.graph import graph_for
 
 from ..inits import glorot, zeros
 from .message_passing import MessagePassing
@@ -30,16 +37,19 @@ class GCNConv(MessagePassing):
         cached (bool): cache the normalised edge_index/norm of the first call.
         bias (bool): learn an additive bias. (default: True)
         normalize (bool): apply the symmetric normalisation. (default: True)
+        aggregate_first (bool): aggregate before the feature transform when
+            in_channels < out_channels. (default: False)
     """
 
     def __init__(self, in_channels, out_channels, improved=False, cached=False, bias=True,
-                 normalize=True, **kwargs):
+                 normalize=True, aggregate_first=False, **kwargs):
         super(GCNConv, self).__init__(aggr="add", **kwargs)
         self.in_channels = in_channels
         self.out_channels = out_channels
         self.improved = improved
         self.cached = cached
         self.normalize = normalize
+        self.aggregate_first = aggregate_first
         self.weight = Parameter(torch.Tensor(in_channels, out_channels))
         if bias:
             self.bias = Parameter(torch.Tensor(out_channels))
@@ -70,7 +80,9 @@ class GCNConv(MessagePassing):
 
     def forward(self, x, edge_index, edge_weight=None):
         """"""
-        x = _ops.feature_transform(x, self.weight)
+        reorder = self.aggregate_first and self.in_channels < self.out_channels
+        if not reorder:
+            x = _ops.feature_transform(x, self.weight)
 
         if self.cached and self.cached_result is not None:
             if edge_index.size(1) != self.cached_num_edges:
@@ -89,6 +101,12 @@ class GCNConv(MessagePassing):
             self.cached_result = edge_index, norm
 
         edge_index, norm = self.cached_result
+        if reorder:
+            n = x.size(self.node_dim)
+            graph = graph_for(edge_index, n, n, self.flow)
+            h = _ops.fused_propagate(graph, x, edge_index, edge_weight=norm, reduce="sum")
+            out = _ops.feature_transform(h, self.weight)
+            return out + self.bias if self.bias is not None else out
         return self.propagate(edge_index, x=x, norm=norm)
 
     def message(self, x_j, norm):

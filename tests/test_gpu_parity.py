@@ -819,3 +819,64 @@ def test_feature_transform_split_k_weight_grad():
     want_x = gout.double() @ w.double().t()
     assert torch.allclose(wd.grad.cpu().double(), want_w, rtol=1e-5, atol=1e-3)
     assert torch.allclose(xd.grad.cpu().double(), want_x, rtol=1e-5, atol=1e-4)
+
+
+def test_data_parallel_replicas_match_batched_model():
+    """nn.DataParallel over a list of small graphs (the reference's
+    examples/data_parallel.py pattern) == the model on the whole Batch."""
+    import torch.nn.functional as Fn
+    from torch_geometric.data import Data, Batch
+    from torch_geometric.nn import DataParallel, GCNConv, global_mean_pool
+    _, _, _, _, pl = _mods()
+    g = torch.Generator().manual_seed(44)
+    graphs = []
+    for i in range(12):
+        n = int(torch.randint(5, 40, (1,), generator=g))
+        graphs.append(Data(x=torch.randn(n, 8, generator=g), edge_index=pl(n, 4 * n, seed=100 + i),
+                           y=torch.tensor([i % 3])))
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super(Net, self).__init__()
+            self.conv = GCNConv(8, 16)
+            self.lin = torch.nn.Linear(16, 3)
+
+        def forward(self, data):
+            h = Fn.relu(self.conv(data.x, data.edge_index))
+            return Fn.log_softmax(self.lin(global_mean_pool(h, data.batch)), dim=1)
+
+    torch.manual_seed(0)
+    net = Net().to(DEV)
+    dp = DataParallel(net)
+    out = dp(graphs)
+    ref = net(Batch.from_data_list(graphs).to(DEV))
+    assert out.shape == (12, 3) and torch.equal(out, ref)
+    loss = Fn.nll_loss(out, torch.cat([d.y for d in graphs]).to(DEV))
+    loss.backward()
+    assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in net.parameters())
+
+
+def test_gcn_aggregate_first_matches_reference_order():
+    """GCNConv(aggregate_first=True) computes (A X) W + b when F_in < F_out:
+    equal to the reference order within fp32 rounding, forward and backward."""
+    from torch_geometric.nn import GCNConv
+    _, _, _, _, pl = _mods()
+    N, E, Fi, Fo = 900, 12000, 16, 64
+    ei = pl(N, E, seed=61).to(DEV)
+    x = torch.randn(N, Fi, generator=torch.Generator().manual_seed(61)).to(DEV)
+    a = GCNConv(Fi, Fo).to(DEV)
+    b = GCNConv(Fi, Fo, aggregate_first=True).to(DEV)
+    with torch.no_grad():
+        b.weight.copy_(a.weight)
+        a.bias.normal_()
+        b.bias.copy_(a.bias)
+    xa = x.clone().requires_grad_(True)
+    xb = x.clone().requires_grad_(True)
+    ya, yb = a(xa, ei), b(xb, ei)
+    assert torch.allclose(ya, yb, rtol=1e-5, atol=1e-5)
+    gout = torch.randn_like(ya)
+    ya.backward(gout)
+    yb.backward(gout)
+    assert torch.allclose(xa.grad, xb.grad, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(a.weight.grad, b.weight.grad, rtol=1e-4, atol=1e-4)
+    assert torch.allclose(a.bias.grad, b.bias.grad, rtol=1e-5, atol=1e-5)

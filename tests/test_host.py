@@ -159,3 +159,35 @@ def test_gcn_structure_cache_matches_reference_loops():
     from torch_geometric.utils import add_remaining_self_loops
     u_ei, u_w = add_remaining_self_loops(ei, w, 2, 4)
     assert torch.equal(u_ei, r_ei) and torch.equal(u_w, r_w)
+
+
+def test_data_batch_semantics():
+    from torch_geometric.data import Data, Batch, DataLoader, DataListLoader
+    d1 = Data(x=torch.randn(3, 4), edge_index=torch.tensor([[0, 1, 2], [1, 2, 0]]), y=torch.tensor([1]),
+              mask=torch.tensor([True, False, True]))
+    d2 = Data(x=torch.randn(2, 4), edge_index=torch.tensor([[0], [1]]), y=torch.tensor([0]),
+              mask=torch.tensor([False, True]))
+    assert d1.num_nodes == 3 and d1.num_edges == 3 and d1.num_node_features == 4
+    assert Data(edge_index=torch.tensor([[0, 5], [1, 2]])).num_nodes == 6
+    assert Data(edge_index=torch.tensor([[0], [1]]), num_nodes=10).num_nodes == 10
+    b = Batch.from_data_list([d1, d2], follow_batch=["x"])
+    # edge_index offset by the running node count, concatenated along the last dim
+    assert b.edge_index.tolist() == [[0, 1, 2, 3], [1, 2, 0, 4]]
+    assert b.batch.tolist() == [0, 0, 0, 1, 1] and b.num_graphs == 2
+    assert torch.equal(b.x, torch.cat([d1.x, d2.x])) and b.y.tolist() == [1, 0]
+    assert b.mask.tolist() == [True, False, True, False, True]        # bool: never offset
+    assert b.x_batch.tolist() == [0, 0, 0, 1, 1]
+    assert d1.contains_self_loops() is False and d1.is_undirected() is False
+    lists = list(DataListLoader([d1, d2, d1], batch_size=2))
+    assert isinstance(lists[0], list) and len(lists[0]) == 2 and len(lists[1]) == 1
+    batches = list(DataLoader([d1, d2, d1], batch_size=3))
+    assert isinstance(batches[0], Batch) and batches[0].num_graphs == 3
+
+
+def test_data_parallel_split_points():
+    from torch_geometric.nn.data_parallel import split_points
+    assert split_points([10, 10, 10, 10], 2) == [0, 2, 4]
+    assert split_points([100, 1, 1, 1], 2) == [0, 1, 4]
+    assert split_points([5, 5, 5], 8) == [0, 1, 2, 3]                  # at most one chunk per graph
+    s = split_points([3, 9, 1, 7, 7, 2, 8, 4], 4)
+    assert s[0] == 0 and s[-1] == 8 and all(a <= b for a, b in zip(s, s[1:]))

@@ -199,6 +199,26 @@ def c3train(dev):
                       "forward_ms": fwd, "forward_backward_ms": step}), flush=True)
 
 
+def c5reorder(dev):
+    """ogbn-products-shaped first layer GCNConv(100, 256): reference order
+    A (X W) vs aggregate_first (A X) W, forward + backward."""
+    from mi355_mp.graphgen import powerlaw_edge_index
+    from torch_geometric.nn import GCNConv
+    N, E = 2_449_029, 123_718_280
+    ei = powerlaw_edge_index(N, E, seed=4, device=dev)
+    x = torch.randn(N, 100, device=dev)
+    res = {}
+    for name, af in (("reference_order", False), ("aggregate_first", True)):
+        torch.manual_seed(0)
+        conv = GCNConv(100, 256, cached=True, aggregate_first=af).to(dev)
+        fwd, step = _train_step_ms(conv, x, ei)
+        res[name] = {"forward_ms": fwd, "forward_backward_ms": step}
+        del conv
+        torch.cuda.empty_cache()
+    print(json.dumps({"config": "c5reorder", "desc": "GCNConv(100, 256) on ogbn-products-scale power law",
+                      **res}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="c3,c4,c5,c2train,c3train")
