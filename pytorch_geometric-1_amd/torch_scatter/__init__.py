@@ -8,6 +8,12 @@ the reference tree -- see SURVEY.md 2b U8/U9):
     scatter_mean(src, index, dim=-1, out=None, dim_size=None)
     scatter_max / scatter_min(src, index, dim=-1, out=None, dim_size=None) -> (out, arg)
     scatter(src, index, dim=-1, out=None, dim_size=None, reduce="sum")
+    segment_csr(src, indptr, out=None, reduce="sum"), gather_csr(src, indptr, out=None)
+    segment_coo(src, index, out=None, dim_size=None, reduce="sum"), gather_coo(src, index, out=None)
+
+The compiled package's dispatcher ops are registered too (torch.ops.torch_scatter.
+scatter_max/min, segment_{sum,mean,min,max}_{csr,coo}, gather_{csr,coo}; the
+schemas of torch_scatter 2.0.4's csrc), so TorchScript-visible callers resolve.
 
 All reductions run as destination-sorted segmented reductions in HIP
 (mi355_mp.ops); fp32 on a ROCm device only -- there is no CPU path.
@@ -20,7 +26,7 @@ from mi355_mp import _lib
 __version__ = "2.0.4"
 
 __all__ = ["scatter", "scatter_sum", "scatter_add", "scatter_mean", "scatter_max", "scatter_min",
-           "segment_csr", "gather_csr"]
+           "segment_csr", "gather_csr", "segment_coo", "gather_coo"]
 
 
 def _index_1d(src, index, dim):
@@ -136,3 +142,67 @@ def gather_csr(src, indptr, out=None):
         out.copy_(res)
         return out
     return res
+
+
+def segment_coo(src, index, out=None, dim_size=None, reduce="sum"):
+    """torch_scatter.segment_coo for a sorted 1-D index along dim 0: the same
+    reduction as scatter (each segment in edge order, first-index argmax)."""
+    _lib.require_device(src, index)
+    if index.numel() > 1 and bool((index[1:] < index[:-1]).any()):
+        raise ValueError("segment_coo: index must be sorted")
+    res = _reduce(src, index, 0, out, dim_size, "sum" if reduce == "add" else reduce)
+    return res if reduce in ("max", "min") else res[0]
+
+
+def gather_coo(src, index, out=None):
+    """torch_scatter.gather_coo along dim 0: out[e] = src[index[e]]."""
+    _lib.require_device(src, index)
+    res = _ops.index_select_rows(src.reshape(src.shape[0], -1), index).reshape((-1,) + tuple(src.shape[1:]))
+    if out is not None:
+        out.copy_(res)
+        return out
+    return res
+
+
+# ---------------------------------------------------------------------------
+# dispatcher registration (torch.ops.torch_scatter.*)
+# ---------------------------------------------------------------------------
+
+def _register_ops():
+    try:
+        lib = torch.library.Library("torch_scatter", "DEF")
+    except RuntimeError:  # namespace already defined by another loader
+        return None
+    defs = {
+        "scatter_max": ("(Tensor src, Tensor index, int dim, Tensor? optional_out, int? dim_size) -> (Tensor, Tensor)",
+                        lambda s, i, d, o, n: scatter_max(s, i, d, o, n)),
+        "scatter_min": ("(Tensor src, Tensor index, int dim, Tensor? optional_out, int? dim_size) -> (Tensor, Tensor)",
+                        lambda s, i, d, o, n: scatter_min(s, i, d, o, n)),
+        "segment_sum_csr": ("(Tensor src, Tensor indptr, Tensor? optional_out) -> Tensor",
+                            lambda s, p, o: segment_csr(s, p, o, "sum")),
+        "segment_mean_csr": ("(Tensor src, Tensor indptr, Tensor? optional_out) -> Tensor",
+                             lambda s, p, o: segment_csr(s, p, o, "mean")),
+        "segment_min_csr": ("(Tensor src, Tensor indptr, Tensor? optional_out) -> (Tensor, Tensor)",
+                            lambda s, p, o: segment_csr(s, p, o, "min")),
+        "segment_max_csr": ("(Tensor src, Tensor indptr, Tensor? optional_out) -> (Tensor, Tensor)",
+                            lambda s, p, o: segment_csr(s, p, o, "max")),
+        "gather_csr": ("(Tensor src, Tensor indptr, Tensor? optional_out) -> Tensor",
+                       lambda s, p, o: gather_csr(s, p, o)),
+        "segment_sum_coo": ("(Tensor src, Tensor index, Tensor? optional_out, int? dim_size) -> Tensor",
+                            lambda s, i, o, n: segment_coo(s, i, o, n, "sum")),
+        "segment_mean_coo": ("(Tensor src, Tensor index, Tensor? optional_out, int? dim_size) -> Tensor",
+                             lambda s, i, o, n: segment_coo(s, i, o, n, "mean")),
+        "segment_min_coo": ("(Tensor src, Tensor index, Tensor? optional_out, int? dim_size) -> (Tensor, Tensor)",
+                            lambda s, i, o, n: segment_coo(s, i, o, n, "min")),
+        "segment_max_coo": ("(Tensor src, Tensor index, Tensor? optional_out, int? dim_size) -> (Tensor, Tensor)",
+                            lambda s, i, o, n: segment_coo(s, i, o, n, "max")),
+        "gather_coo": ("(Tensor src, Tensor index, Tensor? optional_out) -> Tensor",
+                       lambda s, i, o: gather_coo(s, i, o)),
+    }
+    for name, (schema, fn) in defs.items():
+        lib.define(name + schema)
+        lib.impl(name, fn, "CompositeImplicitAutograd")
+    return lib
+
+
+_LIB = _register_ops()

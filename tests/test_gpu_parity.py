@@ -880,3 +880,38 @@ def test_gcn_aggregate_first_matches_reference_order():
     assert torch.allclose(xa.grad, xb.grad, rtol=1e-4, atol=1e-5)
     assert torch.allclose(a.weight.grad, b.weight.grad, rtol=1e-4, atol=1e-4)
     assert torch.allclose(a.bias.grad, b.bias.grad, rtol=1e-5, atol=1e-5)
+
+
+def test_torch_scatter_coo_csr_and_dispatcher_ops():
+    import torch_scatter
+    g = torch.Generator().manual_seed(71)
+    E, N, F = 5000, 300, 24
+    index = torch.sort(torch.randint(0, N, (E,), generator=g)).values
+    src = torch.randint(-3, 4, (E, F), generator=g).to(torch.float32)   # ties
+    sd, idd = src.to(DEV), index.to(DEV)
+    counts = torch.bincount(index, minlength=N)
+    indptr = torch.cat([torch.zeros(1, dtype=torch.long), counts.cumsum(0)])
+    for reduce in ("sum", "mean", "max", "min"):
+        want = S.scatter_loop(src, index, N, reduce) if reduce in ("max", "min") else None
+        got_coo = torch_scatter.segment_coo(sd, idd, dim_size=N, reduce=reduce)
+        got_csr = torch_scatter.segment_csr(sd, indptr.to(DEV), reduce=reduce)
+        op_coo = getattr(torch.ops.torch_scatter, "segment_%s_coo" % reduce)(sd, idd, None, N)
+        op_csr = getattr(torch.ops.torch_scatter, "segment_%s_csr" % reduce)(sd, indptr.to(DEV), None)
+        if reduce in ("max", "min"):
+            for got in (got_coo, got_csr, op_coo, op_csr):
+                assert torch.equal(got[0].cpu(), want[0]) and torch.equal(got[1].cpu(), want[1])
+        else:
+            ref = S.scatter_sum(src, index, N) if reduce == "sum" else S.scatter_mean(src, index, N)
+            for got in (got_coo, got_csr, op_coo, op_csr):
+                assert torch.equal(got.cpu(), ref)
+    assert torch.equal(torch_scatter.gather_coo(sd, idd).cpu(), src[index])
+    y = torch.randn(N, 5, generator=g)
+    assert torch.equal(torch.ops.torch_scatter.gather_csr(y.to(DEV), indptr.to(DEV), None).cpu(), y[index])
+    m1, a1 = torch.ops.torch_scatter.scatter_max(sd, idd, 0, None, N)
+    m2, a2 = torch_scatter.scatter_max(sd, idd, 0, dim_size=N)
+    assert torch.equal(m1, m2) and torch.equal(a1, a2)
+
+    @torch.jit.script
+    def scripted(x: torch.Tensor, p: torch.Tensor) -> torch.Tensor:
+        return torch.ops.torch_scatter.segment_sum_csr(x, p, None)
+    assert torch.equal(scripted(sd, indptr.to(DEV)).cpu(), S.scatter_sum(src, index, N))

@@ -191,3 +191,14 @@ def test_data_parallel_split_points():
     assert split_points([5, 5, 5], 8) == [0, 1, 2, 3]                  # at most one chunk per graph
     s = split_points([3, 9, 1, 7, 7, 2, 8, 4], 4)
     assert s[0] == 0 and s[-1] == 8 and all(a <= b for a, b in zip(s, s[1:]))
+
+
+def test_torch_scatter_dispatcher_ops_registered():
+    import torch_scatter  # noqa: F401  (registers torch.ops.torch_scatter.*)
+    names = ["scatter_max", "scatter_min", "segment_sum_csr", "segment_mean_csr", "segment_min_csr",
+             "segment_max_csr", "gather_csr", "segment_sum_coo", "segment_mean_coo", "segment_min_coo",
+             "segment_max_coo", "gather_coo"]
+    for n in names:
+        assert hasattr(torch.ops.torch_scatter, n), n
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        torch.ops.torch_scatter.segment_sum_csr(torch.ones(3, 2), torch.tensor([0, 2, 3]), None)
