@@ -266,7 +266,7 @@ def main():
                        else "single GPU", "chunk": args.chunk},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_agg_main<SumRed<4,true,false>,VEC=4,U=12,L=32>",
+                         "kernel": "k_agg_flat<SumRed<2,true,false>,VEC=2,U=16,L=64>",
                          "algorithmic_bytes_per_launch": alg_bytes,
                          "avg_launch_ms": main_avg, "median_launch_ms": main_ms[len(main_ms) // 2],
                          "fixup_avg_ms": fix_avg},

@@ -103,6 +103,8 @@ struct AggArgs {
   int32_t F;
   int32_t n_cols;
   uint32_t x_bytes;  // extent of x for the buffer path (0: not used)
+  int32_t flat;      // sum/mean/max/min: run k_agg_flat instead of k_agg_main
+  int32_t fix4;      // VEC=2 main kernel: run the fix-up at VEC=4 (slabs are indexed by feature)
   // features
   const float* w;
   const float* x;
@@ -830,6 +832,139 @@ __global__ __launch_bounds__(kBlock) void k_agg_lane(AggArgs p) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Flat variant of k_agg_main (sum/mean/max/min): a task streams its slots in
+// fixed batches of U across row boundaries and closes rows as it crosses
+// their ends (row ends come from the rowptr window already in registers).
+// k_agg_main starts a new batch at every row, so a short row costs a whole
+// batch of U (clamped) loads and a trip of loop overhead; here every batch
+// but the task's last carries U useful slots, and the next row's loads are
+// in flight while the previous row is finished.  Each row's slots are still
+// consumed in CSR order by one task: results are identical.
+// ---------------------------------------------------------------------------
+template <class Red, int VEC, int U, int L, bool BUF>
+__global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
+  static_assert(!Red::kGat && !Red::kGatB && !Red::kHW, "flat loop: sum/mean/max/min reducers");
+  using GR = Grp<L>;
+  const int lane = lane_id();
+  const int gl = lane & (L - 1);
+  const int bx = (int)blockIdx.x, tile = (int)blockIdx.y;
+  const int wave = bx * kWavesPerBlock + (int)(threadIdx.x >> 6);
+  const int w = GR::un(wave * GR::G + lane / L);
+  if (w >= p.n_waves) return;
+  const int f = tile * L * VEC + gl * VEC;
+  const bool act = f < p.F;
+  const uint32_t foff = (uint32_t)(act ? f : 0) * 4u;
+  const char* xb = reinterpret_cast<const char*>(p.x);
+  const int64_t ldxb = p.ldx * 4;
+  [[maybe_unused]] __amdgpu_buffer_rsrc_t xr;
+  if constexpr (BUF) xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
+
+  const int r_first = GR::un(p.wave_row[w]);
+  const int r_last = GR::un(p.wave_row[w + 1]);
+  const int64_t e_begin = GR::un(p.wave_slot[w]);
+  const int64_t e_end = GR::un(p.wave_slot[w + 1]);
+
+  Red red(p, f, act);
+  SlotWin<Red::kW, Red::kEid, L> win;
+  win.init(p, e_begin, e_end, gl);
+  int rbase = r_first;
+  int rp = (rbase + gl <= p.n_rows) ? p.rowptr[rbase + gl] : 0;
+  // row end / start of row r (r >= rbase), refilling the window when needed
+  auto row_ptr = [&](int r) -> int64_t {
+    if (r - rbase > L - 1) {
+      rbase = r;
+      rp = (rbase + gl <= p.n_rows) ? p.rowptr[rbase + gl] : 0;
+    }
+    return GR::bc(rp, r - rbase);
+  };
+
+  // current row: the continuation of an earlier task's row, or an owned row
+  const int64_t ce = GR::bc(rp, 0);  // rowptr[r_first]
+  bool cont = e_begin < ce;
+  int r = r_first;
+  int64_t rs = ce, re = ce;
+  if (cont) {
+    red.begin(p, r_first - 1, false, f, act);
+  } else if (r < r_last) {
+    re = row_ptr(r + 1);
+    red.begin(p, r, true, f, act);
+  }
+  // close the current row at slot k (k >= its end) and open the next one(s)
+  auto advance = [&](int64_t k) {
+    while (k >= re) {
+      if (cont) {
+        if (act) red.save(slab_ref(p, 2 * (int64_t)w, f, red), false);
+        cont = false;
+      } else {
+        red.finish(p, r, re - rs, f, act);
+        ++r;
+      }
+      if (r >= r_last) {  // cannot happen for a valid schedule: never open a row past the task
+        re = INT64_MAX;
+        break;
+      }
+      rs = re;
+      re = row_ptr(r + 1);
+      red.begin(p, r, true, f, act);
+    }
+  };
+
+  for (int64_t e = e_begin; e < e_end;) {
+    win.ensure(p, e, gl);
+    const int off = (int)(e - win.base);
+    int64_t rem = e_end - e;
+    int n = L - off;
+    if (rem < n) n = (int)rem;
+    if (n > U) n = U;
+    n = GR::un(n);
+    Frag<VEC> v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int uu = u < n ? u : n - 1;
+      const int c = GR::bc(win.col, off + uu);
+      if constexpr (BUF) {
+        v[u] = load_frag_buf<VEC>(xr, (uint32_t)c * (uint32_t)ldxb + foff);
+      } else {
+        v[u] = load_frag<VEC>(reinterpret_cast<const float*>(xb + (int64_t)c * ldxb + foff));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u < n) {
+        advance(e + u);
+        const float wt = Red::kW ? GR::bc(win.w, off + u) : 1.f;
+        const int ei = Red::kEid ? GR::bc(win.eid, off + u) : 0;
+        red.consume(v[u], wt, ei, 0.f);
+      }
+    }
+    e += n;
+  }
+  // tail: the current row, then any rows whose slots all lie in later tasks
+  if (cont) {
+    if (act) red.save(slab_ref(p, 2 * (int64_t)w, f, red), false);
+    cont = false;
+    if (r < r_last) {
+      rs = ce;
+      re = row_ptr(r + 1);
+      red.begin(p, r, true, f, act);
+    }
+  }
+  while (r < r_last) {
+    if (re <= e_end) {
+      red.finish(p, r, re - rs, f, act);
+    } else {
+      if (act) red.save(slab_ref(p, 2 * (int64_t)w + 1, f, red), false);
+    }
+    ++r;
+    if (r < r_last) {
+      rs = re;
+      re = row_ptr(r + 1);
+      red.begin(p, r, true, f, act);
+    }
+  }
+}
+
 // One 4-wave block per split row.  The row's partials form a chain in task
 // order: item 0 = head slab of the owning task, item k = continuation slab of
 // task owner+k.  Wave q reduces items [q*c, (q+1)*c) in order (U loads in
@@ -896,6 +1031,10 @@ struct Shape {
   int vec, lanes;
 };
 
+#ifndef MP_WIDE_FLAT
+#define MP_WIDE_FLAT 1     // rows of >= 256 features, sum/mean/max/min: VEC=2, 64-lane tasks, k_agg_flat
+#endif                     // (A/B vs VEC=4 32-lane groups: -1% sum, -10% max on RMAT21; bit-identical)
+
 #ifndef MP_WIDE_LANES
 #define MP_WIDE_LANES 32   // lanes per task for rows of >= 256 features (A/B: 32 beats 64 by ~9%)
 #endif
@@ -926,6 +1065,20 @@ static Shape pick_shape(int F, int64_t ldx, const void* x, int64_t ldo, const vo
   return {vec, lanes};
 }
 
+// the same reducer at another lane width (fix-up of a VEC=2 main kernel at VEC=4)
+template <class Red, int V>
+struct Rebind {
+  using type = Red;
+};
+template <int VEC, bool W, bool M, int V>
+struct Rebind<SumRed<VEC, W, M>, V> {
+  using type = SumRed<V, W, M>;
+};
+template <int VEC, bool W, bool M, int V>
+struct Rebind<ArgRed<VEC, W, M>, V> {
+  using type = ArgRed<V, W, M>;
+};
+
 template <class Red, int VEC, int L>
 static int launch_l(const AggArgs& a, int stages, hipStream_t s) {
   constexpr int U = VEC == 4 ? (L == 64 ? MP_U_VEC4 : MP_U_NARROW) : 16;
@@ -940,12 +1093,23 @@ static int launch_l(const AggArgs& a, int stages, hipStream_t s) {
       AggArgs b = a;
       b.x_bytes = (uint32_t)xb;
       hipLaunchKernelGGL((k_agg_main<Red, VEC, U, L, MP_BUF_X != 0>), grid, dim3(kBlock), 0, s, b);
+    } else if (a.flat) {
+      if constexpr (!Red::kGat && !Red::kGatB && !Red::kHW)
+        hipLaunchKernelGGL((k_agg_flat<Red, VEC, U, L, false>), grid, dim3(kBlock), 0, s, a);
     } else {
       hipLaunchKernelGGL((k_agg_main<Red, VEC, U, L, false>), grid, dim3(kBlock), 0, s, a);
     }
     MP_CHECK_LAUNCH();
   }
   if ((stages & MP_STAGE_FIXUP) && a.n_split > 0) {
+    if constexpr (VEC == 2 && !Red::kGat && !Red::kGatB && !Red::kHW) {
+      if (a.fix4) {
+        dim3 grid4((unsigned)a.n_split, (unsigned)ceil_div(a.F, 64 * 4));
+        hipLaunchKernelGGL((k_agg_fixup<typename Rebind<Red, 4>::type, 4>), grid4, dim3(kBlock), 0, s, a);
+        MP_CHECK_LAUNCH();
+        return MP_OK;
+      }
+    }
     dim3 grid((unsigned)a.n_split, (unsigned)ceil_div(a.F, 64 * VEC));
     hipLaunchKernelGGL((k_agg_fixup<Red, VEC>), grid, dim3(kBlock), 0, s, a);
     MP_CHECK_LAUNCH();
@@ -1107,7 +1271,13 @@ int mp_aggregate_f32(const mp_csr* g, const float* w, const float* x, int64_t ld
   a.slab_v = (float*)slab;
   a.slab_a = is_arg ? (int32_t*)((char*)slab + v) : nullptr;
   hipStream_t s = as_stream(stream);
-  const Shape sh = pick_shape(F, ldx, x, ldo, out);
+  Shape sh = pick_shape(F, ldx, x, ldo, out);
+  if (MP_WIDE_FLAT && F >= 256 && F % 2 == 0 && sh.vec >= 2) {
+    sh.vec = 2;  // 128-feature tiles, one task per wave, slot batches across rows
+    a.flat = 1;
+    // the fix-up reads slabs by feature: run it 4 wide when out (and bias) allow
+    a.fix4 = F % 4 == 0 && (uintptr_t)out % 16 == 0 && ldo % 4 == 0 && (uintptr_t)bias % 16 == 0;
+  }
   switch (sh.vec) {
     case 4: return dispatch_reduce<4>(a, reduce, stages, s, sh.lanes);
     case 2: return dispatch_reduce<2>(a, reduce, stages, s, 64);

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--F", type=int, default=256)
     ap.add_argument("--reduce", default="sum")
+    ap.add_argument("--graph", default="rmat21", choices=["rmat21", "reddit"])
     args = ap.parse_args()
     import mi355_mp
     from mi355_mp import _lib
@@ -35,9 +36,15 @@ def main():
     from torch_geometric.nn.conv.gcn_conv import GCNConv
     mi355_mp.load_native()
     dev = torch.device("cuda", 0)
-    N = 1 << 21
-    ei = rmat_edge_index(scale=21, n_samples=30_000_000, seed=1, device=dev)
-    ei2, norm = GCNConv.norm(ei, N)
+    if args.graph == "reddit":   # config 4: Reddit-scale power law (x fits the Infinity Cache)
+        from mi355_mp.graphgen import powerlaw_edge_index
+        N = 232_965
+        ei2 = powerlaw_edge_index(N, 114_615_892, seed=3, device=dev)
+        norm = torch.rand(ei2.shape[1], device=dev)
+    else:
+        N = 1 << 21
+        ei = rmat_edge_index(scale=21, n_samples=30_000_000, seed=1, device=dev)
+        ei2, norm = GCNConv.norm(ei, N)
     x = torch.randn(N, args.F, device=dev, generator=torch.Generator(device=dev).manual_seed(1))
     bias = torch.randn(args.F, device=dev) * 0.1
     vdir = os.path.join(ROOT, "tools", "variants")
@@ -51,26 +58,27 @@ def main():
         w = csr.to_csr_order(norm) if args.reduce in ("sum", "mean") else None
         g = csr.struct("other")
         outs = {n: torch.empty(N, args.F, device=dev) for n in names}
-        arg = torch.empty(N, args.F, dtype=torch.int64, device=dev) if red >= 2 else None
+        args_out = {n: torch.empty(N, args.F, dtype=torch.int64, device=dev) if red >= 2 else None for n in names}
         sb = libs[names[0]].mp_aggregate_slab_bytes(g, args.F, red)
         slab = torch.empty(sb, dtype=torch.uint8, device=dev)
         st = torch.cuda.current_stream().cuda_stream
 
-        def launch(lib, out, stages):
+        def launch(lib, out, stages, arg=None):
             _lib.check(lib.mp_aggregate_f32(g, _lib.ptr(w), x.data_ptr(), x.stride(0), args.F, red, 0,
                                             bias.data_ptr(), out.data_ptr(), out.stride(0), _lib.ptr(arg),
                                             slab.data_ptr(), sb, stages, st), "agg")
         for n in names:
-            launch(libs[n], outs[n], _lib.MP_STAGE_ALL)
+            launch(libs[n], outs[n], _lib.MP_STAGE_ALL, args_out[n])
         torch.cuda.synchronize()
-        same = {n: bool(torch.equal(outs[n], outs[names[0]])) for n in names}
+        same = {n: bool(torch.equal(outs[n], outs[names[0]])) and
+                (args_out[n] is None or bool(torch.equal(args_out[n], args_out[names[0]]))) for n in names}
         times = {n: [] for n in names}
         for _ in range(args.rounds):
             for n in names:
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record()
                 for _ in range(args.reps):
-                    launch(libs[n], outs[n], _lib.MP_STAGE_MAIN)
+                    launch(libs[n], outs[n], _lib.MP_STAGE_MAIN, args_out[n])
                 b.record()
                 torch.cuda.synchronize()
                 times[n].append(a.elapsed_time(b) / args.reps)

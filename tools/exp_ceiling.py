@@ -18,6 +18,8 @@ def main():
     from mi355_mp.graphgen import rmat_edge_index
     from torch_geometric.nn.conv.gcn_conv import GCNConv
     lib = mi355_mp.load_native()
+    if os.environ.get("EXP_LIB"):   # a build variant (tools/variants/lib_*.so)
+        lib = _lib.load(os.environ["EXP_LIB"])
     dev = torch.device("cuda", 0)
     N = 1 << 21
     F = int(os.environ.get("EXP_F", "256"))

@@ -6,8 +6,9 @@ Writes profiles/<round>_kernel_stats.csv (copy of the --stats summary),
 profiles/<round>_pmc_traffic.json: per-launch FETCH_SIZE / WRITE_SIZE of the
 dominant kernel, corrected as MI355X_MICROARCH.md 'HBM' prescribes
 (FETCH_SIZE and WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reads half the bytes
-of a 16 B/lane coalesced stream -> doubled; WRITE_SIZE exact for 16 B/lane
-stores), plus the L2 hit rate.  bench.py reads the json for roofline.traffic.
+of a 16 B/lane coalesced stream -> doubled, and profiles/r01_pmc_calibration.json
+measures the same factor for this kernel's 8 B/lane loads; WRITE_SIZE exact
+for 16 B/lane stores), plus the L2 hit rate.  bench.py reads the json for roofline.traffic.
 """
 import csv
 import json
@@ -15,7 +16,7 @@ import os
 import shutil
 import sys
 
-KERNEL = "k_agg_main<mp::SumRed<4, true, false>, 4, 12, 32>"
+KERNEL = "k_agg_flat<mp::SumRed<2, true, false>, 2, 16, 64, false>"
 
 
 def per_launch(path, counter):
@@ -52,7 +53,8 @@ def main():
         "l2_hit_rate": hit / (hit + miss) if hit is not None and miss else None,
         "kernel_trace_avg_ms": avg_ns / 1e6 if avg_ns else None,
         "note": "FETCH_SIZE counts L2->fabric reads (Infinity-Cache hits included): an upper bound "
-                "on HBM reads; doubled per the gfx950 16 B/lane correction",
+                "on HBM reads; doubled per the gfx950 correction (calibrated for this kernel's 8 B/lane "
+                "loads in profiles/r01_pmc_calibration.json)",
     }
     with open("profiles/%s_pmc_traffic.json" % rnd, "w") as f:
         json.dump(out, f, indent=1)
