@@ -29,17 +29,30 @@ __all__ = ["scatter", "scatter_sum", "scatter_add", "scatter_mean", "scatter_max
            "segment_csr", "gather_csr", "segment_coo", "gather_coo"]
 
 
+def _broadcast(index, src, dim):
+    """torch_scatter.utils.broadcast: a 1-D index is laid along `dim`, missing
+    trailing dims are appended, then the index is expanded to src's shape."""
+    if index.dim() == 1:
+        for _ in range(dim):
+            index = index.unsqueeze(0)
+    while index.dim() < src.dim():
+        index = index.unsqueeze(-1)
+    return index.expand_as(src)
+
+
 def _index_1d(src, index, dim):
-    """Reduce torch_scatter's broadcast index to the 1-D index along `dim`."""
+    """The 1-D index along `dim` when torch_scatter's broadcast index is the
+    same for every position of the other dims (PyG's case); None when the
+    index is element-wise (handled by the general path)."""
     if index.dim() == 1:
         if index.numel() != src.size(dim):
             raise ValueError("index of size %d does not match src.size(%d) = %d"
                              % (index.numel(), dim, src.size(dim)))
         return index
-    if index.dim() != src.dim():
-        # torch_scatter.utils.broadcast: trailing singleton dims are appended
-        while index.dim() < src.dim():
-            index = index.unsqueeze(-1)
+    if index.dim() > src.dim():
+        raise ValueError("index has more dimensions than src")
+    while index.dim() < src.dim():
+        index = index.unsqueeze(-1)
     sl = [0] * index.dim()
     sl[dim] = slice(None)
     first = index[tuple(sl)]
@@ -49,8 +62,7 @@ def _index_1d(src, index, dim):
     view[dim] = -1
     if bool((index == first.view(view)).all()):
         return first
-    raise NotImplementedError("mi355_mp: element-wise (non-broadcast) scatter indices are not "
-                              "supported; pass a 1-D index along `dim`")
+    return None
 
 
 def _prepare(src, index, dim, dim_size):
@@ -72,7 +84,48 @@ def _finish(out2, dim, rest):
     return out.movedim(0, dim)
 
 
+def _reduce_general(src, index, dim, out, dim_size, reduce):
+    """Element-wise index: out[..., index[..., e, ...], ...] over every position.
+    Flattened to one 1-D segmented reduction: key = (position of the other
+    dims) * dim_size + index, one feature per element; the stable CSR sort keeps
+    each output's elements in their original order along `dim`."""
+    idx = _broadcast(index, src, dim).to(torch.int64)
+    if out is not None:
+        dim_size = out.size(dim)
+    elif dim_size is None:
+        dim_size = int(idx.max()) + 1 if idx.numel() > 0 else 0
+    s = src.movedim(dim, -1)
+    ix = idx.movedim(dim, -1)
+    lead = tuple(s.shape[:-1])
+    L = s.shape[-1]
+    B = s.numel() // L if L else 0
+    keys = (torch.arange(B, device=src.device).view(-1, 1) * dim_size + ix.reshape(B, L)).reshape(-1)
+    vals = s.reshape(-1, 1)
+    if out is not None:
+        o = out.movedim(dim, -1).reshape(B * dim_size, 1).contiguous()
+        res, arg = _ops.segment_reduce_into(vals, keys, o, reduce)
+        out.copy_(res.view(lead + (dim_size,)).movedim(-1, dim))
+        res_t = out
+    else:
+        res, arg = _ops.segment_reduce(vals, keys, B * dim_size, reduce)
+        res_t = res.view(lead + (dim_size,)).movedim(-1, dim)
+    arg_t = None
+    if arg is not None:   # flat element position -> position along dim (empty: src.size(dim))
+        a = arg.view(-1)
+        a = torch.where(a >= B * L, torch.full_like(a, L), a % max(L, 1))
+        arg_t = a.view(lead + (dim_size,)).movedim(-1, dim)
+    return res_t, arg_t
+
+
 def _reduce(src, index, dim, out, dim_size, reduce):
+    _lib.require_device(src, index)
+    if src.dtype != torch.float32:
+        raise TypeError("mi355_mp: scatter ops are implemented for float32 (got %s)" % src.dtype)
+    d = dim % src.dim() if src.dim() else 0
+    if _index_1d(src, index, d) is None:
+        if out is not None:
+            _lib.require_device(out)
+        return _reduce_general(src, index, d, out, dim_size, reduce)
     if out is not None:
         dim = dim % src.dim()
         dim_size = out.size(dim)

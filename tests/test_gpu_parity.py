@@ -915,3 +915,87 @@ def test_torch_scatter_coo_csr_and_dispatcher_ops():
     def scripted(x: torch.Tensor, p: torch.Tensor) -> torch.Tensor:
         return torch.ops.torch_scatter.segment_sum_csr(x, p, None)
     assert torch.equal(scripted(sd, indptr.to(DEV)).cpu(), S.scatter_sum(src, index, N))
+
+
+# torch_scatter's README scatter_max example (element-wise 2-D index, dim=-1),
+# with the output and argmax printed there
+_README_SRC = [[2, 0, 1, 4, 3], [0, 2, 1, 3, 4]]
+_README_INDEX = [[4, 5, 4, 2, 3], [0, 0, 2, 2, 1]]
+_README_OUT = [[0, 0, 4, 3, 2, 0], [2, 4, 3, 0, 0, 0]]
+_README_ARG = [[5, 5, 3, 4, 0, 1], [1, 4, 3, 5, 5, 5]]
+
+
+def _scatter_loop_general(src, index, dim, dim_size, reduce):
+    """Sequential fp32 loop over src in order along `dim` (torch_scatter CPU semantics)."""
+    s = src.movedim(dim, -1)
+    ix = index.expand_as(src).movedim(dim, -1) if index.dim() == src.dim() else None
+    lead, L = s.shape[:-1], s.shape[-1]
+    out = torch.zeros(lead + (dim_size,), dtype=torch.float32)
+    arg = torch.full(lead + (dim_size,), L, dtype=torch.long)
+    cnt = torch.zeros(lead + (dim_size,), dtype=torch.long)
+    for b in torch.cartesian_prod(*[torch.arange(n) for n in lead]) if len(lead) > 1 else \
+            [torch.tensor([i]) for i in range(lead[0])]:
+        b = tuple(b.tolist())
+        acc = {}
+        for e in range(L):
+            k = int(ix[b + (e,)])
+            v = s[b + (e,)].view(1)
+            if k not in acc:
+                acc[k] = [v.clone(), e]
+                cnt[b + (k,)] = 1
+                continue
+            cnt[b + (k,)] += 1
+            if reduce in ("sum", "mean"):
+                acc[k][0] = acc[k][0] + v
+            elif (reduce == "max" and v > acc[k][0]) or (reduce == "min" and v < acc[k][0]):
+                acc[k] = [v.clone(), e]
+        for k, (v, e) in acc.items():
+            out[b + (k,)] = v if reduce != "mean" else v / cnt[b + (k,)].to(torch.float32)
+            arg[b + (k,)] = e
+    return out.movedim(-1, dim), arg.movedim(-1, dim)
+
+
+def test_torch_scatter_elementwise_index_readme_and_vectors():
+    import torch_scatter
+    src = torch.tensor(_README_SRC, dtype=torch.float32).to(DEV)
+    index = torch.tensor(_README_INDEX).to(DEV)
+    out, arg = torch_scatter.scatter_max(src, index, dim=-1)
+    assert out.tolist() == _README_OUT and arg.tolist() == _README_ARG
+    # the same layout along dim=1 with other reductions (values derived by hand)
+    src2 = torch.tensor([[1, 5, 3, 7, 9, 11], [2, 4, 8, 6, 10, 12]], dtype=torch.float32).to(DEV)
+    idx2 = torch.tensor([[0, 1, 0, 1, 1, 3], [0, 0, 1, 0, 1, 2]]).to(DEV)
+    assert torch_scatter.scatter_sum(src2, idx2, 1).tolist() == [[4, 21, 0, 11], [12, 18, 12, 0]]
+    assert torch_scatter.scatter_mean(src2, idx2, 1).tolist() == [[2, 7, 0, 11], [4, 9, 12, 0]]
+    mn, amn = torch_scatter.scatter_min(src2, idx2, 1)
+    assert mn.tolist() == [[1, 5, 0, 11], [2, 8, 12, 0]] and amn.tolist() == [[0, 1, 6, 5], [0, 2, 5, 6]]
+    mx, amx = torch_scatter.scatter_max(src2, idx2, 1)
+    assert mx.tolist() == [[3, 9, 0, 11], [6, 10, 12, 0]] and amx.tolist() == [[2, 4, 6, 5], [3, 4, 5, 6]]
+
+
+@pytest.mark.parametrize("dim", [-1, 1, 0])
+def test_torch_scatter_elementwise_index_random(dim):
+    import torch_scatter
+    g = torch.Generator().manual_seed(90 + dim)
+    src = torch.randint(-5, 6, (3, 7, 40), generator=g).to(torch.float32) + \
+        torch.rand(3, 7, 40, generator=g) * 0.5
+    n = src.size(dim)
+    index = torch.randint(0, 9, src.shape, generator=g)
+    for reduce in ("sum", "mean", "max", "min"):
+        want, warg = _scatter_loop_general(src, index, dim % 3, 9, reduce)
+        got = torch_scatter.scatter(src.to(DEV), index.to(DEV), dim, dim_size=9, reduce=reduce).cpu()
+        assert torch.equal(got, want), reduce
+        if reduce in ("max", "min"):
+            _, garg = getattr(torch_scatter, "scatter_" + reduce)(src.to(DEV), index.to(DEV), dim, dim_size=9)
+            assert torch.equal(garg.cpu(), warg), reduce
+    # out= accumulates into the given values
+    base = torch.randn(want.shape, generator=g)
+    o = base.clone().to(DEV)
+    torch_scatter.scatter_sum(src.to(DEV), index.to(DEV), dim, out=o)
+    want_sum, _ = _scatter_loop_general(src, index, dim % 3, 9, "sum")
+    assert torch.allclose(o.cpu(), base + want_sum, atol=1e-5)
+    # gradient of sum = gather of grad_out at index
+    s = src.to(DEV).requires_grad_(True)
+    gout = torch.randn(want.shape, generator=g)
+    torch_scatter.scatter_sum(s, index.to(DEV), dim, dim_size=9).backward(gout.to(DEV))
+    assert torch.equal(s.grad.cpu(), torch.gather(gout, dim % 3, index))
+    del n

@@ -159,3 +159,21 @@ def test_golden_fixture_reproduces(name):
     fresh = make_golden.compute(name[:-4], {k: d[k] for k in d.files})
     for k, v in fresh.items():
         assert np.array_equal(np.asarray(v), d[k]), (name, k)
+
+
+def test_oracle_torch_scatter_documented_vectors():
+    """torch_scatter 2.0.4 semantics on its documented small cases (1-D index
+    along dim 0; empty segment -> 0 with arg = src.size(0); first index wins)."""
+    from oracle import scatter_ref as S
+    src = torch.tensor([1., 3, 2, 4, 5, 6])
+    index = torch.tensor([0, 1, 0, 1, 1, 3])
+    assert S.scatter_sum(src.view(-1, 1), index, 4).view(-1).tolist() == [3, 12, 0, 6]
+    assert S.scatter_mean(src.view(-1, 1), index, 4).view(-1).tolist() == [1.5, 4, 0, 6]
+    mn, amn = S.scatter_loop(src.view(-1, 1), index, 4, "min")
+    mx, amx = S.scatter_loop(src.view(-1, 1), index, 4, "max")
+    assert mn.view(-1).tolist() == [1, 3, 0, 6] and amn.view(-1).tolist() == [0, 1, 6, 5]
+    assert mx.view(-1).tolist() == [2, 5, 0, 6] and amx.view(-1).tolist() == [2, 4, 6, 5]
+    src2 = torch.tensor([[1., 2], [5, 6], [3, 4], [7, 8], [9, 10], [11, 12]])
+    assert S.scatter_sum(src2, index, 4).tolist() == [[4, 6], [21, 24], [0, 0], [11, 12]]
+    mx2, amx2 = S.scatter_loop(src2, index, 4, "max")
+    assert mx2.tolist() == [[3, 4], [9, 10], [0, 0], [11, 12]] and amx2.tolist() == [[2, 2], [4, 4], [6, 6], [5, 5]]
