@@ -108,7 +108,7 @@ int mp_csr_build(const int64_t* key, const int64_t* other, int64_t n_edges,
                  int32_t* eid, int32_t* bad, void* ws, size_t ws_bytes,
                  void* stream);
 
-/* Number of wave tasks for `chunk` merged positions per task (chunk % 64 == 0). */
+/* Number of wave tasks for `chunk` merged positions per task (chunk a multiple of 8, >= 16). */
 int32_t mp_schedule_n_waves(int64_t n_rows, int64_t n_edges, int32_t chunk);
 size_t mp_schedule_workspace(int32_t n_waves);
 

@@ -1208,7 +1208,7 @@ static int check_graph(const mp_csr* g, const char* who) {
   MP_CHECK_ARG(g->rowptr && g->wave_row && g->wave_slot && (g->n_split == 0 || g->split_waves),
                "%s: graph has null arrays", who);
   MP_CHECK_ARG(g->n_edges == 0 || g->eid, "%s: graph has null eid", who);
-  MP_CHECK_ARG(g->chunk > 0 && g->chunk % 64 == 0 && g->n_waves >= 1, "%s: bad schedule", who);
+  MP_CHECK_ARG(g->chunk >= 16 && g->chunk % 8 == 0 && g->n_waves >= 1, "%s: bad schedule", who);
   return MP_OK;
 }
 

@@ -232,7 +232,7 @@ size_t mp_schedule_workspace(int32_t n_waves) {
 int mp_schedule_build(const int32_t* rowptr, int64_t n_rows, int64_t n_edges, int32_t chunk,
                       int32_t snap, int32_t* wave_row, int32_t* wave_slot, int32_t* split_waves,
                       int32_t* n_split_dev, void* ws, size_t ws_bytes, void* stream) {
-  MP_CHECK_ARG(chunk > 0 && chunk % 64 == 0, "mp_schedule_build: chunk must be a positive multiple of 64");
+  MP_CHECK_ARG(chunk >= 16 && chunk % 8 == 0, "mp_schedule_build: chunk must be a multiple of 8, >= 16");
   MP_CHECK_ARG(snap >= 0 && snap < chunk - 1, "mp_schedule_build: need 0 <= snap < chunk - 1");
   MP_CHECK_ARG(rowptr && wave_row && wave_slot && split_waves && n_split_dev,
                "mp_schedule_build: null pointer");

@@ -146,7 +146,7 @@ class OverlappedAggregation:
     1e-5 bound of the single-GPU order, not bit-identical to it.
     """
 
-    def __init__(self, plan, edge_weight=None, chunk=256):
+    def __init__(self, plan, edge_weight=None, chunk=None):
         from .graph import Graph
         self.plan = plan
         lei = plan.local_edge_index

@@ -15,7 +15,20 @@ import torch
 
 from . import _lib
 
-DEFAULT_CHUNK = 256
+DEFAULT_CHUNK = None   # auto: see auto_chunk()
+MAX_CHUNK = 256
+
+
+def auto_chunk(n_rows, n_edges):
+    """Merge-path task size: 256 work units (rows + slots) for large graphs, fewer
+    for small ones so the grid still has >= ~4K tasks to spread over 256 CUs
+    (a Cora-sized graph at 256 units per task would run on one or two waves).
+    A power of two in [16, 256]."""
+    units = int(n_rows) + int(n_edges)
+    c = MAX_CHUNK
+    while c > 16 and units // c < 4096:
+        c //= 2
+    return c
 
 
 def default_snap(chunk):
@@ -40,7 +53,7 @@ class CSR:
         self.n_edges = int(E)
         self.n_other = int(n_other)
         self.device = dev
-        self.chunk = int(chunk)
+        self.chunk = auto_chunk(self.n_rows, E) if chunk is None else int(chunk)
         self.snap = default_snap(self.chunk) if snap is None else int(snap)
         self.rowptr = torch.empty(self.n_rows + 1, dtype=torch.int32, device=dev)
         self.col = torch.empty(max(E, 1), dtype=torch.int32, device=dev)
