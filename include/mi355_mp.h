@@ -14,7 +14,9 @@
  *   - Plain pointers to DEVICE memory, int64 sizes, a hipStream_t passed as
  *     `void* stream` (NULL = default stream).  No torch types.
  *   - Every entry point only enqueues work on `stream`; none allocates, frees
- *     or synchronises, so every call is hipGraph-capturable.  The caller owns
+ *     or synchronises, so every call is hipGraph-capturable.  Work runs on
+ *     the stream's device: the calling thread's current device is switched
+ *     for the call when it differs, and restored.  The caller owns
  *     all outputs and workspaces (sizes from the *_bytes queries).
  *   - Return value: MP_OK or an MP_ERR_* code; mp_last_error() gives the text
  *     (thread-local).

@@ -1245,6 +1245,7 @@ size_t mp_aggregate_slab_bytes(const mp_csr* g, int32_t F, int32_t reduce) {
 int mp_aggregate_f32(const mp_csr* g, const float* w, const float* x, int64_t ldx, int32_t F,
                      int32_t reduce, int32_t flags, const float* bias, float* out, int64_t ldo,
                      int64_t* arg_out, void* slab, size_t slab_bytes, int32_t stages, void* stream) {
+  MP_DEVICE_GUARD(stream);
   int rc = check_graph(g, "mp_aggregate_f32");
   if (rc) return rc;
   MP_CHECK_ARG(F > 0, "mp_aggregate_f32: F must be positive");
@@ -1287,6 +1288,7 @@ int mp_aggregate_f32(const mp_csr* g, const float* w, const float* x, int64_t ld
 
 int mp_aggregate_heads_f32(const mp_csr* g, const float* w, int32_t H, const float* x, int64_t ldx, int32_t F,
                            float* out, int64_t ldo, void* slab, size_t slab_bytes, int32_t stages, void* stream) {
+  MP_DEVICE_GUARD(stream);
   int rc = check_graph(g, "mp_aggregate_heads_f32");
   if (rc) return rc;
   MP_CHECK_ARG(F > 0 && H > 0 && F % H == 0, "mp_aggregate_heads_f32: F must be a positive multiple of H");
@@ -1327,6 +1329,7 @@ int mp_gat_aggregate_f32(const mp_csr* g, const float* xw, const float* a_src, c
                          int32_t H, int32_t C, float slope, const float* bias, float* out,
                          int64_t ldo, float* row_stats, void* slab, size_t slab_bytes,
                          int32_t stages, void* stream) {
+  MP_DEVICE_GUARD(stream);
   int rc = check_graph(g, "mp_gat_aggregate_f32");
   if (rc) return rc;
   MP_CHECK_ARG(H > 0 && C > 0, "mp_gat_aggregate_f32: H, C must be positive");
@@ -1367,6 +1370,7 @@ int mp_gat_aggregate_f32(const mp_csr* g, const float* xw, const float* a_src, c
 int mp_gat_backward_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, const float* xw, const float* a_src,
                         const float* pack, const float* att, int32_t H, int32_t C, float slope, float* grad_xw,
                         float* grad_a_src, float* de, void* slab, size_t slab_bytes, int32_t stages, void* stream) {
+  MP_DEVICE_GUARD(stream);
   int rc = check_graph(gt, "mp_gat_backward_f32");
   if (rc) return rc;
   MP_CHECK_ARG(H > 0 && C > 0, "mp_gat_backward_f32: H, C must be positive");

@@ -33,6 +33,26 @@ void set_error(const char* fmt, ...);
 
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Entry points enqueue on the caller's stream, on that stream's device: the
+// calling thread's current device is switched for the call when it differs
+// (a torch stream of cuda:1 while cuda:0 is current) and restored after.
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(void* stream) {
+    if (!stream) return;
+    hipDevice_t d;
+    int cur;
+    if (hipStreamGetDevice(as_stream(stream), &d) != hipSuccess || hipGetDevice(&cur) != hipSuccess) return;
+    if (cur != (int)d && hipSetDevice((int)d) == hipSuccess) prev = cur;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+#define MP_DEVICE_GUARD(stream) DeviceGuard mp_device_guard_(stream)
+
 static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 static inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }

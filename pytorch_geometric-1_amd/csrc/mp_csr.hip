@@ -185,6 +185,7 @@ size_t mp_csr_build_workspace(int64_t n_edges, int64_t n_rows) {
 int mp_csr_build(const int64_t* key, const int64_t* other, int64_t n_edges, int64_t n_rows,
                  int64_t n_other, int32_t* rowptr, int32_t* col, int32_t* eid, int32_t* bad,
                  void* ws, size_t ws_bytes, void* stream) {
+  MP_DEVICE_GUARD(stream);
   MP_CHECK_ARG(n_edges >= 0 && n_rows >= 0, "mp_csr_build: negative size");
   MP_CHECK_ARG(n_edges < (int64_t)INT32_MAX && n_rows < (int64_t)INT32_MAX,
                "mp_csr_build: int32 CSR limits exceeded (E=%lld, N=%lld)", (long long)n_edges,
@@ -232,6 +233,7 @@ size_t mp_schedule_workspace(int32_t n_waves) {
 int mp_schedule_build(const int32_t* rowptr, int64_t n_rows, int64_t n_edges, int32_t chunk,
                       int32_t snap, int32_t* wave_row, int32_t* wave_slot, int32_t* split_waves,
                       int32_t* n_split_dev, void* ws, size_t ws_bytes, void* stream) {
+  MP_DEVICE_GUARD(stream);
   MP_CHECK_ARG(chunk >= 16 && chunk % 8 == 0, "mp_schedule_build: chunk must be a multiple of 8, >= 16");
   MP_CHECK_ARG(snap >= 0 && snap < chunk - 1, "mp_schedule_build: need 0 <= snap < chunk - 1");
   MP_CHECK_ARG(rowptr && wave_row && wave_slot && split_waves && n_split_dev,

@@ -250,6 +250,7 @@ using namespace mp;
 extern "C" {
 
 int mp_csr_slot_rows(const mp_csr* g, int32_t* slot_row, void* stream) {
+  MP_DEVICE_GUARD(stream);
   MP_CHECK_ARG(g && g->rowptr && slot_row, "mp_csr_slot_rows: null pointer");
   if (g->n_edges == 0) return MP_OK;
   k_slot_rows<<<(unsigned)ceil_div(g->n_edges, 256), 256, 0, as_stream(stream)>>>(g->rowptr, g->n_rows,
@@ -261,6 +262,7 @@ int mp_csr_slot_rows(const mp_csr* g, int32_t* slot_row, void* stream) {
 int mp_gat_alpha_csr_f32(const mp_csr* g, const int32_t* slot_row, const float* a_src, const float* a_dst,
                          int32_t H, float slope, const float* row_stats, float* alpha_csr, float* score,
                          void* stream) {
+  MP_DEVICE_GUARD(stream);
   MP_CHECK_ARG(g && H > 0, "mp_gat_alpha_csr_f32: bad argument");
   if (g->n_edges == 0) return MP_OK;
   MP_CHECK_ARG(g->col && slot_row && a_src && a_dst && row_stats && alpha_csr,
@@ -274,6 +276,7 @@ int mp_gat_alpha_csr_f32(const mp_csr* g, const int32_t* slot_row, const float* 
 
 int mp_gat_sddmm_f32(const mp_csr* g, const int32_t* slot_row, const float* grow, int64_t ldg, const float* x,
                      int64_t ldx, int32_t H, int32_t C, float* out, void* stream) {
+  MP_DEVICE_GUARD(stream);
   MP_CHECK_ARG(g && H > 0 && C > 0, "mp_gat_sddmm_f32: bad argument");
   if (g->n_edges == 0) return MP_OK;
   MP_CHECK_ARG(g->col && slot_row && grow && x && out, "mp_gat_sddmm_f32: null pointer");
@@ -306,6 +309,7 @@ int mp_gat_bwd_blocks(int64_t n) {
 int mp_gat_backward_prep_f32(const float* grad_out, int64_t ldg, const float* agg, int64_t lda, const float* a_dst,
                              const float* row_stats, int64_t n, int32_t H, int32_t C, float* pack,
                              float* gsum_part, void* stream) {
+  MP_DEVICE_GUARD(stream);
   MP_CHECK_ARG(H > 0 && C > 0 && n >= 0, "mp_gat_backward_prep_f32: bad sizes");
   if (n == 0) return MP_OK;
   MP_CHECK_ARG(grad_out && agg && a_dst && row_stats && pack, "mp_gat_backward_prep_f32: null pointer");
@@ -330,6 +334,7 @@ int mp_gat_backward_prep_f32(const float* grad_out, int64_t ldg, const float* ag
 
 int mp_gat_backward_finish_f32(float* grad_xw, const float* xw, const float* ga_dst, const float* ga_src,
                                 const float* att, int64_t n, int32_t H, int32_t C, float* att_part, void* stream) {
+  MP_DEVICE_GUARD(stream);
   MP_CHECK_ARG(H > 0 && C > 0 && n >= 0, "mp_gat_backward_finish_f32: bad sizes");
   MP_CHECK_ARG(C % 4 == 0 && H * C <= 256, "mp_gat_backward_finish_f32: needs C %% 4 == 0 and H*C <= 256");
   MP_CHECK_ARG(grad_xw && xw && ga_dst && ga_src && att && att_part, "mp_gat_backward_finish_f32: null pointer");
@@ -343,6 +348,7 @@ int mp_gat_backward_finish_f32(float* grad_xw, const float* xw, const float* ga_
 
 int mp_heads_outer_add_f32(float* y, int64_t ldy, const float* s, int64_t n, int32_t H, int32_t C, const float* att,
                            int64_t att_ld, void* stream) {
+  MP_DEVICE_GUARD(stream);
   MP_CHECK_ARG(H > 0 && C > 0 && n >= 0, "mp_heads_outer_add_f32: bad sizes");
   if (n == 0) return MP_OK;
   MP_CHECK_ARG(y && s && att && ldy >= (int64_t)H * C && att_ld >= C, "mp_heads_outer_add_f32: bad argument");

@@ -152,6 +152,7 @@ extern "C" {
 
 int mp_gather_rows_f32(const float* x, int64_t ldx, const int64_t* idx, int64_t n, int32_t F, float* out,
                        int64_t ldo, void* stream) {
+  MP_DEVICE_GUARD(stream);
   MP_CHECK_ARG(n >= 0 && F >= 0, "mp_gather_rows_f32: negative size");
   if (n == 0 || F == 0) return MP_OK;
   MP_CHECK_ARG(x && idx && out, "mp_gather_rows_f32: null pointer");
@@ -167,6 +168,7 @@ int mp_gather_rows_f32(const float* x, int64_t ldx, const int64_t* idx, int64_t 
 }
 
 int mp_permute_f32(const float* src, const int32_t* perm, int64_t n, float* dst, void* stream) {
+  MP_DEVICE_GUARD(stream);
   if (n == 0) return MP_OK;
   MP_CHECK_ARG(src && perm && dst && n > 0, "mp_permute_f32: bad argument");
   k_permute<<<(unsigned)ceil_div(n, 256), 256, 0, as_stream(stream)>>>(src, perm, n, dst);
@@ -177,6 +179,7 @@ int mp_permute_f32(const float* src, const int32_t* perm, int64_t n, float* dst,
 int mp_scatter_arg_backward_f32(const float* grad_out, const int64_t* arg, int64_t n_rows, int32_t F,
                                 int64_t n_edges, const int64_t* src_map, float* grad, int64_t ldg,
                                 void* stream) {
+  MP_DEVICE_GUARD(stream);
   if (n_rows == 0 || F == 0) return MP_OK;
   MP_CHECK_ARG(grad_out && arg && grad && ldg >= F, "mp_scatter_arg_backward_f32: bad argument");
   int64_t total = n_rows * (int64_t)F;
@@ -188,6 +191,7 @@ int mp_scatter_arg_backward_f32(const float* grad_out, const int64_t* arg, int64
 
 int mp_gcn_norm_f32(const int64_t* row, const int64_t* col, const float* w, int64_t n_edges, int64_t n_nodes,
                     float* deg_ws, float* norm, void* stream) {
+  MP_DEVICE_GUARD(stream);
   MP_CHECK_ARG(n_edges >= 0 && n_nodes >= 0, "mp_gcn_norm_f32: negative size");
   MP_CHECK_ARG(deg_ws && (n_edges == 0 || (row && col && norm)), "mp_gcn_norm_f32: null pointer");
   hipStream_t s = as_stream(stream);
@@ -209,6 +213,7 @@ int mp_gcn_norm_f32(const int64_t* row, const int64_t* col, const float* w, int6
 
 int mp_gat_node_scores_f32(const float* xw, int64_t n_nodes, int32_t H, int32_t C, const float* att,
                            float* a_src, float* a_dst, void* stream) {
+  MP_DEVICE_GUARD(stream);
   MP_CHECK_ARG(H > 0 && C > 0 && n_nodes >= 0, "mp_gat_node_scores_f32: bad sizes");
   if (n_nodes == 0) return MP_OK;
   MP_CHECK_ARG(xw && att && a_src && a_dst, "mp_gat_node_scores_f32: null pointer");
@@ -232,6 +237,7 @@ int mp_gat_node_scores_f32(const float* xw, int64_t n_nodes, int32_t H, int32_t 
 int mp_gat_alpha_f32(const int64_t* src_idx, const int64_t* dst_idx, int64_t n_edges, int32_t H,
                      const float* a_src, const float* a_dst, float slope, const float* row_stats, float* alpha,
                      void* stream) {
+  MP_DEVICE_GUARD(stream);
   if (n_edges == 0) return MP_OK;
   MP_CHECK_ARG(src_idx && dst_idx && a_src && a_dst && row_stats && alpha && H > 0,
                "mp_gat_alpha_f32: bad argument");
