@@ -249,14 +249,18 @@ int mp_gather_rows_f32(const float* x, int64_t ldx, const int64_t* idx,
 int mp_permute_f32(const float* src, const int32_t* perm, int64_t n,
                    float* dst, void* stream);
 
-/* ScatterMax/ScatterMin backward [U8]: for every (r,f) with arg[r,f] != n_edges
- *   src_map == NULL: grad[arg[r,f], f]            = grad_out[r,f]  (plain store)
- *   src_map != NULL: grad[src_map[arg[r,f]], f]  += grad_out[r,f]  (atomic)
- * grad must be zero-initialised by the caller. */
+/* ScatterMax/ScatterMin backward [U8]: for every (r,f) with arg[r,f] = e != n_edges
+ *   src_map == NULL: grad[e, f]            = grad_out[r,f]          (plain store)
+ *   src_map != NULL: grad[src_map[e], f]  += grad_out[r,f] * w[e]   (atomic; w NULL = 1)
+ *   grad_w != NULL:  grad_w[e]            += grad_out[r,f] * x[src_map[e], f]
+ * (the message of a weighted max/min aggregation is w[e] * x[src_map[e]];
+ * grad_w is d w).  grad / grad_w must be zero-initialised by the caller; either
+ * may be NULL. */
 int mp_scatter_arg_backward_f32(const float* grad_out, const int64_t* arg,
                                 int64_t n_rows, int32_t F, int64_t n_edges,
-                                const int64_t* src_map, float* grad,
-                                int64_t ldg, void* stream);
+                                const int64_t* src_map, const float* w, const float* x,
+                                int64_t ldx, float* grad, int64_t ldg, float* grad_w,
+                                void* stream);
 
 /* GCNConv.norm [U5]: deg = scatter_add(w, row); dinv = deg^-1/2 (inf -> 0);
  * norm[e] = dinv[row[e]] * w[e] * dinv[col[e]] (original edge order).

@@ -105,22 +105,28 @@ class _FusedPropagate(torch.autograd.Function):
         if ctx.has_bias and ctx.needs_input_grad[2]:
             gb = grad_out.sum(0)
         if reduce in ("max", "min"):
-            if ctx.needs_input_grad[1] and edge_weight is not None:
-                raise NotImplementedError("mi355_mp: gradient w.r.t. edge weights of a max/min "
-                                          "aggregation is not implemented")
-            if ctx.needs_input_grad[0]:
-                g = grad_out * keep if keep is not None else grad_out
-                gx = torch.zeros((ctx.n_src, x.shape[1]), dtype=torch.float32, device=x.device)
+            want_w = ctx.needs_input_grad[1] and edge_weight is not None
+            if ctx.needs_input_grad[0] or want_w:
+                # message = w_e * x[src_e] at the argmax edge e: d x[src_e] += w_e g,
+                # d w_e += <g, x[src_e]> over the features whose argmax is e
+                g = (grad_out * keep if keep is not None else grad_out).contiguous()
+                dev = x.device
+                if ctx.needs_input_grad[0]:
+                    gx = torch.zeros((ctx.n_src, x.shape[1]), dtype=torch.float32, device=dev)
+                if want_w:
+                    gw = torch.zeros(edge_weight.shape[0], dtype=torch.float32, device=dev)
+                w = edge_weight.to(torch.float32).contiguous() if edge_weight is not None else None
                 other = edge_index[graph.j].contiguous()
                 lib = _lib.load()
-                if edge_weight is not None:  # d(w*x)/dx = w: fold the weight into the scatter
-                    raise NotImplementedError("mi355_mp: weighted max/min backward not implemented")
                 _lib.check(lib.mp_scatter_arg_backward_f32(g.data_ptr(), arg.data_ptr(), g.shape[0],
-                                                           g.shape[1], graph.dst.n_edges,
-                                                           other.data_ptr(), gx.data_ptr(), gx.stride(0),
-                                                           _lib.stream_ptr(x.device)),
+                                                           g.shape[1], graph.dst.n_edges, other.data_ptr(),
+                                                           _lib.ptr(w), x.data_ptr(), x.stride(0), _lib.ptr(gx),
+                                                           gx.stride(0) if gx is not None else 0, _lib.ptr(gw),
+                                                           _lib.stream_ptr(dev)),
                            "mp_scatter_arg_backward_f32")
-            return gx, None, gb, None, None, None, None, None
+                if gw is not None and gw.dtype != edge_weight.dtype:
+                    gw = gw.to(edge_weight.dtype)
+            return gx, gw, gb, None, None, None, None, None
         g = grad_out
         if reduce == "mean":
             deg = graph.dst.degree().clamp(min=1).to(torch.float32)
@@ -184,8 +190,8 @@ class _SegmentReduce(torch.autograd.Function):
             g = grad_out * keep if keep is not None else grad_out
             gs = torch.zeros((ctx.n_src, g.shape[1]), dtype=torch.float32, device=g.device)
             _lib.check(lib.mp_scatter_arg_backward_f32(g.data_ptr(), arg.data_ptr(), g.shape[0], g.shape[1],
-                                                       ctx.n_src, None, gs.data_ptr(), gs.stride(0),
-                                                       _lib.stream_ptr(g.device)),
+                                                       ctx.n_src, None, None, None, 0, gs.data_ptr(), gs.stride(0),
+                                                       None, _lib.stream_ptr(g.device)),
                        "mp_scatter_arg_backward_f32")
             return gs, None, None, None, None
         g = grad_out

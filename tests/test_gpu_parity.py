@@ -1098,3 +1098,30 @@ def test_auto_chunk_small_graph_max_and_gat(F):
     w = torch.rand(E, generator=g)
     o2 = ops.fused_propagate(graph, xs.to(DEV), ei.to(DEV), w.to(DEV), "sum").cpu()
     _bound_ok(o2, S.gather_sum(xs, ei[0], ei[1], w, N), S.gather_sum(xs.abs(), ei[0], ei[1], w, N))
+
+
+@pytest.mark.parametrize("reduce", ["max", "min"])
+def test_weighted_max_min_backward(reduce):
+    """message = w_e * x_j with aggr max/min (GraphConv-style): d x and d w vs
+    float64 autograd of the same argmax selection (continuous data: no ties)."""
+    _, ops, _, Graph, pl = _mods()
+    N, E, F = 400, 6000, 40
+    ei = pl(N, E, seed=81)
+    g = torch.Generator().manual_seed(81)
+    x = torch.randn(N, F, generator=g)
+    w = torch.rand(E, generator=g) + 0.1
+    gout = torch.randn(N, F, generator=g)
+    graph = Graph(ei.to(DEV), N, N)
+    xd = x.to(DEV).requires_grad_(True)
+    wd = w.to(DEV).requires_grad_(True)
+    out = ops.fused_propagate(graph, xd, ei.to(DEV), wd, reduce)
+    out.backward(gout.to(DEV))
+    x64 = x.double().requires_grad_(True)
+    w64 = w.double().requires_grad_(True)
+    msg = w64.view(-1, 1) * x64[ei[0]]
+    ref = torch.zeros(N, F, dtype=torch.float64).scatter_reduce(
+        0, ei[1].view(-1, 1).expand(-1, F), msg, "amax" if reduce == "max" else "amin", include_self=False)
+    assert torch.allclose(out.detach().cpu().double(), ref, rtol=1e-6, atol=1e-6)
+    ref.backward(gout.double())
+    assert torch.allclose(xd.grad.cpu().double(), x64.grad, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(wd.grad.cpu().double(), w64.grad, rtol=1e-4, atol=1e-4)
