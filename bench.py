@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--cpu-sample-edges", type=int, default=48_000_000)
     ap.add_argument("--chunk", type=int, default=256)
     ap.add_argument("--no-overlap", action="store_true", help="N>1: exchange, then aggregate (no overlap)")
+    ap.add_argument("--halo-tile", type=int, default=128,
+                    help="N>1: exchange and finish the boundary edges per feature tile of this width "
+                         "(pipelined); 0 = one exchange of whole rows")
     return ap.parse_args()
 
 
@@ -142,6 +145,13 @@ def main():
         x_local = plan.local_buffer(F_DIM)
         x_local[:plan.n_own].copy_(x_full[plan.lo:plan.hi])
         x = x_local[:plan.n_own]
+        x_tiles = None
+        if args.halo_tile > 0 and not args.no_overlap:
+            x_tiles = plan.local_tiles(F_DIM, args.halo_tile)
+            c0 = 0
+            for xt in x_tiles:
+                xt[:plan.n_own].copy_(x_full[plan.lo:plan.hi, c0:c0 + xt.shape[1]])
+                c0 += xt.shape[1]
         del x_full
         lei = plan.local_edge_index
         graph = Graph(lei, plan.n_own, plan.n_local_src, chunk=args.chunk)
@@ -170,6 +180,8 @@ def main():
             aggregate(x, out=out_buf)
         elif args.no_overlap:
             aggregate(plan.exchange_into(x_local, ops.gather_rows), out=out_buf)
+        elif x_tiles is not None:
+            overlap.step_tiled(x_tiles, out_buf, bias)
         else:
             overlap.step(x_local, out_buf, bias)
 
@@ -277,6 +289,7 @@ def main():
                       "halo_rows_rank0": (plan.n_local_src - plan.n_own) if world > 1 else 0,
                       "interior_edges_rank0": overlap.n_interior if world > 1 else E_local,
                       "overlap": world > 1 and not args.no_overlap,
+                      "halo_tile": args.halo_tile if world > 1 and not args.no_overlap else None,
                       "n_wave_tasks": csr.n_waves,
                       "agg_only_GBps_incl_fixup": alg_bytes / ((main_avg + fix_avg) * 1e-3) / 1e9},
         }

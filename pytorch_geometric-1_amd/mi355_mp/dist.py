@@ -112,6 +112,14 @@ class ShardPlan:
         _a2a(x_local[self.n_own:], send.contiguous(), self.recv_counts, self.send_counts, group)
         return x_local
 
+    def local_tiles(self, F, tile=128, dtype=torch.float32, device=None):
+        """Tile-major [n_own + n_halo, tile] buffers covering F features, for
+        OverlappedAggregation.step_tiled: each tile's halo rows are contiguous,
+        so every tile is exchanged (and received in place) on its own."""
+        dev = device or self.halo_nodes.device
+        widths = [min(tile, F - c0) for c0 in range(0, F, tile)]
+        return [torch.empty((self.n_local_src, w), dtype=dtype, device=dev) for w in widths]
+
     def halo_exchange(self, x_own, gather_rows, group=None):
         """[own rows ; halo rows] for this rank (allocating form)."""
         x_local = self.local_buffer(x_own.shape[1], x_own.dtype, x_own.device)
@@ -180,4 +188,47 @@ class OverlappedAggregation:
             work.wait()
         ops._aggregate(self.g_bnd.dst, "other", x_local, self.w_bnd, "sum", _lib.MP_FLAG_INIT_FROM_OUT, bias,
                        out=out)
+        return out
+
+    def step_tiled(self, x_tiles, out, bias=None, group=None):
+        """step() pipelined over feature tiles (x_tiles from plan.local_tiles):
+          1. pack every tile's requested rows and start its all_to_all (RCCL
+             runs them back to back on its stream while the compute stream
+             packs the next tile),
+          2. aggregate the interior edges of every tile,
+          3. per tile, wait for ITS halo only, then aggregate its boundary
+             edges on top (MP_FLAG_INIT_FROM_OUT) plus that tile's bias.
+        Tile t's boundary pass overlaps tile t+1's exchange.  Per row and
+        feature the arithmetic is that of step(): bitwise the same output."""
+        from . import _lib, ops
+        plan = self.plan
+        gloo = out.is_cuda and dist.get_backend(group) == "gloo"
+        offs = [0]
+        for xt in x_tiles:
+            offs.append(offs[-1] + xt.shape[1])
+        if offs[-1] != out.shape[1]:
+            raise ValueError("step_tiled: tiles cover %d features, out has %d" % (offs[-1], out.shape[1]))
+        pending = []
+        for xt in x_tiles:
+            own = xt[:plan.n_own]
+            send = (ops.gather_rows(own, plan.send_idx) if plan.send_idx.numel()
+                    else xt.new_empty((0, xt.shape[1])))
+            halo = xt[plan.n_own:]
+            if gloo:
+                _a2a(halo, send, plan.recv_counts, plan.send_counts, group)
+                pending.append((None, send))
+            else:
+                work = dist.all_to_all_single(halo, send, output_split_sizes=plan.recv_counts,
+                                              input_split_sizes=plan.send_counts, group=group, async_op=True)
+                pending.append((work, send))
+        for t, xt in enumerate(x_tiles):
+            ops._aggregate(self.g_int.dst, "other", xt[:plan.n_own], self.w_int, "sum", 0, None,
+                           out=out[:, offs[t]:offs[t + 1]])
+        for t, xt in enumerate(x_tiles):
+            work, _send = pending[t]
+            if work is not None:
+                work.wait()
+            b = bias[offs[t]:offs[t + 1]] if bias is not None else None
+            ops._aggregate(self.g_bnd.dst, "other", xt, self.w_bnd, "sum", _lib.MP_FLAG_INIT_FROM_OUT, b,
+                           out=out[:, offs[t]:offs[t + 1]])
         return out

@@ -55,6 +55,13 @@ def _worker(rank, world, port, q):
         gl = Graph(plan.local_edge_index, plan.n_own, plan.n_local_src, chunk=64)
         xl2 = plan.exchange_into(xl, ops.gather_rows)
         out2 = ops._aggregate(gl.dst, "other", xl2, gl.dst.to_csr_order(norm[plan.edge_pos]), "sum", 0, bias)[0]
+        # feature-tile pipeline: bitwise the same as step()
+        tiles = plan.local_tiles(F, 128)
+        for t, xt in enumerate(tiles):
+            xt[:plan.n_own].copy_(x[plan.lo:plan.hi, 128 * t:128 * t + xt.shape[1]])
+        out3 = torch.empty(plan.n_own, F, device=dev)
+        ov.step_tiled(tiles, out3, bias)
+        assert torch.equal(out3, out), "step_tiled must equal step"
         q.put((rank, err, bool(torch.equal(out2, want)), ov.n_interior, ov.n_boundary))
     finally:
         dist.destroy_process_group()
