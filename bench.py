@@ -175,9 +175,21 @@ def main():
 
     out_buf = torch.empty((n_rows, F_DIM), device=dev)
 
-    def step():
+    # dominant-kernel timing inside the timed region (N=1): HIP events on the
+    # stream the kernels run on (torch's current stream), around the main
+    # launch and the fix-up launch of every timed step
+    ev = None
+
+    def step(i=None):
         if world == 1:
-            aggregate(x, out=out_buf)
+            if i is None or ev is None:
+                aggregate(x, out=out_buf)
+            else:
+                ev[i][0].record()
+                aggregate(x, stages=_lib.MP_STAGE_MAIN, out=out_buf)
+                ev[i][1].record()
+                aggregate(x, stages=_lib.MP_STAGE_FIXUP, out=out_buf)
+                ev[i][2].record()
         elif args.no_overlap:
             aggregate(plan.exchange_into(x_local, ops.gather_rows), out=out_buf)
         elif x_tiles is not None:
@@ -187,12 +199,14 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    if world == 1:
+        ev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.steps)]
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for i in range(args.steps):
+        step(i)
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
@@ -223,8 +237,16 @@ def main():
             per.append(a.elapsed_time(b) / reps)
         return sorted(per)
 
-    main_ms = timed(_lib.MP_STAGE_MAIN)
-    fix_ms = timed(_lib.MP_STAGE_FIXUP)
+    if world == 1:
+        main_ms = sorted(a.elapsed_time(b) for a, b, _ in ev)
+        fix_ms = sorted(b.elapsed_time(c) for _, b, c in ev)
+        timing_src = "HIP events around each main / fix-up launch inside the timed steps"
+    else:
+        # N>1: a step is several launches (per tile, interior + boundary); the
+        # per-rank kernel rate is timed on the rank's full local graph instead
+        main_ms = timed(_lib.MP_STAGE_MAIN)
+        fix_ms = timed(_lib.MP_STAGE_FIXUP)
+        timing_src = "HIP events over back-to-back launches on the rank's local graph (after the timed region)"
     main_avg = sum(main_ms) / len(main_ms)
     fix_avg = sum(fix_ms) / len(fix_ms)
     alg_bytes = E_local * BYTES_PER_EDGE + n_rows * BYTES_PER_NODE
@@ -281,7 +303,7 @@ def main():
                          "kernel": "k_agg_flat<SumRed<2,true,false>,VEC=2,U=16,L=64>",
                          "algorithmic_bytes_per_launch": alg_bytes,
                          "avg_launch_ms": main_avg, "median_launch_ms": main_ms[len(main_ms) // 2],
-                         "fixup_avg_ms": fix_avg},
+                         "fixup_avg_ms": fix_avg, "timing": timing_src},
             "cpu_baseline": cpu,
             "extra": {"gemm_xW_ms": gemm_ms, "layer_ms_est": gemm_ms + main_avg + fix_avg,
                       "one_time_build_s": t_build, "graph_gen_s": t_gen,
