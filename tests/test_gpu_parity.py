@@ -1125,3 +1125,76 @@ def test_weighted_max_min_backward(reduce):
     ref.backward(gout.double())
     assert torch.allclose(xd.grad.cpu().double(), x64.grad, rtol=1e-5, atol=1e-5)
     assert torch.allclose(wd.grad.cpu().double(), w64.grad, rtol=1e-4, atol=1e-4)
+
+
+def test_full_size_reddit_max_argmax():
+    """Config 4 at full size (N=232,965, E=114,615,892, F=256): determinism;
+    every argmax is an in-edge of its row whose source value equals the output
+    exactly; values bit-equal to torch's own scatter_reduce('amax') computed in
+    edge chunks (max is order-independent)."""
+    _, ops, _, Graph, _ = _mods()
+    from mi355_mp.graphgen import powerlaw_edge_index
+    N, E, F = 232_965, 114_615_892, 256
+    ei = powerlaw_edge_index(N, E, seed=3, device=DEV)
+    x = torch.randn(N, F, device=DEV, generator=torch.Generator(device=DEV).manual_seed(3))
+    graph = Graph(ei, N, N)
+    out, arg = ops._aggregate(graph.dst, "other", x, None, "max", 0, None)
+    out2, arg2 = ops._aggregate(graph.dst, "other", x, None, "max", 0, None)
+    assert torch.equal(out, out2) and torch.equal(arg, arg2)
+    deg = torch.bincount(ei[1], minlength=N)
+    has = deg > 0
+    a = arg[has]
+    assert bool(((a >= 0) & (a < E)).all())
+    rows = torch.nonzero(has).view(-1)
+    assert bool((ei[1][a] == rows.view(-1, 1)).all())
+    assert torch.equal(torch.gather(x, 0, ei[0][a]), out[has])
+    assert bool((arg[~has] == E).all()) and bool((out[~has] == 0).all())
+    ref = torch.full((N, F), float("-inf"), device=DEV)
+    step = 8_000_000
+    for s in range(0, E, step):
+        src, dst = ei[0, s:s + step], ei[1, s:s + step]
+        ref.scatter_reduce_(0, dst.view(-1, 1).expand(-1, F), x[src], "amax")
+    ref[~has] = 0
+    assert torch.equal(out, ref)
+
+
+def test_full_size_gat_config3():
+    """Config 3 at full size (RMAT21 + self loops, 8 heads x 32): alpha sums to
+    1 per (row, head); alpha and the output vs the reference formula evaluated
+    with plain torch ops in edge chunks (within 1e-5 * sum|terms|)."""
+    _, ops, _, Graph, _ = _mods()
+    from mi355_mp.graphgen import rmat_edge_index
+    from torch_geometric.nn.conv._structure import gat_loops
+    N, H, C = 1 << 21, 8, 32
+    ei = gat_loops(rmat_edge_index(scale=21, n_samples=30_000_000, seed=1, device=DEV), N)
+    E = ei.shape[1]
+    g = torch.Generator(device=DEV).manual_seed(2)
+    xw = torch.randn(N, H * C, device=DEV, generator=g) * 0.5
+    att = torch.randn(1, H, 2 * C, device=DEV, generator=g) * 0.2
+    graph = Graph(ei, N, N)
+    out, alpha = ops.gat_propagate(graph, ei, xw, att, H, C, 0.2, None, return_alpha=True)
+    src, dst = ei[0], ei[1]
+    ssum = torch.zeros(N, H, device=DEV, dtype=torch.float64).index_add_(0, dst, alpha.double())
+    assert torch.allclose(ssum, torch.ones_like(ssum), atol=1e-5)   # hub rows: ~1e5 terms, summed in fp64
+    # reference formula with torch ops (a_i from x_i = xw[dst], a_j from x_j = xw[src])
+    x3 = xw.view(N, H, C)
+    a_dst = (x3 * att[:, :, :C]).sum(-1)
+    a_src = (x3 * att[:, :, C:]).sum(-1)
+    sc = torch.nn.functional.leaky_relu(a_dst[dst] + a_src[src], 0.2)
+    m = torch.full((N, H), float("-inf"), device=DEV).scatter_reduce_(0, dst.view(-1, 1).expand(-1, H), sc, "amax")
+    p = torch.exp(sc - m[dst])
+    den = torch.zeros(N, H, device=DEV).index_add_(0, dst, p)
+    alpha_ref = p / (den[dst] + 1e-16)
+    assert torch.allclose(alpha, alpha_ref, rtol=1e-4, atol=1e-6)
+    del sc, p
+    ref = torch.zeros(N, H, C, device=DEV, dtype=torch.float64)
+    terms = torch.zeros(N, H, C, device=DEV, dtype=torch.float64)
+    step = 4_000_000
+    for s in range(0, E, step):
+        sl = slice(s, s + step)
+        msg = alpha_ref[sl].unsqueeze(-1).double() * x3[src[sl]].double()
+        ref.index_add_(0, dst[sl], msg)
+        terms.index_add_(0, dst[sl], msg.abs())
+    got = out.view(N, H, C).double()
+    tol = 1e-5 * terms.clamp(min=1.0) + 1e-5
+    assert bool(((got - ref).abs() <= tol).all()), float(((got - ref).abs() - tol).max())
