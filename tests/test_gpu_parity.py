@@ -474,6 +474,38 @@ def test_full_size_rmat_gcn_properties():
     o2 = ops.fused_propagate(graph, x2, ei2, norm, "sum")
     o12 = ops.fused_propagate(graph, 2 * x1 - x2, ei2, norm, "sum")
     assert (o12 - (2 * o1 - o2)).abs().max().item() < 1e-4
+    _full_size_bound(o1, x1, ei2, norm)
+
+
+def _full_size_bound(out, x, ei, w, step=4_000_000):
+    """|out - ref| <= 1e-5 * max(1, sum|w x_j|) against a float64 index_add of
+    w * x_j in edge chunks (the whole [E, F] message tensor would not fit)."""
+    N, F = out.shape
+    ref = torch.zeros(N, F, device=DEV, dtype=torch.float64)
+    terms = torch.zeros(N, F, device=DEV, dtype=torch.float64)
+    for s in range(0, ei.shape[1], step):
+        msg = w[s:s + step].double().view(-1, 1) * x[ei[0, s:s + step]].double()
+        ref.index_add_(0, ei[1, s:s + step], msg)
+        terms.index_add_(0, ei[1, s:s + step], msg.abs())
+    tol = 1e-5 * terms.clamp(min=1.0)
+    excess = ((out.double() - ref).abs() - tol).max().item()
+    assert excess <= 0, excess
+
+
+def test_full_size_products_gcn():
+    """Config 5 at full size (ogbn-products scale, N=2,449,029, E'=126M, F=256)
+    on one GPU: within the bound of a float64 reference; deterministic."""
+    _, ops, _, Graph, _ = _mods()
+    from mi355_mp.graphgen import powerlaw_edge_index
+    from torch_geometric.nn.conv.gcn_conv import GCNConv
+    N, E, F = 2_449_029, 123_718_280, 256
+    ei = powerlaw_edge_index(N, E, seed=4, device=DEV)
+    ei2, norm = GCNConv.norm(ei, N)
+    graph = Graph(ei2, N, N)
+    x = torch.randn(N, F, device=DEV, generator=torch.Generator(device=DEV).manual_seed(4))
+    out = ops.fused_propagate(graph, x, ei2, norm, "sum")
+    assert torch.equal(out, ops.fused_propagate(graph, x, ei2, norm, "sum"))
+    _full_size_bound(out, x, ei2, norm)
 
 
 # --------------------------------------------------------------------------
