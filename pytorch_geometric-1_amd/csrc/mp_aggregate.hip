@@ -37,19 +37,22 @@
 #define MP_U_NARROW 12     // x-row loads in flight per task (VEC=4, tasks of < 64 lanes)
 #endif
 #ifndef MP_NT_OUT
-#define MP_NT_OUT 0        // non-temporal output-row stores
+#define MP_NT_OUT 1        // non-temporal output-row stores (A/B: -0.4%)
 #endif
 #ifndef MP_NT_IDX
-#define MP_NT_IDX 0        // non-temporal col/weight/eid stream loads
+#define MP_NT_IDX 1        // non-temporal col/weight/eid stream loads (A/B: -0.3%)
 #endif
 #ifndef MP_NT_X
-#define MP_NT_X 0          // non-temporal x-row loads (all rows)
+#define MP_NT_X 0          // non-temporal x-row loads (A/B: +75%: they bypass L1)
 #endif
 #ifndef MP_XCD_TILES
-#define MP_XCD_TILES 0     // 1: feature tile = (blockIdx % 8) % tiles (XCD-affine tiles, needs 8 % tiles == 0)
+#define MP_XCD_TILES 1     // feature tile = (block % 8) % tiles when tiles divide 8: each XCD's L2 holds one tile (A/B: -1.5%)
 #endif
 #ifndef MP_BUF_X
 #define MP_BUF_X 0         // x rows through one buffer resource (32-bit offsets) when x < 4 GB
+#endif
+#ifndef MP_GAT_NO_ASRC
+#define MP_GAT_NO_ASRC 0   // timing experiment only: skip the per-slot a_src gather (wrong results)
 #endif
 #ifndef MP_GAT_FAST_EXP
 #define MP_GAT_FAST_EXP 0  // 1: softmax exponentials via __expf (v_exp_f32)
@@ -665,7 +668,7 @@ __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p, SlotWin<Re
         const float* src = reinterpret_cast<const float*>(xb + (int64_t)c * ldxb + foff);
         v[u] = MP_NT_X ? load_frag_nt<VEC>(src) : load_frag<VEC>(src);
       }
-      if constexpr (Red::kGat) as[u] = p.a_src[(int64_t)c * p.H + red.h];
+      if constexpr (Red::kGat) as[u] = MP_GAT_NO_ASRC ? 0.f : p.a_src[(int64_t)c * p.H + red.h];
       if constexpr (Red::kGatB) pk[u] = p.pack[(int64_t)c * p.H + red.h];
     }
     if constexpr (Red::kGatB) {
@@ -701,10 +704,12 @@ __global__ __launch_bounds__(kBlock) void k_agg_main(AggArgs p) {
     // speed only): give every XCD one feature tile so its L2 holds only that
     // tile of the hot rows.  tiles = gridDim.y divides 8 (checked on the host).
     const int T = (int)gridDim.y;
-    const int b = (int)(blockIdx.y * gridDim.x + blockIdx.x);
-    const int xcd = b & 7;
-    tile = xcd % T;
-    bx = (b >> 3) * (8 / T) + xcd / T;
+    if (8 % T == 0) {  // the host pads the grid to a multiple of 8/T blocks per tile
+      const int b = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+      const int xcd = b & 7;
+      tile = xcd % T;
+      bx = (b >> 3) * (8 / T) + xcd / T;
+    }
   }
   const int wave = bx * kWavesPerBlock + (int)(threadIdx.x >> 6);
   const int w = GR::un(wave * GR::G + lane / L);  // this group's task
@@ -848,7 +853,16 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
   using GR = Grp<L>;
   const int lane = lane_id();
   const int gl = lane & (L - 1);
-  const int bx = (int)blockIdx.x, tile = (int)blockIdx.y;
+  int bx = (int)blockIdx.x, tile = (int)blockIdx.y;
+  if constexpr (MP_XCD_TILES) {  // see k_agg_main: one feature tile per XCD
+    const int T = (int)gridDim.y;
+    if (8 % T == 0) {  // the host pads the grid to a multiple of 8/T blocks per tile
+      const int b = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+      const int xcd = b & 7;
+      tile = xcd % T;
+      bx = (b >> 3) * (8 / T) + xcd / T;
+    }
+  }
   const int wave = bx * kWavesPerBlock + (int)(threadIdx.x >> 6);
   const int w = GR::un(wave * GR::G + lane / L);
   if (w >= p.n_waves) return;
@@ -926,7 +940,8 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
       if constexpr (BUF) {
         v[u] = load_frag_buf<VEC>(xr, (uint32_t)c * (uint32_t)ldxb + foff);
       } else {
-        v[u] = load_frag<VEC>(reinterpret_cast<const float*>(xb + (int64_t)c * ldxb + foff));
+        const float* src = reinterpret_cast<const float*>(xb + (int64_t)c * ldxb + foff);
+        v[u] = MP_NT_X ? load_frag_nt<VEC>(src) : load_frag<VEC>(src);
       }
     }
 #pragma unroll

@@ -90,7 +90,10 @@ def load(path=None):
             "mi355_mp: native library %s not found; build it with "
             "`python -c 'import __graft_entry__ as g; g.build()'` "
             "(there is no CPU fallback)" % p)
-    lib = ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+    # RTLD_LOCAL: every build keeps its own kernels.  With RTLD_GLOBAL a second build
+    # loaded into the process (an A/B variant) binds its template kernel stubs to the
+    # first build's same-named definitions and silently runs the first build's code.
+    lib = ctypes.CDLL(p, mode=ctypes.RTLD_LOCAL)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res
