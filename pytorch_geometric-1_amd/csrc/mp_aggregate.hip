@@ -595,11 +595,19 @@ struct Grp {
 // Per-group slot window: col / weight / eid of L consecutive CSR slots held one
 // per lane, the next L prefetched.
 // ---------------------------------------------------------------------------
-template <bool W, bool EID, int L>
+template <bool W, bool EID, int L, bool GW = false>
 struct SlotWin {
   int64_t base, limit;
   int col, col_n, eid, eid_n;
   float w, w_n;
+  // GAT (GW, 64-lane tasks, H a power of two <= 8): a_src rows of the current
+  // window staged in the wave's LDS (one load per lane per window instead of
+  // one gather per slot); the column window runs two windows ahead so the
+  // next window's a_src loads are issued a window before they are needed.
+  int col_nn;
+  float asn[8];
+  float* lds;
+  bool gw;
 
   __device__ __forceinline__ void fetch(const AggArgs& p, int64_t b, int gl, int& c, float& wt, int& e) {
     int64_t k = b + gl;
@@ -608,11 +616,49 @@ struct SlotWin {
     if (W) wt = ok ? ld_stream(p.w + k) : 0.f;
     if (EID) e = ok ? ld_stream(p.eid + k) : 0;
   }
-  __device__ __forceinline__ void init(const AggArgs& p, int64_t b, int64_t lim, int gl) {
+  __device__ __forceinline__ void load_as(const AggArgs& p, int c) {
+    const float* r = p.a_src + (int64_t)c * p.H;
+    if (p.H == 8) {
+      f32x4 a = *reinterpret_cast<const f32x4*>(r);
+      f32x4 b = *reinterpret_cast<const f32x4*>(r + 4);
+      asn[0] = a.x; asn[1] = a.y; asn[2] = a.z; asn[3] = a.w;
+      asn[4] = b.x; asn[5] = b.y; asn[6] = b.z; asn[7] = b.w;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) asn[k] = k < p.H ? r[k] : 0.f;
+    }
+  }
+  __device__ __forceinline__ void store_as(const AggArgs& p, int gl) {
+    __builtin_amdgcn_wave_barrier();  // earlier reads of the previous window come first
+    if (p.H == 8) {
+      f32x4 a = {asn[0], asn[1], asn[2], asn[3]};
+      f32x4 b = {asn[4], asn[5], asn[6], asn[7]};
+      *reinterpret_cast<f32x4*>(lds + gl * 8) = a;
+      *reinterpret_cast<f32x4*>(lds + gl * 8 + 4) = b;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (k < p.H) lds[gl * p.H + k] = asn[k];
+    }
+    __builtin_amdgcn_wave_barrier();  // LDS ops of one wave run in order: later reads see the stores
+  }
+  __device__ __forceinline__ void init(const AggArgs& p, int64_t b, int64_t lim, int gl, float* wave_lds = nullptr) {
     base = b;
     limit = lim;
     fetch(p, base, gl, col, w, eid);
     fetch(p, base + L, gl, col_n, w_n, eid_n);
+    if constexpr (GW) {
+      lds = wave_lds;
+      gw = p.H <= 8 && (p.H & (p.H - 1)) == 0;
+      if (gw) {
+        float dw;
+        int de;
+        fetch(p, base + 2 * L, gl, col_nn, dw, de);
+        load_as(p, col);
+        store_as(p, gl);
+        load_as(p, col_n);
+      }
+    }
   }
   __device__ __forceinline__ void ensure(const AggArgs& p, int64_t e, int gl) {
     if (e >= base + L) {  // slots are consumed in order, never skipping a window
@@ -620,8 +666,25 @@ struct SlotWin {
       col = col_n;
       w = w_n;
       eid = eid_n;
+      if constexpr (GW) {
+        if (gw) {
+          col_n = col_nn;
+          float dw;
+          int de;
+          fetch(p, base + 2 * L, gl, col_nn, dw, de);
+          store_as(p, gl);      // asn holds the a_src rows of the new current window
+          load_as(p, col_n);
+          return;
+        }
+      }
       fetch(p, base + L, gl, col_n, w_n, eid_n);
     }
+  }
+  __device__ __forceinline__ float a_src_of(const AggArgs& p, int slot_in_win, int c, int h) const {
+    if constexpr (GW) {
+      if (gw) return lds[slot_in_win * p.H + h];
+    }
+    return p.a_src[(int64_t)c * p.H + h];
   }
 };
 
@@ -631,8 +694,15 @@ struct SlotWin {
 // under an exec mask; only the group-uniform consume loop is bounded by n.
 // For L = 64 the row address is a uniform base (SGPR pair) + one shared
 // 32-bit lane offset, so U rows cost U*VEC data VGPRs only.
+#ifndef MP_GAT_LDS_WIN
+#define MP_GAT_LDS_WIN 1   // GAT forward: a_src of each 64-slot window staged in LDS (see SlotWin)
+#endif
+template <class Red, int L>
+constexpr bool kGatWin = MP_GAT_LDS_WIN && Red::kGat && L == 64;
+
 template <class Red, int VEC, int U, int L, bool BUF>
-__device__ __forceinline__ void run_slots(Red& red, const AggArgs& p, SlotWin<Red::kW, Red::kEid, L>& win,
+__device__ __forceinline__ void run_slots(Red& red, const AggArgs& p,
+                                          SlotWin<Red::kW, Red::kEid, L, kGatWin<Red, L>>& win,
                                           int64_t s, int64_t t, uint32_t foff, int gl) {
   using GR = Grp<L>;
   const char* xb = reinterpret_cast<const char*>(p.x);
@@ -668,7 +738,7 @@ __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p, SlotWin<Re
         const float* src = reinterpret_cast<const float*>(xb + (int64_t)c * ldxb + foff);
         v[u] = MP_NT_X ? load_frag_nt<VEC>(src) : load_frag<VEC>(src);
       }
-      if constexpr (Red::kGat) as[u] = MP_GAT_NO_ASRC ? 0.f : p.a_src[(int64_t)c * p.H + red.h];
+      if constexpr (Red::kGat) as[u] = MP_GAT_NO_ASRC ? 0.f : win.a_src_of(p, off + uu, c, red.h);
       if constexpr (Red::kGatB) pk[u] = p.pack[(int64_t)c * p.H + red.h];
     }
     if constexpr (Red::kGatB) {
@@ -724,8 +794,13 @@ __global__ __launch_bounds__(kBlock) void k_agg_main(AggArgs p) {
   const int64_t e_end = GR::un(p.wave_slot[w + 1]);
 
   Red red(p, f, act);
-  SlotWin<Red::kW, Red::kEid, L> win;
-  win.init(p, e_begin, e_end, gl);
+  SlotWin<Red::kW, Red::kEid, L, kGatWin<Red, L>> win;
+  [[maybe_unused]] float* wave_lds = nullptr;
+  if constexpr (kGatWin<Red, L>) {
+    __shared__ float gat_as[kWavesPerBlock][64 * 8];
+    wave_lds = gat_as[threadIdx.x >> 6];
+  }
+  win.init(p, e_begin, e_end, gl, wave_lds);
 
   // rowptr window: rp = rowptr[rbase + gl]
   int rbase = r_first;
