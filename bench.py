@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-edges", type=int, default=48_000_000)
-    ap.add_argument("--chunk", type=int, default=256)
+    ap.add_argument("--chunk", type=int, default=0, help="merge-path task size (0: auto_chunk)")
     ap.add_argument("--no-overlap", action="store_true", help="N>1: exchange, then aggregate (no overlap)")
     ap.add_argument("--halo-tile", type=int, default=128,
                     help="N>1: exchange and finish the boundary edges per feature tile of this width "
@@ -132,7 +132,7 @@ def main():
     bias = torch.randn(F_DIM, device=dev, generator=torch.Generator(device=dev).manual_seed(7)) * 0.1
     g = torch.Generator(device=dev).manual_seed(1)
     if world == 1:
-        graph = Graph(ei2, N, N, chunk=args.chunk)
+        graph = Graph(ei2, N, N, chunk=args.chunk or None)
         csr = graph.dst
         w_csr = csr.to_csr_order(norm)
         x = torch.randn(N, F_DIM, device=dev, generator=g)
@@ -154,10 +154,10 @@ def main():
                 c0 += xt.shape[1]
         del x_full
         lei = plan.local_edge_index
-        graph = Graph(lei, plan.n_own, plan.n_local_src, chunk=args.chunk)
+        graph = Graph(lei, plan.n_own, plan.n_local_src, chunk=args.chunk or None)
         csr = graph.dst
         w_csr = csr.to_csr_order(norm[plan.edge_pos])
-        overlap = mdist.OverlappedAggregation(plan, norm, chunk=args.chunk)
+        overlap = mdist.OverlappedAggregation(plan, norm, chunk=args.chunk or None)
         n_rows = plan.n_own
         E_local = lei.shape[1]
     torch.cuda.synchronize()
@@ -297,7 +297,7 @@ def main():
                        "30M samples symmetrised + add_remaining_self_loops", "num_nodes": N,
                        "num_edges": E2, "features": F_DIM, "seed": 1,
                        "parallelism": "dst-range shards x%d, RCCL halo all_to_all" % world if world > 1
-                       else "single GPU", "chunk": args.chunk},
+                       else "single GPU", "chunk": csr.chunk},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_agg_flat<SumRed<2,true,false>,VEC=2,U=16,L=64>",

@@ -33,6 +33,9 @@
 #ifndef MP_U_VEC4
 #define MP_U_VEC4 8        // x-row loads in flight per task (VEC=4, 64-lane tasks)
 #endif
+#ifndef MP_U_VEC2
+#define MP_U_VEC2 16       // x-row loads in flight per task (VEC=2: the flat wide-row kernel)
+#endif
 #ifndef MP_U_NARROW
 #define MP_U_NARROW 12     // x-row loads in flight per task (VEC=4, tasks of < 64 lanes)
 #endif
@@ -1171,7 +1174,7 @@ struct Rebind<ArgRed<VEC, W, M>, V> {
 
 template <class Red, int VEC, int L>
 static int launch_l(const AggArgs& a, int stages, hipStream_t s) {
-  constexpr int U = VEC == 4 ? (L == 64 ? MP_U_VEC4 : MP_U_NARROW) : 16;
+  constexpr int U = VEC == 4 ? (L == 64 ? MP_U_VEC4 : MP_U_NARROW) : (VEC == 2 ? MP_U_VEC2 : 16);
   const int ftiles = (int)ceil_div(a.F, L * VEC);
   if (stages & MP_STAGE_MAIN) {
     int64_t nb = ceil_div(a.n_waves, kWavesPerBlock * (64 / L));

@@ -16,18 +16,22 @@ import torch
 from . import _lib
 
 DEFAULT_CHUNK = None   # auto: see auto_chunk()
-MAX_CHUNK = 256
+MIN_CHUNK, MAX_CHUNK = 16, 1024
+TARGET_TASKS = 100_000
 
 
 def auto_chunk(n_rows, n_edges):
-    """Merge-path task size: 256 work units (rows + slots) for large graphs, fewer
-    for small ones so the grid still has >= ~4K tasks to spread over 256 CUs
-    (a Cora-sized graph at 256 units per task would run on one or two waves).
-    A power of two in [16, 256]."""
+    """Merge-path task size in work units (rows + slots): the largest power of
+    two <= units / 100K, clamped to [16, 1024].  Large graphs get big tasks:
+    fewer hub rows cross a task boundary, so the fix-up shrinks and more rows
+    are summed in one task (bit-identical to the sequential order); RMAT21
+    (64M units) gets 512, the Reddit-scale graph (115M units, degree ~490)
+    1024 (step -1.2% / -3..4% vs 256, tools/ab_bench.py).  Small graphs keep
+    enough tasks to spread over 256 CUs (Cora, 13K units: 16 -> 829 tasks)."""
     units = int(n_rows) + int(n_edges)
-    c = MAX_CHUNK
-    while c > 16 and units // c < 4096:
-        c //= 2
+    c = MIN_CHUNK
+    while c * 2 <= MAX_CHUNK and units // (c * 2) >= TARGET_TASKS:
+        c *= 2
     return c
 
 

@@ -73,18 +73,22 @@ def main():
         same = {n: bool(torch.equal(outs[n], outs[names[0]])) and
                 (args_out[n] is None or bool(torch.equal(args_out[n], args_out[names[0]]))) for n in names}
         times = {n: [] for n in names}
+        ftimes = {n: [] for n in names}
         for _ in range(args.rounds):
             for n in names:
-                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                a.record()
-                for _ in range(args.reps):
-                    launch(libs[n], outs[n], _lib.MP_STAGE_MAIN, args_out[n])
-                b.record()
-                torch.cuda.synchronize()
-                times[n].append(a.elapsed_time(b) / args.reps)
+                for stage, acc in ((_lib.MP_STAGE_MAIN, times), (_lib.MP_STAGE_FIXUP, ftimes)):
+                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    a.record()
+                    for _ in range(args.reps):
+                        launch(libs[n], outs[n], stage, args_out[n])
+                    b.record()
+                    torch.cuda.synchronize()
+                    acc[n].append(a.elapsed_time(b) / args.reps)
         for n in names:
             t = sorted(times[n])
+            ft = sorted(ftimes[n])
             results["%s/chunk%d" % (n, chunk)] = {"median_ms": t[len(t) // 2], "min_ms": t[0],
+                                                  "fixup_ms": ft[len(ft) // 2],
                                                   "bitwise_equal_to_%s" % names[0]: same[n],
                                                   "n_split": csr.n_split, "n_waves": csr.n_waves}
     for k, v in results.items():
