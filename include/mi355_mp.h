@@ -92,6 +92,15 @@ typedef struct mp_csr {
 const char* mp_last_error(void);
 int mp_abi_version(void);
 
+/* Process-wide kernel-shape tuning (tests and A/B runs).  Sets `key` to
+ * `value` and returns the previous value; value < 0 only queries.  Unknown
+ * keys return -1.
+ *   MP_TUNE_FLAT_VEC1_MIN_BYTES: sum/mean of rows with >= 256 features over a
+ *     gathered x of at least this many bytes run the 64-feature-tile flat
+ *     kernel (VEC=1); smaller x keeps 128-feature tiles (default 1 GiB). */
+#define MP_TUNE_FLAT_VEC1_MIN_BYTES 1
+int64_t mp_tune(int32_t key, int64_t value);
+
 /* ---- CSR build (replaces the sort/bucketing torch_scatter never did: upstream
  *      scatter_add_ walks edges in original order) ---------------- */
 

@@ -25,6 +25,7 @@
 //     edge order, i.e. exactly the arithmetic of the reference's materialised
 //     `norm*x_j` followed by CPU scatter_add_: rows that fit in one task are
 //     bit-identical to the oracle.
+#include <atomic>
 #include <float.h>
 
 #include "mp_common.h"
@@ -35,6 +36,25 @@
 #endif
 #ifndef MP_U_VEC2
 #define MP_U_VEC2 16       // x-row loads in flight per task (VEC=2: the flat wide-row kernel)
+#endif
+#ifndef MP_U_VEC1
+#define MP_U_VEC1 16       // x-row loads in flight per task (VEC=1)
+#endif
+#ifndef MP_FLAT_VEC
+#define MP_FLAT_VEC 2      // lane width of the flat wide-row kernel, sum/mean (feature tiles of L*VEC)
+#endif
+#ifndef MP_FLAT_VEC1_MIN_BYTES
+// sum/mean over a gathered x of at least this many bytes (4x the 256 MB Infinity
+// Cache) run the flat kernel at VEC=1: 64-feature tiles, each XCD's L2 holds the hot
+// rows of one tile (A/B, bitwise equal: RMAT21 6.98 -> 6.73 ms; on the Reddit-scale
+// graph, whose x is cache-resident, VEC=1 is issue-bound: 8.31 -> 9.54 ms)
+#define MP_FLAT_VEC1_MIN_BYTES (1ll << 30)
+#endif
+#ifndef MP_FLAT_VEC_ARG
+#define MP_FLAT_VEC_ARG 2  // the same for max/min
+#endif
+#ifndef MP_FLAT_LANES
+#define MP_FLAT_LANES 64   // lanes per task of the flat kernel (64 or 32)
 #endif
 #ifndef MP_U_NARROW
 #define MP_U_NARROW 12     // x-row loads in flight per task (VEC=4, tasks of < 64 lanes)
@@ -1174,7 +1194,7 @@ struct Rebind<ArgRed<VEC, W, M>, V> {
 
 template <class Red, int VEC, int L>
 static int launch_l(const AggArgs& a, int stages, hipStream_t s) {
-  constexpr int U = VEC == 4 ? (L == 64 ? MP_U_VEC4 : MP_U_NARROW) : (VEC == 2 ? MP_U_VEC2 : 16);
+  constexpr int U = VEC == 4 ? (L == 64 ? MP_U_VEC4 : MP_U_NARROW) : (VEC == 2 ? MP_U_VEC2 : MP_U_VEC1);
   const int ftiles = (int)ceil_div(a.F, L * VEC);
   if (stages & MP_STAGE_MAIN) {
     int64_t nb = ceil_div(a.n_waves, kWavesPerBlock * (64 / L));
@@ -1195,7 +1215,7 @@ static int launch_l(const AggArgs& a, int stages, hipStream_t s) {
     MP_CHECK_LAUNCH();
   }
   if ((stages & MP_STAGE_FIXUP) && a.n_split > 0) {
-    if constexpr (VEC == 2 && !Red::kGat && !Red::kGatB && !Red::kHW) {
+    if constexpr (VEC != 4 && !Red::kGat && !Red::kGatB && !Red::kHW) {
       if (a.fix4) {
         dim3 grid4((unsigned)a.n_split, (unsigned)ceil_div(a.F, 64 * 4));
         hipLaunchKernelGGL((k_agg_fixup<typename Rebind<Red, 4>::type, 4>), grid4, dim3(kBlock), 0, s, a);
@@ -1260,6 +1280,8 @@ static int launch(const AggArgs& a, int stages, hipStream_t s, int lanes = 64) {
       case 32: return launch_l<Red, 4, 32>(a, stages, s);
       default: break;
     }
+  } else {
+    if (lanes == 32) return launch_l<Red, VEC, 32>(a, stages, s);
   }
   return launch_l<Red, VEC, 64>(a, stages, s);
 }
@@ -1296,6 +1318,9 @@ static int dispatch_reduce(const AggArgs& a, int reduce, int stages, hipStream_t
 
 static int64_t slab_ld_for(int F) { return ceil_div(F, 256) * 256; }
 
+// mp_tune(MP_TUNE_FLAT_VEC1_MIN_BYTES)
+static std::atomic<int64_t> g_flat_vec1_min{MP_FLAT_VEC1_MIN_BYTES};
+
 static int check_graph(const mp_csr* g, const char* who) {
   MP_CHECK_ARG(g != nullptr, "%s: null graph", who);
   MP_CHECK_ARG(g->rowptr && g->wave_row && g->wave_slot && (g->n_split == 0 || g->split_waves),
@@ -1325,6 +1350,14 @@ static void fill_graph(AggArgs& a, const mp_csr* g) {
 using namespace mp;
 
 extern "C" {
+
+int64_t mp_tune(int32_t key, int64_t value) {
+  switch (key) {
+    case MP_TUNE_FLAT_VEC1_MIN_BYTES:
+      return value < 0 ? g_flat_vec1_min.load() : g_flat_vec1_min.exchange(value);
+  }
+  return -1;
+}
 
 size_t mp_aggregate_slab_bytes(const mp_csr* g, int32_t F, int32_t reduce) {
   if (!g || F <= 0) return 256;
@@ -1366,16 +1399,19 @@ int mp_aggregate_f32(const mp_csr* g, const float* w, const float* x, int64_t ld
   a.slab_a = is_arg ? (int32_t*)((char*)slab + v) : nullptr;
   hipStream_t s = as_stream(stream);
   Shape sh = pick_shape(F, ldx, x, ldo, out);
-  if (MP_WIDE_FLAT && F >= 256 && F % 2 == 0 && sh.vec >= 2) {
-    sh.vec = 2;  // 128-feature tiles, one task per wave, slot batches across rows
+  int fvec = is_arg ? MP_FLAT_VEC_ARG : MP_FLAT_VEC;
+  if (!is_arg && (int64_t)g->n_cols * ldx * 4 >= g_flat_vec1_min.load(std::memory_order_relaxed)) fvec = 1;
+  if (MP_WIDE_FLAT && F >= 256 && F % fvec == 0 && sh.vec >= fvec) {
+    sh.vec = fvec;  // narrow feature tiles, slot batches across rows
+    sh.lanes = MP_FLAT_LANES;
     a.flat = 1;
     // the fix-up reads slabs by feature: run it 4 wide when out (and bias) allow
     a.fix4 = F % 4 == 0 && (uintptr_t)out % 16 == 0 && ldo % 4 == 0 && (uintptr_t)bias % 16 == 0;
   }
   switch (sh.vec) {
     case 4: return dispatch_reduce<4>(a, reduce, stages, s, sh.lanes);
-    case 2: return dispatch_reduce<2>(a, reduce, stages, s, 64);
-    default: return dispatch_reduce<1>(a, reduce, stages, s, 64);
+    case 2: return dispatch_reduce<2>(a, reduce, stages, s, a.flat ? sh.lanes : 64);
+    default: return dispatch_reduce<1>(a, reduce, stages, s, a.flat ? sh.lanes : 64);
   }
 }
 

@@ -20,6 +20,7 @@ MP_FLAG_PYG_MASK = 2
 MP_STAGE_MAIN = 1
 MP_STAGE_FIXUP = 2
 MP_STAGE_ALL = 3
+MP_TUNE_FLAT_VEC1_MIN_BYTES = 1
 
 c_p = ctypes.c_void_p
 i64 = ctypes.c_int64
@@ -41,6 +42,7 @@ class MpCsr(ctypes.Structure):
 SIGNATURES = {
     "mp_last_error": (ctypes.c_char_p, []),
     "mp_abi_version": (ctypes.c_int, []),
+    "mp_tune": (i64, [i32, i64]),
     "mp_csr_build_workspace": (sz, [i64, i64]),
     "mp_csr_build": (ctypes.c_int, [c_p, c_p, i64, i64, i64, c_p, c_p, c_p, c_p, c_p, sz, c_p]),
     "mp_schedule_n_waves": (i32, [i64, i64, i32]),

@@ -144,6 +144,39 @@ def test_fused_sum_mean(F, chunk, weighted):
     assert torch.equal(outm[whole], wantm[whole])
 
 
+@pytest.mark.parametrize("F", [256, 300, 512])
+@pytest.mark.parametrize("chunk", [16, 256])
+def test_fused_sum_mean_64_feature_tiles(F, chunk):
+    """Sum/mean of >= 256-feature rows over a gathered x of >= 1 GiB run the
+    flat kernel with 64-feature tiles (VEC=1); mp_tune forces that shape on a
+    small graph.  Same arithmetic per feature: bitwise equal to the default
+    128-feature-tile shape and to the oracle on unsplit rows."""
+    _, ops, _, Graph, pl = _mods()
+    from mi355_mp import _lib
+    lib = _lib.load()
+    N, E = 700, 9000
+    ei = pl(N, E, seed=F + chunk + 1)
+    g = torch.Generator().manual_seed(F + 1)
+    x = torch.randn(N, F, generator=g)
+    w = torch.rand(E, generator=g)
+    graph = Graph(ei.to(DEV), N, N, chunk=chunk)
+    eid = ei.to(DEV)
+    base = {r: ops.fused_propagate(graph, x.to(DEV), eid, w.to(DEV), r).cpu() for r in ("sum", "mean")}
+    prev = lib.mp_tune(_lib.MP_TUNE_FLAT_VEC1_MIN_BYTES, 0)
+    try:
+        got = {r: ops.fused_propagate(graph, x.to(DEV), eid, w.to(DEV), r).cpu() for r in ("sum", "mean")}
+    finally:
+        lib.mp_tune(_lib.MP_TUNE_FLAT_VEC1_MIN_BYTES, prev)
+    assert lib.mp_tune(_lib.MP_TUNE_FLAT_VEC1_MIN_BYTES, -1) == prev
+    for r in ("sum", "mean"):
+        assert torch.equal(got[r], base[r])
+    want = S.gather_sum(x, ei[0], ei[1], w, N)
+    _bound_ok(got["sum"], want, S.gather_sum(x.abs(), ei[0], ei[1], w.abs(), N))
+    split = set(_split_rows(graph.dst))
+    whole = torch.tensor([r for r in range(N) if r not in split], dtype=torch.long)
+    assert torch.equal(got["sum"][whole], want[whole])
+
+
 @pytest.mark.parametrize("F", [1, 5, 64, 256, 602])
 @pytest.mark.parametrize("reduce", ["max", "min"])
 def test_fused_max_min_bit_exact_with_ties(F, reduce):

@@ -46,6 +46,17 @@ def test_abi_version_and_error_string(lib):
     assert isinstance(lib.mp_last_error(), bytes)
 
 
+def test_tuning_knob_set_query_restore(lib):
+    from mi355_mp import _lib
+    k = _lib.MP_TUNE_FLAT_VEC1_MIN_BYTES
+    default = lib.mp_tune(k, -1)
+    assert default == 1 << 30
+    assert lib.mp_tune(k, 123) == default
+    assert lib.mp_tune(k, -1) == 123
+    assert lib.mp_tune(k, default) == 123
+    assert lib.mp_tune(99, 5) == -1
+
+
 def test_host_side_sizes_without_gpu(lib):
     # pure host arithmetic of the C-ABI (no device calls)
     assert lib.mp_schedule_n_waves(100, 1000, 256) == 5

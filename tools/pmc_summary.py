@@ -16,7 +16,7 @@ import os
 import shutil
 import sys
 
-KERNEL = "k_agg_flat<mp::SumRed<2, true, false>, 2, 16, 64, false>"
+KERNEL = None   # the dominant k_agg_flat / k_agg_main instance, from the kernel-trace stats
 
 
 def per_launch(path, counter):
@@ -31,15 +31,25 @@ def main():
     src, rnd = sys.argv[1], sys.argv[2]
     os.makedirs("profiles", exist_ok=True)
     shutil.copy(os.path.join(src, "kt", "kt_kernel_stats.csv"), "profiles/%s_kernel_stats.csv" % rnd)
-    avg_ns = None
+    global KERNEL
+    avg_ns, best = None, -1.0
     for r in csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_stats.csv"))):
-        if KERNEL in r["Name"]:
-            avg_ns = float(r["AverageNs"])
+        if ("k_agg_flat" in r["Name"] or "k_agg_main" in r["Name"]) and float(r["TotalDurationNs"]) > best:
+            best = float(r["TotalDurationNs"])
+            KERNEL, avg_ns = r["Name"], float(r["AverageNs"])
     fetch, nf = per_launch(os.path.join(src, "pmc_fetch", "pmc_counter_collection.csv"), "FETCH_SIZE")
     write, nw = per_launch(os.path.join(src, "pmc_write", "pmc_counter_collection.csv"), "WRITE_SIZE")
     hit, _ = per_launch(os.path.join(src, "pmc_l2", "pmc_counter_collection.csv"), "TCC_HIT_sum")
     miss, _ = per_launch(os.path.join(src, "pmc_l2", "pmc_counter_collection.csv"), "TCC_MISS_sum")
     read_b = 2.0 * fetch * 1024
+    # this kernel's own FETCH_SIZE ratio, measured on a known byte count by
+    # tools/pmc_calibrate.py in the same profile run (pass pmc_calib)
+    ratio = None
+    calib = os.path.join(src, "pmc_calib", "pmc_counter_collection.csv")
+    if os.path.exists(calib):
+        cv, _ = per_launch(calib, "FETCH_SIZE")
+        if cv:
+            ratio = cv * 1024 / 2172780552.0   # expected_read_bytes printed by pmc_calibrate.py
     write_b = write * 1024
     out = {
         "workload": "rmat21_gcn_f256",
@@ -48,13 +58,15 @@ def main():
         "FETCH_SIZE_KiB_raw": fetch,
         "WRITE_SIZE_KiB_raw": write,
         "read_bytes_corrected": read_b,
+        "fetch_ratio_calibrated": ratio,
+        "read_bytes_calibrated": fetch * 1024 / ratio if ratio else None,
         "write_bytes": write_b,
         "hbm_bytes_per_launch": read_b + write_b,
         "l2_hit_rate": hit / (hit + miss) if hit is not None and miss else None,
         "kernel_trace_avg_ms": avg_ns / 1e6 if avg_ns else None,
         "note": "FETCH_SIZE counts L2->fabric reads (Infinity-Cache hits included): an upper bound "
-                "on HBM reads; doubled per the gfx950 correction (calibrated for this kernel's 8 B/lane "
-                "loads in profiles/r01_pmc_calibration.json)",
+                "on HBM reads; doubled per the gfx950 correction (calibrated for this kernel's own "
+                "load width in profiles/r01_pmc_calibration.json)",
     }
     with open("profiles/%s_pmc_traffic.json" % rnd, "w") as f:
         json.dump(out, f, indent=1)

@@ -19,4 +19,6 @@ run kt 600 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv
 run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_agg_(main|flat)" -d $OUT/pmc_fetch -o pmc --output-format csv -- python3 $B
 run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_agg_(main|flat)" -d $OUT/pmc_write -o pmc --output-format csv -- python3 $B
 run pmc_l2 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "k_agg_(main|flat)" -d $OUT/pmc_l2 -o pmc --output-format csv -- python3 $B
-find $OUT -name "*.csv" | head -50
+
+run pmc_calib 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_agg_(main|flat)" -d $OUT/pmc_calib -o pmc --output-format csv -- python3 tools/pmc_calibrate.py
+find $OUT -name "*.csv"
