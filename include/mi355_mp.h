@@ -55,7 +55,8 @@ extern "C" {
 /* aggregate stages (bench times the main kernel on its own) */
 #define MP_STAGE_MAIN 1
 #define MP_STAGE_FIXUP 2
-#define MP_STAGE_ALL 3
+#define MP_STAGE_STATS 4  /* mp_gat_softmax_aggregate_f32: the softmax row-statistics passes */
+#define MP_STAGE_ALL 7
 
 /*
  * Destination-sorted CSR plus its edge-balanced ("merge-path") schedule.
@@ -170,6 +171,22 @@ int mp_gat_aggregate_f32(const mp_csr* g, const float* xw, const float* a_src,
                          const float* bias, float* out, int64_t ldo,
                          float* row_stats, void* slab, size_t slab_bytes,
                          int32_t stages, void* stream);
+
+/* Two-pass form of the same layer, in the reference's own arithmetic
+ * (utils.softmax [U3] then message x_j * alpha and scatter_add in edge order,
+ * GATConv.update + bias [U6]):
+ *   MP_STAGE_STATS: row_stats[r,h,0] = m = max_k leaky(a_src[col_k,h] + a_dst[r,h]),
+ *                   row_stats[r,h,1] = sum_k exp(leaky(.) - m) + 1e-16 (CSR order)
+ *   MP_STAGE_MAIN/FIXUP: out[r,h,:] = sum_k (exp(leaky(.) - m) / den) * xw[col_k,h,:] + bias
+ * slot_row from mp_csr_slot_rows.  Shapes: mp_gat_two_pass_ok(H, C) != 0
+ * (H <= 16; C = 16, 32 or a multiple of 64).  Rows not split across tasks
+ * follow the reference's operation order exactly. */
+int mp_gat_two_pass_ok(int32_t H, int32_t C);
+int mp_gat_softmax_aggregate_f32(const mp_csr* g, const int32_t* slot_row, const float* xw,
+                                 const float* a_src, const float* a_dst, int32_t H, int32_t C,
+                                 float slope, const float* bias, float* out, int64_t ldo,
+                                 float* row_stats, void* slab, size_t slab_bytes,
+                                 int32_t stages, void* stream);
 
 /* ---- GATConv backward pieces ------------------------------ */
 

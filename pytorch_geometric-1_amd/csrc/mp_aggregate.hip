@@ -26,6 +26,7 @@
 //     `norm*x_j` followed by CPU scatter_add_: rows that fit in one task are
 //     bit-identical to the oracle.
 #include <atomic>
+#include <type_traits>
 #include <float.h>
 
 #include "mp_common.h"
@@ -152,6 +153,7 @@ struct AggArgs {
   float slope;
   float* row_stats;
   float* slab_s;
+  const int32_t* slot_row;  // two-pass GAT: row owning each CSR slot
   // GAT backward (transposed CSR: rows = source nodes j, col = destination i)
   const float* y;     // xw, the row's own features (d alpha = <g_i, xw_j>)
   int64_t ldy;
@@ -462,6 +464,119 @@ struct GatRed {
   }
 };
 
+// Two-pass GAT (mp_gat_softmax_aggregate_f32): utils.softmax's row statistics
+// [U3] as their own merge-path passes over x = a_src [N, H] (F = H, one lane
+// task per row holding every head, k_agg_lane), then the aggregation as a
+// weighted sum whose weights are the reference's alpha.
+//   pass 1 (GatMaxRed): m[r,h]   = max_k leaky(a_src[col_k,h] + a_dst[r,h])
+//   pass 2 (GatDenRed): den[r,h] = sum_k exp(leaky(.) - m[r,h]) + 1e-16, in
+//                       CSR (= original edge) order, separately rounded
+// Both write row_stats[r, h, 0|1] (the layout mp_gat_aggregate_f32 leaves).
+__device__ __forceinline__ float gat_leaky(float a, float slope) { return a > 0.f ? a : __fmul_rn(a, slope); }
+
+template <int VEC>
+struct GatMaxRed {
+  static constexpr bool kW = false;
+  static constexpr bool kEid = false;
+  static constexpr bool kGat = false;
+  static constexpr bool kHW = false;
+  static constexpr bool kGatB = false;
+  static constexpr bool kStat = false;
+  struct Part {
+    float v[VEC];
+  };
+  float acc[VEC];
+  float ad[VEC];
+  float slope = 0.f;
+  int h = 0;  // slab_ref: no softmax-stat slab
+
+  __device__ GatMaxRed() {}
+  __device__ GatMaxRed(const AggArgs& p, int, bool) : slope(p.slope) {}
+
+  __device__ __forceinline__ void begin(const AggArgs& p, int64_t row, bool, int f, bool act) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      acc[k] = -INFINITY;
+      ad[k] = (act && f + k < p.F) ? p.a_dst[row * p.H + f + k] : 0.f;
+    }
+  }
+  __device__ __forceinline__ void consume(const Frag<VEC>& v, float, int, float) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = fmaxf(acc[k], gat_leaky(__fadd_rn(v.v[k], ad[k]), slope));
+  }
+  __device__ __forceinline__ void save(PRef r, bool) const {
+    Frag<VEC> o;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) o.v[k] = acc[k];
+    store_frag<VEC>(r.v, o);
+  }
+  static __device__ __forceinline__ Part load(PRef r) {
+    Frag<VEC> o = load_frag<VEC>(r.v);
+    Part q;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) q.v[k] = o.v[k];
+    return q;
+  }
+  __device__ __forceinline__ void set(const Part& q) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = q.v[k];
+  }
+  __device__ __forceinline__ void merge(const Part& q) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = fmaxf(acc[k], q.v[k]);
+  }
+  __device__ __forceinline__ Part part() const {
+    Part q;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) q.v[k] = acc[k];
+    return q;
+  }
+  __device__ __forceinline__ void finish(const AggArgs& p, int64_t row, int64_t, int f, bool act) {
+    if (!act) return;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k)
+      if (f + k < p.F) p.row_stats[(row * p.H + f + k) * 2] = acc[k];
+  }
+};
+
+template <int VEC>
+struct GatDenRed : GatMaxRed<VEC> {
+  using Base = GatMaxRed<VEC>;
+  using typename Base::Part;
+  using Base::acc;
+  using Base::ad;
+  using Base::slope;
+  float m[VEC];
+
+  __device__ GatDenRed() {}
+  __device__ GatDenRed(const AggArgs& p, int f, bool act) : Base(p, f, act) {}
+
+  __device__ __forceinline__ void begin(const AggArgs& p, int64_t row, bool, int f, bool act) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      const bool ok = act && f + k < p.F;
+      acc[k] = 0.f;
+      ad[k] = ok ? p.a_dst[row * p.H + f + k] : 0.f;
+      m[k] = ok ? p.row_stats[(row * p.H + f + k) * 2] : 0.f;
+    }
+  }
+  __device__ __forceinline__ void consume(const Frag<VEC>& v, float, int, float) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k)
+      acc[k] = __fadd_rn(acc[k], expf(__fsub_rn(gat_leaky(__fadd_rn(v.v[k], ad[k]), slope), m[k])));
+  }
+  __device__ __forceinline__ void merge(const Part& q) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = __fadd_rn(acc[k], q.v[k]);
+  }
+  __device__ __forceinline__ void finish(const AggArgs& p, int64_t row, int64_t, int f, bool act) {
+    if (!act) return;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k)
+      if (f + k < p.F) p.row_stats[(row * p.H + f + k) * 2 + 1] = __fadd_rn(acc[k], 1e-16f);
+  }
+};
+
 // Per-head weighted sum (GAT backward: d out / d x_j = alpha[e,h]): the weight
 // of slot k for this lane's head h = f / C is w[k*H + h].
 template <int VEC>
@@ -711,6 +826,82 @@ struct SlotWin {
   }
 };
 
+// Two-pass GAT aggregation window (k_agg_flat, 64-lane tasks, 64-feature
+// tiles): lane k computes the reference's alpha for slot base+k and each of the
+// hpt heads of this tile once per window,
+//   alpha = exp(leaky(a_src[col,h] + a_dst[r,h]) - m[r,h]) / den[r,h],  r = slot_row,
+// into the wave's LDS; a slot then costs one LDS read per lane (lane's head =
+// its feature / C).  Columns and slot rows run two windows ahead and the
+// per-slot gathers (a_src, a_dst, row stats) one window ahead.
+struct GatAlphaWin {
+  int64_t base, limit;
+  int col, col_n, col_nn, row_n, row_nn;
+  float g_as[4], g_ad[4], g_m[4], g_d[4];
+  float* lds;
+  int h0, hpt, j;
+
+  __device__ __forceinline__ void fetch(const AggArgs& p, int64_t b, int lane, int& c, int& r) {
+    const int64_t k = b + lane;
+    const bool ok = k < limit;
+    c = ok ? ld_stream(p.col + k) : 0;
+    r = ok ? ld_stream(p.slot_row + k) : 0;
+  }
+  __device__ __forceinline__ void gather(const AggArgs& p, int c, int r) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (q < hpt) {
+        const int64_t hr = (int64_t)r * p.H + h0 + q;
+        g_as[q] = p.a_src[(int64_t)c * p.H + h0 + q];
+        g_ad[q] = p.a_dst[hr];
+        const f32x2 st = *reinterpret_cast<const f32x2*>(p.row_stats + hr * 2);
+        g_m[q] = st.x;
+        g_d[q] = st.y;
+      }
+    }
+  }
+  __device__ __forceinline__ void publish(const AggArgs& p, int lane) {
+    float al[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      al[q] = q < hpt ? __fdiv_rn(expf(__fsub_rn(gat_leaky(__fadd_rn(g_as[q], g_ad[q]), p.slope), g_m[q])), g_d[q])
+                      : 0.f;
+    __builtin_amdgcn_wave_barrier();  // earlier reads of the previous window come first
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (q < hpt) lds[lane * hpt + q] = al[q];
+    __builtin_amdgcn_wave_barrier();  // LDS ops of one wave run in order: later reads see the stores
+  }
+  __device__ __forceinline__ void init(const AggArgs& p, int64_t b, int64_t lim, int lane, float* wave_lds,
+                                       int tile) {
+    base = b;
+    limit = lim;
+    lds = wave_lds;
+    // tile t holds features [64t, 64t+64): heads h0 .. h0+hpt-1, lane's head h0 + lane/C
+    h0 = tile * 64 / p.C;
+    hpt = p.C >= 64 ? 1 : min(64 / p.C, p.H - h0);  // a last partial tile holds fewer heads
+    j = p.C >= 64 ? 0 : lane / p.C;                  // lanes past F read some slot's alpha, unused
+    int r;
+    fetch(p, base, lane, col, r);
+    fetch(p, base + 64, lane, col_n, row_n);
+    fetch(p, base + 128, lane, col_nn, row_nn);
+    gather(p, col, r);
+    publish(p, lane);
+    gather(p, col_n, row_n);
+  }
+  __device__ __forceinline__ void ensure(const AggArgs& p, int64_t e, int lane) {
+    if (e >= base + 64) {  // slots are consumed in order, never skipping a window
+      base += 64;
+      col = col_n;
+      publish(p, lane);  // the gathers issued a window ago
+      col_n = col_nn;
+      row_n = row_nn;
+      fetch(p, base + 128, lane, col_nn, row_nn);
+      gather(p, col_n, row_n);
+    }
+  }
+  __device__ __forceinline__ float alpha(int slot_in_win) const { return lds[slot_in_win * hpt + j]; }
+};
+
 // Process CSR slots [s, t) of the current (partial) row.
 // All U row loads are issued unconditionally (indices past the segment are
 // clamped to its last slot, inactive lanes read feature 0) so no load sits
@@ -945,9 +1136,12 @@ __global__ __launch_bounds__(kBlock) void k_agg_lane(AggArgs p) {
 // in flight while the previous row is finished.  Each row's slots are still
 // consumed in CSR order by one task: results are identical.
 // ---------------------------------------------------------------------------
-template <class Red, int VEC, int U, int L, bool BUF>
+// GA: two-pass GAT aggregation (Red = SumRed<1, true, false>, L = 64): the slot
+// weights are the reference's alpha from GatAlphaWin instead of w.
+template <class Red, int VEC, int U, int L, bool BUF, bool GA = false>
 __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
   static_assert(!Red::kGat && !Red::kGatB && !Red::kHW, "flat loop: sum/mean/max/min reducers");
+  static_assert(!GA || (L == 64 && VEC == 1 && Red::kW), "two-pass GAT: 64-lane tasks, 64-feature tiles");
   using GR = Grp<L>;
   const int lane = lane_id();
   const int gl = lane & (L - 1);
@@ -978,8 +1172,13 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
   const int64_t e_end = GR::un(p.wave_slot[w + 1]);
 
   Red red(p, f, act);
-  SlotWin<Red::kW, Red::kEid, L> win;
-  win.init(p, e_begin, e_end, gl);
+  std::conditional_t<GA, GatAlphaWin, SlotWin<Red::kW, Red::kEid, L>> win;
+  if constexpr (GA) {
+    __shared__ float ga_lds[kWavesPerBlock][64 * 4];
+    win.init(p, e_begin, e_end, gl, ga_lds[threadIdx.x >> 6], tile);
+  } else {
+    win.init(p, e_begin, e_end, gl);
+  }
   int rbase = r_first;
   int rp = (rbase + gl <= p.n_rows) ? p.rowptr[rbase + gl] : 0;
   // row end / start of row r (r >= rbase), refilling the window when needed
@@ -1031,6 +1230,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
     if (n > U) n = U;
     n = GR::un(n);
     Frag<VEC> v[U];
+    [[maybe_unused]] float al[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int uu = u < n ? u : n - 1;
@@ -1041,13 +1241,17 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
         const float* src = reinterpret_cast<const float*>(xb + (int64_t)c * ldxb + foff);
         v[u] = MP_NT_X ? load_frag_nt<VEC>(src) : load_frag<VEC>(src);
       }
+      if constexpr (GA) al[u] = win.alpha(off + uu);  // LDS reads of the batch issued with its loads
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (u < n) {
         advance(e + u);
-        const float wt = Red::kW ? GR::bc(win.w, off + u) : 1.f;
-        const int ei = Red::kEid ? GR::bc(win.eid, off + u) : 0;
+        float wt = 1.f;
+        if constexpr (GA) wt = al[u];
+        else if constexpr (Red::kW) wt = GR::bc(win.w, off + u);
+        int ei = 0;
+        if constexpr (!GA && Red::kEid) ei = GR::bc(win.eid, off + u);
         red.consume(v[u], wt, ei, 0.f);
       }
     }
@@ -1194,7 +1398,8 @@ struct Rebind<ArgRed<VEC, W, M>, V> {
 
 template <class Red, int VEC, int L>
 static int launch_l(const AggArgs& a, int stages, hipStream_t s) {
-  constexpr int U = VEC == 4 ? (L == 64 ? MP_U_VEC4 : MP_U_NARROW) : (VEC == 2 ? MP_U_VEC2 : MP_U_VEC1);
+  constexpr int U = VEC == 4 ? (L == 64 ? MP_U_VEC4 : MP_U_NARROW)
+                             : (VEC == 2 ? MP_U_VEC2 : (L < MP_U_VEC1 ? L : MP_U_VEC1));  // VEC=1 groups < 16 lanes: GAT stats
   const int ftiles = (int)ceil_div(a.F, L * VEC);
   if (stages & MP_STAGE_MAIN) {
     int64_t nb = ceil_div(a.n_waves, kWavesPerBlock * (64 / L));
@@ -1494,6 +1699,86 @@ int mp_gat_aggregate_f32(const mp_csr* g, const float* xw, const float* a_src, c
     case 2: return launch<GatRed<2>, 2>(a, stages, s);
     default: return launch<GatRed<1>, 1>(a, stages, s);
   }
+}
+
+int mp_gat_two_pass_ok(int32_t H, int32_t C) {
+  return H >= 1 && H <= 16 && (C == 16 || C == 32 || (C >= 64 && C % 64 == 0)) ? 1 : 0;
+}
+
+// Two-pass GAT: row statistics (two lane-task passes over a_src), then the
+// reference-order weighted aggregation (k_agg_flat<.., GA>, 64-feature tiles).
+int mp_gat_softmax_aggregate_f32(const mp_csr* g, const int32_t* slot_row, const float* xw, const float* a_src,
+                                 const float* a_dst, int32_t H, int32_t C, float slope, const float* bias,
+                                 float* out, int64_t ldo, float* row_stats, void* slab, size_t slab_bytes,
+                                 int32_t stages, void* stream) {
+  MP_DEVICE_GUARD(stream);
+  int rc = check_graph(g, "mp_gat_softmax_aggregate_f32");
+  if (rc) return rc;
+  MP_CHECK_ARG(mp_gat_two_pass_ok(H, C),
+               "mp_gat_softmax_aggregate_f32: needs H <= 16 and C in {16, 32} or a multiple of 64");
+  MP_CHECK_ARG(g->n_edges == 0 || g->col != nullptr, "mp_gat_softmax_aggregate_f32: graph needs a column array");
+  MP_CHECK_ARG(xw && a_src && a_dst && out && row_stats && (g->n_edges == 0 || slot_row),
+               "mp_gat_softmax_aggregate_f32: null input");
+  MP_CHECK_ARG((uintptr_t)row_stats % 8 == 0, "mp_gat_softmax_aggregate_f32: row_stats must be 8-byte aligned");
+  const int F = H * C;
+  MP_CHECK_ARG(ldo >= F, "mp_gat_softmax_aggregate_f32: ldo < H*C");
+  MP_CHECK_ARG(slab != nullptr && slab_bytes >= mp_gat_slab_bytes(g, H, C),
+               "mp_gat_softmax_aggregate_f32: slab workspace too small");
+  hipStream_t s = as_stream(stream);
+  AggArgs a{};
+  fill_graph(a, g);
+  a.a_src = a_src;
+  a.a_dst = a_dst;
+  a.H = H;
+  a.C = C;
+  a.slope = slope;
+  a.row_stats = row_stats;
+  a.slot_row = slot_row;
+  a.slab_v = (float*)slab;
+  if (stages & MP_STAGE_STATS) {
+    // passes 1 and 2: x = a_src [N, H], F = H
+    AggArgs t = a;
+    t.F = H;
+    t.x = a_src;
+    t.ldx = H;
+    t.slab_ld = slab_ld_for(H);
+    for (int pass = 0; pass < 2; ++pass) {
+      // k_agg_main lane groups, one lane per head: H <= 4 -> 4 lanes, <= 8 -> 8, else 16
+      if (H <= 4) rc = pass ? launch_l<GatDenRed<1>, 1, 4>(t, MP_STAGE_ALL, s) : launch_l<GatMaxRed<1>, 1, 4>(t, MP_STAGE_ALL, s);
+      else if (H <= 8) rc = pass ? launch_l<GatDenRed<1>, 1, 8>(t, MP_STAGE_ALL, s) : launch_l<GatMaxRed<1>, 1, 8>(t, MP_STAGE_ALL, s);
+      else rc = pass ? launch_l<GatDenRed<1>, 1, 16>(t, MP_STAGE_ALL, s) : launch_l<GatMaxRed<1>, 1, 16>(t, MP_STAGE_ALL, s);
+      if (rc) return rc;
+    }
+  }
+  a.F = F;
+  a.w = a_src;  // any non-null pointer: the HAS_W reducer multiplies by the window's alpha
+  a.x = xw;
+  a.ldx = F;
+  a.bias = bias;
+  a.out = out;
+  a.ldo = ldo;
+  a.slab_ld = slab_ld_for(F);
+  a.flat = 1;
+  using Red = SumRed<1, true, false>;
+  const int ftiles = (int)ceil_div(F, 64);
+  if ((stages & MP_STAGE_MAIN) && a.n_waves > 0) {
+    int64_t nb = ceil_div(a.n_waves, kWavesPerBlock);
+    if (MP_XCD_TILES && 8 % ftiles == 0) nb = ceil_div(nb, 8 / ftiles) * (8 / ftiles);
+    hipLaunchKernelGGL((k_agg_flat<Red, 1, MP_U_VEC1, 64, false, true>), dim3((unsigned)nb, (unsigned)ftiles),
+                       dim3(kBlock), 0, s, a);
+    MP_CHECK_LAUNCH();
+  }
+  if ((stages & MP_STAGE_FIXUP) && a.n_split > 0) {
+    if (F % 4 == 0 && (uintptr_t)out % 16 == 0 && ldo % 4 == 0 && (uintptr_t)bias % 16 == 0) {
+      hipLaunchKernelGGL((k_agg_fixup<SumRed<4, true, false>, 4>), dim3((unsigned)a.n_split, (unsigned)ceil_div(F, 256)),
+                         dim3(kBlock), 0, s, a);
+    } else {
+      hipLaunchKernelGGL((k_agg_fixup<Red, 1>), dim3((unsigned)a.n_split, (unsigned)ceil_div(F, 64)), dim3(kBlock), 0,
+                         s, a);
+    }
+    MP_CHECK_LAUNCH();
+  }
+  return MP_OK;
 }
 
 int mp_gat_backward_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, const float* xw, const float* a_src,

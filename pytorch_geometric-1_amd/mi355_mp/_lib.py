@@ -19,7 +19,8 @@ MP_FLAG_INIT_FROM_OUT = 1
 MP_FLAG_PYG_MASK = 2
 MP_STAGE_MAIN = 1
 MP_STAGE_FIXUP = 2
-MP_STAGE_ALL = 3
+MP_STAGE_STATS = 4
+MP_STAGE_ALL = 7
 MP_TUNE_FLAT_VEC1_MIN_BYTES = 1
 
 c_p = ctypes.c_void_p
@@ -55,6 +56,9 @@ SIGNATURES = {
     "mp_gat_slab_bytes": (sz, [ctypes.POINTER(MpCsr), i32, i32]),
     "mp_gat_aggregate_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, c_p, i32, i32, f32, c_p,
                                             c_p, i64, c_p, c_p, sz, i32, c_p]),
+    "mp_gat_two_pass_ok": (ctypes.c_int, [i32, i32]),
+    "mp_gat_softmax_aggregate_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, c_p, c_p, i32, i32, f32,
+                                                    c_p, c_p, i64, c_p, c_p, sz, i32, c_p]),
     "mp_gat_alpha_f32": (ctypes.c_int, [c_p, c_p, i64, i32, c_p, c_p, f32, c_p, c_p, c_p]),
     "mp_csr_slot_rows": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p]),
     "mp_gat_alpha_csr_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, c_p, i32, f32, c_p, c_p, c_p,

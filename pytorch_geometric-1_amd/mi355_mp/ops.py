@@ -279,6 +279,20 @@ def gcn_norm_weights(edge_index, num_nodes, edge_weight=None):
 # GATConv fused attention aggregation (GATConv.message + utils.softmax [U3,U6])
 # ---------------------------------------------------------------------------
 
+# GAT forward form.  Default: one online-softmax pass (mp_gat_aggregate_f32).
+# GAT_TWO_PASS = True selects mp_gat_softmax_aggregate_f32, which follows the
+# reference's operation order (softmax row max, then the denominator summed in
+# edge order, then alpha * x_j summed in edge order) at a cost: on config 3 its
+# two statistics passes take 3.6 ms and its 64-feature-tile aggregation 10.6 ms
+# (one a_src gather per slot per tile), against 8.6 ms for the single pass
+# (DESIGN.md section 3.3).
+GAT_TWO_PASS = False
+
+
+def gat_two_pass(csr, H, C):
+    return GAT_TWO_PASS and bool(_lib.load().mp_gat_two_pass_ok(H, C))
+
+
 def _gat_forward(graph, edge_index, xw, att, H, C, slope, bias, want_alpha):
     lib = _lib.load()
     dev = xw.device
@@ -298,9 +312,16 @@ def _gat_forward(graph, edge_index, xw, att, H, C, slope, bias, want_alpha):
     g = csr.struct("other")
     sb = lib.mp_gat_slab_bytes(g, H, C)
     slab = torch.empty(sb, dtype=torch.uint8, device=dev)
-    _lib.check(lib.mp_gat_aggregate_f32(g, xw.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(), H, C, float(slope),
-                                        _lib.ptr(bias), out.data_ptr(), out.stride(0), stats.data_ptr(),
-                                        slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st), "mp_gat_aggregate_f32")
+    if gat_two_pass(csr, H, C):
+        _lib.check(lib.mp_gat_softmax_aggregate_f32(g, csr.slot_rows().data_ptr(), xw.data_ptr(), a_src.data_ptr(),
+                                                    a_dst.data_ptr(), H, C, float(slope), _lib.ptr(bias),
+                                                    out.data_ptr(), out.stride(0), stats.data_ptr(), slab.data_ptr(),
+                                                    sb, _lib.MP_STAGE_ALL, st), "mp_gat_softmax_aggregate_f32")
+    else:
+        _lib.check(lib.mp_gat_aggregate_f32(g, xw.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(), H, C,
+                                            float(slope), _lib.ptr(bias), out.data_ptr(), out.stride(0),
+                                            stats.data_ptr(), slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
+                   "mp_gat_aggregate_f32")
     alpha = None
     if want_alpha:
         E = edge_index.shape[1]

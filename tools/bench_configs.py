@@ -82,14 +82,45 @@ def c3(dev):
         _lib.check(lib.mp_gat_aggregate_f32(s, xw.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(), H, C, 0.2,
                                             bias.data_ptr(), out.data_ptr(), H * C, None, slab.data_ptr(), sb,
                                             stages, st), "gat")
+    stats = torch.empty(N, H, 2, device=dev)
+    sr = csr.slot_rows()
+
+    def agg2(stages):
+        _lib.check(lib.mp_gat_softmax_aggregate_f32(s, sr.data_ptr(), xw.data_ptr(), a_src.data_ptr(),
+                                                    a_dst.data_ptr(), H, C, 0.2, bias.data_ptr(), out.data_ptr(),
+                                                    H * C, stats.data_ptr(), slab.data_ptr(), sb, stages, st),
+                   "gat2")
     scores()
-    ms_main = timed(lambda: agg(_lib.MP_STAGE_MAIN))
-    ms_fix = timed(lambda: agg(_lib.MP_STAGE_FIXUP))
     ms_scores = timed(scores)
     E = csr.n_edges
-    report("c3", "RMAT21 GATConv heads=8 C=32, fused leaky_relu+softmax(+1e-16)+aggregate+bias",
-           E, N, 4 * H * C + 4 + 4 * H, 4 * H * C + 4 * H + 4, ms_main, ms_main + ms_fix + ms_scores,
-           {"fixup_ms": ms_fix, "node_scores_ms": ms_scores, "n_split": csr.n_split})
+    # one pass (online softmax, one 256-feature tile)
+    ms_main1 = timed(lambda: agg(_lib.MP_STAGE_MAIN))
+    ms_fix1 = timed(lambda: agg(_lib.MP_STAGE_FIXUP))
+    agg(_lib.MP_STAGE_ALL)
+    one = out.clone()
+    # two pass (row statistics, then 64-feature tiles with the reference's alpha)
+    ms_stats = timed(lambda: agg2(_lib.MP_STAGE_STATS))
+    ms_main = timed(lambda: agg2(_lib.MP_STAGE_MAIN))
+    ms_fix = timed(lambda: agg2(_lib.MP_STAGE_FIXUP))
+    agg2(_lib.MP_STAGE_ALL)
+    diff = ((out - one).abs().max() / one.abs().max()).item()
+    del one
+    path = "two_pass" if ops.gat_two_pass(csr, H, C) else "one_pass"
+    tot1 = ms_main1 + ms_fix1 + ms_scores
+    tot2 = ms_stats + ms_main + ms_fix + ms_scores
+    if path == "two_pass":
+        report("c3", "RMAT21 GATConv heads=8 C=32: softmax row-stat passes + 64-feature-tile aggregation with the "
+               "reference's alpha + bias (GATConv forward path)",
+               E, N, 4 * H * C + 8 + 4 * H, 4 * H * C + 12 * H + 4, ms_main, tot2,
+               {"stats_ms": ms_stats, "fixup_ms": ms_fix, "node_scores_ms": ms_scores, "n_split": csr.n_split,
+                "one_pass": {"main_kernel_ms": ms_main1, "fixup_ms": ms_fix1, "aggregate_ms": tot1},
+                "max_rel_diff_two_vs_one_pass": diff})
+    else:
+        report("c3", "RMAT21 GATConv heads=8 C=32, fused leaky_relu+softmax(+1e-16)+aggregate+bias",
+               E, N, 4 * H * C + 4 + 4 * H, 4 * H * C + 4 * H + 4, ms_main1, tot1,
+               {"fixup_ms": ms_fix1, "node_scores_ms": ms_scores, "n_split": csr.n_split,
+                "two_pass": {"stats_ms": ms_stats, "main_kernel_ms": ms_main, "fixup_ms": ms_fix,
+                             "aggregate_ms": tot2}})
     # parity spot check against the generic PyG formula on identical inputs (one row block)
     del graph
 
