@@ -54,6 +54,13 @@
 #ifndef MP_FLAT_VEC_ARG
 #define MP_FLAT_VEC_ARG 2  // the same for max/min
 #endif
+#ifndef MP_QUAD
+#define MP_QUAD 0          // VEC=1 flat kernel: four slots per dwordx4 gather + 4x4 lane transpose
+                           // (off: measured +0.2..+0.5% on RMAT21, DESIGN.md §3.1 "tried and rejected")
+#endif
+#ifndef MP_U_QUAD
+#define MP_U_QUAD 16       // slots in flight per task of the quad kernel (multiple of 4)
+#endif
 #ifndef MP_FLAT_LANES
 #define MP_FLAT_LANES 64   // lanes per task of the flat kernel (64 or 32)
 #endif
@@ -132,6 +139,7 @@ struct AggArgs {
   uint32_t x_bytes;  // extent of x for the buffer path (0: not used)
   int32_t flat;      // sum/mean/max/min: run k_agg_flat instead of k_agg_main
   int32_t fix4;      // VEC=2 main kernel: run the fix-up at VEC=4 (slabs are indexed by feature)
+  int32_t quad;      // VEC=1 flat kernel: four-slot dwordx4 gathers + lane transpose (k_agg_flat QUAD)
   // features
   const float* w;
   const float* x;
@@ -1126,6 +1134,21 @@ __global__ __launch_bounds__(kBlock) void k_agg_lane(AggArgs p) {
   }
 }
 
+// 4x4 transpose across the four 16-lane rows: on entry lane (g, i) holds
+// element j of a = (slot g, feature 4i+j); on exit element s = (slot s,
+// feature 4i+g).  Two v_permlane32_swap (rows 0,1 <-> 2,3) and two
+// v_permlane16_swap (rows 0,2 <-> 1,3).
+__device__ __forceinline__ void quad_transpose(f32x4& a) {
+  auto s02 = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.x), __float_as_uint(a.z), false, false);
+  auto s13 = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.y), __float_as_uint(a.w), false, false);
+  auto t01 = __builtin_amdgcn_permlane16_swap(s02[0], s13[0], false, false);
+  auto t23 = __builtin_amdgcn_permlane16_swap(s02[1], s13[1], false, false);
+  a.x = __uint_as_float(t01[0]);
+  a.y = __uint_as_float(t01[1]);
+  a.z = __uint_as_float(t23[0]);
+  a.w = __uint_as_float(t23[1]);
+}
+
 // ---------------------------------------------------------------------------
 // Flat variant of k_agg_main (sum/mean/max/min): a task streams its slots in
 // fixed batches of U across row boundaries and closes rows as it crosses
@@ -1138,10 +1161,18 @@ __global__ __launch_bounds__(kBlock) void k_agg_lane(AggArgs p) {
 // ---------------------------------------------------------------------------
 // GA: two-pass GAT aggregation (Red = SumRed<1, true, false>, L = 64): the slot
 // weights are the reference's alpha from GatAlphaWin instead of w.
-template <class Red, int VEC, int U, int L, bool BUF, bool GA = false>
+// QUAD (VEC = 1, L = 64, F % 64 == 0, 16-byte rows): a 64-feature tile is
+// gathered four slots per load instruction -- lane (g, i) = (lane / 16,
+// lane % 16) loads features 4i..4i+3 of slot 4q+g as one dwordx4 -- and a 4x4
+// transpose across the lane rows (quad_transpose) leaves every lane with ONE
+// feature, 4i+g, of the four slots in slot order.  From there the row walk is
+// the VEC=1 one (each lane adds its feature's products in CSR order): the same
+// arithmetic with a quarter of the gather instructions.
+template <class Red, int VEC, int U, int L, bool BUF, bool GA = false, bool QUAD = false>
 __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
   static_assert(!Red::kGat && !Red::kGatB && !Red::kHW, "flat loop: sum/mean/max/min reducers");
   static_assert(!GA || (L == 64 && VEC == 1 && Red::kW), "two-pass GAT: 64-lane tasks, 64-feature tiles");
+  static_assert(!QUAD || (L == 64 && VEC == 1 && U % 4 == 0 && !GA), "quad gathers: 64-lane tasks, 64-feature tiles");
   using GR = Grp<L>;
   const int lane = lane_id();
   const int gl = lane & (L - 1);
@@ -1158,9 +1189,10 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
   const int wave = bx * kWavesPerBlock + (int)(threadIdx.x >> 6);
   const int w = GR::un(wave * GR::G + lane / L);
   if (w >= p.n_waves) return;
-  const int f = tile * L * VEC + gl * VEC;
+  // QUAD: the lane owns feature 4i+g of the tile and loads features 4i..4i+3
+  const int f = QUAD ? tile * 64 + 4 * (lane & 15) + (lane >> 4) : tile * L * VEC + gl * VEC;
   const bool act = f < p.F;
-  const uint32_t foff = (uint32_t)(act ? f : 0) * 4u;
+  const uint32_t foff = QUAD ? (uint32_t)(tile * 64 + 4 * (lane & 15)) * 4u : (uint32_t)(act ? f : 0) * 4u;
   const char* xb = reinterpret_cast<const char*>(p.x);
   const int64_t ldxb = p.ldx * 4;
   [[maybe_unused]] __amdgpu_buffer_rsrc_t xr;
@@ -1231,6 +1263,26 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
     n = GR::un(n);
     Frag<VEC> v[U];
     [[maybe_unused]] float al[U];
+    if constexpr (QUAD) {
+      const int g = lane >> 4;
+      f32x4 q4[U / 4];
+#pragma unroll
+      for (int q = 0; q < U / 4; ++q) {
+        int cs[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) cs[t] = readlane(win.col, off + min(4 * q + t, n - 1));
+        const int c = g == 0 ? cs[0] : (g == 1 ? cs[1] : (g == 2 ? cs[2] : cs[3]));
+        q4[q] = *reinterpret_cast<const f32x4*>(xb + (int64_t)c * ldxb + foff);
+      }
+#pragma unroll
+      for (int q = 0; q < U / 4; ++q) {
+        quad_transpose(q4[q]);
+        v[4 * q + 0].v[0] = q4[q].x;
+        v[4 * q + 1].v[0] = q4[q].y;
+        v[4 * q + 2].v[0] = q4[q].z;
+        v[4 * q + 3].v[0] = q4[q].w;
+      }
+    } else {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int uu = u < n ? u : n - 1;
@@ -1242,6 +1294,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
         v[u] = MP_NT_X ? load_frag_nt<VEC>(src) : load_frag<VEC>(src);
       }
       if constexpr (GA) al[u] = win.alpha(off + uu);  // LDS reads of the batch issued with its loads
+    }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -1412,13 +1465,22 @@ static int launch_l(const AggArgs& a, int stages, hipStream_t s) {
       b.x_bytes = (uint32_t)xb;
       hipLaunchKernelGGL((k_agg_main<Red, VEC, U, L, MP_BUF_X != 0>), grid, dim3(kBlock), 0, s, b);
     } else if (a.flat) {
-      if constexpr (!Red::kGat && !Red::kGatB && !Red::kHW)
+      if constexpr (!Red::kGat && !Red::kGatB && !Red::kHW) {
+        if constexpr (VEC == 1 && L == 64 && !Red::kEid) {
+          if (a.quad) {
+            hipLaunchKernelGGL((k_agg_flat<Red, 1, MP_U_QUAD, 64, false, false, true>), grid, dim3(kBlock), 0, s, a);
+            MP_CHECK_LAUNCH();
+            goto fixup;
+          }
+        }
         hipLaunchKernelGGL((k_agg_flat<Red, VEC, U, L, false>), grid, dim3(kBlock), 0, s, a);
+      }
     } else {
       hipLaunchKernelGGL((k_agg_main<Red, VEC, U, L, false>), grid, dim3(kBlock), 0, s, a);
     }
     MP_CHECK_LAUNCH();
   }
+fixup:
   if ((stages & MP_STAGE_FIXUP) && a.n_split > 0) {
     if constexpr (VEC != 4 && !Red::kGat && !Red::kGatB && !Red::kHW) {
       if (a.fix4) {
@@ -1606,6 +1668,8 @@ int mp_aggregate_f32(const mp_csr* g, const float* w, const float* x, int64_t ld
   Shape sh = pick_shape(F, ldx, x, ldo, out);
   int fvec = is_arg ? MP_FLAT_VEC_ARG : MP_FLAT_VEC;
   if (!is_arg && (int64_t)g->n_cols * ldx * 4 >= g_flat_vec1_min.load(std::memory_order_relaxed)) fvec = 1;
+  // VEC=1 sum/mean over 64-feature tiles: gather four slots per dwordx4 (k_agg_flat QUAD)
+  a.quad = MP_QUAD && fvec == 1 && F % 64 == 0 && ldx % 4 == 0 && (uintptr_t)x % 16 == 0;
   if (MP_WIDE_FLAT && F >= 256 && F % fvec == 0 && sh.vec >= fvec) {
     sh.vec = fvec;  // narrow feature tiles, slot batches across rows
     sh.lanes = MP_FLAT_LANES;

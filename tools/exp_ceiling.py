@@ -47,7 +47,7 @@ def main():
     for k, c in cols.items():
         structs[k] = _lib.MpCsr(csr.rowptr.data_ptr(), c.data_ptr(), csr.eid.data_ptr(), csr.wave_row.data_ptr(),
                                 csr.wave_slot.data_ptr(), csr.split_waves.data_ptr(), N, E, csr.chunk,
-                                csr.n_waves, csr.n_split, 0)
+                                csr.n_waves, csr.n_split, N)  # n_cols = N: the VEC=1 shape of the real launch
 
     def launch(s):
         _lib.check(lib.mp_aggregate_f32(s, w.data_ptr(), x.data_ptr(), F, F, 0, 0, bias.data_ptr(),
