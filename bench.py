@@ -250,6 +250,8 @@ def main():
     # the flat kernel's lane width: VEC=1 (64-feature tiles) when the gathered x
     # is >= 1 GiB, else VEC=2 (mp_aggregate.hip, MP_FLAT_VEC1_MIN_BYTES)
     vec = 1 if x_src.shape[0] * F_DIM * 4 >= (1 << 30) else 2
+    # scalar-load slot batches + soffset gathers while x spans < 4 GiB (MP_FLAT_SMEM)
+    sm = ",SM" if 0 < x_src.shape[0] * F_DIM * 4 <= 0xFFFFFFF0 else ""
     main_avg = sum(main_ms) / len(main_ms)
     fix_avg = sum(fix_ms) / len(fix_ms)
     alg_bytes = E_local * BYTES_PER_EDGE + n_rows * BYTES_PER_NODE
@@ -303,7 +305,7 @@ def main():
                        else "single GPU", "chunk": csr.chunk},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_agg_flat<SumRed<%d,true,false>,VEC=%d,U=16,L=64>" % (vec, vec),
+                         "kernel": "k_agg_flat<SumRed<%d,true,false>,VEC=%d,U=16,L=64%s>" % (vec, vec, sm),
                          "algorithmic_bytes_per_launch": alg_bytes,
                          "avg_launch_ms": main_avg, "median_launch_ms": main_ms[len(main_ms) // 2],
                          "fixup_avg_ms": fix_avg, "timing": timing_src},

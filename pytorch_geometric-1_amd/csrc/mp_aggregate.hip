@@ -58,6 +58,9 @@
 #define MP_QUAD 0          // VEC=1 flat kernel: four slots per dwordx4 gather + 4x4 lane transpose
                            // (off: measured +0.2..+0.5% on RMAT21, DESIGN.md §3.1 "tried and rejected")
 #endif
+#ifndef MP_FLAT_SMEM
+#define MP_FLAT_SMEM 1     // flat sum/mean kernel: slot columns/weights via s_load_dwordx16 batches
+#endif
 #ifndef MP_U_QUAD
 #define MP_U_QUAD 16       // slots in flight per task of the quad kernel (multiple of 4)
 #endif
@@ -140,6 +143,7 @@ struct AggArgs {
   int32_t flat;      // sum/mean/max/min: run k_agg_flat instead of k_agg_main
   int32_t fix4;      // VEC=2 main kernel: run the fix-up at VEC=4 (slabs are indexed by feature)
   int32_t quad;      // VEC=1 flat kernel: four-slot dwordx4 gathers + lane transpose (k_agg_flat QUAD)
+  int32_t smem;      // flat sum/mean kernel: slot columns/weights through scalar loads (k_agg_flat SM)
   // features
   const float* w;
   const float* x;
@@ -1168,11 +1172,36 @@ __device__ __forceinline__ void quad_transpose(f32x4& a) {
 // feature, 4i+g, of the four slots in slot order.  From there the row walk is
 // the VEC=1 one (each lane adds its feature's products in CSR order): the same
 // arithmetic with a quarter of the gather instructions.
-template <class Red, int VEC, int U, int L, bool BUF, bool GA = false, bool QUAD = false>
+// SM (L = 64, no edge ids, col != nullptr, x below 4 GiB): the column and
+// weight of every slot of a batch come straight into SGPRs through scalar
+// loads (s_load_dwordx16 via the scalar cache) -- the next batch's columns
+// issued with the current batch, the current batch's weights consumed only
+// after its gathers are in flight -- and each gather is a buffer load with the
+// row offset in soffset: per slot one SALU multiply and one VMEM instruction,
+// no v_readlane from a one-slot-per-lane window.
+template <int U, class T>
+__device__ __forceinline__ void scalar_batch(const T* a, int64_t n, int64_t e, T (&v)[U]) {
+  typedef T tv __attribute__((ext_vector_type(U), aligned(4)));
+  typedef __attribute__((address_space(4))) const tv ctv;
+  typedef __attribute__((address_space(4))) const T ct;
+  // slots [e, e + U); slots past the end of the array are clamped to the last
+  // one (never consumed: the caller stops at the task's end)
+  if (e + U <= n) {
+    const tv t = *(ctv*)(a + e);
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = t[u];
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = ((ct*)a)[e + u < n ? e + u : n - 1];
+  }
+}
+
+template <class Red, int VEC, int U, int L, bool BUF, bool GA = false, bool QUAD = false, bool SM = false>
 __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
   static_assert(!Red::kGat && !Red::kGatB && !Red::kHW, "flat loop: sum/mean/max/min reducers");
   static_assert(!GA || (L == 64 && VEC == 1 && Red::kW), "two-pass GAT: 64-lane tasks, 64-feature tiles");
   static_assert(!QUAD || (L == 64 && VEC == 1 && U % 4 == 0 && !GA), "quad gathers: 64-lane tasks, 64-feature tiles");
+  static_assert(!SM || (L == 64 && !GA && !QUAD && !BUF && !Red::kEid), "scalar batches: 64-lane sum/mean tasks");
   using GR = Grp<L>;
   const int lane = lane_id();
   const int gl = lane & (L - 1);
@@ -1208,8 +1237,13 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
   if constexpr (GA) {
     __shared__ float ga_lds[kWavesPerBlock][64 * 4];
     win.init(p, e_begin, e_end, gl, ga_lds[threadIdx.x >> 6], tile);
-  } else {
+  } else if constexpr (!SM) {
     win.init(p, e_begin, e_end, gl);
+  }
+  [[maybe_unused]] int c_nxt[U];
+  if constexpr (SM) {
+    xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
+    if (e_begin < e_end) scalar_batch<U>(p.col, p.n_edges, e_begin, c_nxt);
   }
   int rbase = r_first;
   int rp = (rbase + gl <= p.n_rows) ? p.rowptr[rbase + gl] : 0;
@@ -1254,6 +1288,30 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
   };
 
   for (int64_t e = e_begin; e < e_end;) {
+    if constexpr (SM) {
+      // batches start at e_begin + k*U: every batch but the task's last is full
+      const int64_t rem = e_end - e;
+      const int n = rem < U ? (int)rem : U;
+      [[maybe_unused]] float wb[U];
+      if constexpr (Red::kW) scalar_batch<U>(p.w, p.n_edges, e, wb);
+      Frag<VEC> v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = load_frag_buf<VEC>(xr, foff, (uint32_t)c_nxt[u] * (uint32_t)ldxb);
+      // the columns are dead once the gathers are issued: the next batch's
+      // land in the same SGPRs while this batch's rows are in flight
+      if (e + U < e_end) scalar_batch<U>(p.col, p.n_edges, e + U, c_nxt);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (u < n) {
+          advance(e + u);
+          float wt = 1.f;
+          if constexpr (Red::kW) wt = wb[u];
+          red.consume(v[u], wt, 0, 0.f);
+        }
+      }
+      e += n;
+      continue;
+    }
     win.ensure(p, e, gl);
     const int off = (int)(e - win.base);
     int64_t rem = e_end - e;
@@ -1473,6 +1531,14 @@ static int launch_l(const AggArgs& a, int stages, hipStream_t s) {
             goto fixup;
           }
         }
+        if constexpr (L == 64 && !Red::kEid) {
+          if (a.smem) {
+            hipLaunchKernelGGL((k_agg_flat<Red, VEC, U, 64, false, false, false, true>), grid, dim3(kBlock), 0, s,
+                               a);
+            MP_CHECK_LAUNCH();
+            goto fixup;
+          }
+        }
         hipLaunchKernelGGL((k_agg_flat<Red, VEC, U, L, false>), grid, dim3(kBlock), 0, s, a);
       }
     } else {
@@ -1670,6 +1736,12 @@ int mp_aggregate_f32(const mp_csr* g, const float* w, const float* x, int64_t ld
   if (!is_arg && (int64_t)g->n_cols * ldx * 4 >= g_flat_vec1_min.load(std::memory_order_relaxed)) fvec = 1;
   // VEC=1 sum/mean over 64-feature tiles: gather four slots per dwordx4 (k_agg_flat QUAD)
   a.quad = MP_QUAD && fvec == 1 && F % 64 == 0 && ldx % 4 == 0 && (uintptr_t)x % 16 == 0;
+  // sum/mean: slot columns and weights through scalar loads (k_agg_flat SM)
+  {
+    const int64_t xbytes = (int64_t)g->n_cols * ldx * 4;  // 32-bit buffer offsets (soffset + lane offset)
+    a.smem = MP_FLAT_SMEM && !is_arg && a.col != nullptr && !a.quad && g->n_cols > 0 && xbytes <= 0xFFFFFFF0LL;
+    if (a.smem) a.x_bytes = (uint32_t)xbytes;
+  }
   if (MP_WIDE_FLAT && F >= 256 && F % fvec == 0 && sh.vec >= fvec) {
     sh.vec = fvec;  // narrow feature tiles, slot batches across rows
     sh.lanes = MP_FLAT_LANES;

@@ -16,6 +16,8 @@ import os
 import shutil
 import sys
 
+N_CU = 256      # MI355X compute units (one TCP each)
+N_XCD = 8
 KERNEL = None   # the dominant k_agg_flat / k_agg_main instance, from the kernel-trace stats
 
 
@@ -51,6 +53,21 @@ def main():
         if cv:
             ratio = cv * 1024 / 2172780552.0   # expected_read_bytes printed by pmc_calibrate.py
     write_b = write * 1024
+    # where the kernel waits: L1 (TCP) input stalled on misses pending from L2
+    stall = {}
+    sp = os.path.join(src, "pmc_stall", "pmc_counter_collection.csv")
+    if os.path.exists(sp):
+        for c in ("GRBM_GUI_ACTIVE", "TCP_PENDING_STALL_CYCLES_sum", "TCP_TCC_READ_REQ_sum", "TA_BUSY_avr",
+                  "SQ_WAIT_ANY", "SQ_WAVE_CYCLES"):
+            stall[c], _ = per_launch(sp, c)
+        # GRBM_GUI_ACTIVE is summed over the 8 XCDs: per-XCD active cycles = kernel clocks
+        cyc = stall["GRBM_GUI_ACTIVE"] / N_XCD if stall.get("GRBM_GUI_ACTIVE") else None
+        stall["kernel_cycles"] = cyc
+        if cyc:
+            stall["tcp_pending_stall_frac"] = stall["TCP_PENDING_STALL_CYCLES_sum"] / (N_CU * cyc)
+            stall["ta_busy_frac"] = stall["TA_BUSY_avr"] / cyc
+        if stall.get("SQ_WAVE_CYCLES"):
+            stall["wave_waiting_frac"] = stall["SQ_WAIT_ANY"] / stall["SQ_WAVE_CYCLES"]
     out = {
         "workload": "rmat21_gcn_f256",
         "kernel": KERNEL,
@@ -64,6 +81,7 @@ def main():
         "hbm_bytes_per_launch": read_b + write_b,
         "l2_hit_rate": hit / (hit + miss) if hit is not None and miss else None,
         "kernel_trace_avg_ms": avg_ns / 1e6 if avg_ns else None,
+        "stall": stall or None,
         "note": "FETCH_SIZE counts L2->fabric reads (Infinity-Cache hits included): an upper bound "
                 "on HBM reads; doubled per the gfx950 correction (calibrated for this kernel's own "
                 "load width in profiles/r01_pmc_calibration.json)",

@@ -18,6 +18,7 @@ B="bench.py --steps 20 --warmup 5 --no-cpu-baseline ${BENCH_ARGS:-}"
 run kt 600 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- python3 $B
 run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_agg_(main|flat)" -d $OUT/pmc_fetch -o pmc --output-format csv -- python3 $B
 run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_agg_(main|flat)" -d $OUT/pmc_write -o pmc --output-format csv -- python3 $B
+run pmc_stall 600 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY TCP_PENDING_STALL_CYCLES_sum TCP_TCC_READ_REQ_sum TA_BUSY_avr --kernel-include-regex "k_agg_(main|flat)" -d $OUT/pmc_stall -o pmc --output-format csv -- python3 $B
 run pmc_l2 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "k_agg_(main|flat)" -d $OUT/pmc_l2 -o pmc --output-format csv -- python3 $B
 
 run pmc_calib 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_agg_(main|flat)" -d $OUT/pmc_calib -o pmc --output-format csv -- python3 tools/pmc_calibrate.py
