@@ -98,8 +98,13 @@ int mp_abi_version(void);
  * keys return -1.
  *   MP_TUNE_FLAT_VEC1_MIN_BYTES: sum/mean of rows with >= 256 features over a
  *     gathered x of at least this many bytes run the 64-feature-tile flat
- *     kernel (VEC=1); smaller x keeps 128-feature tiles (default 1 GiB). */
+ *     kernel (VEC=1); smaller x keeps 128-feature tiles (default 1 GiB).
+ *   MP_TUNE_FLAT_SMEM: 1 (default) = the flat sum/mean kernel reads slot
+ *     columns / weights through scalar-cache batches and gathers with 32-bit
+ *     buffer offsets whenever the gathered x spans < 4 GiB; 0 = the per-lane
+ *     slot window (same results bit for bit). */
 #define MP_TUNE_FLAT_VEC1_MIN_BYTES 1
+#define MP_TUNE_FLAT_SMEM 2
 int64_t mp_tune(int32_t key, int64_t value);
 
 /* ---- CSR build (replaces the sort/bucketing torch_scatter never did: upstream

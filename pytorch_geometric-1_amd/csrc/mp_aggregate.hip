@@ -1653,6 +1653,8 @@ static int64_t slab_ld_for(int F) { return ceil_div(F, 256) * 256; }
 
 // mp_tune(MP_TUNE_FLAT_VEC1_MIN_BYTES)
 static std::atomic<int64_t> g_flat_vec1_min{MP_FLAT_VEC1_MIN_BYTES};
+// mp_tune(MP_TUNE_FLAT_SMEM)
+static std::atomic<int64_t> g_flat_smem{MP_FLAT_SMEM};
 
 static int check_graph(const mp_csr* g, const char* who) {
   MP_CHECK_ARG(g != nullptr, "%s: null graph", who);
@@ -1688,6 +1690,8 @@ int64_t mp_tune(int32_t key, int64_t value) {
   switch (key) {
     case MP_TUNE_FLAT_VEC1_MIN_BYTES:
       return value < 0 ? g_flat_vec1_min.load() : g_flat_vec1_min.exchange(value);
+    case MP_TUNE_FLAT_SMEM:
+      return value < 0 ? g_flat_smem.load() : g_flat_smem.exchange(value ? 1 : 0);
   }
   return -1;
 }
@@ -1739,7 +1743,7 @@ int mp_aggregate_f32(const mp_csr* g, const float* w, const float* x, int64_t ld
   // sum/mean: slot columns and weights through scalar loads (k_agg_flat SM)
   {
     const int64_t xbytes = (int64_t)g->n_cols * ldx * 4;  // 32-bit buffer offsets (soffset + lane offset)
-    a.smem = MP_FLAT_SMEM && !is_arg && a.col != nullptr && !a.quad && g->n_cols > 0 && xbytes <= 0xFFFFFFF0LL;
+    a.smem = g_flat_smem.load(std::memory_order_relaxed) && !is_arg && a.col != nullptr && !a.quad && g->n_cols > 0 && xbytes <= 0xFFFFFFF0LL;
     if (a.smem) a.x_bytes = (uint32_t)xbytes;
   }
   if (MP_WIDE_FLAT && F >= 256 && F % fvec == 0 && sh.vec >= fvec) {

@@ -22,6 +22,7 @@ MP_STAGE_FIXUP = 2
 MP_STAGE_STATS = 4
 MP_STAGE_ALL = 7
 MP_TUNE_FLAT_VEC1_MIN_BYTES = 1
+MP_TUNE_FLAT_SMEM = 2
 
 c_p = ctypes.c_void_p
 i64 = ctypes.c_int64

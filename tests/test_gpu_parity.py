@@ -177,6 +177,72 @@ def test_fused_sum_mean_64_feature_tiles(F, chunk):
     assert torch.equal(got["sum"][whole], want[whole])
 
 
+@pytest.mark.parametrize("F,N,E", [(256, 700, 9000), (300, 700, 9000), (512, 300, 4000), (256, 5, 7), (256, 40, 17)])
+@pytest.mark.parametrize("vec1", [False, True])
+def test_flat_scalar_slot_batches_match_slot_window(F, N, E, vec1):
+    """The flat sum/mean kernel's scalar-cache slot batches (MP_TUNE_FLAT_SMEM,
+    default on) against the per-lane slot window: bitwise equal, including
+    graphs with fewer slots than one batch (the clamped tail path)."""
+    _, ops, _, Graph, pl = _mods()
+    from mi355_mp import _lib
+    lib = _lib.load()
+    ei = pl(N, E, seed=F + E)
+    g = torch.Generator().manual_seed(F + N)
+    x = torch.randn(N, F, generator=g)
+    w = torch.rand(E, generator=g)
+    graph = Graph(ei.to(DEV), N, N, chunk=16)
+    eid = ei.to(DEV)
+    prev_v = lib.mp_tune(_lib.MP_TUNE_FLAT_VEC1_MIN_BYTES, 0 if vec1 else -1)
+    got = {}
+    try:
+        for sm in (1, 0):
+            prev_s = lib.mp_tune(_lib.MP_TUNE_FLAT_SMEM, sm)
+            try:
+                got[sm] = {(r, wt): ops.fused_propagate(graph, x.to(DEV), eid, w.to(DEV) if wt else None, r).cpu()
+                           for r in ("sum", "mean") for wt in (False, True)}
+            finally:
+                lib.mp_tune(_lib.MP_TUNE_FLAT_SMEM, prev_s)
+    finally:
+        if vec1:
+            lib.mp_tune(_lib.MP_TUNE_FLAT_VEC1_MIN_BYTES, prev_v)
+    assert lib.mp_tune(_lib.MP_TUNE_FLAT_SMEM, -1) == 1
+    for k in got[1]:
+        assert torch.equal(got[1][k], got[0][k]), k
+    want = S.gather_sum(x, ei[0], ei[1], w, N)
+    _bound_ok(got[1][("sum", True)], want, S.gather_sum(x.abs(), ei[0], ei[1], w.abs(), N))
+
+
+def test_gathered_x_over_4gib():
+    """A gathered x spanning more than 4 GiB (beyond 32-bit buffer offsets):
+    the flat kernel takes 64-bit row addresses (no scalar slot batches) with
+    64-feature tiles.  Sources sit all over the 4.3 GB allocation, including
+    its last rows; only the referenced rows are initialised and checked."""
+    _, ops, _, Graph, _ = _mods()
+    F = 256
+    Ns = (1 << 22) + 1024                      # 4.3 GB of fp32 rows
+    Nd, E = 600, 12000
+    g = torch.Generator().manual_seed(4)
+    uniq = torch.unique(torch.cat([torch.randint(Ns, (3000,), generator=g), torch.arange(Ns - 8, Ns)]))
+    pick = torch.randint(uniq.numel(), (E,), generator=g)
+    src = uniq[pick]
+    dst = torch.randint(Nd, (E,), generator=g)
+    ei = torch.stack([src, dst])
+    xs = torch.randn(uniq.numel(), F, generator=g)
+    w = torch.rand(E, generator=g)
+    x = torch.empty(Ns, F, device=DEV)
+    x[uniq.to(DEV)] = xs.to(DEV)
+    assert x.numel() * 4 > (1 << 32)
+    graph = Graph(ei.to(DEV), Nd, Ns)
+    out = ops.fused_propagate(graph, x, ei.to(DEV), w.to(DEV), "sum").cpu()
+    del x
+    torch.cuda.empty_cache()
+    want = S.gather_sum(xs, pick, dst, w, Nd)
+    _bound_ok(out, want, S.gather_sum(xs.abs(), pick, dst, w.abs(), Nd))
+    split = set(_split_rows(graph.dst))
+    whole = torch.tensor([r for r in range(Nd) if r not in split], dtype=torch.long)
+    assert torch.equal(out[whole], want[whole])
+
+
 @pytest.mark.parametrize("F", [1, 5, 64, 256, 602])
 @pytest.mark.parametrize("reduce", ["max", "min"])
 def test_fused_max_min_bit_exact_with_ties(F, reduce):
