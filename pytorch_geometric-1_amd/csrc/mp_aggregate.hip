@@ -103,6 +103,9 @@ __device__ __forceinline__ float gat_exp(float v) {
 #ifndef MP_FORCE_VEC
 #define MP_FORCE_VEC 0     // 1/2/4: force the lane width (feature tiles of 64*VEC run in turn)
 #endif
+#ifndef MP_COLD_AUX
+#define MP_COLD_AUX 2      // cache-policy bits of a flagged (cold) row's load (2 = nt)
+#endif
 #ifndef MP_COLD_FLAG
 #define MP_COLD_FLAG 0     // col < 0 marks a cold source row: ~col is the row, loaded non-temporal
 #endif
@@ -1296,7 +1299,15 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
       if constexpr (Red::kW) scalar_batch<U>(p.w, p.n_edges, e, wb);
       Frag<VEC> v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = load_frag_buf<VEC>(xr, foff, (uint32_t)c_nxt[u] * (uint32_t)ldxb);
+      for (int u = 0; u < U; ++u) {
+        if constexpr (MP_COLD_FLAG) {  // experiment: flagged (cold) rows with a cache-policy hint
+          if (c_nxt[u] < 0) {
+            v[u] = load_frag_buf<VEC, MP_COLD_AUX>(xr, foff, (uint32_t)(c_nxt[u] & 0x7fffffff) * (uint32_t)ldxb);
+            continue;
+          }
+        }
+        v[u] = load_frag_buf<VEC>(xr, foff, (uint32_t)c_nxt[u] * (uint32_t)ldxb);
+      }
       // the columns are dead once the gathers are issued: the next batch's
       // land in the same SGPRs while this batch's rows are in flight
       if (e + U < e_end) scalar_batch<U>(p.col, p.n_edges, e + U, c_nxt);

@@ -138,17 +138,17 @@ __device__ __forceinline__ Frag<VEC> load_frag_nt(const float* p) {
 
 // Fragment load through a buffer resource (32-bit byte offset, range-checked;
 // soff: a wave-uniform byte offset added in the soffset field).
-template <int VEC>
+template <int VEC, int AUX = 0>  // AUX: cache-policy bits (gfx950: 1 = sc0, 2 = nt, 16 = sc1)
 __device__ __forceinline__ Frag<VEC> load_frag_buf(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t soff = 0) {
   Frag<VEC> f;
   if constexpr (VEC == 4) {
-    f32x4 t = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, soff, 0));
+    f32x4 t = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, soff, AUX));
     f.v[0] = t.x; f.v[1] = t.y; f.v[2] = t.z; f.v[3] = t.w;
   } else if constexpr (VEC == 2) {
-    f32x2 t = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(r, off, soff, 0));
+    f32x2 t = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(r, off, soff, AUX));
     f.v[0] = t.x; f.v[1] = t.y;
   } else {
-    f.v[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, soff, 0));
+    f.v[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, soff, AUX));
   }
   return f;
 }

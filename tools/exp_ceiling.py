@@ -39,8 +39,16 @@ def main():
         is_hot = torch.zeros(N, dtype=torch.bool, device=dev)
         is_hot[order[:K]] = True
         hot["hot%d_to_one" % K] = torch.where(is_hot[csr.col.long()], order[0].to(torch.int32), csr.col)
+    # cold rows flagged in the column's sign bit (variant libraries built with
+    # -DMP_COLD_FLAG=1 load them with the MP_COLD_AUX cache-policy bits)
+    cold = {}
+    for t in [int(v) for v in os.environ.get("EXP_COLD", "").split(",") if v]:
+        is_cold = (outdeg <= t)[csr.col.long()]
+        cold["cold_deg%d" % t] = torch.where(is_cold, csr.col.long() - (1 << 31), csr.col.long()).to(torch.int32)
+        print("cold_deg%d: %.1f%% of slots" % (t, 100.0 * float(is_cold.float().mean())))
     cols = {
         "real": csr.col,
+        **cold,
         **hot,
         "l2_4MB": (csr.col % 4096).to(torch.int32),
         "mall_128MB": (csr.col % 131072).to(torch.int32),
