@@ -1474,6 +1474,10 @@ struct Shape {
 #define MP_WIDE_FLAT 1     // rows of >= 256 features, sum/mean/max/min: VEC=2, 64-lane tasks, k_agg_flat
 #endif                     // (A/B vs VEC=4 32-lane groups: -1% sum, -10% max on RMAT21; bit-identical)
 
+#ifndef MP_FLAT_MIN_F
+#define MP_FLAT_MIN_F 256  // narrowest rows that take the flat kernel
+#endif
+
 #ifndef MP_WIDE_LANES
 #define MP_WIDE_LANES 32   // lanes per task for rows of >= 256 features (A/B: 32 beats 64 by ~9%)
 #endif
@@ -1757,7 +1761,7 @@ int mp_aggregate_f32(const mp_csr* g, const float* w, const float* x, int64_t ld
     a.smem = g_flat_smem.load(std::memory_order_relaxed) && !is_arg && a.col != nullptr && !a.quad && g->n_cols > 0 && xbytes <= 0xFFFFFFF0LL;
     if (a.smem) a.x_bytes = (uint32_t)xbytes;
   }
-  if (MP_WIDE_FLAT && F >= 256 && F % fvec == 0 && sh.vec >= fvec) {
+  if (MP_WIDE_FLAT && F >= MP_FLAT_MIN_F && F % fvec == 0 && sh.vec >= fvec) {
     sh.vec = fvec;  // narrow feature tiles, slot batches across rows
     sh.lanes = MP_FLAT_LANES;
     a.flat = 1;
