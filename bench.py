@@ -35,9 +35,13 @@ F_DIM = 256
 SCALE = 21
 SAMPLES = 30_000_000
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md chip table)
-BYTES_PER_EDGE = 4 * F_DIM + 4 + 4   # x_j row + col + norm   
+# SURVEY 8(d) / BASELINE.md section 2 algorithmic bytes: every gathered x_j row
+# counted at full size, no cache-reuse credit.  Reported, but its ratio to the
+# peak is NOT a roofline fraction (hub rows are re-served from L2 / Infinity
+# Cache, so it can exceed 1).
+BYTES_PER_EDGE = 4 * F_DIM + 4 + 4   # x_j row + col + norm
 BYTES_PER_NODE = 4 * F_DIM + 4       # out row + rowptr
-PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
 
 
 def parse():
@@ -79,13 +83,38 @@ def barrier(world):
         dist.barrier()
 
 
+def cpu_info():
+    """(CPU model, threads available to this process).  The thread count is the
+    affinity mask, capped by a cgroup CPU quota when one is set: on the GPU box
+    os.cpu_count() reports the whole machine while the job gets a share of it,
+    and more threads than that share would only oversubscribe it."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = max(1, min(n, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return model, n, os.cpu_count() or 1
+
+
 def cpu_baseline(ei_loops, norm, x, sample_edges):
     """The reference algorithm on the host (oracle, kind 'port'): index_select
     -> norm * x_j -> scatter_add_ (torch_scatter scatter_sum), timed on a
     bounded sample of the same edges in their original order, in 4M-edge
     chunks (the materialised x_j of all 62M edges is 64 GB)."""
     from oracle import pyg_ref  # noqa: F401  (checker/baseline only)
-    threads = min(16, os.cpu_count() or 1)
+    model, threads, machine = cpu_info()
     torch.set_num_threads(threads)
     E = min(sample_edges, ei_loops.shape[1])
     ei = ei_loops[:, :E].cpu()
@@ -103,8 +132,10 @@ def cpu_baseline(ei_loops, norm, x, sample_edges):
     dt = time.perf_counter() - t0
     del out, xc
     return {"value": E / dt, "unit": "edges/s", "cores": threads, "kind": "port",
+            "cpu_model": model, "machine_cpus": machine,
             "sample": "first %d of the %d edges (original order), F=%d, torch CPU index_select+mul+"
-                      "scatter_add_ in 4M-edge chunks, %.1f s" % (E, ei_loops.shape[1], N and F_DIM, dt)}
+                      "scatter_add_ in 4M-edge chunks, %d threads (the CPUs this job may use; the machine "
+                      "has %d), %.1f s" % (E, ei_loops.shape[1], N and F_DIM, threads, machine, dt)}
 
 
 def main():
@@ -247,15 +278,18 @@ def main():
         main_ms = timed(_lib.MP_STAGE_MAIN)
         fix_ms = timed(_lib.MP_STAGE_FIXUP)
         timing_src = "HIP events over back-to-back launches on the rank's local graph (after the timed region)"
-    # the flat kernel's lane width: VEC=1 (64-feature tiles) when the gathered x
-    # is >= 1 GiB, else VEC=2 (mp_aggregate.hip, MP_FLAT_VEC1_MIN_BYTES)
-    vec = 1 if x_src.shape[0] * F_DIM * 4 >= (1 << 30) else 2
-    # scalar-load slot batches + soffset gathers while x spans < 4 GiB (MP_FLAT_SMEM)
-    sm = ",SM" if 0 < x_src.shape[0] * F_DIM * 4 <= 0xFFFFFFF0 else ""
+    # the kernel the library dispatches for exactly these arguments (no heuristic copy)
+    kernel = _lib.kernel_name(st_main, w_csr.data_ptr(), x_src.data_ptr(), x_src.stride(0), F_DIM, "sum",
+                              bias.data_ptr(), out_buf.data_ptr(), out_buf.stride(0), dev)
     main_avg = sum(main_ms) / len(main_ms)
     fix_avg = sum(fix_ms) / len(fix_ms)
     alg_bytes = E_local * BYTES_PER_EDGE + n_rows * BYTES_PER_NODE
-    achieved = alg_bytes / (main_avg * 1e-3) / 1e9
+    # compulsory bytes: every input read once and the output written once
+    # (x, col, norm, rowptr, out) -- the least any implementation must move,
+    # so achieved / peak <= 1 is a true HBM-roofline fraction
+    n_src_rows = x_src.shape[0]
+    comp_bytes = n_src_rows * F_DIM * 4 + E_local * 8 + (n_rows + 1) * 4 + n_rows * F_DIM * 4
+    achieved = comp_bytes / (main_avg * 1e-3) / 1e9
 
     # GEMM (reported separately, the only MFMA work)
     W = torch.randn(F_DIM, F_DIM, device=dev) * 0.06
@@ -270,13 +304,21 @@ def main():
     torch.cuda.synchronize()
     gemm_ms = e0.elapsed_time(e1) / 10
 
-    traffic = None
-    if os.path.exists(PMC_FILE):
+    # counter traffic (FETCH_SIZE + WRITE_SIZE, corrected) of THIS build's
+    # dispatched kernel, from the committed profile summary -- used only when the
+    # summary names the same kernel and the same native source hash
+    traffic, traffic_src = None, "no profile for this build"
+    src_hash = _lib.source_hash()
+    if os.path.exists(PMC_FILE) and world == 1:
         try:
             with open(PMC_FILE) as f:
                 pmc = json.load(f)
-            if pmc.get("workload") == "rmat21_gcn_f256" and world == 1:
+            if (pmc.get("workload") == "rmat21_gcn_f256" and pmc.get("kernel") == kernel
+                    and pmc.get("source_hash") == src_hash):
                 traffic = pmc.get("hbm_bytes_per_launch")
+                traffic_src = os.path.relpath(PMC_FILE, ROOT)
+            else:
+                traffic_src = "%s is for another build (kernel/source hash differ)" % os.path.relpath(PMC_FILE, ROOT)
         except (OSError, ValueError):
             traffic = None
 
@@ -305,8 +347,14 @@ def main():
                        else "single GPU", "chunk": csr.chunk},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_agg_flat<SumRed<%d,true,false>,VEC=%d,U=16,L=64%s>" % (vec, vec, sm),
+                         "traffic_frac": (traffic / (main_avg * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
+                         "traffic_source": traffic_src,
+                         "bytes": "achieved = compulsory bytes (x read once, out written once, col + norm + "
+                                  "rowptr) / avg launch time",
+                         "compulsory_bytes_per_launch": comp_bytes,
                          "algorithmic_bytes_per_launch": alg_bytes,
+                         "algorithmic_GBps_no_cache_credit": alg_bytes / (main_avg * 1e-3) / 1e9,
+                         "kernel": kernel, "source_hash": src_hash,
                          "avg_launch_ms": main_avg, "median_launch_ms": main_ms[len(main_ms) // 2],
                          "fixup_avg_ms": fix_avg, "timing": timing_src},
             "cpu_baseline": cpu,

@@ -73,7 +73,7 @@ extern "C" {
  *   split_waves[n_split]  for each row whose slots span several tasks, the
  *                         last task touching it (fix-up list)
  *   n_cols                number of rows of the gathered tensor (x, or the
- *                         messages when col == eid)
+ *                         messages when col == eid); required (> 0) with col
  */
 typedef struct mp_csr {
   const int32_t* rowptr;
@@ -87,24 +87,35 @@ typedef struct mp_csr {
   int32_t chunk;
   int32_t n_waves;
   int32_t n_split;
-  int32_t n_cols;   /* rows of the gathered x (bounds the 32-bit buffer offsets) */
+  int32_t n_cols;   /* rows of the gathered x; must be > 0 whenever col != NULL (MP_ERR_ARG
+                       otherwise).  It bounds the 32-bit buffer offsets of the gather. */
 } mp_csr;
 
 const char* mp_last_error(void);
 int mp_abi_version(void);
 
-/* Process-wide kernel-shape tuning (tests and A/B runs).  Sets `key` to
- * `value` and returns the previous value; value < 0 only queries.  Unknown
- * keys return -1.
- *   MP_TUNE_FLAT_VEC1_MIN_BYTES: sum/mean of rows with >= 256 features over a
- *     gathered x of at least this many bytes run the 64-feature-tile flat
- *     kernel (VEC=1); smaller x keeps 128-feature tiles (default 1 GiB).
+/* Process-wide dispatch table (tests and in-process A/B runs).  Sets `key`
+ * to `value` and returns the previous value; value < 0 only queries.
+ * Unknown keys return -1.  Every setting gives bitwise-identical results;
+ * only the kernel shape changes.  "Flat kernel" = k_agg_flat, the
+ * sum/mean/max/min kernel whose tasks stream their slots across row ends.
+ *   MP_TUNE_FLAT_VEC1_MIN_BYTES: flat sum/mean over a gathered x of at least
+ *     this many bytes use 64-feature tiles (VEC=1); smaller x keeps
+ *     128-feature tiles (VEC=2).  Default 1 GiB.
  *   MP_TUNE_FLAT_SMEM: 1 (default) = the flat sum/mean kernel reads slot
  *     columns / weights through scalar-cache batches and gathers with 32-bit
  *     buffer offsets whenever the gathered x spans < 4 GiB; 0 = the per-lane
- *     slot window (same results bit for bit). */
+ *     slot window.
+ *   MP_TUNE_FLAT_MIN_F: narrowest sum/mean row (features) that takes the
+ *     flat kernel (default 64); narrower rows use lane groups / lane tasks.
+ *   MP_TUNE_FLAT_MIN_F_ARG: the same for max/min (default 64).
+ *   MP_TUNE_FLAT_NARROW_VEC1: 1 = flat rows of fewer than 128 features use
+ *     64-feature tiles (VEC=1) instead of 128-feature tiles (default 0). */
 #define MP_TUNE_FLAT_VEC1_MIN_BYTES 1
 #define MP_TUNE_FLAT_SMEM 2
+#define MP_TUNE_FLAT_MIN_F 3
+#define MP_TUNE_FLAT_MIN_F_ARG 4
+#define MP_TUNE_FLAT_NARROW_VEC1 5
 int64_t mp_tune(int32_t key, int64_t value);
 
 /* ---- CSR build (replaces the sort/bucketing torch_scatter never did: upstream
@@ -158,6 +169,15 @@ int mp_aggregate_f32(const mp_csr* g, const float* w, const float* x,
                      const float* bias, float* out, int64_t ldo,
                      int64_t* arg_out, void* slab, size_t slab_bytes,
                      int32_t stages, void* stream);
+
+/* Name (demangled) of the main kernel mp_aggregate_f32 would launch for these
+ * arguments (same shape selection, nothing launched), written to buf.  Lets a
+ * profile summary be matched to the dispatched kernel (bench.py).  Needs a
+ * HIP device for the name lookup; MP_ERR_ARG when none is available. */
+int mp_aggregate_kernel_name(const mp_csr* g, const float* w, const float* x,
+                             int64_t ldx, int32_t F, int32_t reduce,
+                             const float* bias, const float* out, int64_t ldo,
+                             char* buf, size_t buf_len, void* stream);
 
 /* ---- GATConv fused attention aggregation (call stack 3.2) ---
  * a_dst[n,h] = <xw[n,h,:], att[h,0:C]>,  a_src[n,h] = <xw[n,h,:], att[h,C:2C]>
@@ -267,6 +287,33 @@ int mp_gat_alpha_f32(const int64_t* src_idx, const int64_t* dst_idx,
                      int64_t n_edges, int32_t H, const float* a_src,
                      const float* a_dst, float slope, const float* row_stats,
                      float* alpha, void* stream);
+
+/* ---- self-loop rewrites (PyG 1.4.3 utils.loop [U4]) -----
+ * Output edge order is upstream's: the kept edges in original order, then the
+ * loop edges (n, n) for n = 0..N-1.
+ *   MP_LOOPS_REMOVE         remove_self_loops: the non-loop edges
+ *   MP_LOOPS_ADD            add_self_loops: every edge, then the N loops
+ *   MP_LOOPS_ADD_REMAINING  add_remaining_self_loops: the non-loop edges, then
+ *                           the N loops
+ * out_pos[k] = position of the input edge whose weight output edge k carries:
+ * kept edges their own position; a loop of ADD_REMAINING the position of the
+ * node's LAST pre-existing loop (upstream's sequential index_put_ keeps the
+ * last one), else -1; a loop of ADD -1.  Weights: mp_gather_fill_f32(w, out_pos,
+ * fill).  n_kept = n_edges - mp_self_loop_count(...) for REMOVE and
+ * ADD_REMAINING, n_edges for ADD; the outputs hold n_kept (+ N) entries.
+ * out_pos is also the compaction buffer (needed unless nothing is removed). */
+#define MP_LOOPS_REMOVE 0
+#define MP_LOOPS_ADD 1
+#define MP_LOOPS_ADD_REMAINING 2
+int mp_self_loop_count(const int64_t* row, const int64_t* col, int64_t n_edges,
+                       int64_t* count_dev, void* stream);
+size_t mp_self_loops_workspace(int64_t n_edges, int64_t n_nodes);
+int mp_self_loops(const int64_t* row, const int64_t* col, int64_t n_edges, int64_t n_nodes,
+                  int32_t mode, int64_t n_kept, int64_t* out_row, int64_t* out_col,
+                  int64_t* out_pos, void* ws, size_t ws_bytes, void* stream);
+/* out[k] = pos[k] >= 0 ? src[pos[k]] : fill */
+int mp_gather_fill_f32(const float* src, const int64_t* pos, int64_t n, float fill,
+                       float* out, void* stream);
 
 /* ---- helpers on the path -------------------------------------------------- */
 

@@ -26,101 +26,42 @@
 //     `norm*x_j` followed by CPU scatter_add_: rows that fit in one task are
 //     bit-identical to the oracle.
 #include <atomic>
+#include <cxxabi.h>
+#include <stdlib.h>
 #include <type_traits>
 #include <float.h>
 
 #include "mp_common.h"
 
-// Build-time tuning knobs (A/B-tested in one process by tools/ab_bench.py).
-#ifndef MP_U_VEC4
-#define MP_U_VEC4 8        // x-row loads in flight per task (VEC=4, 64-lane tasks)
-#endif
-#ifndef MP_U_VEC2
-#define MP_U_VEC2 16       // x-row loads in flight per task (VEC=2: the flat wide-row kernel)
-#endif
-#ifndef MP_U_VEC1
-#define MP_U_VEC1 16       // x-row loads in flight per task (VEC=1)
-#endif
-#ifndef MP_FLAT_VEC
-#define MP_FLAT_VEC 2      // lane width of the flat wide-row kernel, sum/mean (feature tiles of L*VEC)
-#endif
-#ifndef MP_FLAT_VEC1_MIN_BYTES
-// sum/mean over a gathered x of at least this many bytes (4x the 256 MB Infinity
-// Cache) run the flat kernel at VEC=1: 64-feature tiles, each XCD's L2 holds the hot
-// rows of one tile (A/B, bitwise equal: RMAT21 6.98 -> 6.73 ms; on the Reddit-scale
-// graph, whose x is cache-resident, VEC=1 is issue-bound: 8.31 -> 9.54 ms)
-#define MP_FLAT_VEC1_MIN_BYTES (1ll << 30)
-#endif
-#ifndef MP_FLAT_VEC_ARG
-#define MP_FLAT_VEC_ARG 2  // the same for max/min
-#endif
-#ifndef MP_QUAD
-#define MP_QUAD 0          // VEC=1 flat kernel: four slots per dwordx4 gather + 4x4 lane transpose
-                           // (off: measured +0.2..+0.5% on RMAT21, DESIGN.md §3.1 "tried and rejected")
-#endif
-#ifndef MP_FLAT_SMEM
-#define MP_FLAT_SMEM 1     // flat sum/mean kernel: slot columns/weights via s_load_dwordx16 batches
-#endif
-#ifndef MP_U_QUAD
-#define MP_U_QUAD 16       // slots in flight per task of the quad kernel (multiple of 4)
-#endif
-#ifndef MP_FLAT_LANES
-#define MP_FLAT_LANES 64   // lanes per task of the flat kernel (64 or 32)
-#endif
-#ifndef MP_U_NARROW
-#define MP_U_NARROW 12     // x-row loads in flight per task (VEC=4, tasks of < 64 lanes)
-#endif
-#ifndef MP_NT_OUT
-#define MP_NT_OUT 1        // non-temporal output-row stores (A/B: -0.4%)
-#endif
-#ifndef MP_NT_IDX
-#define MP_NT_IDX 1        // non-temporal col/weight/eid stream loads (A/B: -0.3%)
-#endif
-#ifndef MP_NT_X
-#define MP_NT_X 0          // non-temporal x-row loads (A/B: +75%: they bypass L1)
-#endif
-#ifndef MP_XCD_TILES
-#define MP_XCD_TILES 1     // feature tile = (block % 8) % tiles when tiles divide 8: each XCD's L2 holds one tile (A/B: -1.5%)
-#endif
-#ifndef MP_BUF_X
-#define MP_BUF_X 0         // x rows through one buffer resource (32-bit offsets) when x < 4 GB
-#endif
-#ifndef MP_GAT_NO_ASRC
-#define MP_GAT_NO_ASRC 0   // timing experiment only: skip the per-slot a_src gather (wrong results)
-#endif
-#ifndef MP_GAT_FAST_EXP
-#define MP_GAT_FAST_EXP 0  // 1: softmax exponentials via __expf (v_exp_f32)
-#endif
-
-__device__ __forceinline__ float gat_exp(float v) {
-  if constexpr (MP_GAT_FAST_EXP) return __expf(v);
-  else return expf(v);
-}
-
-#ifndef MP_GAT_LANES
-#define MP_GAT_LANES 64    // lanes per GAT task for H*C >= 256
-#endif
-#ifndef MP_FORCE_VEC
-#define MP_FORCE_VEC 0     // 1/2/4: force the lane width (feature tiles of 64*VEC run in turn)
-#endif
-#ifndef MP_COLD_AUX
-#define MP_COLD_AUX 2      // cache-policy bits of a flagged (cold) row's load (2 = nt)
-#endif
-#ifndef MP_COLD_FLAG
-#define MP_COLD_FLAG 0     // col < 0 marks a cold source row: ~col is the row, loaded non-temporal
-#endif
+// Kernel-shape constants.  Every value below was chosen by an in-process A/B
+// with bitwise-equal outputs; dispatch-level choices that
+// tests and A/B runs switch at run time go through mp_tune (one table, below).
+namespace mp {
+constexpr int kU_Vec4 = 8;      // x-row loads in flight per task (VEC=4, 64-lane tasks: GAT)
+constexpr int kU_Vec2 = 16;     // x-row loads in flight per task (VEC=2: the flat kernel, 128-feature tiles)
+constexpr int kU_Vec1 = 16;     // x-row loads in flight per task (VEC=1)
+constexpr int kU_Narrow = 12;   // x-row loads in flight per task (VEC=4, tasks of < 64 lanes)
+constexpr int kWideLanes = 32;  // lanes per task of k_agg_main for rows of >= 256 features (32 beats 64 by ~9%)
+constexpr int kGatLanes = 64;   // lanes per GAT task for H*C >= 256
+constexpr bool kNtOut = true;   // non-temporal output-row stores (A/B: -0.4%)
+constexpr bool kNtIdx = true;   // non-temporal col/weight/eid stream loads (A/B: -0.3%)
+constexpr bool kXcdTiles = true;  // feature tile = (block % 8) % tiles when tiles divide 8: each XCD's L2
+                                  // holds one tile (A/B: -1.5%)
+constexpr int kLaneMaxF = 8;    // rows of 2..this many features: one task per lane (A/B: wins at F=4,8)
+constexpr int kULane = 8;       // slots in flight per lane task
+}  // namespace mp
 
 namespace mp {
 
 template <int VEC>
 __device__ __forceinline__ void store_out(float* p, const Frag<VEC>& f) {
-  if constexpr (MP_NT_OUT) store_frag_nt<VEC>(p, f);
+  if constexpr (kNtOut) store_frag_nt<VEC>(p, f);
   else store_frag<VEC>(p, f);
 }
 
 template <class T>
 __device__ __forceinline__ T ld_stream(const T* p) {
-  if constexpr (MP_NT_IDX) return __builtin_nontemporal_load(p);
+  if constexpr (kNtIdx) return __builtin_nontemporal_load(p);
   else return *p;
 }
 
@@ -142,10 +83,9 @@ struct AggArgs {
   int32_t n_split;
   int32_t F;
   int32_t n_cols;
-  uint32_t x_bytes;  // extent of x for the buffer path (0: not used)
+  uint32_t x_bytes;  // extent of x for the scalar-batch buffer path (0: not used)
   int32_t flat;      // sum/mean/max/min: run k_agg_flat instead of k_agg_main
   int32_t fix4;      // VEC=2 main kernel: run the fix-up at VEC=4 (slabs are indexed by feature)
-  int32_t quad;      // VEC=1 flat kernel: four-slot dwordx4 gathers + lane transpose (k_agg_flat QUAD)
   int32_t smem;      // flat sum/mean kernel: slot columns/weights through scalar loads (k_agg_flat SM)
   // features
   const float* w;
@@ -411,8 +351,8 @@ struct GatRed {
     float a = as + ad;
     a = a > 0.f ? a : a * p.slope;  // F.leaky_relu
     float mn = fmaxf(m, a);
-    float sc = gat_exp(m - mn);
-    float pe = gat_exp(a - mn);
+    float sc = expf(m - mn);
+    float pe = expf(a - mn);
     s = s * sc + pe;
 #pragma unroll
     for (int k = 0; k < VEC; ++k) acc[k] = acc[k] * sc + pe * v.v[k];
@@ -923,21 +863,17 @@ struct GatAlphaWin {
 // under an exec mask; only the group-uniform consume loop is bounded by n.
 // For L = 64 the row address is a uniform base (SGPR pair) + one shared
 // 32-bit lane offset, so U rows cost U*VEC data VGPRs only.
-#ifndef MP_GAT_LDS_WIN
-#define MP_GAT_LDS_WIN 1   // GAT forward: a_src of each 64-slot window staged in LDS (see SlotWin)
-#endif
+// GAT forward: a_src of each 64-slot window staged in LDS (see SlotWin; 8.85 -> 8.66 ms, bitwise the same)
 template <class Red, int L>
-constexpr bool kGatWin = MP_GAT_LDS_WIN && Red::kGat && L == 64;
+constexpr bool kGatWin = Red::kGat && L == 64;
 
-template <class Red, int VEC, int U, int L, bool BUF>
+template <class Red, int VEC, int U, int L>
 __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p,
                                           SlotWin<Red::kW, Red::kEid, L, kGatWin<Red, L>>& win,
                                           int64_t s, int64_t t, uint32_t foff, int gl) {
   using GR = Grp<L>;
   const char* xb = reinterpret_cast<const char*>(p.x);
   const int64_t ldxb = p.ldx * 4;
-  [[maybe_unused]] __amdgpu_buffer_rsrc_t xr;
-  if constexpr (BUF) xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
   int64_t e = s;
   while (e < t) {
     win.ensure(p, e, gl);
@@ -955,19 +891,9 @@ __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p,
     for (int u = 0; u < U; ++u) {
       const int uu = u < n ? u : n - 1;
       if constexpr (Red::kHW) hw[u] = p.w[(e + uu) * p.H + red.h];
-      int c = GR::bc(win.col, off + uu);
-      if constexpr (MP_COLD_FLAG) {
-        const bool cold = c < 0;
-        c = c & 0x7fffffff;
-        const float* src = reinterpret_cast<const float*>(xb + (int64_t)c * ldxb + foff);
-        v[u] = cold ? load_frag_nt<VEC>(src) : load_frag<VEC>(src);
-      } else if constexpr (BUF) {
-        v[u] = load_frag_buf<VEC>(xr, (uint32_t)c * (uint32_t)ldxb + foff);
-      } else {
-        const float* src = reinterpret_cast<const float*>(xb + (int64_t)c * ldxb + foff);
-        v[u] = MP_NT_X ? load_frag_nt<VEC>(src) : load_frag<VEC>(src);
-      }
-      if constexpr (Red::kGat) as[u] = MP_GAT_NO_ASRC ? 0.f : win.a_src_of(p, off + uu, c, red.h);
+      const int c = GR::bc(win.col, off + uu);
+      v[u] = load_frag<VEC>(reinterpret_cast<const float*>(xb + (int64_t)c * ldxb + foff));
+      if constexpr (Red::kGat) as[u] = win.a_src_of(p, off + uu, c, red.h);
       if constexpr (Red::kGatB) pk[u] = p.pack[(int64_t)c * p.H + red.h];
     }
     if constexpr (Red::kGatB) {
@@ -992,13 +918,13 @@ __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p,
   }
 }
 
-template <class Red, int VEC, int U, int L, bool BUF>
+template <class Red, int VEC, int U, int L>
 __global__ __launch_bounds__(kBlock) void k_agg_main(AggArgs p) {
   using GR = Grp<L>;
   const int lane = lane_id();
   const int gl = lane & (L - 1);
   int bx = (int)blockIdx.x, tile = (int)blockIdx.y;
-  if constexpr (MP_XCD_TILES) {
+  if constexpr (kXcdTiles) {
     // blocks b and b+8 share an XCD (dispatch is round-robin over the 8 XCDs;
     // speed only): give every XCD one feature tile so its L2 holds only that
     // tile of the hot rows.  tiles = gridDim.y divides 8 (checked on the host).
@@ -1040,7 +966,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_main(AggArgs p) {
     const int64_t ce = GR::bc(rp, 0);  // rowptr[r_first] (== n_edges when r_first == n_rows)
     if (e_begin < ce) {
       red.begin(p, r_first - 1, false, f, act);
-      run_slots<Red, VEC, U, L, BUF>(red, p, win, e_begin, ce < e_end ? ce : e_end, foff, gl);
+      run_slots<Red, VEC, U, L>(red, p, win, e_begin, ce < e_end ? ce : e_end, foff, gl);
       if (act) red.save(slab_ref(p, 2 * (int64_t)w, f, red), Red::kStat && (f % p.C == 0));
     }
   }
@@ -1054,10 +980,10 @@ __global__ __launch_bounds__(kBlock) void k_agg_main(AggArgs p) {
     const int64_t re = GR::bc(rp, r - rbase + 1);
     red.begin(p, r, true, f, act);
     if (re <= e_end) {
-      run_slots<Red, VEC, U, L, BUF>(red, p, win, rs, re, foff, gl);
+      run_slots<Red, VEC, U, L>(red, p, win, rs, re, foff, gl);
       red.finish(p, r, re - rs, f, act);
     } else {
-      run_slots<Red, VEC, U, L, BUF>(red, p, win, rs, e_end, foff, gl);
+      run_slots<Red, VEC, U, L>(red, p, win, rs, e_end, foff, gl);
       if (act) red.save(slab_ref(p, 2 * (int64_t)w + 1, f, red), Red::kStat && (f % p.C == 0));
     }
   }
@@ -1141,21 +1067,6 @@ __global__ __launch_bounds__(kBlock) void k_agg_lane(AggArgs p) {
   }
 }
 
-// 4x4 transpose across the four 16-lane rows: on entry lane (g, i) holds
-// element j of a = (slot g, feature 4i+j); on exit element s = (slot s,
-// feature 4i+g).  Two v_permlane32_swap (rows 0,1 <-> 2,3) and two
-// v_permlane16_swap (rows 0,2 <-> 1,3).
-__device__ __forceinline__ void quad_transpose(f32x4& a) {
-  auto s02 = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.x), __float_as_uint(a.z), false, false);
-  auto s13 = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.y), __float_as_uint(a.w), false, false);
-  auto t01 = __builtin_amdgcn_permlane16_swap(s02[0], s13[0], false, false);
-  auto t23 = __builtin_amdgcn_permlane16_swap(s02[1], s13[1], false, false);
-  a.x = __uint_as_float(t01[0]);
-  a.y = __uint_as_float(t01[1]);
-  a.z = __uint_as_float(t23[0]);
-  a.w = __uint_as_float(t23[1]);
-}
-
 // ---------------------------------------------------------------------------
 // Flat variant of k_agg_main (sum/mean/max/min): a task streams its slots in
 // fixed batches of U across row boundaries and closes rows as it crosses
@@ -1168,13 +1079,6 @@ __device__ __forceinline__ void quad_transpose(f32x4& a) {
 // ---------------------------------------------------------------------------
 // GA: two-pass GAT aggregation (Red = SumRed<1, true, false>, L = 64): the slot
 // weights are the reference's alpha from GatAlphaWin instead of w.
-// QUAD (VEC = 1, L = 64, F % 64 == 0, 16-byte rows): a 64-feature tile is
-// gathered four slots per load instruction -- lane (g, i) = (lane / 16,
-// lane % 16) loads features 4i..4i+3 of slot 4q+g as one dwordx4 -- and a 4x4
-// transpose across the lane rows (quad_transpose) leaves every lane with ONE
-// feature, 4i+g, of the four slots in slot order.  From there the row walk is
-// the VEC=1 one (each lane adds its feature's products in CSR order): the same
-// arithmetic with a quarter of the gather instructions.
 // SM (L = 64, no edge ids, col != nullptr, x below 4 GiB): the column and
 // weight of every slot of a batch come straight into SGPRs through scalar
 // loads (s_load_dwordx16 via the scalar cache) -- the next batch's columns
@@ -1199,17 +1103,16 @@ __device__ __forceinline__ void scalar_batch(const T* a, int64_t n, int64_t e, T
   }
 }
 
-template <class Red, int VEC, int U, int L, bool BUF, bool GA = false, bool QUAD = false, bool SM = false>
+template <class Red, int VEC, int U, int L, bool GA = false, bool SM = false>
 __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
   static_assert(!Red::kGat && !Red::kGatB && !Red::kHW, "flat loop: sum/mean/max/min reducers");
   static_assert(!GA || (L == 64 && VEC == 1 && Red::kW), "two-pass GAT: 64-lane tasks, 64-feature tiles");
-  static_assert(!QUAD || (L == 64 && VEC == 1 && U % 4 == 0 && !GA), "quad gathers: 64-lane tasks, 64-feature tiles");
-  static_assert(!SM || (L == 64 && !GA && !QUAD && !BUF && !Red::kEid), "scalar batches: 64-lane sum/mean tasks");
+  static_assert(!SM || (L == 64 && !GA && !Red::kEid), "scalar batches: 64-lane sum/mean tasks");
   using GR = Grp<L>;
   const int lane = lane_id();
   const int gl = lane & (L - 1);
   int bx = (int)blockIdx.x, tile = (int)blockIdx.y;
-  if constexpr (MP_XCD_TILES) {  // see k_agg_main: one feature tile per XCD
+  if constexpr (kXcdTiles) {  // see k_agg_main: one feature tile per XCD
     const int T = (int)gridDim.y;
     if (8 % T == 0) {  // the host pads the grid to a multiple of 8/T blocks per tile
       const int b = (int)(blockIdx.y * gridDim.x + blockIdx.x);
@@ -1221,14 +1124,12 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
   const int wave = bx * kWavesPerBlock + (int)(threadIdx.x >> 6);
   const int w = GR::un(wave * GR::G + lane / L);
   if (w >= p.n_waves) return;
-  // QUAD: the lane owns feature 4i+g of the tile and loads features 4i..4i+3
-  const int f = QUAD ? tile * 64 + 4 * (lane & 15) + (lane >> 4) : tile * L * VEC + gl * VEC;
+  const int f = tile * L * VEC + gl * VEC;
   const bool act = f < p.F;
-  const uint32_t foff = QUAD ? (uint32_t)(tile * 64 + 4 * (lane & 15)) * 4u : (uint32_t)(act ? f : 0) * 4u;
+  const uint32_t foff = (uint32_t)(act ? f : 0) * 4u;
   const char* xb = reinterpret_cast<const char*>(p.x);
   const int64_t ldxb = p.ldx * 4;
   [[maybe_unused]] __amdgpu_buffer_rsrc_t xr;
-  if constexpr (BUF) xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
 
   const int r_first = GR::un(p.wave_row[w]);
   const int r_last = GR::un(p.wave_row[w + 1]);
@@ -1299,15 +1200,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
       if constexpr (Red::kW) scalar_batch<U>(p.w, p.n_edges, e, wb);
       Frag<VEC> v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if constexpr (MP_COLD_FLAG) {  // experiment: flagged (cold) rows with a cache-policy hint
-          if (c_nxt[u] < 0) {
-            v[u] = load_frag_buf<VEC, MP_COLD_AUX>(xr, foff, (uint32_t)(c_nxt[u] & 0x7fffffff) * (uint32_t)ldxb);
-            continue;
-          }
-        }
-        v[u] = load_frag_buf<VEC>(xr, foff, (uint32_t)c_nxt[u] * (uint32_t)ldxb);
-      }
+      for (int u = 0; u < U; ++u) v[u] = load_frag_buf<VEC>(xr, foff, (uint32_t)c_nxt[u] * (uint32_t)ldxb);
       // the columns are dead once the gathers are issued: the next batch's
       // land in the same SGPRs while this batch's rows are in flight
       if (e + U < e_end) scalar_batch<U>(p.col, p.n_edges, e + U, c_nxt);
@@ -1332,38 +1225,12 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
     n = GR::un(n);
     Frag<VEC> v[U];
     [[maybe_unused]] float al[U];
-    if constexpr (QUAD) {
-      const int g = lane >> 4;
-      f32x4 q4[U / 4];
-#pragma unroll
-      for (int q = 0; q < U / 4; ++q) {
-        int cs[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) cs[t] = readlane(win.col, off + min(4 * q + t, n - 1));
-        const int c = g == 0 ? cs[0] : (g == 1 ? cs[1] : (g == 2 ? cs[2] : cs[3]));
-        q4[q] = *reinterpret_cast<const f32x4*>(xb + (int64_t)c * ldxb + foff);
-      }
-#pragma unroll
-      for (int q = 0; q < U / 4; ++q) {
-        quad_transpose(q4[q]);
-        v[4 * q + 0].v[0] = q4[q].x;
-        v[4 * q + 1].v[0] = q4[q].y;
-        v[4 * q + 2].v[0] = q4[q].z;
-        v[4 * q + 3].v[0] = q4[q].w;
-      }
-    } else {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int uu = u < n ? u : n - 1;
       const int c = GR::bc(win.col, off + uu);
-      if constexpr (BUF) {
-        v[u] = load_frag_buf<VEC>(xr, (uint32_t)c * (uint32_t)ldxb + foff);
-      } else {
-        const float* src = reinterpret_cast<const float*>(xb + (int64_t)c * ldxb + foff);
-        v[u] = MP_NT_X ? load_frag_nt<VEC>(src) : load_frag<VEC>(src);
-      }
+      v[u] = load_frag<VEC>(reinterpret_cast<const float*>(xb + (int64_t)c * ldxb + foff));
       if constexpr (GA) al[u] = win.alpha(off + uu);  // LDS reads of the batch issued with its loads
-    }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -1470,18 +1337,6 @@ struct Shape {
   int vec, lanes;
 };
 
-#ifndef MP_WIDE_FLAT
-#define MP_WIDE_FLAT 1     // rows of >= 256 features, sum/mean/max/min: VEC=2, 64-lane tasks, k_agg_flat
-#endif                     // (A/B vs VEC=4 32-lane groups: -1% sum, -10% max on RMAT21; bit-identical)
-
-#ifndef MP_FLAT_MIN_F
-#define MP_FLAT_MIN_F 64   // narrowest rows that take the flat kernel (A/B vs 256, RMAT21 sum: -13% at F=128, -24% at F=64; bit-identical)
-#endif
-
-#ifndef MP_WIDE_LANES
-#define MP_WIDE_LANES 32   // lanes per task for rows of >= 256 features (A/B: 32 beats 64 by ~9%)
-#endif
-
 static int next_pow2(int v) {
   int r = 1;
   while (r < v) r <<= 1;
@@ -1495,15 +1350,13 @@ static Shape pick_shape(int F, int64_t ldx, const void* x, int64_t ldo, const vo
     return ((uintptr_t)ptr % (4 * v) == 0) && (ld % v == 0);
   };
   int vec = 1;
-  if (MP_FORCE_VEC && F % MP_FORCE_VEC == 0 && aligned(x, ldx, MP_FORCE_VEC) && aligned(out, ldo, MP_FORCE_VEC))
-    vec = MP_FORCE_VEC;
-  else if (F % 4 == 0 && aligned(x, ldx, 4) && aligned(out, ldo, 4)) vec = 4;
+  if (F % 4 == 0 && aligned(x, ldx, 4) && aligned(out, ldo, 4)) vec = 4;
   else if (F % 2 == 0 && F > 64 && aligned(x, ldx, 2) && aligned(out, ldo, 2)) vec = 2;
   int lanes = 64;
   if (vec == 4) {
     int need = next_pow2((F + 3) / 4);
     lanes = need < 4 ? 4 : (need > 64 ? 64 : need);
-    if (F >= 256) lanes = MP_WIDE_LANES;
+    if (F >= 256) lanes = kWideLanes;
   }
   return {vec, lanes};
 }
@@ -1522,46 +1375,45 @@ struct Rebind<ArgRed<VEC, W, M>, V> {
   using type = ArgRed<V, W, M>;
 };
 
+// Kernel query (mp_aggregate_kernel_name): while set, the main-stage launch
+// records the kernel the dispatcher chose instead of launching it.
+static thread_local bool g_query = false;
+static thread_local const void* g_query_kernel = nullptr;
+
+static int launch_main(void (*k)(AggArgs), dim3 grid, hipStream_t s, const AggArgs& a) {
+  if (g_query) {
+    g_query_kernel = reinterpret_cast<const void*>(k);
+    return MP_OK;
+  }
+  hipLaunchKernelGGL(k, grid, dim3(kBlock), 0, s, a);
+  MP_CHECK_LAUNCH();
+  return MP_OK;
+}
+
 template <class Red, int VEC, int L>
 static int launch_l(const AggArgs& a, int stages, hipStream_t s) {
-  constexpr int U = VEC == 4 ? (L == 64 ? MP_U_VEC4 : MP_U_NARROW)
-                             : (VEC == 2 ? MP_U_VEC2 : (L < MP_U_VEC1 ? L : MP_U_VEC1));  // VEC=1 groups < 16 lanes: GAT stats
+  constexpr int U = VEC == 4 ? (L == 64 ? kU_Vec4 : kU_Narrow)
+                             : (VEC == 2 ? kU_Vec2 : (L < kU_Vec1 ? L : kU_Vec1));  // VEC=1 groups < 16 lanes: GAT stats
   const int ftiles = (int)ceil_div(a.F, L * VEC);
   if (stages & MP_STAGE_MAIN) {
     int64_t nb = ceil_div(a.n_waves, kWavesPerBlock * (64 / L));
-    if (MP_XCD_TILES && 8 % ftiles == 0) nb = ceil_div(nb, 8 / ftiles) * (8 / ftiles);
+    if (kXcdTiles && 8 % ftiles == 0) nb = ceil_div(nb, 8 / ftiles) * (8 / ftiles);
     dim3 grid((unsigned)nb, (unsigned)ftiles);
-    // 32-bit buffer offsets when every gathered byte lies below 4 GiB
-    const int64_t xb = (int64_t)a.n_cols * a.ldx * 4;
-    if (MP_BUF_X && a.n_cols > 0 && xb <= (int64_t)0xFFFFFFF0) {
-      AggArgs b = a;
-      b.x_bytes = (uint32_t)xb;
-      hipLaunchKernelGGL((k_agg_main<Red, VEC, U, L, MP_BUF_X != 0>), grid, dim3(kBlock), 0, s, b);
-    } else if (a.flat) {
+    int rc = MP_OK;
+    if (a.flat) {
       if constexpr (!Red::kGat && !Red::kGatB && !Red::kHW) {
-        if constexpr (VEC == 1 && L == 64 && !Red::kEid) {
-          if (a.quad) {
-            hipLaunchKernelGGL((k_agg_flat<Red, 1, MP_U_QUAD, 64, false, false, true>), grid, dim3(kBlock), 0, s, a);
-            MP_CHECK_LAUNCH();
-            goto fixup;
-          }
-        }
         if constexpr (L == 64 && !Red::kEid) {
-          if (a.smem) {
-            hipLaunchKernelGGL((k_agg_flat<Red, VEC, U, 64, false, false, false, true>), grid, dim3(kBlock), 0, s,
-                               a);
-            MP_CHECK_LAUNCH();
-            goto fixup;
-          }
+          if (a.smem) rc = launch_main(k_agg_flat<Red, VEC, U, 64, false, true>, grid, s, a);
+          else rc = launch_main(k_agg_flat<Red, VEC, U, L>, grid, s, a);
+        } else {
+          rc = launch_main(k_agg_flat<Red, VEC, U, L>, grid, s, a);
         }
-        hipLaunchKernelGGL((k_agg_flat<Red, VEC, U, L, false>), grid, dim3(kBlock), 0, s, a);
       }
     } else {
-      hipLaunchKernelGGL((k_agg_main<Red, VEC, U, L, false>), grid, dim3(kBlock), 0, s, a);
+      rc = launch_main(k_agg_main<Red, VEC, U, L>, grid, s, a);
     }
-    MP_CHECK_LAUNCH();
+    if (rc) return rc;
   }
-fixup:
   if ((stages & MP_STAGE_FIXUP) && a.n_split > 0) {
     if constexpr (VEC != 4 && !Red::kGat && !Red::kGatB && !Red::kHW) {
       if (a.fix4) {
@@ -1578,20 +1430,13 @@ fixup:
   return MP_OK;
 }
 
-#ifndef MP_LANE_MAX_F
-#define MP_LANE_MAX_F 8    // rows of 2..this many features: one task per lane (0: off; A/B: wins at F=4,8, loses at 1,16)
-#endif
-#ifndef MP_U_LANE
-#define MP_U_LANE 8        // slots in flight per lane task
-#endif
-
 template <class Red, int VEC, int NV>
 static int launch_lane(const AggArgs& a, int stages, hipStream_t s) {
   if (stages & MP_STAGE_MAIN) {
     dim3 grid((unsigned)ceil_div(a.n_waves, kBlock));
-    constexpr int U = VEC * NV >= 16 ? (MP_U_LANE + 1) / 2 : MP_U_LANE;  // 16-float rows: keep VGPRs < 128
-    hipLaunchKernelGGL((k_agg_lane<Red, VEC, NV, U>), grid, dim3(kBlock), 0, s, a);
-    MP_CHECK_LAUNCH();
+    constexpr int U = VEC * NV >= 16 ? (kULane + 1) / 2 : kULane;  // 16-float rows: keep VGPRs < 128
+    int rc = launch_main(k_agg_lane<Red, VEC, NV, U>, grid, s, a);
+    if (rc) return rc;
   }
   if ((stages & MP_STAGE_FIXUP) && a.n_split > 0) {
     dim3 grid((unsigned)a.n_split, (unsigned)ceil_div(a.F, 64 * VEC));
@@ -1601,19 +1446,17 @@ static int launch_lane(const AggArgs& a, int stages, hipStream_t s) {
   return MP_OK;
 }
 
-// lane-task shape for F <= MP_LANE_MAX_F: VEC=4 with NV in {1,2,4} or VEC=1
+// lane-task shape for F <= kLaneMaxF: VEC=4 with NV in {1,2,4} or VEC=1
 // with NV in {4,8,16}; -1 when the row is too wide
 template <class Red, int VEC>
 static int try_lane(const AggArgs& a, int stages, hipStream_t s) {
-  if (a.F > MP_LANE_MAX_F || a.F > 16 || a.F < 2) return -1;
+  if (a.F > kLaneMaxF || a.F < 2) return -1;
   if constexpr (VEC == 4) {
     if (a.F <= 4) return launch_lane<Red, 4, 1>(a, stages, s);
-    if (a.F <= 8) return launch_lane<Red, 4, 2>(a, stages, s);
-    return launch_lane<Red, 4, 4>(a, stages, s);
+    return launch_lane<Red, 4, 2>(a, stages, s);
   } else if constexpr (VEC == 1) {
     if (a.F <= 4) return launch_lane<Red, 1, 4>(a, stages, s);
-    if (a.F <= 8) return launch_lane<Red, 1, 8>(a, stages, s);
-    return launch_lane<Red, 1, 16>(a, stages, s);
+    return launch_lane<Red, 1, 8>(a, stages, s);
   }
   return -1;
 }
@@ -1628,8 +1471,6 @@ static int launch(const AggArgs& a, int stages, hipStream_t s, int lanes = 64) {
       case 32: return launch_l<Red, 4, 32>(a, stages, s);
       default: break;
     }
-  } else {
-    if (lanes == 32) return launch_l<Red, VEC, 32>(a, stages, s);
   }
   return launch_l<Red, VEC, 64>(a, stages, s);
 }
@@ -1666,10 +1507,32 @@ static int dispatch_reduce(const AggArgs& a, int reduce, int stages, hipStream_t
 
 static int64_t slab_ld_for(int F) { return ceil_div(F, 256) * 256; }
 
-// mp_tune(MP_TUNE_FLAT_VEC1_MIN_BYTES)
-static std::atomic<int64_t> g_flat_vec1_min{MP_FLAT_VEC1_MIN_BYTES};
-// mp_tune(MP_TUNE_FLAT_SMEM)
-static std::atomic<int64_t> g_flat_smem{MP_FLAT_SMEM};
+// ---------------------------------------------------------------------------
+// mp_tune: the one table of run-time dispatch choices (include/mi355_mp.h).
+// Defaults are the A/B winners; every alternative gives
+// bitwise-identical results.
+// ---------------------------------------------------------------------------
+struct Tune {
+  std::atomic<int64_t> flat_vec1_min_bytes{1ll << 30};  // 4x the 256 MB Infinity Cache
+  std::atomic<int64_t> flat_smem{1};
+  std::atomic<int64_t> flat_min_f{64};
+  std::atomic<int64_t> flat_min_f_arg{64};
+  std::atomic<int64_t> flat_narrow_vec1{0};
+};
+static Tune g_tune;
+
+static std::atomic<int64_t>* tune_slot(int32_t key) {
+  switch (key) {
+    case MP_TUNE_FLAT_VEC1_MIN_BYTES: return &g_tune.flat_vec1_min_bytes;
+    case MP_TUNE_FLAT_SMEM: return &g_tune.flat_smem;
+    case MP_TUNE_FLAT_MIN_F: return &g_tune.flat_min_f;
+    case MP_TUNE_FLAT_MIN_F_ARG: return &g_tune.flat_min_f_arg;
+    case MP_TUNE_FLAT_NARROW_VEC1: return &g_tune.flat_narrow_vec1;
+  }
+  return nullptr;
+}
+
+static inline int64_t tuned(std::atomic<int64_t>& v) { return v.load(std::memory_order_relaxed); }
 
 static int check_graph(const mp_csr* g, const char* who) {
   MP_CHECK_ARG(g != nullptr, "%s: null graph", who);
@@ -1677,6 +1540,9 @@ static int check_graph(const mp_csr* g, const char* who) {
                "%s: graph has null arrays", who);
   MP_CHECK_ARG(g->n_edges == 0 || g->eid, "%s: graph has null eid", who);
   MP_CHECK_ARG(g->chunk >= 16 && g->chunk % 8 == 0 && g->n_waves >= 1, "%s: bad schedule", who);
+  MP_CHECK_ARG(g->col == nullptr || g->n_edges == 0 || g->n_cols > 0,
+               "%s: n_cols must be the row count of the gathered x (got %d with a column array)", who,
+               (int)g->n_cols);
   return MP_OK;
 }
 
@@ -1695,6 +1561,37 @@ static void fill_graph(AggArgs& a, const mp_csr* g) {
   a.n_cols = g->n_cols;
 }
 
+// Shape selection and launch of one mp_aggregate_f32 call (args checked).
+static int aggregate_dispatch(AggArgs& a, const mp_csr* g, int reduce, int stages, hipStream_t s) {
+  const int F = a.F;
+  const bool is_arg = reduce == MP_REDUCE_MAX || reduce == MP_REDUCE_MIN;
+  Shape sh = pick_shape(F, a.ldx, a.x, a.ldo, a.out);
+  // flat kernel lane width: 128-feature tiles (VEC=2); 64-feature tiles (VEC=1)
+  // for sum/mean over a gathered x too large for the Infinity Cache, where an
+  // XCD's L2 holding one narrow tile of the hot rows pays
+  const int64_t xbytes = (int64_t)g->n_cols * a.ldx * 4;
+  int fvec = 2;
+  if (!is_arg && xbytes >= tuned(g_tune.flat_vec1_min_bytes)) fvec = 1;
+  if (F < 128 && tuned(g_tune.flat_narrow_vec1)) fvec = 1;
+  // sum/mean: slot columns and weights through scalar loads (k_agg_flat SM),
+  // 32-bit buffer offsets (soffset + lane offset) while x spans < 4 GiB
+  a.smem = tuned(g_tune.flat_smem) && !is_arg && a.col != nullptr && g->n_cols > 0 && xbytes <= 0xFFFFFFF0LL;
+  if (a.smem) a.x_bytes = (uint32_t)xbytes;
+  const int64_t min_f = is_arg ? tuned(g_tune.flat_min_f_arg) : tuned(g_tune.flat_min_f);
+  if (F >= min_f && F % fvec == 0 && sh.vec >= fvec) {
+    sh.vec = fvec;  // narrow feature tiles, slot batches across rows
+    sh.lanes = 64;
+    a.flat = 1;
+    // the fix-up reads slabs by feature: run it 4 wide when out (and bias) allow
+    a.fix4 = F % 4 == 0 && (uintptr_t)a.out % 16 == 0 && a.ldo % 4 == 0 && (uintptr_t)a.bias % 16 == 0;
+  }
+  switch (sh.vec) {
+    case 4: return dispatch_reduce<4>(a, reduce, stages, s, sh.lanes);
+    case 2: return dispatch_reduce<2>(a, reduce, stages, s, 64);
+    default: return dispatch_reduce<1>(a, reduce, stages, s, 64);
+  }
+}
+
 }  // namespace mp
 
 using namespace mp;
@@ -1702,13 +1599,11 @@ using namespace mp;
 extern "C" {
 
 int64_t mp_tune(int32_t key, int64_t value) {
-  switch (key) {
-    case MP_TUNE_FLAT_VEC1_MIN_BYTES:
-      return value < 0 ? g_flat_vec1_min.load() : g_flat_vec1_min.exchange(value);
-    case MP_TUNE_FLAT_SMEM:
-      return value < 0 ? g_flat_smem.load() : g_flat_smem.exchange(value ? 1 : 0);
-  }
-  return -1;
+  std::atomic<int64_t>* v = tune_slot(key);
+  if (!v) return -1;
+  if (value < 0) return v->load();
+  if (key == MP_TUNE_FLAT_SMEM || key == MP_TUNE_FLAT_NARROW_VEC1) value = value ? 1 : 0;
+  return v->exchange(value);
 }
 
 size_t mp_aggregate_slab_bytes(const mp_csr* g, int32_t F, int32_t reduce) {
@@ -1749,30 +1644,41 @@ int mp_aggregate_f32(const mp_csr* g, const float* w, const float* x, int64_t ld
   size_t v = align_up(2 * (size_t)g->n_waves * (size_t)a.slab_ld * 4, 256);
   a.slab_v = (float*)slab;
   a.slab_a = is_arg ? (int32_t*)((char*)slab + v) : nullptr;
-  hipStream_t s = as_stream(stream);
-  Shape sh = pick_shape(F, ldx, x, ldo, out);
-  int fvec = is_arg ? MP_FLAT_VEC_ARG : MP_FLAT_VEC;
-  if (!is_arg && (int64_t)g->n_cols * ldx * 4 >= g_flat_vec1_min.load(std::memory_order_relaxed)) fvec = 1;
-  // VEC=1 sum/mean over 64-feature tiles: gather four slots per dwordx4 (k_agg_flat QUAD)
-  a.quad = MP_QUAD && fvec == 1 && F % 64 == 0 && ldx % 4 == 0 && (uintptr_t)x % 16 == 0;
-  // sum/mean: slot columns and weights through scalar loads (k_agg_flat SM)
-  {
-    const int64_t xbytes = (int64_t)g->n_cols * ldx * 4;  // 32-bit buffer offsets (soffset + lane offset)
-    a.smem = g_flat_smem.load(std::memory_order_relaxed) && !is_arg && a.col != nullptr && !a.quad && g->n_cols > 0 && xbytes <= 0xFFFFFFF0LL;
-    if (a.smem) a.x_bytes = (uint32_t)xbytes;
-  }
-  if (MP_WIDE_FLAT && F >= MP_FLAT_MIN_F && F % fvec == 0 && sh.vec >= fvec) {
-    sh.vec = fvec;  // narrow feature tiles, slot batches across rows
-    sh.lanes = MP_FLAT_LANES;
-    a.flat = 1;
-    // the fix-up reads slabs by feature: run it 4 wide when out (and bias) allow
-    a.fix4 = F % 4 == 0 && (uintptr_t)out % 16 == 0 && ldo % 4 == 0 && (uintptr_t)bias % 16 == 0;
-  }
-  switch (sh.vec) {
-    case 4: return dispatch_reduce<4>(a, reduce, stages, s, sh.lanes);
-    case 2: return dispatch_reduce<2>(a, reduce, stages, s, a.flat ? sh.lanes : 64);
-    default: return dispatch_reduce<1>(a, reduce, stages, s, a.flat ? sh.lanes : 64);
-  }
+  return aggregate_dispatch(a, g, reduce, stages, as_stream(stream));
+}
+
+int mp_aggregate_kernel_name(const mp_csr* g, const float* w, const float* x, int64_t ldx, int32_t F,
+                             int32_t reduce, const float* bias, const float* out, int64_t ldo, char* buf,
+                             size_t buf_len, void* stream) {
+  int rc = check_graph(g, "mp_aggregate_kernel_name");
+  if (rc) return rc;
+  MP_CHECK_ARG(F > 0 && ldx >= F && ldo >= F && buf != nullptr && buf_len > 0,
+               "mp_aggregate_kernel_name: bad arguments");
+  MP_CHECK_ARG(reduce >= MP_REDUCE_SUM && reduce <= MP_REDUCE_MIN, "mp_aggregate_kernel_name: unknown reduce %d",
+               reduce);
+  AggArgs a{};
+  fill_graph(a, g);
+  a.F = F;
+  a.w = w;
+  a.x = x;
+  a.ldx = ldx;
+  a.bias = bias;
+  a.out = const_cast<float*>(out);
+  a.ldo = ldo;
+  g_query = true;
+  g_query_kernel = nullptr;
+  rc = aggregate_dispatch(a, g, reduce, MP_STAGE_MAIN, as_stream(stream));
+  g_query = false;
+  if (rc) return rc;
+  MP_CHECK_ARG(g_query_kernel != nullptr, "mp_aggregate_kernel_name: no main kernel selected");
+  const char* mangled = hipKernelNameRefByPtr(g_query_kernel, as_stream(stream));
+  MP_CHECK_ARG(mangled != nullptr, "mp_aggregate_kernel_name: HIP has no name for the kernel (no device?)");
+  int st = 0;
+  char* dem = abi::__cxa_demangle(mangled, nullptr, nullptr, &st);
+  const char* name = (st == 0 && dem) ? dem : mangled;
+  snprintf(buf, buf_len, "%s", name);
+  free(dem);
+  return MP_OK;
 }
 
 int mp_aggregate_heads_f32(const mp_csr* g, const float* w, int32_t H, const float* x, int64_t ldx, int32_t F,
@@ -1850,7 +1756,7 @@ int mp_gat_aggregate_f32(const mp_csr* g, const float* xw, const float* a_src, c
   if (vec == 2 && F <= 64) vec = 1;
   while (vec > 1 && C % vec != 0) vec >>= 1;  // a lane's features must share a head
   switch (vec) {
-    case 4: return launch<GatRed<4>, 4>(a, stages, s, F >= 256 ? MP_GAT_LANES : 64);
+    case 4: return launch<GatRed<4>, 4>(a, stages, s, F >= 256 ? kGatLanes : 64);
     case 2: return launch<GatRed<2>, 2>(a, stages, s);
     default: return launch<GatRed<1>, 1>(a, stages, s);
   }
@@ -1918,8 +1824,8 @@ int mp_gat_softmax_aggregate_f32(const mp_csr* g, const int32_t* slot_row, const
   const int ftiles = (int)ceil_div(F, 64);
   if ((stages & MP_STAGE_MAIN) && a.n_waves > 0) {
     int64_t nb = ceil_div(a.n_waves, kWavesPerBlock);
-    if (MP_XCD_TILES && 8 % ftiles == 0) nb = ceil_div(nb, 8 / ftiles) * (8 / ftiles);
-    hipLaunchKernelGGL((k_agg_flat<Red, 1, MP_U_VEC1, 64, false, true>), dim3((unsigned)nb, (unsigned)ftiles),
+    if (kXcdTiles && 8 % ftiles == 0) nb = ceil_div(nb, 8 / ftiles) * (8 / ftiles);
+    hipLaunchKernelGGL((k_agg_flat<Red, 1, kU_Vec1, 64, true>), dim3((unsigned)nb, (unsigned)ftiles),
                        dim3(kBlock), 0, s, a);
     MP_CHECK_LAUNCH();
   }
@@ -1975,7 +1881,7 @@ int mp_gat_backward_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, co
   const bool v4 = C % 4 == 0 && pow2(C / 4) && (uintptr_t)grad_out % 16 == 0 && ldg % 4 == 0 &&
                   (uintptr_t)xw % 16 == 0 && (uintptr_t)grad_xw % 16 == 0;
   if (v4) {
-    int lanes = F >= 256 ? MP_GAT_LANES : pick_shape(F, ldg, grad_out, F, grad_xw).lanes;
+    int lanes = F >= 256 ? kGatLanes : pick_shape(F, ldg, grad_out, F, grad_xw).lanes;
     if (lanes < C / 4) lanes = C / 4;
     return launch<GatBwdRed<4>, 4>(a, stages, s, lanes);
   }

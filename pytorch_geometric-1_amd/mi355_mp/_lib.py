@@ -23,6 +23,12 @@ MP_STAGE_STATS = 4
 MP_STAGE_ALL = 7
 MP_TUNE_FLAT_VEC1_MIN_BYTES = 1
 MP_TUNE_FLAT_SMEM = 2
+MP_TUNE_FLAT_MIN_F = 3
+MP_TUNE_FLAT_MIN_F_ARG = 4
+MP_TUNE_FLAT_NARROW_VEC1 = 5
+MP_LOOPS_REMOVE = 0
+MP_LOOPS_ADD = 1
+MP_LOOPS_ADD_REMAINING = 2
 
 c_p = ctypes.c_void_p
 i64 = ctypes.c_int64
@@ -53,6 +59,8 @@ SIGNATURES = {
     "mp_aggregate_slab_bytes": (sz, [ctypes.POINTER(MpCsr), i32, i32]),
     "mp_aggregate_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, i64, i32, i32, i32, c_p,
                                         c_p, i64, c_p, c_p, sz, i32, c_p]),
+    "mp_aggregate_kernel_name": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, i64, i32, i32, c_p, c_p, i64,
+                                                ctypes.c_char_p, sz, c_p]),
     "mp_gat_node_scores_f32": (ctypes.c_int, [c_p, i64, i32, i32, c_p, c_p, c_p, c_p]),
     "mp_gat_slab_bytes": (sz, [ctypes.POINTER(MpCsr), i32, i32]),
     "mp_gat_aggregate_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, c_p, i32, i32, f32, c_p,
@@ -76,6 +84,10 @@ SIGNATURES = {
     "mp_gather_rows_f32": (ctypes.c_int, [c_p, i64, c_p, i64, i32, c_p, i64, c_p]),
     "mp_permute_f32": (ctypes.c_int, [c_p, c_p, i64, c_p, c_p]),
     "mp_scatter_arg_backward_f32": (ctypes.c_int, [c_p, c_p, i64, i32, i64, c_p, c_p, c_p, i64, c_p, i64, c_p, c_p]),
+    "mp_self_loop_count": (ctypes.c_int, [c_p, c_p, i64, c_p, c_p]),
+    "mp_self_loops_workspace": (sz, [i64, i64]),
+    "mp_self_loops": (ctypes.c_int, [c_p, c_p, i64, i64, i32, i64, c_p, c_p, c_p, c_p, sz, c_p]),
+    "mp_gather_fill_f32": (ctypes.c_int, [c_p, c_p, i64, f32, c_p, c_p]),
     "mp_gcn_norm_f32": (ctypes.c_int, [c_p, c_p, c_p, i64, i64, c_p, c_p, c_p]),
 }
 
@@ -108,6 +120,33 @@ def load(path=None):
     if path is None:
         _lib = lib
     return lib
+
+
+def source_hash():
+    """sha256 over the native sources the library is built from (csrc/*.hip,
+    csrc/*.h, csrc/Makefile, include/mi355_mp.h).  Profile summaries record it,
+    so a committed counter profile is only used for the build it measured."""
+    import glob
+    import hashlib
+    csrc = os.path.join(os.path.dirname(_HERE), "csrc")
+    files = sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.h")))
+    files += [os.path.join(csrc, "Makefile"),
+              os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "mi355_mp.h")]
+    h = hashlib.sha256()
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def kernel_name(csr_struct, w, x, ldx, F, reduce, bias, out, ldo, device=None):
+    """Demangled name of the main kernel mp_aggregate_f32 dispatches for these
+    arguments (mp_aggregate_kernel_name)."""
+    buf = ctypes.create_string_buffer(1024)
+    check(load().mp_aggregate_kernel_name(csr_struct, w, x, ldx, F, MP_REDUCE[reduce], bias, out, ldo, buf, 1024,
+                                          stream_ptr(device)), "mp_aggregate_kernel_name")
+    return buf.value.decode()
 
 
 def check(rc, what):

@@ -253,6 +253,78 @@ def index_select_rows(x, idx):
 
 
 # ---------------------------------------------------------------------------
+# self-loop rewrites (PyG 1.4.3 utils.loop [U4])
+# ---------------------------------------------------------------------------
+
+_LOOP_MODES = {"remove": _lib.MP_LOOPS_REMOVE, "add": _lib.MP_LOOPS_ADD,
+               "add_remaining": _lib.MP_LOOPS_ADD_REMAINING}
+
+
+def self_loops(edge_index, num_nodes, mode):
+    """Native loop rewrite of a [2, E] int64 device edge_index (mp_self_loops).
+
+    Returns (edge_index_out, pos): the kept edges in original order, then (for
+    'add' / 'add_remaining') the loops 0..N-1; pos[k] = input position whose
+    weight output edge k carries (-1: fill value).  One host sync reads the
+    number of self loops (the output size), like upstream's boolean-mask
+    indexing."""
+    _lib.require_device(edge_index)
+    lib = _lib.load()
+    dev = edge_index.device
+    st = _lib.stream_ptr(dev)
+    N = int(num_nodes)
+    E = int(edge_index.shape[1])
+    row = edge_index[0].to(torch.int64).contiguous()
+    col = edge_index[1].to(torch.int64).contiguous()
+    m = _LOOP_MODES[mode]
+    n_kept = E
+    if m != _lib.MP_LOOPS_ADD and E:
+        cnt = torch.empty(1, dtype=torch.int64, device=dev)
+        _lib.check(lib.mp_self_loop_count(row.data_ptr(), col.data_ptr(), E, cnt.data_ptr(), st),
+                   "mp_self_loop_count")
+        n_kept = E - int(cnt.item())
+    n_out = n_kept + (0 if m == _lib.MP_LOOPS_REMOVE else N)
+    out = torch.empty((2, n_out), dtype=torch.int64, device=dev)
+    pos = torch.empty(max(n_out, 1), dtype=torch.int64, device=dev)
+    wsb = lib.mp_self_loops_workspace(E, N)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    _lib.check(lib.mp_self_loops(row.data_ptr(), col.data_ptr(), E, N, m, n_kept, out[0].data_ptr(),
+                                 out[1].data_ptr(), pos.data_ptr(), ws.data_ptr(), wsb, st), "mp_self_loops")
+    return out, pos[:n_out]
+
+
+class _GatherFill(torch.autograd.Function):
+    """out[k] = w[pos[k]] if pos[k] >= 0 else fill (native); every input
+    position appears at most once in pos, so the backward is a plain scatter."""
+
+    @staticmethod
+    def forward(ctx, w, pos, fill):
+        ctx.n = w.shape[0]
+        ctx.save_for_backward(pos)
+        out = torch.empty(pos.shape[0], dtype=torch.float32, device=w.device)
+        _lib.check(_lib.load().mp_gather_fill_f32(w.data_ptr(), pos.data_ptr(), pos.shape[0], float(fill),
+                                                  out.data_ptr(), _lib.stream_ptr(w.device)), "mp_gather_fill_f32")
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (pos,) = ctx.saved_tensors
+        keep = pos >= 0
+        gw = torch.zeros(ctx.n, dtype=g.dtype, device=g.device)
+        gw[pos[keep]] = g[keep]
+        return gw, None, None
+
+
+def gather_fill(w, pos, fill):
+    """Per-edge weights of a loop rewrite: w[pos] with `fill` where pos < 0."""
+    _lib.require_device(w, pos)
+    if w.dtype != torch.float32:
+        v = w[pos.clamp(min=0)]
+        return torch.where(pos >= 0, v, torch.full_like(v, fill))
+    return _GatherFill.apply(w.contiguous(), pos, fill)
+
+
+# ---------------------------------------------------------------------------
 # GCN normalisation (GCNConv.norm [U5])
 # ---------------------------------------------------------------------------
 

@@ -66,16 +66,16 @@ class GCNConv(MessagePassing):
     @staticmethod
     def norm(edge_index, num_nodes, edge_weight=None, improved=False, dtype=None):
         fill_value = 1 if not improved else 2
-        ei, mask, loops = remaining_loops_structure(edge_index, num_nodes)
+        ei, pos = remaining_loops_structure(edge_index, num_nodes)
         if edge_weight is None:
             # depends on the structure only: cache it with the structure
             def build():
                 ones = torch.ones((edge_index.size(1),), dtype=torch.float32, device=edge_index.device)
-                w = remaining_loops_weight(ones, mask, loops, num_nodes, fill_value)
+                w = remaining_loops_weight(ones, pos, fill_value)
                 return _ops.gcn_norm_weights(ei, num_nodes, w)
             norm = cached_value(edge_index, ("gcn_norm", int(num_nodes), fill_value), build)
             return ei, norm
-        w = remaining_loops_weight(edge_weight, mask, loops, num_nodes, fill_value)
+        w = remaining_loops_weight(edge_weight, pos, fill_value)
         return ei, _ops.gcn_norm_weights(ei, num_nodes, w)
 
     def forward(self, x, edge_index, edge_weight=None):

@@ -38,9 +38,9 @@ class SAGEConv(MessagePassing):
         if not self.concat and torch.is_tensor(x):
             # add_remaining_self_loops(edge_index, edge_weight, 1, N), structure cached on edge_index
             N = x.size(self.node_dim)
-            ei, mask, loops = remaining_loops_structure(edge_index, N)
+            ei, pos = remaining_loops_structure(edge_index, N)
             if edge_weight is not None:
-                edge_weight = remaining_loops_weight(edge_weight, mask, loops, N, 1)
+                edge_weight = remaining_loops_weight(edge_weight, pos, 1)
             edge_index = ei
         return self.propagate(edge_index, size=size, x=x, edge_weight=edge_weight, res_n_id=res_n_id)
 

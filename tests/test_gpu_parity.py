@@ -34,6 +34,26 @@ def _bound_ok(got, want, terms, rel=1e-5):
     assert not bool(bad.any()), "max excess %g" % float(((got - want).abs() - tol).max())
 
 
+class _tuned:
+    """Set mp_tune keys for the duration of a block (restored on exit)."""
+
+    def __init__(self, **kv):
+        from mi355_mp import _lib
+        self.lib = _lib.load()
+        self.kv = {getattr(_lib, "MP_TUNE_" + k.upper()): v for k, v in kv.items()}
+        self.prev = {}
+
+    def __enter__(self):
+        for k, v in self.kv.items():
+            self.prev[k] = self.lib.mp_tune(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.prev.items():
+            self.lib.mp_tune(k, v)
+        return False
+
+
 def _split_rows(csr):
     """Rows whose slots span more than one merge-path task (host mirror)."""
     rp = csr.rowptr.cpu().numpy()
@@ -144,13 +164,14 @@ def test_fused_sum_mean(F, chunk, weighted):
     assert torch.equal(outm[whole], wantm[whole])
 
 
-@pytest.mark.parametrize("F", [256, 300, 512])
+@pytest.mark.parametrize("F", [64, 130, 256, 300, 512])
 @pytest.mark.parametrize("chunk", [16, 256])
 def test_fused_sum_mean_64_feature_tiles(F, chunk):
     """Sum/mean of >= 256-feature rows over a gathered x of >= 1 GiB run the
     flat kernel with 64-feature tiles (VEC=1); mp_tune forces that shape on a
-    small graph.  Same arithmetic per feature: bitwise equal to the default
-    128-feature-tile shape and to the oracle on unsplit rows."""
+    small graph (F = 64 / 130: the 64..255-feature flat route, including a
+    partial last tile).  Same arithmetic per feature: bitwise equal to the
+    default 128-feature-tile shape and to the oracle on unsplit rows."""
     _, ops, _, Graph, pl = _mods()
     from mi355_mp import _lib
     lib = _lib.load()
@@ -177,7 +198,8 @@ def test_fused_sum_mean_64_feature_tiles(F, chunk):
     assert torch.equal(got["sum"][whole], want[whole])
 
 
-@pytest.mark.parametrize("F,N,E", [(256, 700, 9000), (300, 700, 9000), (512, 300, 4000), (256, 5, 7), (256, 40, 17)])
+@pytest.mark.parametrize("F,N,E", [(256, 700, 9000), (300, 700, 9000), (512, 300, 4000), (256, 5, 7), (256, 40, 17),
+                                   (64, 700, 9000), (130, 700, 9000), (100, 40, 17)])
 @pytest.mark.parametrize("vec1", [False, True])
 def test_flat_scalar_slot_batches_match_slot_window(F, N, E, vec1):
     """The flat sum/mean kernel's scalar-cache slot batches (MP_TUNE_FLAT_SMEM,
@@ -243,7 +265,7 @@ def test_gathered_x_over_4gib():
     assert torch.equal(out[whole], want[whole])
 
 
-@pytest.mark.parametrize("F", [1, 5, 64, 256, 602])
+@pytest.mark.parametrize("F", [1, 5, 64, 130, 256, 602])
 @pytest.mark.parametrize("reduce", ["max", "min"])
 def test_fused_max_min_bit_exact_with_ties(F, reduce):
     _, ops, _, Graph, pl = _mods()
@@ -262,6 +284,45 @@ def test_fused_max_min_bit_exact_with_ties(F, reduce):
     o2, a2 = ops.segment_reduce(msg, ei[1].to(DEV), N, reduce)
     assert torch.equal(o2.cpu(), want)
     assert torch.equal(a2.cpu(), arg)
+
+
+@pytest.mark.parametrize("F", [1, 5, 64, 130, 256, 602])
+@pytest.mark.parametrize("chunk", [16, 64])
+@pytest.mark.parametrize("reduce", ["max", "min"])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_fused_gather_argmax_matches_oracle_first_edge(F, chunk, reduce, weighted):
+    """The fused-gather max/min path (gather = x[src], no materialised
+    messages: GraphConv/SAGE/EdgeConv aggr='max', README.md:35-49) returns the
+    VALUES and the ARG (original edge id) of torch_scatter 2.0.4's serial loop:
+    strict compare in edge order, so the first edge attaining the extremum wins
+    (oracle: scatter_loop.c on the materialised w * x[src]).  Tie-heavy small
+    integers, a power-law graph with duplicate (src, dst) edges (exact ties),
+    weights from {0.5, 1, 2} (products exact), chunk 16 so hub rows split over
+    many merge-path tasks (their partials are merged in task order)."""
+    _, ops, _, Graph, pl = _mods()
+    N, E = 600, 12000
+    ei = pl(N, E, seed=F + chunk)
+    g = torch.Generator().manual_seed(F + 7)
+    x = torch.randint(-3, 4, (N, F), generator=g).to(torch.float32)
+    w = torch.tensor([0.5, 1.0, 2.0])[torch.randint(3, (E,), generator=g)] if weighted else None
+    pairs = ei[0] * N + ei[1]
+    assert pairs.unique().numel() < E, "the graph must hold duplicate edges (exact ties)"
+    graph = Graph(ei.to(DEV), N, N, chunk=chunk)
+    csr = graph.dst
+    assert csr.n_split > 0
+    w_csr = csr.to_csr_order(w.to(DEV)) if weighted else None
+    out, arg = ops._aggregate(csr, "other", x.to(DEV), w_csr, reduce, 0, None)
+    msg = x[ei[0]] if w is None else w.view(-1, 1) * x[ei[0]]
+    want, warg = S.scatter_loop(msg, ei[1], N, reduce)
+    assert torch.equal(out.cpu(), want)
+    assert torch.equal(arg.cpu(), warg), "argmax must be the first maximal edge (bit-exact)"
+    if not weighted and reduce == "max":
+        o3, a3 = S.gather_max(x, ei[0], ei[1], N)
+        assert torch.equal(out.cpu(), o3) and torch.equal(arg.cpu(), a3)
+    # the same through the 32-lane-group kernel (flat route switched off)
+    with _tuned(flat_min_f_arg=1 << 30):
+        o2, a2 = ops._aggregate(csr, "other", x.to(DEV), w_csr, reduce, 0, None)
+    assert torch.equal(o2.cpu(), want) and torch.equal(a2.cpu(), warg)
 
 
 def test_max_special_values_and_pyg_mask():
@@ -742,9 +803,13 @@ def test_gat_training_flow():
     assert all(np.isfinite(losses)) and losses[-1] < 0.7 * losses[0]
 
 
-@pytest.mark.parametrize("F", [2, 4, 7, 8, 12, 16, 32, 64, 100, 128])
-def test_small_feature_widths_lane_groups(F):
-    """F <= 128 packs several merge-path tasks per wave (L = F/4 lanes)."""
+@pytest.mark.parametrize("F", [2, 4, 7, 8, 12, 16, 32, 48, 60, 64, 100, 128])
+@pytest.mark.parametrize("flat", [True, False])
+def test_small_feature_widths_lane_groups(F, flat):
+    """Narrow rows: F <= 8 runs one task per lane, F < 64 packs several
+    merge-path tasks per wave (L = F/4 lanes, k_agg_main), 64 <= F < 256 takes
+    the flat kernel.  flat=False switches the flat route off (mp_tune), so the
+    lane-group kernel is covered at 64..128 features as well."""
     _, ops, _, Graph, pl = _mods()
     N, E = 800, 15000
     ei = pl(N, E, seed=F + 100)
@@ -752,7 +817,12 @@ def test_small_feature_widths_lane_groups(F):
     x = torch.randn(N, F, generator=g)
     w = torch.rand(E, generator=g)
     graph = Graph(ei.to(DEV), N, N, chunk=64)
-    out = ops.fused_propagate(graph, x.to(DEV), ei.to(DEV), w.to(DEV), "sum").cpu()
+    big = 1 << 30
+    with _tuned(flat_min_f=64 if flat else big, flat_min_f_arg=64 if flat else big):
+        out = ops.fused_propagate(graph, x.to(DEV), ei.to(DEV), w.to(DEV), "sum").cpu()
+        fo, fa = ops._aggregate(graph.dst, "other", x.to(DEV), None, "max", 0, None)
+    wm0, wa0 = S.gather_max(x, ei[0], ei[1], N)
+    assert torch.equal(fo.cpu(), wm0) and torch.equal(fa.cpu(), wa0)
     want = S.gather_sum(x, ei[0], ei[1], w, N)
     _bound_ok(out, want, S.gather_sum(x.abs(), ei[0], ei[1], w, N))
     split = set(_split_rows(graph.dst))
@@ -1314,7 +1384,8 @@ def test_full_size_reddit_max_argmax():
     """Config 4 at full size (N=232,965, E=114,615,892, F=256): determinism;
     every argmax is an in-edge of its row whose source value equals the output
     exactly; values bit-equal to torch's own scatter_reduce('amax') computed in
-    edge chunks (max is order-independent)."""
+    edge chunks (max is order-independent); every argmax is the FIRST such
+    edge (the reference's tie rule; the graph keeps duplicate edges)."""
     _, ops, _, Graph, _ = _mods()
     from mi355_mp.graphgen import powerlaw_edge_index
     N, E, F = 232_965, 114_615_892, 256
@@ -1339,6 +1410,19 @@ def test_full_size_reddit_max_argmax():
         ref.scatter_reduce_(0, dst.view(-1, 1).expand(-1, F), x[src], "amax")
     ref[~has] = 0
     assert torch.equal(out, ref)
+    del ref
+    # first-edge rule (torch_scatter's strict '>' in edge order): arg is the
+    # SMALLEST edge id whose source value equals the row's maximum, computed
+    # independently with a chunked scatter_reduce('amin') over edge ids
+    first = torch.full((N, F), E, dtype=torch.int64, device=DEV)
+    step = 2_000_000
+    for s in range(0, E, step):
+        src, dst = ei[0, s:s + step], ei[1, s:s + step]
+        ids = torch.arange(s, s + src.numel(), device=DEV).view(-1, 1).expand(-1, F)
+        cand = torch.where(x[src] == out[dst], ids, torch.full_like(ids, E))
+        first.scatter_reduce_(0, dst.view(-1, 1).expand(-1, F), cand, "amin")
+        del ids, cand
+    assert torch.equal(arg, first), "argmax must be the first maximal in-edge of every (row, feature)"
 
 
 def test_full_size_gat_config3():
@@ -1381,3 +1465,106 @@ def test_full_size_gat_config3():
     got = out.view(N, H, C).double()
     tol = 1e-5 * terms.clamp(min=1.0) + 1e-5
     assert bool(((got - ref).abs() <= tol).all()), float(((got - ref).abs() - tol).max())
+
+
+# --------------------------------------------------------------------------
+# standalone utilities on the device
+# --------------------------------------------------------------------------
+
+@pytest.mark.parametrize("shape", [(1,), (8,), (3, 4)])
+def test_utils_softmax_matches_reference(shape):
+    """torch_geometric.utils.softmax (native segment max / sum + gathers) vs the
+    reference formula exp(s - max_seg(s)[i]) / (sum_seg(.)[i] + 1e-16) on the CPU
+    (P.softmax), with multi-dimensional src, empty segments and a hub row
+    split across merge-path tasks."""
+    from torch_geometric.utils import softmax
+    _, _, _, _, pl = _mods()
+    N, E = 500, 20000
+    ei = pl(N, E, seed=61)
+    idx = ei[1]
+    g = torch.Generator().manual_seed(61)
+    src = torch.randn((E,) + shape, generator=g) * 4
+    idx_d = idx.to(DEV)
+    got = softmax(src.to(DEV), idx_d, N).cpu()
+    want = P.softmax(src, idx, N)
+    assert got.shape == want.shape
+    err = (got - want).abs().reshape(E, -1).amax(1)
+    # north-star fp32 bound everywhere; <= 1e-6 on segments summed in one
+    # merge-path task (the denominator then has the reference's summation
+    # order; what is left is exp's last-bit difference between GPU and CPU)
+    assert float(err.max()) <= 1e-5
+    from mi355_mp.graph import csr_for_index
+    split = torch.tensor(_split_rows(csr_for_index(idx_d, N)), dtype=torch.long)
+    assert split.numel() > 0, "the test graph must hold a segment split across tasks"
+    whole = ~torch.isin(idx, split)
+    assert float(err[whole].max()) <= 1e-6
+    sums = torch.zeros((N,) + shape).index_add_(0, idx, got)
+    has = torch.bincount(idx, minlength=N) > 0
+    assert torch.allclose(sums[has], torch.ones_like(sums[has]), atol=1e-5)
+
+
+def _loop_graph(seed, N=300, E=5000):
+    """Power-law edges plus self loops: duplicate loops of one node (the last one's
+    weight must win), loops in the middle and at the end of the edge list."""
+    _, _, _, _, pl = _mods()
+    ei = pl(N, E, seed=seed)
+    g = torch.Generator().manual_seed(seed)
+    loops = torch.randint(N, (400,), generator=g)
+    loops = torch.cat([loops, loops[:50], torch.tensor([N - 1, 0, N - 1])])
+    lei = torch.stack([loops, loops])
+    pos = torch.randint(ei.shape[1], (lei.shape[1],), generator=g).sort().values
+    parts, last = [], 0
+    for k, p in enumerate(pos.tolist()):
+        parts.append(ei[:, last:p])
+        parts.append(lei[:, k:k + 1])
+        last = p
+    parts.append(ei[:, last:])
+    ei = torch.cat(parts, dim=1)
+    w = torch.rand(ei.shape[1], generator=g) + 0.5
+    return ei, w
+
+
+@pytest.mark.parametrize("seed", [71, 72])
+def test_self_loop_utilities_bit_exact(seed):
+    """utils.loop on the device (mp_self_loops) vs the oracle's sequential
+    restatement: edge order, loop order and loop weights (last duplicate loop
+    wins; `improved` fill 2) bit for bit; also GCNConv's cached structure and
+    a graph without any self loop."""
+    from torch_geometric.utils import add_remaining_self_loops, add_self_loops, remove_self_loops
+    from torch_geometric.nn.conv._structure import remaining_loops_structure, remaining_loops_weight
+    N = 300
+    ei, w = _loop_graph(seed, N)
+    eid, wd = ei.to(DEV), w.to(DEV)
+    for fill in (1, 2):
+        got_ei, got_w = add_remaining_self_loops(eid, wd, fill, N)
+        r_ei, r_w = P.add_remaining_self_loops(ei, w, fill, N)
+        assert torch.equal(got_ei.cpu(), r_ei) and torch.equal(got_w.cpu(), r_w)
+    got_ei, none = add_remaining_self_loops(eid, None, 1, N)
+    assert none is None and torch.equal(got_ei.cpu(), r_ei)
+    got_ei, got_w = add_self_loops(eid, wd, 3.0, N)
+    r_ei, r_w = P.add_self_loops(ei, w, 3.0, N)
+    assert torch.equal(got_ei.cpu(), r_ei) and torch.equal(got_w.cpu(), r_w)
+    got_ei, got_w = remove_self_loops(eid, wd)
+    r_ei, r_w = P.remove_self_loops(ei, w)
+    assert torch.equal(got_ei.cpu(), r_ei) and torch.equal(got_w.cpu(), r_w)
+    # cached structure (GCNConv / SAGEConv) and GATConv's remove + add
+    s_ei, pos = remaining_loops_structure(eid, N)
+    assert remaining_loops_structure(eid, N)[0] is s_ei
+    r_ei, r_w = P.add_remaining_self_loops(ei, w, 2, N)
+    assert torch.equal(s_ei.cpu(), r_ei)
+    assert torch.equal(remaining_loops_weight(wd, pos, 2).cpu(), r_w)
+    g_ei, _ = P.add_self_loops(P.remove_self_loops(ei)[0], None, 1, N)
+    assert torch.equal(s_ei.cpu(), g_ei)
+    # no self loops at all: identity compaction
+    plain = ei[:, ei[0] != ei[1]]
+    got_ei, got_w = add_remaining_self_loops(plain.to(DEV), w[:plain.shape[1]].to(DEV), 1, N)
+    r_ei, r_w = P.add_remaining_self_loops(plain, w[:plain.shape[1]], 1, N)
+    assert torch.equal(got_ei.cpu(), r_ei) and torch.equal(got_w.cpu(), r_w)
+    # weights that require grad: d w = the scatter of the loop-rewritten weights' grad
+    wg = wd.clone().requires_grad_(True)
+    _, w2 = add_remaining_self_loops(eid, wg, 1, N)
+    gout = torch.randn(w2.shape[0], generator=torch.Generator().manual_seed(seed))
+    w2.backward(gout.to(DEV))
+    w64 = w.double().requires_grad_(True)
+    P.add_remaining_self_loops(ei, w64, 1, N)[1].backward(gout.double())
+    assert torch.equal(wg.grad.cpu().double(), w64.grad)

@@ -76,6 +76,36 @@ def test_argument_errors_are_reported(lib):
     assert rc == 1 and b"chunk" in lib.mp_last_error()
 
 
+
+def test_column_array_requires_n_cols(lib):
+    """A graph with a gather column but n_cols = 0 (e.g. a C caller that left the
+    last mp_csr field zero) is rejected before anything is launched: n_cols bounds
+    the 32-bit buffer offsets and selects the kernel shape."""
+    from mi355_mp import _lib
+    fake = 0x1000  # never dereferenced: the argument check fails first
+    g = _lib.MpCsr(fake, fake, fake, fake, fake, None, 10, 40, 256, 1, 0, 0)
+    rc = lib.mp_aggregate_f32(g, None, fake, 4, 4, 0, 0, None, fake, 4, None, fake, 1 << 20, 3, None)
+    assert rc == 1 and b"n_cols" in lib.mp_last_error()
+    buf = __import__("ctypes").create_string_buffer(256)
+    rc = lib.mp_aggregate_kernel_name(g, None, fake, 4, 4, 0, None, fake, 4, buf, 256, None)
+    assert rc == 1 and b"n_cols" in lib.mp_last_error()
+    # identity gather (col = NULL) needs no n_cols
+    g2 = _lib.MpCsr(fake, None, fake, fake, fake, None, 10, 40, 256, 1, 0, 0)
+    rc = lib.mp_aggregate_f32(g2, None, fake, 4, 4, 0, 0, None, fake, 4, None, None, 0, 3, None)
+    assert rc == 1 and b"slab" in lib.mp_last_error()
+
+
+def test_tune_table_keys(lib):
+    from mi355_mp import _lib
+    for key in (_lib.MP_TUNE_FLAT_VEC1_MIN_BYTES, _lib.MP_TUNE_FLAT_SMEM, _lib.MP_TUNE_FLAT_MIN_F,
+                _lib.MP_TUNE_FLAT_MIN_F_ARG, _lib.MP_TUNE_FLAT_NARROW_VEC1):
+        v = lib.mp_tune(key, -1)
+        assert v >= 0
+        assert lib.mp_tune(key, v) == v
+    assert lib.mp_tune(_lib.MP_TUNE_FLAT_MIN_F, -1) == 64
+    assert lib.mp_tune(_lib.MP_TUNE_FLAT_MIN_F_ARG, -1) == 64
+
+
 def test_no_cpu_fallback_guard():
     import torch_scatter
     from mi355_mp import ops
@@ -154,21 +184,20 @@ def test_graph_generators_deterministic_and_shaped():
     assert int(d["train_mask"].sum()) == 140
 
 
-def test_gcn_structure_cache_matches_reference_loops():
-    from oracle import pyg_ref as P
-    from torch_geometric.nn.conv._structure import remaining_loops_structure, remaining_loops_weight
-    # node 1 has two self loops (weights 2 and 6): the last one wins, as on the CPU
+def test_loop_utilities_have_no_cpu_fallback():
+    """utils.loop runs on the native engine (mp_self_loops); host tensors raise
+    instead of silently taking a CPU path (GPU parity: test_gpu_parity.py
+    test_self_loop_utilities_bit_exact)."""
+    from torch_geometric.utils import add_remaining_self_loops, add_self_loops, remove_self_loops
     ei = torch.tensor([[0, 1, 1, 2, 2, 1], [1, 1, 2, 0, 2, 1]])
-    w = torch.tensor([1., 2., 3., 4., 5., 6.])
-    ei2, mask, loops = remaining_loops_structure(ei, 4)
-    w2 = remaining_loops_weight(w, mask, loops, 4, 2)
-    r_ei, r_w = P.add_remaining_self_loops(ei, w, 2, 4)
-    assert torch.equal(ei2, r_ei) and torch.equal(w2, r_w)
+    for fn in (add_remaining_self_loops, add_self_loops, remove_self_loops):
+        with pytest.raises(RuntimeError, match="no CPU fallback"):
+            fn(ei)
+    # the oracle's own KAT: node 1 has two self loops (weights 2 and 6), the last wins
+    from oracle import pyg_ref as P
+    r_ei, r_w = P.add_remaining_self_loops(ei, torch.tensor([1., 2., 3., 4., 5., 6.]), 2, 4)
     assert r_w.tolist()[-4:] == [2., 6., 5., 2.]
-    assert remaining_loops_structure(ei, 4)[0] is ei2    # cached on the tensor
-    from torch_geometric.utils import add_remaining_self_loops
-    u_ei, u_w = add_remaining_self_loops(ei, w, 2, 4)
-    assert torch.equal(u_ei, r_ei) and torch.equal(u_w, r_w)
+    assert r_ei[:, :3].tolist() == [[0, 1, 2], [1, 2, 0]]
 
 
 def test_data_batch_semantics():

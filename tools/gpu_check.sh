@@ -12,10 +12,15 @@ step() {  # name timeout cmd...
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
+{ nproc; python3 -c "import os; print('cpu_count', os.cpu_count(), 'affinity', len(os.sched_getaffinity(0)))";
+  cat /sys/fs/cgroup/cpu.max 2>/dev/null; grep -m1 "model name" /proc/cpuinfo; } > gpurun_out/host_probe.log 2>&1
+PT="python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread"
 if [ -n "${PYTEST_K:-}" ]; then
-  step pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout=600 -k "$PYTEST_K"
+  step pytest_gpu 1100 $PT -k "$PYTEST_K"
 else
-  step pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout=600
+  step pytest_gpu 1100 $PT
 fi
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench 600 python bench.py --steps 20 --warmup 5
+if [ -z "${NO_BENCH:-}" ]; then
+  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+  step bench 600 python bench.py --steps 20 --warmup 5
+fi

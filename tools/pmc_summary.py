@@ -8,13 +8,18 @@ dominant kernel, corrected as MI355X_MICROARCH.md 'HBM' prescribes
 (FETCH_SIZE and WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reads half the bytes
 of a 16 B/lane coalesced stream -> doubled, and profiles/r01_pmc_calibration.json
 measures the same factor for this kernel's 8 B/lane loads; WRITE_SIZE exact
-for 16 B/lane stores), plus the L2 hit rate.  bench.py reads the json for roofline.traffic.
+for 16 B/lane stores), plus the L2 hit rate.  bench.py reads the json for
+roofline.traffic only when its kernel name and native source hash match the
+running build.  Run it on the tree the profile was taken from.
 """
 import csv
 import json
 import os
 import shutil
 import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "pytorch_geometric-1_amd"))
+from mi355_mp._lib import source_hash  # noqa: E402
 
 N_CU = 256      # MI355X compute units (one TCP each)
 N_XCD = 8
@@ -71,6 +76,7 @@ def main():
     out = {
         "workload": "rmat21_gcn_f256",
         "kernel": KERNEL,
+        "source_hash": source_hash(),
         "launches": {"fetch": nf, "write": nw},
         "FETCH_SIZE_KiB_raw": fetch,
         "WRITE_SIZE_KiB_raw": write,
