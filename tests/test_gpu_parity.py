@@ -204,7 +204,8 @@ def test_fused_sum_mean_64_feature_tiles(F, chunk):
 def test_flat_scalar_slot_batches_match_slot_window(F, N, E, vec1):
     """The flat sum/mean kernel's scalar-cache slot batches (MP_TUNE_FLAT_SMEM,
     default on) against the per-lane slot window: bitwise equal, including
-    graphs with fewer slots than one batch (the clamped tail path)."""
+    graphs with fewer slots than one batch (the clamped tail path) and partial
+    feature tiles."""
     _, ops, _, Graph, pl = _mods()
     from mi355_mp import _lib
     lib = _lib.load()
@@ -214,24 +215,19 @@ def test_flat_scalar_slot_batches_match_slot_window(F, N, E, vec1):
     w = torch.rand(E, generator=g)
     graph = Graph(ei.to(DEV), N, N, chunk=16)
     eid = ei.to(DEV)
-    prev_v = lib.mp_tune(_lib.MP_TUNE_FLAT_VEC1_MIN_BYTES, 0 if vec1 else -1)
     got = {}
-    try:
-        for sm in (1, 0):
-            prev_s = lib.mp_tune(_lib.MP_TUNE_FLAT_SMEM, sm)
-            try:
-                got[sm] = {(r, wt): ops.fused_propagate(graph, x.to(DEV), eid, w.to(DEV) if wt else None, r).cpu()
-                           for r in ("sum", "mean") for wt in (False, True)}
-            finally:
-                lib.mp_tune(_lib.MP_TUNE_FLAT_SMEM, prev_s)
-    finally:
-        if vec1:
-            lib.mp_tune(_lib.MP_TUNE_FLAT_VEC1_MIN_BYTES, prev_v)
+    for sm in (1, 0):
+        with _tuned(flat_vec1_min_bytes=0 if vec1 else 1 << 30, flat_smem=sm):
+            got[sm] = {(r, wt): ops.fused_propagate(graph, x.to(DEV), eid, w.to(DEV) if wt else None, r).cpu()
+                       for r in ("sum", "mean") for wt in (False, True)}
     assert lib.mp_tune(_lib.MP_TUNE_FLAT_SMEM, -1) == 1
     for k in got[1]:
         assert torch.equal(got[1][k], got[0][k]), k
     want = S.gather_sum(x, ei[0], ei[1], w, N)
     _bound_ok(got[1][("sum", True)], want, S.gather_sum(x.abs(), ei[0], ei[1], w.abs(), N))
+    split = set(_split_rows(graph.dst))
+    whole = torch.tensor([r for r in range(N) if r not in split], dtype=torch.long)
+    assert torch.equal(got[1][("sum", True)][whole], want[whole])
 
 
 def test_gathered_x_over_4gib():
