@@ -126,16 +126,49 @@ class ShardPlan:
         x_local[:self.n_own].copy_(x_own)
         return self.exchange_into(x_local, gather_rows, group)
 
+    def return_halo(self, halo_rows, group=None):
+        """The reverse of exchange_into: rows living in this rank's halo
+        ([n_halo, F], halo order) go back to their owners.  Returns the rows
+        this rank receives, [len(send_idx), F], aligned with send_idx (peer
+        order, then each peer's request order) -- the caller adds them into
+        its own rows (a row requested by several peers appears once per peer)."""
+        F = halo_rows.shape[1]
+        out = halo_rows.new_empty((int(self.send_idx.numel()), F))
+        _a2a(out, halo_rows.contiguous(), self.send_counts, self.recv_counts, group)
+        return out
 
-def sharded_propagate(plan, x_own, local_aggregate, gather_rows, edge_weight=None, group=None):
+    def global_edge_ids(self, arg_local, n_edges_global):
+        """Arg of a max/min over this rank's edges (local positions; the local
+        edge list is the global one restricted, in global order, so the first
+        maximal local edge IS the first maximal global edge) -> global edge
+        ids; the empty-row sentinel (number of local edges) becomes the
+        reference's sentinel, the global edge count (edge ids stay
+        global, argmax bit-exact)."""
+        n_local = int(self.edge_pos.numel())
+        if n_local == 0:
+            return torch.full_like(arg_local, n_edges_global)
+        ids = self.edge_pos[arg_local.clamp(max=n_local - 1)]
+        return torch.where(arg_local >= n_local, torch.full_like(ids, n_edges_global), ids)
+
+
+def sharded_propagate(plan, x_own, local_aggregate, gather_rows, edge_weight=None, group=None, n_edges_global=None):
     """One sharded aggregation: halo exchange then local aggregation.
 
-    local_aggregate(x_local, local_edge_index, n_dst, n_src, edge_weight) -> [n_own, F]
+    local_aggregate(x_local, local_edge_index, n_dst, n_src, edge_weight) ->
+    [n_own, F], or (out, arg) for max/min with arg in LOCAL edge positions:
+    then arg is returned as global edge ids (n_edges_global = the sentinel).
     edge_weight: per-edge weights in GLOBAL edge order (sliced by the plan).
+    The backward of a sum is the same call on the transposed plan (see
+    ShardedGraph): the gradient rows of remote destinations come in as halo
+    rows, so every source row is summed in global edge order by its owner.
     """
     x_local = plan.halo_exchange(x_own, gather_rows, group)
     w = edge_weight[plan.edge_pos] if edge_weight is not None else None
-    return local_aggregate(x_local, plan.local_edge_index, plan.n_own, plan.n_local_src, w)
+    res = local_aggregate(x_local, plan.local_edge_index, plan.n_own, plan.n_local_src, w)
+    if isinstance(res, tuple):
+        out, arg = res
+        return out, plan.global_edge_ids(arg, n_edges_global)
+    return res
 
 
 class OverlappedAggregation:
@@ -232,3 +265,184 @@ class OverlappedAggregation:
             ops._aggregate(self.g_bnd.dst, "other", xt, self.w_bnd, "sum", _lib.MP_FLAG_INIT_FROM_OUT, b,
                            out=out[:, offs[t]:offs[t + 1]])
         return out
+
+
+def transposed_plan(edge_index, num_nodes, rank, world, cuts, group=None):
+    """The plan of the backward pass: rank p owns the SOURCE rows [lo_p, hi_p)
+    of the same cuts, its edges are the out-edges of those rows (global order)
+    and its halo the remote destinations whose gradient rows it gathers."""
+    return ShardPlan(edge_index, num_nodes, rank, world, cuts=cuts, flow="target_to_source").exchange_requests(group)
+
+
+class ShardedGraph:
+    """One graph sharded by destination-node range over the ranks of `group`
+    (SURVEY 8e), with everything a layer needs for forward AND backward:
+
+      fwd : ShardPlan of the in-edges of this rank's rows (halo = remote sources)
+      bwd : ShardPlan of the out-edges of this rank's rows (halo = remote
+            destinations), same cuts: the backward of the aggregation is a
+            forward over the transposed graph, so d x_j is summed by j's owner
+            in global edge order -- no partial sums cross ranks.
+      g_fwd / g_bwd : native CSR graphs of the rank's local edge lists.
+
+    Built once per (edge_index, weights) like GCNConv(cached=True).  Every rank
+    passes the full edge_index (one-time plan construction)."""
+
+    def __init__(self, edge_index, num_nodes, rank, world, group=None, cuts=None, chunk=None):
+        from .graph import Graph
+        self.group = group
+        self.num_nodes = int(num_nodes)
+        self.n_edges = int(edge_index.shape[1])
+        self.fwd = ShardPlan(edge_index, num_nodes, rank, world, cuts=cuts).exchange_requests(group)
+        self.bwd = transposed_plan(edge_index, num_nodes, rank, world, self.fwd.cuts, group)
+        self.lo, self.hi, self.n_own = self.fwd.lo, self.fwd.hi, self.fwd.n_own
+        self.g_fwd = Graph(self.fwd.local_edge_index, self.n_own, self.fwd.n_local_src, chunk=chunk)
+        # bwd.local_edge_index = [local row (= source j), local column (= destination i)]
+        self.g_bwd = Graph(self.bwd.local_edge_index, self.n_own, self.bwd.n_local_src,
+                           flow="target_to_source", chunk=chunk)
+        self._w = None
+
+    @classmethod
+    def for_gcn(cls, edge_index, num_nodes, rank, world, group=None, improved=False, edge_weight=None, chunk=None):
+        """GCNConv's graph (add_remaining_self_loops + symmetric norm, [U5]),
+        built from the full edge list, sharded, with the norm as edge weight."""
+        from torch_geometric.nn.conv.gcn_conv import GCNConv
+        ei2, norm = GCNConv.norm(edge_index, num_nodes, edge_weight, improved)
+        return cls(ei2, num_nodes, rank, world, group=group, chunk=chunk).set_edge_weight(norm)
+
+    def set_edge_weight(self, edge_weight):
+        """Per-edge weights in GLOBAL edge order (e.g. the GCN norm), permuted
+        once into both local CSR orders."""
+        if edge_weight is None:
+            self._w = None
+            return self
+        if edge_weight.requires_grad:
+            raise NotImplementedError("mi355_mp.dist: edge weights of a sharded graph carry no gradient")
+        w = edge_weight.to(torch.float32)
+        w_fwd = w[self.fwd.edge_pos].contiguous()
+        self._w = (self.g_fwd.dst.to_csr_order(w_fwd), self.g_bwd.dst.to_csr_order(w[self.bwd.edge_pos].contiguous()),
+                   w_fwd)
+        return self
+
+    def propagate(self, x_own, reduce="sum"):
+        """Sharded MessagePassing.propagate for message = w * x_j: this rank's
+        rows of REDUCE_{e: dst(e) = i} w_e x[src(e)] (autograd included).
+        max/min return (out, arg) with arg = GLOBAL edge ids."""
+        from . import ops
+        reduce = "sum" if reduce == "add" else reduce
+        if reduce not in ("sum", "mean", "max", "min"):
+            raise ValueError("unknown reduce %r" % (reduce,))
+        x_own = ops._f32_2d(x_own, "x")
+        if x_own.shape[0] != self.n_own:
+            raise ValueError("mi355_mp.dist: x_own has %d rows, this rank owns %d" % (x_own.shape[0], self.n_own))
+        out, arg = _ShardedAggregate.apply(x_own, self, reduce)
+        return (out, arg) if reduce in ("max", "min") else out
+
+
+class _ShardedAggregate(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x_own, sg, reduce):
+        from . import ops
+        plan = sg.fwd
+        F = x_own.shape[1]
+        x_local = plan.local_buffer(F, device=x_own.device)
+        x_local[:plan.n_own].copy_(x_own)
+        plan.exchange_into(x_local, ops.gather_rows, sg.group)
+        w_fwd = sg._w[0] if sg._w is not None else None
+        out, arg = ops._aggregate(sg.g_fwd.dst, "other", x_local, w_fwd, reduce, 0, None)
+        ctx.sg, ctx.reduce = sg, reduce
+        arg_g = None
+        if arg is not None:
+            ctx.save_for_backward(arg)
+            arg_g = plan.global_edge_ids(arg, sg.n_edges)
+            ctx.mark_non_differentiable(arg_g)
+        return out, arg_g
+
+    @staticmethod
+    def backward(ctx, grad_out, _grad_arg=None):
+        from . import _lib, ops
+        sg, reduce = ctx.sg, ctx.reduce
+        g = grad_out.contiguous()
+        F = g.shape[1]
+        if reduce in ("max", "min"):
+            # gradient lands on the argmax edge's source, which may live in the halo:
+            # accumulate per local column, then return the halo rows to their owners
+            (arg,) = ctx.saved_tensors
+            plan = sg.fwd
+            lib = _lib.load()
+            gl = torch.zeros((plan.n_local_src, F), dtype=torch.float32, device=g.device)
+            src_map = plan.local_edge_index[0].contiguous()
+            w = sg._w[2] if sg._w is not None else None  # local edge order: the arg's positions
+            _lib.check(lib.mp_scatter_arg_backward_f32(g.data_ptr(), arg.data_ptr(), g.shape[0], F,
+                                                       int(plan.edge_pos.numel()), src_map.data_ptr(), _lib.ptr(w),
+                                                       None, 0, gl.data_ptr(), gl.stride(0), None,
+                                                       _lib.stream_ptr(g.device)), "mp_scatter_arg_backward_f32")
+            gx = gl[:plan.n_own].clone()
+            back = plan.return_halo(gl[plan.n_own:], sg.group)
+            if back.shape[0]:
+                gx.index_add_(0, plan.send_idx, back)
+            return gx, None, None
+        if reduce == "mean":
+            g = g / sg.g_fwd.dst.degree().clamp(min=1).to(torch.float32).view(-1, 1)
+        plan = sg.bwd
+        g_local = plan.local_buffer(F, device=g.device)
+        g_local[:plan.n_own].copy_(g)
+        plan.exchange_into(g_local, ops.gather_rows, sg.group)
+        w_bwd = sg._w[1] if sg._w is not None else None
+        gx, _ = ops._aggregate(sg.g_bwd.dst, "other", g_local, w_bwd, "sum", 0, None)
+        return gx, None, None
+
+
+def broadcast_parameters(module, src=0, group=None):
+    """Give every rank rank `src`'s parameter values (replicated layer weights,
+    as DDP does at construction)."""
+    for p in module.parameters():
+        with torch.no_grad():
+            if p.is_cuda and dist.get_backend(group) == "gloo":
+                t = p.detach().cpu()
+                dist.broadcast(t, src, group=group)
+                p.copy_(t)
+            else:
+                dist.broadcast(p.data, src, group=group)
+
+
+def allreduce_gradients(module, group=None):
+    """Sum the gradients of replicated parameters over the ranks (each rank's
+    weight gradient covers its own rows only), as DDP would."""
+    for p in module.parameters():
+        if p.grad is not None:
+            if p.grad.is_cuda and dist.get_backend(group) == "gloo":
+                t = p.grad.cpu()
+                dist.all_reduce(t, group=group)
+                p.grad.copy_(t)
+            else:
+                dist.all_reduce(p.grad, group=group)
+
+
+class ShardedGCNConv(torch.nn.Module):
+    """GCNConv [U5] over a ShardedGraph: this rank's rows of
+    D^-1/2 (A+I) D^-1/2 (X W) + b.  x_own holds the rank's rows of X; the X W
+    GEMM is local (hipBLASLt), the aggregation exchanges halo rows of X W
+    (forward) and of the output gradient (backward).  Parameters are
+    replicated: broadcast_parameters(module) once at setup, and after backward
+    allreduce_gradients(module) sums the weight and bias gradients over the
+    ranks.  Same parameter names and init as
+    GCNConv, so a GCNConv state_dict loads unchanged."""
+
+    def __init__(self, in_channels, out_channels, bias=True):
+        super().__init__()
+        from torch.nn import Parameter
+        from torch_geometric.nn.inits import glorot, zeros
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.weight = Parameter(torch.Tensor(in_channels, out_channels))
+        self.bias = Parameter(torch.Tensor(out_channels)) if bias else None
+        glorot(self.weight)
+        zeros(self.bias)
+
+    def forward(self, x_own, sg):
+        from . import ops
+        out = sg.propagate(ops.feature_transform(x_own, self.weight), "sum")
+        return out + self.bias if self.bias is not None else out
+
+    def __repr__(self):
+        return "{}({}, {})".format(self.__class__.__name__, self.in_channels, self.out_channels)

@@ -2,7 +2,9 @@
 exchange (mi355_mp.dist).  The local aggregation is the CPU oracle here (the
 GPU runs the same plan with the native kernel and RCCL); every rank's rows
 must equal the single-process oracle bit for bit, because a rank keeps its
-edges in global order and so sums every row in the same order."""
+edges in global order and so sums every row in the same order: sum, max/min
+with global argmax ids, and the backward of the sum (a forward over the
+transposed plan)."""
 import os
 import socket
 
@@ -43,12 +45,36 @@ def _worker(rank, world, port, result_q):
         def local_aggregate(xl, lei, n_dst, n_src, wl):
             return S.gather_sum(xl, lei[0], lei[1], wl, n_dst)
 
-        out = mdist.sharded_propagate(plan, x[plan.lo:plan.hi].contiguous(), local_aggregate,
-                                      lambda t, idx: t[idx], edge_weight=w)
+        rows = lambda t, idx: t[idx]  # noqa: E731
+        out = mdist.sharded_propagate(plan, x[plan.lo:plan.hi].contiguous(), local_aggregate, rows, edge_weight=w)
         want = S.gather_sum(x, ei[0], ei[1], w, N)[plan.lo:plan.hi]
         ok = torch.equal(out, want)
+        # max / min + arg: local args map to GLOBAL edge ids, first maximal edge wins
+        # (tie-heavy small integers, duplicate edges)
+        xi = torch.randint(-3, 4, (N, F), generator=g).to(torch.float32)
+        for red in ("max", "min"):
+            def local_arg(xl, lei, n_dst, n_src, wl, red=red):
+                return S.scatter_loop(xl[lei[0]], lei[1], n_dst, red)
+            o, a = mdist.sharded_propagate(plan, xi[plan.lo:plan.hi].contiguous(), local_arg, rows,
+                                           n_edges_global=E)
+            wo, wa = S.scatter_loop(xi[ei[0]], ei[1], N, red)
+            ok = ok and torch.equal(o, wo[plan.lo:plan.hi]) and torch.equal(a, wa[plan.lo:plan.hi])
+        # backward of the sum = a forward over the transposed plan: d x_j summed by
+        # j's owner in global edge order (bit-equal to the single-process transpose)
+        plan_t = mdist.transposed_plan(ei, N, rank, world, plan.cuts)
+        gout = torch.randn(N, F, generator=torch.Generator().manual_seed(99))
+
+        def local_t(xl, lei, n_dst, n_src, wl):
+            return S.gather_sum(xl, lei[1], lei[0], wl, n_dst)
+        gx = mdist.sharded_propagate(plan_t, gout[plan.lo:plan.hi].contiguous(), local_t, rows, edge_weight=w)
+        gwant = S.gather_sum(gout, ei[1], ei[0], w, N)[plan.lo:plan.hi]
+        ok_bwd = torch.equal(gx, gwant)
+        # return_halo: every halo row goes back to its owner, aligned with send_idx
+        back = plan.return_halo(x[plan.halo_nodes])
+        ok_ret = torch.equal(back, x[plan.send_idx + plan.lo])
         # edge balance: every rank holds about E / world edges
-        result_q.put((rank, ok, plan.lo, plan.hi, int(plan.edge_pos.numel()), plan.recv_counts))
+        result_q.put((rank, ok and ok_bwd and ok_ret, plan.lo, plan.hi, int(plan.edge_pos.numel()),
+                      plan.recv_counts, (ok, ok_bwd, ok_ret)))
     finally:
         dist.destroy_process_group()
 
