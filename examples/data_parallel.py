@@ -68,7 +68,7 @@ def main(argv=None):
             loss = F.nll_loss(output, y)
             loss.backward()
             optimizer.step()
-            losses.append(float(loss))
+            losses.append(float(loss.detach()))
         print("Outside Model: num graphs: {}, loss {:.4f}".format(output.size(0), losses[-1]))
     return losses
 

@@ -1087,7 +1087,8 @@ def test_feature_transform_split_k_weight_grad():
 
 def test_data_parallel_replicas_match_batched_model():
     """nn.DataParallel over a list of small graphs (the reference's
-    examples/data_parallel.py pattern) == the model on the whole Batch."""
+    examples/data_parallel.py pattern, ConvexPruning.py:530) with two real
+    replicas: outputs and parameter gradients == the model on the whole Batch."""
     import torch.nn.functional as Fn
     from torch_geometric.data import Data, Batch
     from torch_geometric.nn import DataParallel, GCNConv, global_mean_pool
@@ -1111,13 +1112,25 @@ def test_data_parallel_replicas_match_batched_model():
 
     torch.manual_seed(0)
     net = Net().to(DEV)
-    dp = DataParallel(net)
-    out = dp(graphs)
+    y = torch.cat([d.y for d in graphs]).to(DEV)
     ref = net(Batch.from_data_list(graphs).to(DEV))
-    assert out.shape == (12, 3) and torch.equal(out, ref)
-    loss = Fn.nll_loss(out, torch.cat([d.y for d in graphs]).to(DEV))
-    loss.backward()
-    assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in net.parameters())
+    Fn.nll_loss(ref, y).backward()
+    ref_grads = [p.grad.clone() for p in net.parameters()]
+    net.zero_grad()
+    # two replicas on the one device of the box: scatter -> replicate (parameter
+    # broadcast) -> parallel_apply (one host thread per replica) -> gather all run,
+    # and the backward reduces the replicas' gradients (ReduceAddCoalesced)
+    dp = DataParallel(net, device_ids=[0, 0])
+    chunks = dp.scatter(graphs, dp.device_ids)
+    assert len(chunks) == 2 and sum(c[0].num_graphs for c in chunks) == 12
+    out = dp(graphs)
+    assert out.shape == (12, 3)
+    assert torch.allclose(out, ref, rtol=1e-6, atol=1e-6)
+    Fn.nll_loss(out, y).backward()
+    for p, g0 in zip(net.parameters(), ref_grads):
+        assert p.grad is not None and torch.allclose(p.grad, g0, rtol=1e-5, atol=1e-6)
+    # a single device id takes the one-replica path: the model on the whole Batch
+    assert torch.equal(DataParallel(net)(graphs), ref)
 
 
 def test_gcn_aggregate_first_matches_reference_order():
@@ -1317,12 +1330,18 @@ def test_hip_graph_capture_of_gcn_forward_and_training_step():
     torch.manual_seed(3)
     net_g = Net().to(DEV)
     net_g.load_state_dict(net_e.state_dict())
+    y = d["y"].to(DEV)
+    loss_e = Fn.nll_loss(net_e(x), y)
+    loss_e.backward()
+    del loss_e                              # no eager autograd graph outlives its step
+    torch.cuda.synchronize()
     xg = x.clone().requires_grad_(False)
     graphed = torch.cuda.make_graphed_callables(net_g, (xg,))
-    y = d["y"].to(DEV)
-    for m in (net_e, graphed):
-        loss = Fn.nll_loss(m(x), y)
-        loss.backward()
+    net_g.zero_grad(set_to_none=True)       # drop the warm-up iterations' gradients
+    loss_g = Fn.nll_loss(graphed(x), y)
+    loss_g.backward()
+    del loss_g
+    torch.cuda.synchronize()
     for (n1, p1), (n2, p2) in zip(net_e.named_parameters(), net_g.named_parameters()):
         assert torch.allclose(p1.grad, p2.grad, rtol=1e-5, atol=1e-7), n1
 

@@ -6,9 +6,12 @@
   c5  ogbn-products-scale N=2,449,029 E=123,718,280 GCNConv F=256 (1 GPU)
 
 For each: dominant-kernel time (HIP events over back-to-back launches),
-edges/s, algorithmic GB/s with BASELINE.md's byte formulas, fraction of the
-8 TB/s spec.  One JSON line per config.
-    python tools/bench_configs.py [--configs c3,c4,c5]
+edges/s, algorithmic GB/s with BASELINE.md's byte formulas (no cache
+credit), compulsory-byte HBM fraction, and -- with --cpu-baseline -- the
+reference algorithm timed on the host on a bounded sample of the same edges
+(the CPU baseline leg, like bench.py's, is the only
+place the oracle is used).  One JSON line per config.
+    python tools/bench_configs.py [--configs c3,c4,c5] [--cpu-baseline]
 """
 import argparse
 import json
@@ -22,7 +25,10 @@ for p in (ROOT, os.path.join(ROOT, "pytorch_geometric-1_amd")):
 
 import torch  # noqa: E402
 
+from bench import cpu_info  # noqa: E402
+
 PEAK = 8000.0
+CPU_BASELINE = False
 
 
 def timed(fn, reps=10, rounds=3):
@@ -40,15 +46,100 @@ def timed(fn, reps=10, rounds=3):
     return sorted(per)[len(per) // 2]
 
 
-def report(name, desc, E, N, bpe, bpn, ms_main, ms_total, extra=None):
+def report(name, desc, E, N, bpe, bpn, ms_main, ms_total, extra=None, comp_bytes=None, cpu=None):
     alg = E * bpe + N * bpn
     gbs = alg / (ms_main * 1e-3) / 1e9
     line = {"config": name, "desc": desc, "num_nodes": N, "num_edges": E,
             "edges_per_s": E / (ms_total * 1e-3), "main_kernel_ms": ms_main, "aggregate_ms": ms_total,
-            "algorithmic_bytes": alg, "achieved_GBps": gbs, "frac_of_8TBps": gbs / PEAK}
+            "algorithmic_bytes": alg, "algorithmic_GBps_no_cache_credit": gbs}
+    if comp_bytes is not None:
+        line["compulsory_bytes"] = comp_bytes
+        line["roofline_frac_compulsory"] = comp_bytes / (ms_main * 1e-3) / 1e9 / PEAK
     if extra:
         line.update(extra)
+    if cpu is not None:
+        line["cpu_baseline"] = cpu
+        line["gpu_over_cpu"] = line["edges_per_s"] / cpu["value"]
     print(json.dumps(line), flush=True)
+
+
+def _cpu_threads():
+    model, threads, machine = cpu_info()
+    torch.set_num_threads(threads)
+    return model, threads, machine
+
+
+def cpu_sum_baseline(ei, w, x, sample):
+    """GCN sum: index_select -> norm * x_j -> scatter_add_,
+    4M-edge chunks in original edge order."""
+    import time
+    model, threads, machine = _cpu_threads()
+    E = min(sample, ei.shape[1])
+    eic, wc, xc = ei[:, :E].cpu(), w[:E].cpu(), x.cpu()
+    out = torch.zeros_like(xc)
+    t0 = time.perf_counter()
+    for s0 in range(0, E, 4_000_000):
+        e1 = min(E, s0 + 4_000_000)
+        msg = wc[s0:e1].view(-1, 1) * xc.index_select(0, eic[0, s0:e1])
+        out.scatter_add_(0, eic[1, s0:e1].view(-1, 1).expand_as(msg), msg)
+    dt = time.perf_counter() - t0
+    return {"value": E / dt, "unit": "edges/s", "cores": threads, "kind": "port", "cpu_model": model,
+            "machine_cpus": machine, "sample": "first %d of %d edges, torch CPU index_select+mul+scatter_add_ "
+            "(4M-edge chunks), %.1f s" % (E, ei.shape[1], dt)}
+
+
+def cpu_max_baseline(ei, x, sample):
+    """max + argmax: index_select (threaded) then torch_scatter 2.0.4's serial
+    CPU loop (scatter_cpu.cpp, restated in oracle/scatter_loop.c), 4M-edge chunks
+    accumulated through `out` (the loop's has_out path)."""
+    import time
+    from oracle import scatter_ref as S  # CPU-baseline leg only
+    model, threads, machine = _cpu_threads()
+    E = min(sample, ei.shape[1])
+    eic, xc = ei[:, :E].cpu(), x.cpu()
+    N, F = xc.shape
+    out = torch.full((N, F), -3.4028234663852886e38)
+    t_sel = t_loop = 0.0
+    for s0 in range(0, E, 4_000_000):
+        e1 = min(E, s0 + 4_000_000)
+        t0 = time.perf_counter()
+        msg = xc.index_select(0, eic[0, s0:e1])
+        t1 = time.perf_counter()
+        out, _ = S.scatter_loop(msg, eic[1, s0:e1], N, "max", out=out)
+        t_loop += time.perf_counter() - t1
+        t_sel += t1 - t0
+    dt = t_sel + t_loop
+    return {"value": E / dt, "unit": "edges/s", "cores": threads, "kind": "port", "cpu_model": model,
+            "machine_cpus": machine, "index_select_s": t_sel, "serial_loop_s": t_loop,
+            "sample": "first %d of %d edges: torch index_select (%d threads) + serial scatter_max loop "
+            "(1 thread, oracle/scatter_loop.c), %.1f s" % (E, ei.shape[1], threads, dt)}
+
+
+def cpu_gat_baseline(ei, xw, att, H, C, sample):
+    """GATConv's reference pipeline (oracle/pyg_ref.gat_conv after x @ W):
+    x_i / x_j index_select, (cat[x_i, x_j] * att).sum(-1), leaky_relu,
+    utils.softmax (serial scatter_max loop + scatter_add_), x_j * alpha,
+    scatter_add_ -- on the first `sample` edges."""
+    import time
+    import torch.nn.functional as Fn
+    from oracle import pyg_ref as P, scatter_ref as S  # CPU-baseline leg only
+    model, threads, machine = _cpu_threads()
+    E = min(sample, ei.shape[1])
+    eic, h = ei[:, :E].cpu(), xw.cpu()
+    N = h.shape[0]
+    a = att.cpu()
+    t0 = time.perf_counter()
+    x_i = h.index_select(0, eic[1]).view(-1, H, C)
+    x_j = h.index_select(0, eic[0]).view(-1, H, C)
+    alpha = (torch.cat([x_i, x_j], dim=-1) * a).sum(dim=-1)
+    alpha = Fn.leaky_relu(alpha, 0.2)
+    alpha = P.softmax(alpha, eic[1], N)
+    out = S.scatter_sum(x_j * alpha.view(-1, H, 1), eic[1], N)
+    dt = time.perf_counter() - t0
+    del out, x_i, x_j
+    return {"value": E / dt, "unit": "edges/s", "cores": threads, "kind": "port", "cpu_model": model,
+            "machine_cpus": machine, "sample": "first %d of %d edges, oracle GATConv pipeline (torch CPU ops + "
+            "serial scatter_max loop in the softmax), %.1f s" % (E, ei.shape[1], dt)}
 
 
 def c3(dev):
@@ -108,19 +199,22 @@ def c3(dev):
     path = "two_pass" if ops.gat_two_pass(csr, H, C) else "one_pass"
     tot1 = ms_main1 + ms_fix1 + ms_scores
     tot2 = ms_stats + ms_main + ms_fix + ms_scores
+    # compulsory: xw read once + a_src/a_dst + col + rowptr + out written once
+    comp = N * H * C * 4 * 2 + N * H * 8 + E * 4 + (N + 1) * 4
+    cpu = cpu_gat_baseline(ei, xw, att, H, C, 3_000_000) if CPU_BASELINE else None
     if path == "two_pass":
         report("c3", "RMAT21 GATConv heads=8 C=32: softmax row-stat passes + 64-feature-tile aggregation with the "
                "reference's alpha + bias (GATConv forward path)",
                E, N, 4 * H * C + 8 + 4 * H, 4 * H * C + 12 * H + 4, ms_main, tot2,
                {"stats_ms": ms_stats, "fixup_ms": ms_fix, "node_scores_ms": ms_scores, "n_split": csr.n_split,
                 "one_pass": {"main_kernel_ms": ms_main1, "fixup_ms": ms_fix1, "aggregate_ms": tot1},
-                "max_rel_diff_two_vs_one_pass": diff})
+                "max_rel_diff_two_vs_one_pass": diff}, comp, cpu)
     else:
         report("c3", "RMAT21 GATConv heads=8 C=32, fused leaky_relu+softmax(+1e-16)+aggregate+bias",
                E, N, 4 * H * C + 4 + 4 * H, 4 * H * C + 4 * H + 4, ms_main1, tot1,
                {"fixup_ms": ms_fix1, "node_scores_ms": ms_scores, "n_split": csr.n_split,
                 "two_pass": {"stats_ms": ms_stats, "main_kernel_ms": ms_main, "fixup_ms": ms_fix,
-                             "aggregate_ms": tot2}})
+                             "aggregate_ms": tot2}}, comp, cpu)
     # parity spot check against the generic PyG formula on identical inputs (one row block)
     del graph
 
@@ -149,10 +243,12 @@ def c4(dev):
                    "max")
     ms_main = timed(lambda: agg(_lib.MP_STAGE_MAIN))
     ms_fix = timed(lambda: agg(_lib.MP_STAGE_FIXUP))
+    comp = N * F * 4 + csr.n_edges * 4 + (N + 1) * 4 + N * F * 12
+    cpu = cpu_max_baseline(ei, x, 12_000_000) if CPU_BASELINE else None
     report("c4", "Reddit-scale power-law, aggr='max' + int64 first-index argmax, PyG -10000 mask",
            csr.n_edges, N, 4 * F + 4, 4 * F + 8 * F + 4, ms_main, ms_main + ms_fix,
            {"fixup_ms": ms_fix, "n_split": csr.n_split,
-            "note": "x is 238 MB: it fits the 256 MB Infinity Cache, so gathers are mostly on-die"})
+            "note": "x is 238 MB: it fits the 256 MB Infinity Cache, so gathers are mostly on-die"}, comp, cpu)
 
 
 def c5(dev):
@@ -176,8 +272,11 @@ def c5(dev):
         ops._aggregate(csr, "other", x, w, "sum", 0, bias, out=out, stages=stages, slab=slab)
     ms_main = timed(lambda: agg(_lib.MP_STAGE_MAIN))
     ms_fix = timed(lambda: agg(_lib.MP_STAGE_FIXUP))
+    comp = N * F * 8 + csr.n_edges * 8 + (N + 1) * 4
+    cpu = cpu_sum_baseline(ei2, norm, x, 40_000_000) if CPU_BASELINE else None
     report("c5", "ogbn-products-scale power-law GCNConv F=256 on ONE GPU", csr.n_edges, N,
-           4 * F + 8, 4 * F + 4, ms_main, ms_main + ms_fix, {"fixup_ms": ms_fix, "n_split": csr.n_split})
+           4 * F + 8, 4 * F + 4, ms_main, ms_main + ms_fix, {"fixup_ms": ms_fix, "n_split": csr.n_split}, comp,
+           cpu)
 
 
 def _train_step_ms(conv, x, ei):
@@ -313,7 +412,10 @@ def c1graph(dev):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="c3,c4,c5,c2train,c3train,c1graph")
+    ap.add_argument("--cpu-baseline", action="store_true")
     args = ap.parse_args()
+    global CPU_BASELINE
+    CPU_BASELINE = args.cpu_baseline
     import mi355_mp
     mi355_mp.load_native()
     dev = torch.device("cuda", 0)
