@@ -110,12 +110,17 @@ int mp_abi_version(void);
  *     flat kernel (default 64); narrower rows use lane groups / lane tasks.
  *   MP_TUNE_FLAT_MIN_F_ARG: the same for max/min (default 64).
  *   MP_TUNE_FLAT_NARROW_VEC1: 1 = flat rows of fewer than 128 features use
- *     64-feature tiles (VEC=1) instead of 128-feature tiles (default 0). */
+ *     64-feature tiles (VEC=1) instead of 128-feature tiles (default 0).
+ *   MP_TUNE_FLAT_VEC / MP_TUNE_FLAT_VEC_ARG: features per lane of the flat
+ *     kernel for sum/mean (below the VEC1 size threshold) and for max/min:
+ *     1, 2 (default) or 4 -- feature tiles of 64, 128 or 256. */
 #define MP_TUNE_FLAT_VEC1_MIN_BYTES 1
 #define MP_TUNE_FLAT_SMEM 2
 #define MP_TUNE_FLAT_MIN_F 3
 #define MP_TUNE_FLAT_MIN_F_ARG 4
 #define MP_TUNE_FLAT_NARROW_VEC1 5
+#define MP_TUNE_FLAT_VEC 6
+#define MP_TUNE_FLAT_VEC_ARG 7
 int64_t mp_tune(int32_t key, int64_t value);
 
 /* ---- CSR build (replaces the sort/bucketing torch_scatter never did: upstream

@@ -1518,6 +1518,8 @@ struct Tune {
   std::atomic<int64_t> flat_min_f{64};
   std::atomic<int64_t> flat_min_f_arg{64};
   std::atomic<int64_t> flat_narrow_vec1{0};
+  std::atomic<int64_t> flat_vec{2};
+  std::atomic<int64_t> flat_vec_arg{2};
 };
 static Tune g_tune;
 
@@ -1528,6 +1530,8 @@ static std::atomic<int64_t>* tune_slot(int32_t key) {
     case MP_TUNE_FLAT_MIN_F: return &g_tune.flat_min_f;
     case MP_TUNE_FLAT_MIN_F_ARG: return &g_tune.flat_min_f_arg;
     case MP_TUNE_FLAT_NARROW_VEC1: return &g_tune.flat_narrow_vec1;
+    case MP_TUNE_FLAT_VEC: return &g_tune.flat_vec;
+    case MP_TUNE_FLAT_VEC_ARG: return &g_tune.flat_vec_arg;
   }
   return nullptr;
 }
@@ -1570,7 +1574,7 @@ static int aggregate_dispatch(AggArgs& a, const mp_csr* g, int reduce, int stage
   // for sum/mean over a gathered x too large for the Infinity Cache, where an
   // XCD's L2 holding one narrow tile of the hot rows pays
   const int64_t xbytes = (int64_t)g->n_cols * a.ldx * 4;
-  int fvec = 2;
+  int fvec = (int)(is_arg ? tuned(g_tune.flat_vec_arg) : tuned(g_tune.flat_vec));
   if (!is_arg && xbytes >= tuned(g_tune.flat_vec1_min_bytes)) fvec = 1;
   if (F < 128 && tuned(g_tune.flat_narrow_vec1)) fvec = 1;
   // sum/mean: slot columns and weights through scalar loads (k_agg_flat SM),
@@ -1603,6 +1607,7 @@ int64_t mp_tune(int32_t key, int64_t value) {
   if (!v) return -1;
   if (value < 0) return v->load();
   if (key == MP_TUNE_FLAT_SMEM || key == MP_TUNE_FLAT_NARROW_VEC1) value = value ? 1 : 0;
+  if ((key == MP_TUNE_FLAT_VEC || key == MP_TUNE_FLAT_VEC_ARG) && value != 1 && value != 2 && value != 4) return -1;
   return v->exchange(value);
 }
 

@@ -73,6 +73,24 @@ def main():
             stall["ta_busy_frac"] = stall["TA_BUSY_avr"] / cyc
         if stall.get("SQ_WAVE_CYCLES"):
             stall["wave_waiting_frac"] = stall["SQ_WAIT_ANY"] / stall["SQ_WAVE_CYCLES"]
+    # memory side of the L2 (tools/profile.sh passes pmc_ea, pmc_lat)
+    mem = {}
+    for sub, names in (("pmc_ea", ("TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_DRAM_sum", "TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum",
+                                   "TCC_READ_REQ_LATENCY_sum")),
+                       ("pmc_lat", ("TCC_READ_REQ_sum", "TCC_TAG_STALL_sum", "TCC_LATENCY_FIFO_FULL_sum",
+                                    "TCC_BUSY_sum"))):
+        path = os.path.join(src, sub, "pmc_counter_collection.csv")
+        if os.path.exists(path):
+            for c in names:
+                mem[c], _ = per_launch(path, c)
+    if mem.get("TCC_READ_REQ_LATENCY_sum") and mem.get("TCC_READ_REQ_sum"):
+        mem["avg_l2_read_latency_cycles"] = mem["TCC_READ_REQ_LATENCY_sum"] / mem["TCC_READ_REQ_sum"]
+    if mem.get("TCC_EA0_RDREQ_DRAM_sum") and mem.get("TCC_EA0_RDREQ_sum"):
+        mem["dram_share_of_fabric_reads"] = mem["TCC_EA0_RDREQ_DRAM_sum"] / mem["TCC_EA0_RDREQ_sum"]
+    cyc = stall.get("kernel_cycles") if stall else None
+    if cyc and mem.get("TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum") is not None:
+        # summed over the 16 L2 channels of each of the 8 XCDs
+        mem["dram_credit_stall_frac_per_channel"] = mem["TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum"] / (128 * cyc)
     out = {
         "workload": "rmat21_gcn_f256",
         "kernel": KERNEL,
@@ -88,6 +106,7 @@ def main():
         "l2_hit_rate": hit / (hit + miss) if hit is not None and miss else None,
         "kernel_trace_avg_ms": avg_ns / 1e6 if avg_ns else None,
         "stall": stall or None,
+        "memory_side": mem or None,
         "note": "FETCH_SIZE counts L2->fabric reads (Infinity-Cache hits included): an upper bound "
                 "on HBM reads; doubled per the gfx950 correction (calibrated for this kernel's own "
                 "load width in profiles/r01_pmc_calibration.json)",

@@ -20,6 +20,10 @@ run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_agg_(main
 run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_agg_(main|flat)" -d $OUT/pmc_write -o pmc --output-format csv -- python3 $B
 run pmc_stall 600 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY TCP_PENDING_STALL_CYCLES_sum TCP_TCC_READ_REQ_sum TA_BUSY_avr --kernel-include-regex "k_agg_(main|flat)" -d $OUT/pmc_stall -o pmc --output-format csv -- python3 $B
 run pmc_l2 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "k_agg_(main|flat)" -d $OUT/pmc_l2 -o pmc --output-format csv -- python3 $B
+# memory-side requests: DRAM-targeted reads (Infinity-Cache hits still counted), DRAM credit
+# stalls (fabric back-pressure), accumulated L2 read latency
+run pmc_ea 600 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_READ_REQ_LATENCY_sum --kernel-include-regex "k_agg_(main|flat)" -d $OUT/pmc_ea -o pmc --output-format csv -- python3 $B
+run pmc_lat 600 rocprofv3 --pmc TCC_READ_REQ_sum TCC_TAG_STALL_sum TCC_LATENCY_FIFO_FULL_sum TCC_BUSY_sum --kernel-include-regex "k_agg_(main|flat)" -d $OUT/pmc_lat -o pmc --output-format csv -- python3 $B
 
 run pmc_calib 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_agg_(main|flat)" -d $OUT/pmc_calib -o pmc --output-format csv -- python3 tools/pmc_calibrate.py
 find $OUT -name "*.csv"
