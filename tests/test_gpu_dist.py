@@ -175,10 +175,11 @@ def test_sharded_gcnconv_forward_backward_on_one_gpu():
     kernel, and the max backward through return_halo."""
     res = _spawn(_layer_worker)
     for rank, r in res:
+        # tolerance only: the rank's x @ W has M = n_own rows, and hipBLASLt picks
+        # its GEMM kernel (and so its k-order) by M; d x also sums the local and the
+        # returned halo contributions separately.  The bitwise fractions are
+        # reported, not asserted (round 2 saw 0.93 / 0.70 on a fresh box).
         assert r["out"] < 1e-5 and r["gx"] < 1e-5, r
-        # same per-row arithmetic except rows split across merge-path tasks (the
-        # rank-local CSR has its own task boundaries): mostly bit-identical
-        assert r["out_bitwise_frac"] > 0.9 and r["gx_bitwise_frac"] > 0.9, r
         assert r["gw"] < 1e-5 and r["gb"] < 1e-5, r
         assert r["max_exact"], r
         assert r["gmax"] < 1e-4, r   # float atomics on both sides (argmax sources shared by rows)
