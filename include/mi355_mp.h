@@ -109,11 +109,14 @@ int mp_abi_version(void);
  *   MP_TUNE_FLAT_MIN_F: narrowest sum/mean row (features) that takes the
  *     flat kernel (default 64); narrower rows use lane groups / lane tasks.
  *   MP_TUNE_FLAT_MIN_F_ARG: the same for max/min (default 64).
- *   MP_TUNE_FLAT_NARROW_VEC1: 1 = flat rows of fewer than 128 features use
- *     64-feature tiles (VEC=1) instead of 128-feature tiles (default 0).
+ *   MP_TUNE_FLAT_NARROW_VEC1: flat rows of at most this many features use
+ *     64-feature tiles (VEC=1) whatever the other keys say (default 64: a
+ *     64-feature row fills one VEC=1 tile, where VEC=2 would idle half the lanes).
  *   MP_TUNE_FLAT_VEC / MP_TUNE_FLAT_VEC_ARG: features per lane of the flat
  *     kernel for sum/mean (below the VEC1 size threshold) and for max/min:
- *     1, 2 (default) or 4 -- feature tiles of 64, 128 or 256. */
+ *     1, 2 (default) or 4 -- feature tiles of 64, 128 or 256.
+ *   MP_TUNE_FLAT_SEQ_TILES: 1 = the flat kernel's feature tiles run one after
+ *     another on all eight XCDs; 0 (default) = XCD-affine tiles. */
 #define MP_TUNE_FLAT_VEC1_MIN_BYTES 1
 #define MP_TUNE_FLAT_SMEM 2
 #define MP_TUNE_FLAT_MIN_F 3
@@ -121,6 +124,7 @@ int mp_abi_version(void);
 #define MP_TUNE_FLAT_NARROW_VEC1 5
 #define MP_TUNE_FLAT_VEC 6
 #define MP_TUNE_FLAT_VEC_ARG 7
+#define MP_TUNE_FLAT_SEQ_TILES 8
 int64_t mp_tune(int32_t key, int64_t value);
 
 /* ---- CSR build (replaces the sort/bucketing torch_scatter never did: upstream

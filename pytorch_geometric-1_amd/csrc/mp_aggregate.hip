@@ -87,6 +87,7 @@ struct AggArgs {
   int32_t flat;      // sum/mean/max/min: run k_agg_flat instead of k_agg_main
   int32_t fix4;      // VEC=2 main kernel: run the fix-up at VEC=4 (slabs are indexed by feature)
   int32_t smem;      // flat sum/mean kernel: slot columns/weights through scalar loads (k_agg_flat SM)
+  int32_t seq_tiles; // flat kernel: feature tiles one after another on all XCDs (no XCD-affine map)
   // features
   const float* w;
   const float* x;
@@ -1114,7 +1115,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
   int bx = (int)blockIdx.x, tile = (int)blockIdx.y;
   if constexpr (kXcdTiles) {  // see k_agg_main: one feature tile per XCD
     const int T = (int)gridDim.y;
-    if (8 % T == 0) {  // the host pads the grid to a multiple of 8/T blocks per tile
+    if (8 % T == 0 && !p.seq_tiles) {  // the host pads the grid to a multiple of 8/T blocks per tile
       const int b = (int)(blockIdx.y * gridDim.x + blockIdx.x);
       const int xcd = b & 7;
       tile = xcd % T;
@@ -1517,9 +1518,10 @@ struct Tune {
   std::atomic<int64_t> flat_smem{1};
   std::atomic<int64_t> flat_min_f{64};
   std::atomic<int64_t> flat_min_f_arg{64};
-  std::atomic<int64_t> flat_narrow_vec1{0};
+  std::atomic<int64_t> flat_narrow_vec1{64};  // F=64: one full 64-feature tile, -26% vs a half-used 128 tile
   std::atomic<int64_t> flat_vec{2};
   std::atomic<int64_t> flat_vec_arg{2};
+  std::atomic<int64_t> flat_seq_tiles{0};
 };
 static Tune g_tune;
 
@@ -1532,6 +1534,7 @@ static std::atomic<int64_t>* tune_slot(int32_t key) {
     case MP_TUNE_FLAT_NARROW_VEC1: return &g_tune.flat_narrow_vec1;
     case MP_TUNE_FLAT_VEC: return &g_tune.flat_vec;
     case MP_TUNE_FLAT_VEC_ARG: return &g_tune.flat_vec_arg;
+    case MP_TUNE_FLAT_SEQ_TILES: return &g_tune.flat_seq_tiles;
   }
   return nullptr;
 }
@@ -1575,12 +1578,23 @@ static int aggregate_dispatch(AggArgs& a, const mp_csr* g, int reduce, int stage
   // XCD's L2 holding one narrow tile of the hot rows pays
   const int64_t xbytes = (int64_t)g->n_cols * a.ldx * 4;
   int fvec = (int)(is_arg ? tuned(g_tune.flat_vec_arg) : tuned(g_tune.flat_vec));
-  if (!is_arg && xbytes >= tuned(g_tune.flat_vec1_min_bytes)) fvec = 1;
-  if (F < 128 && tuned(g_tune.flat_narrow_vec1)) fvec = 1;
+  // The L1 miss queue holds 256-B segments: a 64-feature
+  // tile of a row that does not start on a 256-B boundary straddles two of
+  // them.  Such rows take the widest per-lane vector the layout allows, which
+  // touches the fewest segments per row (F=200: 8.43 -> 6.93 ms sum, 8.34 ->
+  // 7.16 ms max; F=130 sum 6.78 -> 6.44 ms on RMAT21).
+  const bool seg_aligned = (a.ldx * 4) % 256 == 0 && (uintptr_t)a.x % 256 == 0;
+  if (!seg_aligned) {
+    fvec = sh.vec;
+  } else {
+    if (!is_arg && xbytes >= tuned(g_tune.flat_vec1_min_bytes)) fvec = 1;
+    if (F <= tuned(g_tune.flat_narrow_vec1)) fvec = 1;
+  }
   // sum/mean: slot columns and weights through scalar loads (k_agg_flat SM),
   // 32-bit buffer offsets (soffset + lane offset) while x spans < 4 GiB
   a.smem = tuned(g_tune.flat_smem) && !is_arg && a.col != nullptr && g->n_cols > 0 && xbytes <= 0xFFFFFFF0LL;
   if (a.smem) a.x_bytes = (uint32_t)xbytes;
+  a.seq_tiles = (int32_t)tuned(g_tune.flat_seq_tiles);
   const int64_t min_f = is_arg ? tuned(g_tune.flat_min_f_arg) : tuned(g_tune.flat_min_f);
   if (F >= min_f && F % fvec == 0 && sh.vec >= fvec) {
     sh.vec = fvec;  // narrow feature tiles, slot batches across rows
@@ -1606,7 +1620,7 @@ int64_t mp_tune(int32_t key, int64_t value) {
   std::atomic<int64_t>* v = tune_slot(key);
   if (!v) return -1;
   if (value < 0) return v->load();
-  if (key == MP_TUNE_FLAT_SMEM || key == MP_TUNE_FLAT_NARROW_VEC1) value = value ? 1 : 0;
+  if (key == MP_TUNE_FLAT_SMEM || key == MP_TUNE_FLAT_SEQ_TILES) value = value ? 1 : 0;
   if ((key == MP_TUNE_FLAT_VEC || key == MP_TUNE_FLAT_VEC_ARG) && value != 1 && value != 2 && value != 4) return -1;
   return v->exchange(value);
 }

@@ -182,10 +182,16 @@ def test_fused_sum_mean_64_feature_tiles(F, chunk):
     w = torch.rand(E, generator=g)
     graph = Graph(ei.to(DEV), N, N, chunk=chunk)
     eid = ei.to(DEV)
-    base = {r: ops.fused_propagate(graph, x.to(DEV), eid, w.to(DEV), r).cpu() for r in ("sum", "mean")}
+    # rows on 256-B boundaries (row stride a multiple of 64 floats): otherwise the
+    # dispatcher takes the widest lane vector whatever the tune table says
+    ld = -(-F // 64) * 64
+    xd = torch.zeros(N, ld, device=DEV)[:, :F]
+    xd.copy_(x)
+    assert xd.stride(0) % 64 == 0 and xd.data_ptr() % 256 == 0
+    base = {r: ops.fused_propagate(graph, xd, eid, w.to(DEV), r).cpu() for r in ("sum", "mean")}
     prev = lib.mp_tune(_lib.MP_TUNE_FLAT_VEC1_MIN_BYTES, 0)
     try:
-        got = {r: ops.fused_propagate(graph, x.to(DEV), eid, w.to(DEV), r).cpu() for r in ("sum", "mean")}
+        got = {r: ops.fused_propagate(graph, xd, eid, w.to(DEV), r).cpu() for r in ("sum", "mean")}
     finally:
         lib.mp_tune(_lib.MP_TUNE_FLAT_VEC1_MIN_BYTES, prev)
     assert lib.mp_tune(_lib.MP_TUNE_FLAT_VEC1_MIN_BYTES, -1) == prev
@@ -196,6 +202,63 @@ def test_fused_sum_mean_64_feature_tiles(F, chunk):
     split = set(_split_rows(graph.dst))
     whole = torch.tensor([r for r in range(N) if r not in split], dtype=torch.long)
     assert torch.equal(got["sum"][whole], want[whole])
+
+
+@pytest.mark.parametrize("F", [130, 200, 250, 602])
+@pytest.mark.parametrize("reduce", ["sum", "mean", "max"])
+def test_unaligned_rows_widest_vector_bitwise_equal(F, reduce):
+    """Rows whose stride is not a multiple of 256 B take the widest per-lane
+    vector (fewest 256-B segments per gathered row); the same rows laid out on
+    256-B boundaries take 64/128-feature tiles.  Same per-feature arithmetic in
+    the same slot order: outputs (and argmax) bitwise equal, and equal to the
+    oracle on rows not split across tasks."""
+    _, ops, _, Graph, pl = _mods()
+    from mi355_mp import _lib
+    N, E = 800, 12000
+    ei = pl(N, E, seed=F + 5)
+    g = torch.Generator().manual_seed(F + 5)
+    x = torch.randint(-4, 5, (N, F), generator=g).to(torch.float32) if reduce == "max" else torch.randn(N, F, generator=g)
+    w = torch.rand(E, generator=g)
+    graph = Graph(ei.to(DEV), N, N, chunk=64)
+    eid = ei.to(DEV)
+    xu = x.to(DEV)                                   # stride F: unaligned rows
+    ld = -(-F // 64) * 64
+    xa = torch.zeros(N, ld, device=DEV)[:, :F]       # stride multiple of 64 floats
+    xa.copy_(x)
+    lib = _lib.load()
+    # aligned rows: force 64-feature tiles, so the two layouts run different shapes
+    keys = {_lib.MP_TUNE_FLAT_VEC1_MIN_BYTES: 0, _lib.MP_TUNE_FLAT_VEC_ARG: 1}
+    prev = {k: lib.mp_tune(k, v) for k, v in keys.items()}
+    try:
+        names = []
+        for xx in (xu, xa):
+            out = torch.empty(N, F, device=DEV)
+            buf = __import__("ctypes").create_string_buffer(512)
+            _lib.check(lib.mp_aggregate_kernel_name(graph.dst.struct("other"), 0, xx.data_ptr(), xx.stride(0), F,
+                                                    _lib.MP_REDUCE[reduce], 0, out.data_ptr(), out.stride(0), buf,
+                                                    512, torch.cuda.current_stream().cuda_stream), "kernel_name")
+            names.append(buf.value.decode())
+        assert names[0] != names[1] and "k_agg_flat" in names[1] and ", 1, 16, 64" in names[1], names
+        if reduce == "max":
+            ou, au = ops._aggregate(graph.dst, "other", xu, None, "max", 0, None)
+            oa, aa = ops._aggregate(graph.dst, "other", xa, None, "max", 0, None)
+        else:
+            ou = ops.fused_propagate(graph, xu, eid, w.to(DEV), reduce).cpu()
+            oa = ops.fused_propagate(graph, xa, eid, w.to(DEV), reduce).cpu()
+    finally:
+        for k, v in prev.items():
+            lib.mp_tune(k, v)
+    if reduce == "max":
+        assert torch.equal(ou, oa) and torch.equal(au, aa)
+        wm, wa = S.gather_max(x, ei[0], ei[1], N)
+        assert torch.equal(ou.cpu(), wm) and torch.equal(au.cpu(), wa)
+        return
+    assert torch.equal(ou, oa)
+    if reduce == "sum":
+        want = S.gather_sum(x, ei[0], ei[1], w, N)
+        split = set(_split_rows(graph.dst))
+        whole = torch.tensor([r for r in range(N) if r not in split], dtype=torch.long)
+        assert torch.equal(ou[whole], want[whole])
 
 
 @pytest.mark.parametrize("F,N,E", [(256, 700, 9000), (300, 700, 9000), (512, 300, 4000), (256, 5, 7), (256, 40, 17),
@@ -1336,12 +1399,22 @@ def test_hip_graph_capture_of_gcn_forward_and_training_step():
     del loss_e                              # no eager autograd graph outlives its step
     torch.cuda.synchronize()
     xg = x.clone().requires_grad_(False)
-    graphed = torch.cuda.make_graphed_callables(net_g, (xg,))
-    net_g.zero_grad(set_to_none=True)       # drop the warm-up iterations' gradients
-    loss_g = Fn.nll_loss(graphed(x), y)
-    loss_g.backward()
-    del loss_g
-    torch.cuda.synchronize()
+    # make_graphed_callables warms up (and creates the parameters' AccumulateGrad
+    # nodes) on its own side stream, while the captured backward then feeds them
+    # from the replay stream: torch warns about the stream change of those nodes.
+    # The synchronisation it inserts is what makes the gradients correct here, so
+    # the warning is silenced for this block only.
+    warn = torch.autograd.graph.set_warn_on_accumulate_grad_stream_mismatch
+    warn(False)
+    try:
+        graphed = torch.cuda.make_graphed_callables(net_g, (xg,))
+        net_g.zero_grad(set_to_none=True)   # drop the warm-up iterations' gradients
+        loss_g = Fn.nll_loss(graphed(x), y)
+        loss_g.backward()
+        del loss_g
+        torch.cuda.synchronize()
+    finally:
+        warn(True)
     for (n1, p1), (n2, p2) in zip(net_e.named_parameters(), net_g.named_parameters()):
         assert torch.allclose(p1.grad, p2.grad, rtol=1e-5, atol=1e-7), n1
 
