@@ -205,6 +205,15 @@ int mp_gat_aggregate_f32(const mp_csr* g, const float* xw, const float* a_src,
                          const float* bias, float* out, int64_t ldo,
                          float* row_stats, void* slab, size_t slab_bytes,
                          int32_t stages, void* stream);
+/* The same with att [H, 2C] (GATConv.att): where C % 4 == 0 and C/4 is a
+ * power of two <= 64, the kernel recomputes a_src[j,h] from each gathered xw
+ * row (bitwise the value mp_gat_node_scores_f32 stores) instead of gathering
+ * it; other shapes, or att == NULL, read a_src. */
+int mp_gat_aggregate_att_f32(const mp_csr* g, const float* xw, const float* a_src,
+                             const float* a_dst, const float* att, int32_t H,
+                             int32_t C, float slope, const float* bias, float* out,
+                             int64_t ldo, float* row_stats, void* slab,
+                             size_t slab_bytes, int32_t stages, void* stream);
 
 /* Two-pass form of the same layer, in the reference's own arithmetic
  * (utils.softmax [U3] then message x_j * alpha and scatter_add in edge order,

@@ -323,11 +323,19 @@ struct ArgRed {
 // GATConv [U6] + utils.softmax [U3], online: per (row, head) running max m,
 // denominator s and accumulator acc, rescaled when the max grows.  Every lane
 // of a head carries the same m/s (no cross-lane traffic).
-template <int VEC>
+//
+// OWN: a_src[j, h] is recomputed from the gathered row itself,
+//   a_src[j,h] = <xw[j,h,:], att[h,C:2C]>  (lane partial of its VEC features,
+// then group_sum over the head's lanes -- the same arithmetic, in the same
+// order, as k_gat_node_scores_wave, so bitwise the value that kernel stores).
+// It saves the per-slot a_src gather (one 256-B L1-queue segment per slot on
+// top of the row's four).
+template <int VEC, bool OWN = false>
 struct GatRed {
   static constexpr bool kW = false;
   static constexpr bool kEid = false;
   static constexpr bool kGat = true;
+  static constexpr bool kOwnAs = OWN;
   static constexpr bool kHW = false;
   static constexpr bool kGatB = false;
   static constexpr bool kStat = true;
@@ -338,8 +346,26 @@ struct GatRed {
   float acc[VEC];
   float m, s, ad;
   int h;
+  [[maybe_unused]] float y[OWN ? VEC : 1];
+  [[maybe_unused]] int hl = 1;
 
-  __device__ GatRed(const AggArgs& p, int f, bool act) : h(act ? f / p.C : 0) {}
+  __device__ GatRed(const AggArgs& p, int f, bool act) : h(act ? f / p.C : 0) {
+    if constexpr (OWN) {
+      hl = p.C / VEC;
+      const int c = act ? f % p.C : 0;
+      Frag<VEC> o = load_frag<VEC>(p.att + (int64_t)h * 2 * p.C + p.C + c);
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) y[k] = act ? o.v[k] : 0.f;
+    }
+  }
+  // <row, att_src> over the head's lanes: v.x*y.x + v.y*y.y + ... separately
+  // rounded left to right (-ffp-contract=off), then group_sum
+  __device__ __forceinline__ float own_as(const Frag<VEC>& v) const {
+    float t = v.v[0] * y[0];
+#pragma unroll
+    for (int k = 1; k < VEC; ++k) t = t + v.v[k] * y[k];
+    return group_sum(t, hl);
+  }
 
   __device__ __forceinline__ void begin(const AggArgs& p, int64_t row, bool, int, bool) {
 #pragma unroll
@@ -865,8 +891,12 @@ struct GatAlphaWin {
 // For L = 64 the row address is a uniform base (SGPR pair) + one shared
 // 32-bit lane offset, so U rows cost U*VEC data VGPRs only.
 // GAT forward: a_src of each 64-slot window staged in LDS (see SlotWin; 8.85 -> 8.66 ms, bitwise the same)
+template <class Red>
+constexpr bool own_as_v = false;
+template <int VEC>
+constexpr bool own_as_v<GatRed<VEC, true>> = true;
 template <class Red, int L>
-constexpr bool kGatWin = Red::kGat && L == 64;
+constexpr bool kGatWin = Red::kGat && !own_as_v<Red> && L == 64;
 
 template <class Red, int VEC, int U, int L>
 __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p,
@@ -894,7 +924,7 @@ __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p,
       if constexpr (Red::kHW) hw[u] = p.w[(e + uu) * p.H + red.h];
       const int c = GR::bc(win.col, off + uu);
       v[u] = load_frag<VEC>(reinterpret_cast<const float*>(xb + (int64_t)c * ldxb + foff));
-      if constexpr (Red::kGat) as[u] = win.a_src_of(p, off + uu, c, red.h);
+      if constexpr (Red::kGat && !own_as_v<Red>) as[u] = win.a_src_of(p, off + uu, c, red.h);
       if constexpr (Red::kGatB) pk[u] = p.pack[(int64_t)c * p.H + red.h];
     }
     if constexpr (Red::kGatB) {
@@ -905,7 +935,9 @@ __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p,
     for (int u = 0; u < U; ++u) {
       if (u < n) {
         if constexpr (Red::kGat) {
-          red.consume_gat(p, v[u], as[u]);
+          // own_as next to its consume: slot u waits only for its own row
+          if constexpr (own_as_v<Red>) red.consume_gat(p, v[u], red.own_as(v[u]));
+          else red.consume_gat(p, v[u], as[u]);
         } else if constexpr (Red::kGatB) {
           red.consume_gatb(p, v[u], as[u], pk[u], GR::bc(win.eid, off + u));
         } else {
@@ -1743,6 +1775,14 @@ int mp_gat_aggregate_f32(const mp_csr* g, const float* xw, const float* a_src, c
                          int32_t H, int32_t C, float slope, const float* bias, float* out,
                          int64_t ldo, float* row_stats, void* slab, size_t slab_bytes,
                          int32_t stages, void* stream) {
+  return mp_gat_aggregate_att_f32(g, xw, a_src, a_dst, nullptr, H, C, slope, bias, out, ldo, row_stats, slab,
+                                  slab_bytes, stages, stream);
+}
+
+int mp_gat_aggregate_att_f32(const mp_csr* g, const float* xw, const float* a_src, const float* a_dst,
+                             const float* att, int32_t H, int32_t C, float slope, const float* bias, float* out,
+                             int64_t ldo, float* row_stats, void* slab, size_t slab_bytes, int32_t stages,
+                             void* stream) {
   MP_DEVICE_GUARD(stream);
   int rc = check_graph(g, "mp_gat_aggregate_f32");
   if (rc) return rc;
@@ -1774,6 +1814,13 @@ int mp_gat_aggregate_f32(const mp_csr* g, const float* xw, const float* a_src, c
   int vec = pick_shape(F, F, xw, ldo, out).vec;
   if (vec == 2 && F <= 64) vec = 1;
   while (vec > 1 && C % vec != 0) vec >>= 1;  // a lane's features must share a head
+  // a_src from the gathered rows: the node-score kernel's 4-feature lane
+  // partials and head groups of C/4 lanes (a power of two <= 64)
+  const int hl4 = C / 4;
+  if (att && vec == 4 && C % 4 == 0 && hl4 <= 64 && (hl4 & (hl4 - 1)) == 0 && (uintptr_t)att % 16 == 0) {
+    a.att = att;
+    return launch<GatRed<4, true>, 4>(a, stages, s, F >= 256 ? kGatLanes : 64);
+  }
   switch (vec) {
     case 4: return launch<GatRed<4>, 4>(a, stages, s, F >= 256 ? kGatLanes : 64);
     case 2: return launch<GatRed<2>, 2>(a, stages, s);

@@ -123,10 +123,9 @@ __global__ __launch_bounds__(256) void k_gat_node_scores_wave(const float* __res
         sd = v.x * ad.x + v.y * ad.y + v.z * ad.z + v.w * ad.w;
         ss = v.x * as.x + v.y * as.y + v.z * as.z + v.w * as.w;
       }
-      for (int o = G >> 1; o > 0; o >>= 1) {
-        sd += __shfl_xor(sd, o);
-        ss += __shfl_xor(ss, o);
-      }
+      // the reduction GatRed<4, true>::own_as repeats per gathered row (bitwise)
+      sd = group_sum(sd, G);
+      ss = group_sum(ss, G);
       if (f < HC && (lane & (G - 1)) == 0) {
         a_dst[n * H + h] = sd;
         a_src[n * H + h] = ss;

@@ -359,6 +359,9 @@ def gcn_norm_weights(edge_index, num_nodes, edge_weight=None):
 # (one a_src gather per slot per tile), against 8.6 ms for the single pass
 # (DESIGN.md section 3.3).
 GAT_TWO_PASS = False
+# The single pass recomputes a_src[j] from each gathered xw row (bitwise the
+# node-score kernel's value) instead of gathering it: mp_gat_aggregate_att_f32.
+GAT_OWN_A_SRC = True
 
 
 def gat_two_pass(csr, H, C):
@@ -390,10 +393,11 @@ def _gat_forward(graph, edge_index, xw, att, H, C, slope, bias, want_alpha):
                                                     out.data_ptr(), out.stride(0), stats.data_ptr(), slab.data_ptr(),
                                                     sb, _lib.MP_STAGE_ALL, st), "mp_gat_softmax_aggregate_f32")
     else:
-        _lib.check(lib.mp_gat_aggregate_f32(g, xw.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(), H, C,
-                                            float(slope), _lib.ptr(bias), out.data_ptr(), out.stride(0),
-                                            stats.data_ptr(), slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
-                   "mp_gat_aggregate_f32")
+        _lib.check(lib.mp_gat_aggregate_att_f32(g, xw.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(),
+                                                att_c.data_ptr() if GAT_OWN_A_SRC else None, H, C, float(slope),
+                                                _lib.ptr(bias), out.data_ptr(), out.stride(0), stats.data_ptr(),
+                                                slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
+                   "mp_gat_aggregate_att_f32")
     alpha = None
     if want_alpha:
         E = edge_index.shape[1]

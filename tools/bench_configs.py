@@ -170,9 +170,11 @@ def c3(dev):
                                               a_dst.data_ptr(), st), "scores")
 
     def agg(stages):
-        _lib.check(lib.mp_gat_aggregate_f32(s, xw.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(), H, C, 0.2,
-                                            bias.data_ptr(), out.data_ptr(), H * C, None, slab.data_ptr(), sb,
-                                            stages, st), "gat")
+        # the GATConv forward path: a_src recomputed from the gathered rows (ops.GAT_OWN_A_SRC)
+        _lib.check(lib.mp_gat_aggregate_att_f32(s, xw.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(),
+                                                att_c.data_ptr() if ops.GAT_OWN_A_SRC else None, H, C, 0.2,
+                                                bias.data_ptr(), out.data_ptr(), H * C, None, slab.data_ptr(), sb,
+                                                stages, st), "gat")
     stats = torch.empty(N, H, 2, device=dev)
     sr = csr.slot_rows()
 
