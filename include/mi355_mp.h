@@ -100,8 +100,8 @@ int mp_abi_version(void);
  * only the kernel shape changes.  "Flat kernel" = k_agg_flat, the
  * sum/mean/max/min kernel whose tasks stream their slots across row ends.
  *   MP_TUNE_FLAT_VEC1_MIN_BYTES: flat sum/mean over a gathered x of at least
- *     this many bytes use 64-feature tiles (VEC=1); smaller x keeps
- *     128-feature tiles (VEC=2).  Default 1 GiB.
+ *     this many bytes use 64-feature tiles (VEC=1); smaller x uses
+ *     MP_TUNE_FLAT_VEC.  Default 0 (always 64-feature tiles).
  *   MP_TUNE_FLAT_SMEM: 1 (default) = the flat sum/mean kernel reads slot
  *     columns / weights through scalar-cache batches and gathers with 32-bit
  *     buffer offsets whenever the gathered x spans < 4 GiB; 0 = the per-lane

@@ -1546,7 +1546,7 @@ static int64_t slab_ld_for(int F) { return ceil_div(F, 256) * 256; }
 // bitwise-identical results.
 // ---------------------------------------------------------------------------
 struct Tune {
-  std::atomic<int64_t> flat_vec1_min_bytes{1ll << 30};  // 4x the 256 MB Infinity Cache
+  std::atomic<int64_t> flat_vec1_min_bytes{0};  // sum/mean: 64-feature tiles at every x size (scalar batches)
   std::atomic<int64_t> flat_smem{1};
   std::atomic<int64_t> flat_min_f{64};
   std::atomic<int64_t> flat_min_f_arg{64};
@@ -1605,9 +1605,11 @@ static int aggregate_dispatch(AggArgs& a, const mp_csr* g, int reduce, int stage
   const int F = a.F;
   const bool is_arg = reduce == MP_REDUCE_MAX || reduce == MP_REDUCE_MIN;
   Shape sh = pick_shape(F, a.ldx, a.x, a.ldo, a.out);
-  // flat kernel lane width: 128-feature tiles (VEC=2); 64-feature tiles (VEC=1)
-  // for sum/mean over a gathered x too large for the Infinity Cache, where an
-  // XCD's L2 holding one narrow tile of the hot rows pays
+  // flat kernel lane width: 64-feature tiles (VEC=1) for sum/mean, where an
+  // XCD's L2 holding one narrow tile of the hot rows pays (Reddit-scale x of
+  // 238 MB: 8.28 -> 7.25 ms; RMAT21 x of 2 GB 6.98 -> 6.73 ms); 128-feature
+  // tiles (VEC=2) for max/min, whose compare-and-select per element is bound
+  // by the texture-address unit rather than by L2 misses (VEC=1: +15..29%)
   const int64_t xbytes = (int64_t)g->n_cols * a.ldx * 4;
   int fvec = (int)(is_arg ? tuned(g_tune.flat_vec_arg) : tuned(g_tune.flat_vec));
   // The L1 miss queue holds 256-B segments: a 64-feature
@@ -1623,7 +1625,10 @@ static int aggregate_dispatch(AggArgs& a, const mp_csr* g, int reduce, int stage
     if (F <= tuned(g_tune.flat_narrow_vec1)) fvec = 1;
   }
   // sum/mean: slot columns and weights through scalar loads (k_agg_flat SM),
-  // 32-bit buffer offsets (soffset + lane offset) while x spans < 4 GiB
+  // 32-bit buffer offsets (soffset + lane offset) while x spans < 4 GiB.
+  // (Max/min through the same batches, edge ids included: bitwise equal and
+  // no faster -- Reddit-scale 8.67 vs 8.67 ms, RMAT21 7.77 vs 7.76 ms,
+  // profiles/r02_ab_smem_arg.log -- so they keep the slot window.)
   a.smem = tuned(g_tune.flat_smem) && !is_arg && a.col != nullptr && g->n_cols > 0 && xbytes <= 0xFFFFFFF0LL;
   if (a.smem) a.x_bytes = (uint32_t)xbytes;
   a.seq_tiles = (int32_t)tuned(g_tune.flat_seq_tiles);

@@ -167,11 +167,10 @@ def test_fused_sum_mean(F, chunk, weighted):
 @pytest.mark.parametrize("F", [64, 130, 256, 300, 512])
 @pytest.mark.parametrize("chunk", [16, 256])
 def test_fused_sum_mean_64_feature_tiles(F, chunk):
-    """Sum/mean of >= 256-feature rows over a gathered x of >= 1 GiB run the
-    flat kernel with 64-feature tiles (VEC=1); mp_tune forces that shape on a
-    small graph (F = 64 / 130: the 64..255-feature flat route, including a
-    partial last tile).  Same arithmetic per feature: bitwise equal to the
-    default 128-feature-tile shape and to the oracle on unsplit rows."""
+    """Sum/mean run the flat kernel with 64-feature tiles (VEC=1, the default;
+    F = 64 / 130: the 64..255-feature flat route, including a partial last
+    tile).  Same arithmetic per feature: bitwise equal to the 128-feature-tile
+    shape (forced through mp_tune) and to the oracle on unsplit rows."""
     _, ops, _, Graph, pl = _mods()
     from mi355_mp import _lib
     lib = _lib.load()
@@ -188,10 +187,10 @@ def test_fused_sum_mean_64_feature_tiles(F, chunk):
     xd = torch.zeros(N, ld, device=DEV)[:, :F]
     xd.copy_(x)
     assert xd.stride(0) % 64 == 0 and xd.data_ptr() % 256 == 0
-    base = {r: ops.fused_propagate(graph, xd, eid, w.to(DEV), r).cpu() for r in ("sum", "mean")}
-    prev = lib.mp_tune(_lib.MP_TUNE_FLAT_VEC1_MIN_BYTES, 0)
+    got = {r: ops.fused_propagate(graph, xd, eid, w.to(DEV), r).cpu() for r in ("sum", "mean")}
+    prev = lib.mp_tune(_lib.MP_TUNE_FLAT_VEC1_MIN_BYTES, 1 << 62)   # 128-feature tiles
     try:
-        got = {r: ops.fused_propagate(graph, xd, eid, w.to(DEV), r).cpu() for r in ("sum", "mean")}
+        base = {r: ops.fused_propagate(graph, xd, eid, w.to(DEV), r).cpu() for r in ("sum", "mean")}
     finally:
         lib.mp_tune(_lib.MP_TUNE_FLAT_VEC1_MIN_BYTES, prev)
     assert lib.mp_tune(_lib.MP_TUNE_FLAT_VEC1_MIN_BYTES, -1) == prev

@@ -50,7 +50,7 @@ def test_tuning_knob_set_query_restore(lib):
     from mi355_mp import _lib
     k = _lib.MP_TUNE_FLAT_VEC1_MIN_BYTES
     default = lib.mp_tune(k, -1)
-    assert default == 1 << 30
+    assert default == 0
     assert lib.mp_tune(k, 123) == default
     assert lib.mp_tune(k, -1) == 123
     assert lib.mp_tune(k, default) == 123
