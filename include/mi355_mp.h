@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MP_ABI_VERSION 1
+#define MP_ABI_VERSION 2
 
 /* status codes */
 #define MP_OK 0
@@ -89,6 +89,10 @@ typedef struct mp_csr {
   int32_t n_split;
   int32_t n_cols;   /* rows of the gathered x; must be > 0 whenever col != NULL (MP_ERR_ARG
                        otherwise).  It bounds the 32-bit buffer offsets of the gather. */
+  int64_t n_ids;    /* size of the edge-id space the eid array indexes: the arg an empty
+                       max/min row reports (torch_scatter's src.size(0)).  0 = n_edges.  A CSR
+                       whose slots are a subset of the edges (first occurrences of repeated
+                       (row, column) pairs) sets it to the full edge count.  (ABI 2) */
 } mp_csr;
 
 const char* mp_last_error(void);

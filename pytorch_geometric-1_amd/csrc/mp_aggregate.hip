@@ -78,6 +78,7 @@ struct AggArgs {
   const int32_t* split_waves;
   int64_t n_rows;
   int64_t n_edges;
+  int64_t n_ids;     // edge-id space (empty max/min rows report this arg)
   int32_t chunk;
   int32_t n_waves;
   int32_t n_split;
@@ -231,7 +232,7 @@ struct ArgRed {
   int sentinel;
 
   __device__ ArgRed() {}
-  __device__ ArgRed(const AggArgs& p, int, bool) : sentinel((int)p.n_edges) {}
+  __device__ ArgRed(const AggArgs& p, int, bool) : sentinel((int)p.n_ids) {}
 
   static __device__ __forceinline__ float init_val() { return IS_MAX ? -FLT_MAX : FLT_MAX; }
   static __device__ __forceinline__ bool better(float v, float cur) { return IS_MAX ? (v > cur) : (v < cur); }
@@ -1578,6 +1579,8 @@ static int check_graph(const mp_csr* g, const char* who) {
   MP_CHECK_ARG(g->rowptr && g->wave_row && g->wave_slot && (g->n_split == 0 || g->split_waves),
                "%s: graph has null arrays", who);
   MP_CHECK_ARG(g->n_edges == 0 || g->eid, "%s: graph has null eid", who);
+  MP_CHECK_ARG(g->n_ids == 0 || (g->n_ids >= g->n_edges && g->n_ids <= INT32_MAX),
+               "%s: n_ids must be 0 or in [n_edges, 2^31)", who);
   MP_CHECK_ARG(g->chunk >= 16 && g->chunk % 8 == 0 && g->n_waves >= 1, "%s: bad schedule", who);
   MP_CHECK_ARG(g->col == nullptr || g->n_edges == 0 || g->n_cols > 0,
                "%s: n_cols must be the row count of the gathered x (got %d with a column array)", who,
@@ -1594,6 +1597,7 @@ static void fill_graph(AggArgs& a, const mp_csr* g) {
   a.split_waves = g->split_waves;
   a.n_rows = g->n_rows;
   a.n_edges = g->n_edges;
+  a.n_ids = g->n_ids > 0 ? g->n_ids : g->n_edges;
   a.chunk = g->chunk;
   a.n_waves = g->n_waves;
   a.n_split = g->n_split;

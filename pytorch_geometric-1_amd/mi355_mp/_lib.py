@@ -45,7 +45,7 @@ class MpCsr(ctypes.Structure):
         ("rowptr", c_p), ("col", c_p), ("eid", c_p), ("wave_row", c_p),
         ("wave_slot", c_p), ("split_waves", c_p), ("n_rows", i64),
         ("n_edges", i64), ("chunk", i32), ("n_waves", i32), ("n_split", i32),
-        ("n_cols", i32),
+        ("n_cols", i32), ("n_ids", i64),
     ]
 
 

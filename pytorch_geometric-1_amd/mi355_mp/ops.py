@@ -29,10 +29,28 @@ def _f32_2d(x, what):
     return x
 
 
+# Unweighted max / min over x[col] read each (row, column) pair once: from the
+# (FIRST_OCCURRENCE_AFTER + 1)-th such aggregation over one CSR on, the CSR's
+# first-occurrence form (graph.CSR.first_occurrences: bit-identical results,
+# no repeated gathers) is built once and used.  A one-off aggregation never
+# pays for its sort; a layer reused every epoch does.  None disables it.
+FIRST_OCCURRENCE_AFTER = 2
+
+
+def _max_csr(csr):
+    if FIRST_OCCURRENCE_AFTER is None:
+        return csr
+    n = getattr(csr, "_max_uses", 0) + 1
+    csr._max_uses = n
+    return csr.first_occurrences() if n > FIRST_OCCURRENCE_AFTER else csr
+
+
 def _aggregate(csr, gather, x, w_csr, reduce, flags, bias, out=None, stages=_lib.MP_STAGE_ALL, slab=None,
                arg=None):
     """Launch mp_aggregate_f32; returns (out, arg_or_None)."""
     lib = _lib.load()
+    if reduce in ("max", "min") and w_csr is None and gather == "other" and stages == _lib.MP_STAGE_ALL:
+        csr = _max_csr(csr)
     F = x.shape[1]
     dev = x.device
     if out is None:

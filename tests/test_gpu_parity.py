@@ -344,6 +344,44 @@ def test_fused_max_min_bit_exact_with_ties(F, reduce):
     assert torch.equal(a2.cpu(), arg)
 
 
+@pytest.mark.parametrize("F", [1, 5, 64, 256])
+@pytest.mark.parametrize("reduce", ["max", "min"])
+def test_first_occurrence_csr_bit_exact(F, reduce):
+    """Unweighted max/min from the third aggregation over a CSR on run over
+    its first-occurrence form (repeated (row, column) slots dropped, the first
+    edge's id kept): structure checked against a host computation, values and
+    argmax equal to torch_scatter's serial loop on EVERY call, before and after
+    the switch.  A small node set with many edges makes most edges repeats."""
+    _, ops, _, Graph, pl = _mods()
+    N, E = 300, 40000
+    ei = pl(N, E, seed=F + 11)
+    g = torch.Generator().manual_seed(F + 11)
+    x = torch.randint(-4, 5, (N, F), generator=g).to(torch.float32)
+    graph = Graph(ei.to(DEV), N, N, chunk=64)
+    csr = graph.dst
+    u = csr.first_occurrences()
+    assert u is not csr and u.n_edges < csr.n_edges
+    # host: first edge of every (dst, src) pair, in CSR order (by dst, then edge id)
+    key = ei[1] * N + ei[0]
+    first = {}
+    for e, k in enumerate(key.tolist()):
+        first.setdefault(k, e)
+    keep = sorted(first.values(), key=lambda e: (int(ei[1, e]), e))
+    assert u.n_edges == len(keep)
+    assert torch.equal(u.eid[:u.n_edges].cpu().long(), torch.tensor(keep))
+    assert torch.equal(u.col[:u.n_edges].cpu().long(), ei[0, keep])
+    rp = torch.zeros(N + 1, dtype=torch.long)
+    rp[1:] = torch.cumsum(torch.bincount(ei[1, keep], minlength=N), 0)
+    assert torch.equal(u.rowptr.cpu().long(), rp)
+    want, arg = S.scatter_loop(x[ei[0]], ei[1], N, reduce)
+    csr._max_uses = 0
+    for call in range(4):
+        out, a = ops._aggregate(csr, "other", x.to(DEV), None, reduce, 0, None)
+        assert torch.equal(out.cpu(), want), call
+        assert torch.equal(a.cpu(), arg), call
+    assert csr._max_uses == 4
+
+
 @pytest.mark.parametrize("F", [1, 5, 64, 130, 256, 602])
 @pytest.mark.parametrize("chunk", [16, 64])
 @pytest.mark.parametrize("reduce", ["max", "min"])

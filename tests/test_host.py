@@ -42,7 +42,7 @@ def test_ctypes_signatures_cover_the_header():
 
 
 def test_abi_version_and_error_string(lib):
-    assert lib.mp_abi_version() == 1
+    assert lib.mp_abi_version() == 2
     assert isinstance(lib.mp_last_error(), bytes)
 
 
@@ -62,14 +62,14 @@ def test_host_side_sizes_without_gpu(lib):
     assert lib.mp_schedule_n_waves(100, 1000, 256) == 5
     assert lib.mp_schedule_n_waves(0, 0, 256) == 1
     from mi355_mp import _lib
-    g = _lib.MpCsr(None, None, None, None, None, None, 1000, 5000, 256, 24, 3, 0)
+    g = _lib.MpCsr(None, None, None, None, None, None, 1000, 5000, 256, 24, 3, 0, 0)
     assert lib.mp_aggregate_slab_bytes(g, 256, 0) >= 2 * 24 * 256 * 4
     assert lib.mp_aggregate_slab_bytes(g, 256, 2) >= 2 * 2 * 24 * 256 * 4
 
 
 def test_argument_errors_are_reported(lib):
     from mi355_mp import _lib
-    g = _lib.MpCsr(None, None, None, None, None, None, 10, 10, 256, 1, 0, 0)
+    g = _lib.MpCsr(None, None, None, None, None, None, 10, 10, 256, 1, 0, 0, 0)
     rc = lib.mp_aggregate_f32(g, None, None, 0, 4, 0, 0, None, None, 4, None, None, 0, 3, None)
     assert rc == 1 and b"null" in lib.mp_last_error()
     rc = lib.mp_schedule_build(None, 0, 0, 100, 10, None, None, None, None, None, 0, None)
@@ -83,14 +83,14 @@ def test_column_array_requires_n_cols(lib):
     the 32-bit buffer offsets and selects the kernel shape."""
     from mi355_mp import _lib
     fake = 0x1000  # never dereferenced: the argument check fails first
-    g = _lib.MpCsr(fake, fake, fake, fake, fake, None, 10, 40, 256, 1, 0, 0)
+    g = _lib.MpCsr(fake, fake, fake, fake, fake, None, 10, 40, 256, 1, 0, 0, 0)
     rc = lib.mp_aggregate_f32(g, None, fake, 4, 4, 0, 0, None, fake, 4, None, fake, 1 << 20, 3, None)
     assert rc == 1 and b"n_cols" in lib.mp_last_error()
     buf = __import__("ctypes").create_string_buffer(256)
     rc = lib.mp_aggregate_kernel_name(g, None, fake, 4, 4, 0, None, fake, 4, buf, 256, None)
     assert rc == 1 and b"n_cols" in lib.mp_last_error()
     # identity gather (col = NULL) needs no n_cols
-    g2 = _lib.MpCsr(fake, None, fake, fake, fake, None, 10, 40, 256, 1, 0, 0)
+    g2 = _lib.MpCsr(fake, None, fake, fake, fake, None, 10, 40, 256, 1, 0, 0, 0)
     rc = lib.mp_aggregate_f32(g2, None, fake, 4, 4, 0, 0, None, fake, 4, None, None, 0, 3, None)
     assert rc == 1 and b"slab" in lib.mp_last_error()
 
