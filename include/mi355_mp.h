@@ -120,7 +120,10 @@ int mp_abi_version(void);
  *     kernel for sum/mean (below the VEC1 size threshold) and for max/min:
  *     1, 2 (default) or 4 -- feature tiles of 64, 128 or 256.
  *   MP_TUNE_FLAT_SEQ_TILES: 1 = the flat kernel's feature tiles run one after
- *     another on all eight XCDs; 0 (default) = XCD-affine tiles. */
+ *     another on all eight XCDs; 0 (default) = XCD-affine tiles.
+ *   MP_TUNE_FLAT_FAR_MIN_BYTES: the scalar-batch sum/mean kernel keeps 8
+ *     instead of 16 row loads in flight per wave over a gathered x larger than
+ *     this (default 256 MiB, the Infinity Cache). */
 #define MP_TUNE_FLAT_VEC1_MIN_BYTES 1
 #define MP_TUNE_FLAT_SMEM 2
 #define MP_TUNE_FLAT_MIN_F 3
@@ -129,6 +132,7 @@ int mp_abi_version(void);
 #define MP_TUNE_FLAT_VEC 6
 #define MP_TUNE_FLAT_VEC_ARG 7
 #define MP_TUNE_FLAT_SEQ_TILES 8
+#define MP_TUNE_FLAT_FAR_MIN_BYTES 9
 int64_t mp_tune(int32_t key, int64_t value);
 
 /* ---- CSR build (replaces the sort/bucketing torch_scatter never did: upstream

@@ -40,6 +40,7 @@ namespace mp {
 constexpr int kU_Vec4 = 8;      // x-row loads in flight per task (VEC=4, 64-lane tasks: GAT)
 constexpr int kU_Vec2 = 16;     // x-row loads in flight per task (VEC=2: the flat kernel, 128-feature tiles)
 constexpr int kU_Vec1 = 16;     // x-row loads in flight per task (VEC=1)
+constexpr int kU_Vec1Far = 8;   // ... scalar-batch sum/mean over an x larger than the Infinity Cache
 constexpr int kU_Narrow = 12;   // x-row loads in flight per task (VEC=4, tasks of < 64 lanes)
 constexpr int kWideLanes = 32;  // lanes per task of k_agg_main for rows of >= 256 features (32 beats 64 by ~9%)
 constexpr int kGatLanes = 64;   // lanes per GAT task for H*C >= 256
@@ -89,6 +90,7 @@ struct AggArgs {
   int32_t fix4;      // VEC=2 main kernel: run the fix-up at VEC=4 (slabs are indexed by feature)
   int32_t smem;      // flat sum/mean kernel: slot columns/weights through scalar loads (k_agg_flat SM)
   int32_t seq_tiles; // flat kernel: feature tiles one after another on all XCDs (no XCD-affine map)
+  int32_t far;       // flat SM kernel: x larger than the Infinity Cache (batches of kU_Vec1Far)
   // features
   const float* w;
   const float* x;
@@ -1437,7 +1439,13 @@ static int launch_l(const AggArgs& a, int stages, hipStream_t s) {
     if (a.flat) {
       if constexpr (!Red::kGat && !Red::kGatB && !Red::kHW) {
         if constexpr (L == 64 && !Red::kEid) {
-          if (a.smem) rc = launch_main(k_agg_flat<Red, VEC, U, 64, false, true>, grid, s, a);
+          bool far = false;
+          if constexpr (VEC == 1) {
+            far = a.smem && a.far;
+            if (far) rc = launch_main(k_agg_flat<Red, 1, kU_Vec1Far, 64, false, true>, grid, s, a);
+          }
+          if (far) {
+          } else if (a.smem) rc = launch_main(k_agg_flat<Red, VEC, U, 64, false, true>, grid, s, a);
           else rc = launch_main(k_agg_flat<Red, VEC, U, L>, grid, s, a);
         } else {
           rc = launch_main(k_agg_flat<Red, VEC, U, L>, grid, s, a);
@@ -1555,6 +1563,7 @@ struct Tune {
   std::atomic<int64_t> flat_vec{2};
   std::atomic<int64_t> flat_vec_arg{2};
   std::atomic<int64_t> flat_seq_tiles{0};
+  std::atomic<int64_t> flat_far_min_bytes{256ll << 20};  // the Infinity Cache
 };
 static Tune g_tune;
 
@@ -1568,6 +1577,7 @@ static std::atomic<int64_t>* tune_slot(int32_t key) {
     case MP_TUNE_FLAT_VEC: return &g_tune.flat_vec;
     case MP_TUNE_FLAT_VEC_ARG: return &g_tune.flat_vec_arg;
     case MP_TUNE_FLAT_SEQ_TILES: return &g_tune.flat_seq_tiles;
+    case MP_TUNE_FLAT_FAR_MIN_BYTES: return &g_tune.flat_far_min_bytes;
   }
   return nullptr;
 }
@@ -1635,6 +1645,11 @@ static int aggregate_dispatch(AggArgs& a, const mp_csr* g, int reduce, int stage
   // profiles/r02_ab_smem_arg.log -- so they keep the slot window.)
   a.smem = tuned(g_tune.flat_smem) && !is_arg && a.col != nullptr && g->n_cols > 0 && xbytes <= 0xFFFFFFF0LL;
   if (a.smem) a.x_bytes = (uint32_t)xbytes;
+  // In-flight depth of the scalar-batch kernel: 16 row loads per wave while x
+  // fits the Infinity Cache (Reddit-scale, 238 MB: 7.25 ms vs 7.64 at 8); 8
+  // beyond it (RMAT21 6.71 -> 6.58 ms, ogbn-products-scale 15.0 -> 14.6 ms;
+  // profiles/r02_ab_batch_u.log)
+  a.far = xbytes > tuned(g_tune.flat_far_min_bytes) ? 1 : 0;
   a.seq_tiles = (int32_t)tuned(g_tune.flat_seq_tiles);
   const int64_t min_f = is_arg ? tuned(g_tune.flat_min_f_arg) : tuned(g_tune.flat_min_f);
   if (F >= min_f && F % fvec == 0 && sh.vec >= fvec) {

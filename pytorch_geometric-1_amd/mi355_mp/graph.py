@@ -16,6 +16,9 @@ import torch
 from . import _lib
 
 DEFAULT_CHUNK = None   # auto: see auto_chunk()
+# Per-slot arrays (col, eid, CSR-order weights) are allocated this many
+# elements past their end: scalar slot batches may read whole batches there.
+SLOT_PAD = 64
 MIN_CHUNK, MAX_CHUNK = 16, 1024
 TARGET_TASKS = 100_000
 
@@ -60,8 +63,8 @@ class CSR:
         self.chunk = auto_chunk(self.n_rows, E) if chunk is None else int(chunk)
         self.snap = default_snap(self.chunk) if snap is None else int(snap)
         self.rowptr = torch.empty(self.n_rows + 1, dtype=torch.int32, device=dev)
-        self.col = torch.empty(max(E, 1), dtype=torch.int32, device=dev)
-        self.eid = torch.empty(max(E, 1), dtype=torch.int32, device=dev)
+        self.col = torch.zeros(E + SLOT_PAD, dtype=torch.int32, device=dev)
+        self.eid = torch.zeros(E + SLOT_PAD, dtype=torch.int32, device=dev)
         bad = torch.zeros(1, dtype=torch.int32, device=dev)
         st = _lib.stream_ptr(dev)
         ws_bytes = lib.mp_csr_build_workspace(E, self.n_rows)
@@ -106,8 +109,10 @@ class CSR:
         self.chunk = auto_chunk(self.n_rows, E) if chunk is None else int(chunk)
         self.snap = default_snap(self.chunk)
         self.rowptr = rowptr.to(torch.int32).contiguous()
-        self.col = col.to(torch.int32).contiguous() if E else torch.zeros(1, dtype=torch.int32, device=self.device)
-        self.eid = eid.to(torch.int32).contiguous() if E else torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.col = torch.zeros(E + SLOT_PAD, dtype=torch.int32, device=self.device)
+        self.eid = torch.zeros(E + SLOT_PAD, dtype=torch.int32, device=self.device)
+        self.col[:E] = col
+        self.eid[:E] = eid
         self._build_schedule()
         return self
 
@@ -202,7 +207,8 @@ class CSR:
         """Permute a per-edge fp32 vector (original order) into CSR slot order."""
         lib = _lib.load()
         edge_values = edge_values.contiguous()
-        out = torch.empty_like(edge_values)
+        out = torch.zeros(edge_values.numel() + SLOT_PAD, dtype=edge_values.dtype,
+                          device=edge_values.device)[:edge_values.numel()]
         if self.n_edges:
             _lib.check(lib.mp_permute_f32(edge_values.data_ptr(), self.eid.data_ptr(), self.n_edges,
                                           out.data_ptr(), _lib.stream_ptr(self.device)),

@@ -278,13 +278,17 @@ def test_flat_scalar_slot_batches_match_slot_window(F, N, E, vec1):
     graph = Graph(ei.to(DEV), N, N, chunk=16)
     eid = ei.to(DEV)
     got = {}
-    for sm in (1, 0):
-        with _tuned(flat_vec1_min_bytes=0 if vec1 else 1 << 30, flat_smem=sm):
+    # sm 1: scalar batches of 16 (x within the Infinity Cache), 2: of 8 (the
+    # far-x depth, forced), 0: the per-lane slot window
+    for sm, far in ((1, 1 << 40), (2, 0), (0, 1 << 40)):
+        with _tuned(flat_vec1_min_bytes=0 if vec1 else 1 << 30, flat_smem=1 if sm else 0, flat_far_min_bytes=far):
             got[sm] = {(r, wt): ops.fused_propagate(graph, x.to(DEV), eid, w.to(DEV) if wt else None, r).cpu()
                        for r in ("sum", "mean") for wt in (False, True)}
     assert lib.mp_tune(_lib.MP_TUNE_FLAT_SMEM, -1) == 1
+    assert lib.mp_tune(_lib.MP_TUNE_FLAT_FAR_MIN_BYTES, -1) == 256 << 20
     for k in got[1]:
         assert torch.equal(got[1][k], got[0][k]), k
+        assert torch.equal(got[2][k], got[0][k]), k
     want = S.gather_sum(x, ei[0], ei[1], w, N)
     _bound_ok(got[1][("sum", True)], want, S.gather_sum(x.abs(), ei[0], ei[1], w.abs(), N))
     split = set(_split_rows(graph.dst))

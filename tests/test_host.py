@@ -99,7 +99,7 @@ def test_tune_table_keys(lib):
     from mi355_mp import _lib
     for key in (_lib.MP_TUNE_FLAT_VEC1_MIN_BYTES, _lib.MP_TUNE_FLAT_SMEM, _lib.MP_TUNE_FLAT_MIN_F,
                 _lib.MP_TUNE_FLAT_MIN_F_ARG, _lib.MP_TUNE_FLAT_NARROW_VEC1, _lib.MP_TUNE_FLAT_VEC,
-                _lib.MP_TUNE_FLAT_VEC_ARG, _lib.MP_TUNE_FLAT_SEQ_TILES):
+                _lib.MP_TUNE_FLAT_VEC_ARG, _lib.MP_TUNE_FLAT_SEQ_TILES, _lib.MP_TUNE_FLAT_FAR_MIN_BYTES):
         v = lib.mp_tune(key, -1)
         assert v >= 0
         assert lib.mp_tune(key, v) == v
