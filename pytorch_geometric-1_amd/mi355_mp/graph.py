@@ -20,17 +20,18 @@ DEFAULT_CHUNK = None   # auto: see auto_chunk()
 # elements past their end: scalar slot batches may read whole batches there.
 SLOT_PAD = 64
 MIN_CHUNK, MAX_CHUNK = 16, 1024
-TARGET_TASKS = 100_000
+TARGET_TASKS = 50_000
 
 
 def auto_chunk(n_rows, n_edges):
     """Merge-path task size in work units (rows + slots): the largest power of
-    two <= units / 100K, clamped to [16, 1024].  Large graphs get big tasks:
+    two <= units / 50K, clamped to [16, 1024].  Large graphs get big tasks:
     fewer hub rows cross a task boundary, so the fix-up shrinks and more rows
     are summed in one task (bit-identical to the sequential order); RMAT21
-    (64M units) gets 512, the Reddit-scale graph (115M units, degree ~490)
-    1024 (step -1.2% / -3..4% vs 256, tools/ab_bench.py).  Small graphs keep
-    enough tasks to spread over 256 CUs (Cora, 13K units: 16 -> 829 tasks)."""
+    (64M units) gets 1024 (main + fix-up 6.65 -> 6.61 ms vs 512, 6.79 ms at
+    256; profiles/r02_ab_chunk.log), the Reddit-scale graph (115M units, degree
+    ~490) 1024 (-3..4% vs 256, tools/ab_bench.py).  Small graphs keep enough
+    tasks to spread over 256 CUs (Cora, 13K units: 16 -> 829 tasks)."""
     units = int(n_rows) + int(n_edges)
     c = MIN_CHUNK
     while c * 2 <= MAX_CHUNK and units // (c * 2) >= TARGET_TASKS:
