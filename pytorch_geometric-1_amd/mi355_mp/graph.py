@@ -21,9 +21,13 @@ DEFAULT_CHUNK = None   # auto: see auto_chunk()
 SLOT_PAD = 64
 MIN_CHUNK, MAX_CHUNK = 16, 1024
 TARGET_TASKS = 50_000
+# GAT's per-slot softmax work favours more, shorter tasks: its fused backward
+# pass over the transposed CSR runs 1.9 ms longer at chunk 1024 than at 512 on
+# RMAT21 (layer forward + backward 32.0 vs 33.9 ms, profiles/r02_ab_chunk_train.log)
+GAT_TARGET_TASKS = 100_000
 
 
-def auto_chunk(n_rows, n_edges):
+def auto_chunk(n_rows, n_edges, target=None):
     """Merge-path task size in work units (rows + slots): the largest power of
     two <= units / 50K, clamped to [16, 1024].  Large graphs get big tasks:
     fewer hub rows cross a task boundary, so the fix-up shrinks and more rows
@@ -33,8 +37,9 @@ def auto_chunk(n_rows, n_edges):
     ~490) 1024 (-3..4% vs 256, tools/ab_bench.py).  Small graphs keep enough
     tasks to spread over 256 CUs (Cora, 13K units: 16 -> 829 tasks)."""
     units = int(n_rows) + int(n_edges)
+    target = TARGET_TASKS if target is None else int(target)
     c = MIN_CHUNK
-    while c * 2 <= MAX_CHUNK and units // (c * 2) >= TARGET_TASKS:
+    while c * 2 <= MAX_CHUNK and units // (c * 2) >= target:
         c *= 2
     return c
 
@@ -50,7 +55,7 @@ class CSR:
     rowptr[n_rows+1], col[E] (= other[eid] or eid), eid[E] : int32 on device.
     """
 
-    def __init__(self, key, other, n_rows, n_other, chunk=DEFAULT_CHUNK, snap=None):
+    def __init__(self, key, other, n_rows, n_other, chunk=DEFAULT_CHUNK, snap=None, target_tasks=None):
         _lib.require_device(key)
         lib = _lib.load()
         dev = key.device
@@ -61,7 +66,7 @@ class CSR:
         self.n_edges = int(E)
         self.n_other = int(n_other)
         self.device = dev
-        self.chunk = auto_chunk(self.n_rows, E) if chunk is None else int(chunk)
+        self.chunk = auto_chunk(self.n_rows, E, target_tasks) if chunk is None else int(chunk)
         self.snap = default_snap(self.chunk) if snap is None else int(snap)
         self.rowptr = torch.empty(self.n_rows + 1, dtype=torch.int32, device=dev)
         self.col = torch.zeros(E + SLOT_PAD, dtype=torch.int32, device=dev)
@@ -230,7 +235,7 @@ class Graph:
     """
 
     def __init__(self, edge_index, n_dst, n_src, flow="source_to_target", chunk=DEFAULT_CHUNK,
-                 weak=False):
+                 weak=False, target_tasks=None):
         self.i, self.j = (1, 0) if flow == "source_to_target" else (0, 1)
         if weak:
             self._ei = weakref.ref(edge_index)
@@ -238,6 +243,7 @@ class Graph:
             self._ei = lambda ei=edge_index: ei
         self.n_dst, self.n_src = int(n_dst), int(n_src)
         self.chunk = chunk
+        self.target_tasks = target_tasks
         self._dst = None
         self._src = None
 
@@ -251,14 +257,16 @@ class Graph:
     def dst(self):
         if self._dst is None:
             ei = self._edge_index()
-            self._dst = CSR(ei[self.i], ei[self.j], self.n_dst, self.n_src, self.chunk)
+            self._dst = CSR(ei[self.i], ei[self.j], self.n_dst, self.n_src, self.chunk,
+                            target_tasks=self.target_tasks)
         return self._dst
 
     @property
     def src(self):
         if self._src is None:
             ei = self._edge_index()
-            self._src = CSR(ei[self.j], ei[self.i], self.n_src, self.n_dst, self.chunk)
+            self._src = CSR(ei[self.j], ei[self.i], self.n_src, self.n_dst, self.chunk,
+                            target_tasks=self.target_tasks)
         return self._src
 
     def src_with_dst_slots(self):
@@ -313,10 +321,10 @@ _graph_cache = _Cache()
 _index_cache = _Cache()
 
 
-def graph_for(edge_index, n_dst, n_src, flow="source_to_target"):
+def graph_for(edge_index, n_dst, n_src, flow="source_to_target", target_tasks=None):
     """Cached Graph for an edge_index tensor (rebuilt if it is modified in place)."""
-    return _graph_cache.get(edge_index, (int(n_dst), int(n_src), flow),
-                            lambda: Graph(edge_index, n_dst, n_src, flow, weak=True))
+    return _graph_cache.get(edge_index, (int(n_dst), int(n_src), flow, target_tasks),
+                            lambda: Graph(edge_index, n_dst, n_src, flow, weak=True, target_tasks=target_tasks))
 
 
 def csr_for_index(index, n_rows):

@@ -16,7 +16,7 @@ import torch.nn.functional as F
 from torch.nn import Parameter
 
 from mi355_mp import ops as _ops
-from mi355_mp.graph import graph_for
+from mi355_mp.graph import GAT_TARGET_TASKS, graph_for
 
 from ...utils import softmax
 from ..inits import glorot, zeros
@@ -73,7 +73,7 @@ class GATConv(MessagePassing):
         if self._can_fuse(x, size):
             xw = _ops.feature_transform(x, self.weight)
             N = xw.size(0)
-            graph = graph_for(edge_index, N, N, self.flow)
+            graph = graph_for(edge_index, N, N, self.flow, target_tasks=GAT_TARGET_TASKS)
             fused_bias = self.bias if self.concat else None
             out, alpha = _ops.gat_propagate(graph, edge_index, xw, self.att, self.heads, self.out_channels,
                                             self.negative_slope, fused_bias, return_attention_weights)

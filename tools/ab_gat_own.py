@@ -32,7 +32,8 @@ def main():
     dev = torch.device("cuda", 0)
     N, H, C = 1 << 21, args.heads, args.C
     ei = gat_loops(rmat_edge_index(scale=21, n_samples=30_000_000, seed=1, device=dev), N)
-    csr = Graph(ei, N, N).dst
+    from mi355_mp.graph import GAT_TARGET_TASKS
+    csr = Graph(ei, N, N, target_tasks=GAT_TARGET_TASKS).dst
     del ei
     gen = torch.Generator(device=dev).manual_seed(2)
     xw = torch.randn(N, H * C, device=dev, generator=gen)

@@ -149,8 +149,9 @@ def c3(dev):
     from mi355_mp.graphgen import rmat_edge_index
     from torch_geometric.nn.conv._structure import gat_loops
     N, H, C = 1 << 21, 8, 32
+    from mi355_mp.graph import GAT_TARGET_TASKS
     ei = gat_loops(rmat_edge_index(scale=21, n_samples=30_000_000, seed=1, device=dev), N)
-    graph = Graph(ei, N, N)
+    graph = Graph(ei, N, N, target_tasks=GAT_TARGET_TASKS)   # as GATConv builds it
     csr = graph.dst
     g = torch.Generator(device=dev).manual_seed(2)
     xw = torch.randn(N, H * C, device=dev, generator=g)
