@@ -42,7 +42,10 @@ constexpr int kU_Vec2 = 16;     // x-row loads in flight per task (VEC=2: the fl
 constexpr int kU_Vec1 = 16;     // x-row loads in flight per task (VEC=1)
 constexpr int kU_Vec1Far = 8;   // ... scalar-batch sum/mean over an x larger than the Infinity Cache
 constexpr int kU_Gat = 16;      // ... fused GAT on 64/128-feature tiles (scalar batches)
-constexpr int kU_GatFar = 8;    // ... the same over an x larger than the Infinity Cache
+#ifndef MP_U_GAT_FAR
+#define MP_U_GAT_FAR 8
+#endif
+constexpr int kU_GatFar = MP_U_GAT_FAR;    // ... the same over an x larger than the Infinity Cache
 constexpr int kU_Narrow = 12;  // x-row loads in flight per task (VEC=4, tasks of < 64 lanes)
 constexpr int kWideLanes = 32;  // lanes per task of k_agg_main for rows of >= 256 features (32 beats 64 by ~9%)
 constexpr int kGatLanes = 64;   // lanes per GAT task for H*C >= 256
@@ -1179,7 +1182,7 @@ template <class Red, int VEC, int U, int L, bool GA = false, bool SM = false>
 __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
   static_assert(!Red::kGatB && !Red::kHW && (!Red::kGat || own_as_v<Red>),
                 "flat loop: sum/mean/max/min reducers, fused GAT with own a_src");
-  static_assert(!Red::kGat || (L == 64 && VEC <= 2 && !GA), "fused GAT: 64-lane tasks, 64/128-feature tiles");
+  static_assert(!Red::kGat || (L == 64 && !GA), "fused GAT: 64-lane tasks");
   static_assert(!GA || (L == 64 && VEC == 1 && Red::kW), "two-pass GAT: 64-lane tasks, 64-feature tiles");
   static_assert(!SM || (L == 64 && !GA && !Red::kEid), "scalar batches: 64-lane sum/mean/GAT tasks");
   constexpr bool kG = Red::kGat;
@@ -1212,8 +1215,9 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
   const int64_t e_end = GR::un(p.wave_slot[w + 1]);
 
   Red red(p, f, act);
-  // fused GAT: a_dst[abase + gl, h0 + q] for the tile's hpt heads (q < hpt <= 4)
-  [[maybe_unused]] float adw[4];
+  // fused GAT: a_dst[abase + gl, h0 + q] for the tile's hpt heads (q < hpt <= kAdw)
+  constexpr int kAdw = VEC == 4 ? 8 : 4;
+  [[maybe_unused]] float adw[kAdw];
   [[maybe_unused]] int abase = 0;
   [[maybe_unused]] const int hpt = kG ? (L * VEC) / p.C : 1;
   [[maybe_unused]] const int h0 = kG ? tile * hpt : 0;
@@ -1222,7 +1226,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
     abase = b;
     const int64_t rr = (int64_t)b + gl;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) adw[q] = (q < hpt && rr < p.n_rows) ? p.a_dst[rr * p.H + h0 + q] : 0.f;
+    for (int q = 0; q < kAdw; ++q) adw[q] = (q < hpt && rr < p.n_rows) ? p.a_dst[rr * p.H + h0 + q] : 0.f;
   };
   // begin owned row rr (rows are opened in increasing order)
   auto begin_row = [&](int rr) {
@@ -1231,7 +1235,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
       const int i = rr - abase;
       float a = readlane(adw[0], i);
 #pragma unroll
-      for (int q = 1; q < 4; ++q) {
+      for (int q = 1; q < kAdw; ++q) {
         if (q < hpt) {
           const float t = readlane(adw[q], i);
           a = hq == q ? t : a;
@@ -1526,7 +1530,7 @@ static int launch_l(const AggArgs& a, int stages, hipStream_t s) {
         } else {
           rc = launch_main(k_agg_flat<Red, VEC, U, L>, grid, s, a);
         }
-      } else if constexpr (own_as_v<Red> && VEC <= 2 && L == 64) {  // fused GAT on feature tiles
+      } else if constexpr (own_as_v<Red> && L == 64) {  // fused GAT on feature tiles
         if (a.smem && a.far) rc = launch_main(k_agg_flat<Red, VEC, kU_GatFar, 64, false, true>, grid, s, a);
         else if (a.smem) rc = launch_main(k_agg_flat<Red, VEC, kU_Gat, 64, false, true>, grid, s, a);
         else rc = launch_main(k_agg_flat<Red, VEC, kU_Gat, 64>, grid, s, a);
@@ -1763,7 +1767,7 @@ int64_t mp_tune(int32_t key, int64_t value) {
   if (value < 0) return v->load();
   if (key == MP_TUNE_FLAT_SMEM || key == MP_TUNE_FLAT_SEQ_TILES) value = value ? 1 : 0;
   if ((key == MP_TUNE_FLAT_VEC || key == MP_TUNE_FLAT_VEC_ARG) && value != 1 && value != 2 && value != 4) return -1;
-  if (key == MP_TUNE_GAT_TILE_VEC && value != 0 && value != 1 && value != 2) return -1;
+  if (key == MP_TUNE_GAT_TILE_VEC && value != 0 && value != 1 && value != 2 && value != 4) return -1;
   return v->exchange(value);
 }
 
@@ -1934,7 +1938,7 @@ int mp_gat_aggregate_att_f32(const mp_csr* g, const float* xw, const float* a_sr
   // per tile.  Same per-head arithmetic as the 256-feature tile (a_src
   // bitwise, GatRed::own_as); the accumulation order of a row is unchanged.
   const int tv = (int)tuned(g_tune.gat_tile_vec);
-  if (own_ok && tv > 0 && (tv == 1 || C % 2 == 0) && (64 * tv) % C == 0 && (64 * tv) / C <= 4 &&
+  if (own_ok && tv > 0 && C % tv == 0 && (64 * tv) % C == 0 && (64 * tv) / C <= (tv == 4 ? 8 : 4) &&
       F % (64 * tv) == 0 && (F * 4) % 256 == 0 && (uintptr_t)xw % 256 == 0 && g->col != nullptr) {
     a.att = att;
     a.flat = 1;
@@ -1943,7 +1947,8 @@ int mp_gat_aggregate_att_f32(const mp_csr* g, const float* xw, const float* a_sr
     if (a.smem) a.x_bytes = (uint32_t)xbytes;
     a.far = xbytes > tuned(g_tune.flat_far_min_bytes) ? 1 : 0;
     if (tv == 1) return launch<GatRed<1, true>, 1>(a, stages, s, 64);
-    return launch<GatRed<2, true>, 2>(a, stages, s, 64);
+    if (tv == 2) return launch<GatRed<2, true>, 2>(a, stages, s, 64);
+    return launch<GatRed<4, true>, 4>(a, stages, s, 64);
   }
   if (own_ok && vec == 4) {
     a.att = att;

@@ -615,11 +615,11 @@ def test_gat_feature_tiles_bitwise_equal_to_full_row_tile(H, C, chunk, mode):
     graph = Graph(ei.to(DEV), N, N, chunk=chunk)
     res = {}
     knobs = {"scalar": {}, "far": {"flat_far_min_bytes": 0}, "window": {"flat_smem": 0}}[mode]
-    for v in (0, 1, 2):
+    for v in (0, 1, 2, 4):
         with _tuned(gat_tile_vec=v, **knobs):
             out, alpha = ops.gat_propagate(graph, ei.to(DEV), xw.to(DEV), att.to(DEV), H, C, 0.2, None, True)
         res[v] = (out.cpu(), alpha.cpu())
-    for v in (1, 2):
+    for v in (1, 2, 4):
         assert torch.equal(res[v][0], res[0][0]), "tile VEC=%d output differs from the 256-feature tile" % v
         assert torch.equal(res[v][1], res[0][1]), "tile VEC=%d alpha differs" % v
     x_i = xw[ei[1]].view(-1, H, C)
