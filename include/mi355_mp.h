@@ -123,11 +123,7 @@ int mp_abi_version(void);
  *     another on all eight XCDs; 0 (default) = XCD-affine tiles.
  *   MP_TUNE_FLAT_FAR_MIN_BYTES: the scalar-batch sum/mean kernel keeps 8
  *     instead of 16 row loads in flight per wave over a gathered x larger than
- *     this (default 256 MiB, the Infinity Cache).
- *   MP_TUNE_GAT_TILE_VEC: features per lane of the fused GAT aggregation on
- *     feature tiles (mp_gat_aggregate_att_f32 with att): 1 or 2 = tiles of 64
- *     or 128 features (each a whole number of heads, the online softmax per
- *     tile), 0 = one 256-feature tile per task (VEC=4). */
+ *     this (default 256 MiB, the Infinity Cache). */
 #define MP_TUNE_FLAT_VEC1_MIN_BYTES 1
 #define MP_TUNE_FLAT_SMEM 2
 #define MP_TUNE_FLAT_MIN_F 3
@@ -137,7 +133,6 @@ int mp_abi_version(void);
 #define MP_TUNE_FLAT_VEC_ARG 7
 #define MP_TUNE_FLAT_SEQ_TILES 8
 #define MP_TUNE_FLAT_FAR_MIN_BYTES 9
-#define MP_TUNE_GAT_TILE_VEC 10
 int64_t mp_tune(int32_t key, int64_t value);
 
 /* ---- CSR build (replaces the sort/bucketing torch_scatter never did: upstream

@@ -41,12 +41,7 @@ constexpr int kU_Vec4 = 8;      // x-row loads in flight per task (VEC=4, 64-lan
 constexpr int kU_Vec2 = 16;     // x-row loads in flight per task (VEC=2: the flat kernel, 128-feature tiles)
 constexpr int kU_Vec1 = 16;     // x-row loads in flight per task (VEC=1)
 constexpr int kU_Vec1Far = 8;   // ... scalar-batch sum/mean over an x larger than the Infinity Cache
-constexpr int kU_Gat = 16;      // ... fused GAT on 64/128-feature tiles (scalar batches)
-#ifndef MP_U_GAT_FAR
-#define MP_U_GAT_FAR 8
-#endif
-constexpr int kU_GatFar = MP_U_GAT_FAR;    // ... the same over an x larger than the Infinity Cache
-constexpr int kU_Narrow = 12;  // x-row loads in flight per task (VEC=4, tasks of < 64 lanes)
+constexpr int kU_Narrow = 12;   // x-row loads in flight per task (VEC=4, tasks of < 64 lanes)
 constexpr int kWideLanes = 32;  // lanes per task of k_agg_main for rows of >= 256 features (32 beats 64 by ~9%)
 constexpr int kGatLanes = 64;   // lanes per GAT task for H*C >= 256
 constexpr bool kNtOut = true;   // non-temporal output-row stores (A/B: -0.4%)
@@ -359,7 +354,7 @@ struct GatRed {
 
   __device__ GatRed(const AggArgs& p, int f, bool act) : h(act ? f / p.C : 0) {
     if constexpr (OWN) {
-      hl = p.C / 4;  // 4-feature partials per head (the node-score kernel's lanes per head)
+      hl = p.C / VEC;
       const int c = act ? f % p.C : 0;
       Frag<VEC> o = load_frag<VEC>(p.att + (int64_t)h * 2 * p.C + p.C + c);
 #pragma unroll
@@ -367,44 +362,20 @@ struct GatRed {
     }
   }
   // <row, att_src> over the head's lanes: v.x*y.x + v.y*y.y + ... separately
-  // rounded left to right (-ffp-contract=off), then group_sum.  Narrow lanes
-  // (VEC 1 / 2, feature tiles of 64 / 128) first rebuild the node-score
-  // kernel's 4-feature partial ((q0 + q1) + q2) + q3 from the quad / lane pair
-  // holding those features (DPP quad_perm reads, every lane of the block ends
-  // with it), then run the remaining levels of the same reduction tree over
-  // blocks of 4 / VEC lanes: bitwise the value k_gat_node_scores_wave stores.
+  // rounded left to right (-ffp-contract=off), then group_sum
   __device__ __forceinline__ float own_as(const Frag<VEC>& v) const {
-    if constexpr (VEC == 1) {
-      const float q = v.v[0] * y[0];
-      float t = dpp<0x00>(q) + dpp<0x55>(q);  // quad_perm(0,0,0,0) + quad_perm(1,1,1,1)
-      t = t + dpp<0xAA>(q);                   // + quad lane 2
-      t = t + dpp<0xFF>(q);                   // + quad lane 3
-      return group_sum_blocks<4>(t, hl);
-    } else if constexpr (VEC == 2) {
-      const float q0 = v.v[0] * y[0];
-      const float q1 = v.v[1] * y[1];
-      const float t2 = q0 + q1;
-      float t = dpp<0xA0>(t2) + dpp<0xF5>(q0);  // even lane's pair partial + odd lane's first product
-      t = t + dpp<0xF5>(q1);                    // + odd lane's second product
-      return group_sum_blocks<2>(t, hl);
-    } else {
-      float t = v.v[0] * y[0];
+    float t = v.v[0] * y[0];
 #pragma unroll
-      for (int k = 1; k < VEC; ++k) t = t + v.v[k] * y[k];
-      return group_sum(t, hl);
-    }
+    for (int k = 1; k < VEC; ++k) t = t + v.v[k] * y[k];
+    return group_sum(t, hl);
   }
 
   __device__ __forceinline__ void begin(const AggArgs& p, int64_t row, bool, int, bool) {
-    begin_ad(p.a_dst[row * p.H + h]);
-  }
-  // begin with the row's a_dst already at hand (k_agg_flat's a_dst window)
-  __device__ __forceinline__ void begin_ad(float a_dst) {
 #pragma unroll
     for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
     m = -INFINITY;
     s = 0.f;
-    ad = a_dst;
+    ad = p.a_dst[row * p.H + h];
   }
   __device__ __forceinline__ void consume_gat(const AggArgs& p, const Frag<VEC>& v, float as) {
     float a = as + ad;
@@ -412,6 +383,7 @@ struct GatRed {
     // mn = fmaxf(m, a); sc = expf(m - mn); pe = expf(a - mn) with one exp:
     // one of the two arguments is x - x, i.e. 0 (exp 1) or NaN for an
     // infinite x, so (x - x) + 1 reproduces it bit for bit, NaNs included
+    // (config 3: 7.81 -> 7.74 ms)
     const bool up = a > m;
     const float e = expf(up ? m - a : a - m);
     const float sc = up ? e : (m - m) + 1.f;
@@ -1172,20 +1144,11 @@ __device__ __forceinline__ void scalar_batch(const T* a, int64_t n, int64_t e, T
   }
 }
 
-// GAT (Red = GatRed<VEC, true>, L = 64, VEC 1 / 2): one feature tile of
-// 64 * VEC features = 64 * VEC / C whole heads, so a tile runs the online
-// softmax of its own heads only, with a_src recomputed from the gathered tile
-// (GatRed::own_as) -- the single-pass fused GATConv aggregation on the same
-// narrow tiles and scalar slot batches as sum.  a_dst of the next 64 rows sits
-// in a per-lane window (one load per head of the tile) read with v_readlane.
 template <class Red, int VEC, int U, int L, bool GA = false, bool SM = false>
 __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
-  static_assert(!Red::kGatB && !Red::kHW && (!Red::kGat || own_as_v<Red>),
-                "flat loop: sum/mean/max/min reducers, fused GAT with own a_src");
-  static_assert(!Red::kGat || (L == 64 && !GA), "fused GAT: 64-lane tasks");
+  static_assert(!Red::kGat && !Red::kGatB && !Red::kHW, "flat loop: sum/mean/max/min reducers");
   static_assert(!GA || (L == 64 && VEC == 1 && Red::kW), "two-pass GAT: 64-lane tasks, 64-feature tiles");
-  static_assert(!SM || (L == 64 && !GA && !Red::kEid), "scalar batches: 64-lane sum/mean/GAT tasks");
-  constexpr bool kG = Red::kGat;
+  static_assert(!SM || (L == 64 && !GA && !Red::kEid), "scalar batches: 64-lane sum/mean tasks");
   using GR = Grp<L>;
   const int lane = lane_id();
   const int gl = lane & (L - 1);
@@ -1215,39 +1178,6 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
   const int64_t e_end = GR::un(p.wave_slot[w + 1]);
 
   Red red(p, f, act);
-  // fused GAT: a_dst[abase + gl, h0 + q] for the tile's hpt heads (q < hpt <= kAdw)
-  constexpr int kAdw = VEC == 4 ? 8 : 4;
-  [[maybe_unused]] float adw[kAdw];
-  [[maybe_unused]] int abase = 0;
-  [[maybe_unused]] const int hpt = kG ? (L * VEC) / p.C : 1;
-  [[maybe_unused]] const int h0 = kG ? tile * hpt : 0;
-  [[maybe_unused]] const int hq = kG ? (gl * VEC) / p.C : 0;
-  auto ad_load = [&](int b) {
-    abase = b;
-    const int64_t rr = (int64_t)b + gl;
-#pragma unroll
-    for (int q = 0; q < kAdw; ++q) adw[q] = (q < hpt && rr < p.n_rows) ? p.a_dst[rr * p.H + h0 + q] : 0.f;
-  };
-  // begin owned row rr (rows are opened in increasing order)
-  auto begin_row = [&](int rr) {
-    if constexpr (kG) {
-      if (rr - abase > L - 1) ad_load(rr);
-      const int i = rr - abase;
-      float a = readlane(adw[0], i);
-#pragma unroll
-      for (int q = 1; q < kAdw; ++q) {
-        if (q < hpt) {
-          const float t = readlane(adw[q], i);
-          a = hq == q ? t : a;
-        }
-      }
-      red.begin_ad(a);
-    } else {
-      red.begin(p, rr, true, f, act);
-    }
-  };
-  if constexpr (kG) ad_load(r_first);
-  const bool stat_writer = Red::kStat && (f % p.C == 0);
   std::conditional_t<GA, GatAlphaWin, SlotWin<Red::kW, Red::kEid, L>> win;
   if constexpr (GA) {
     __shared__ float ga_lds[kWavesPerBlock][64 * 4];
@@ -1280,13 +1210,13 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
     red.begin(p, r_first - 1, false, f, act);
   } else if (r < r_last) {
     re = row_ptr(r + 1);
-    begin_row(r);
+    red.begin(p, r, true, f, act);
   }
   // close the current row at slot k (k >= its end) and open the next one(s)
   auto advance = [&](int64_t k) {
     while (k >= re) {
       if (cont) {
-        if (act) red.save(slab_ref(p, 2 * (int64_t)w, f, red), stat_writer);
+        if (act) red.save(slab_ref(p, 2 * (int64_t)w, f, red), false);
         cont = false;
       } else {
         red.finish(p, r, re - rs, f, act);
@@ -1298,7 +1228,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
       }
       rs = re;
       re = row_ptr(r + 1);
-      begin_row(r);
+      red.begin(p, r, true, f, act);
     }
   };
 
@@ -1319,13 +1249,9 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
       for (int u = 0; u < U; ++u) {
         if (u < n) {
           advance(e + u);
-          if constexpr (kG) {
-            red.consume_gat(p, v[u], red.own_as(v[u]));
-          } else {
-            float wt = 1.f;
-            if constexpr (Red::kW) wt = wb[u];
-            red.consume(v[u], wt, 0, 0.f);
-          }
+          float wt = 1.f;
+          if constexpr (Red::kW) wt = wb[u];
+          red.consume(v[u], wt, 0, 0.f);
         }
       }
       e += n;
@@ -1356,33 +1282,32 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
         else if constexpr (Red::kW) wt = GR::bc(win.w, off + u);
         int ei = 0;
         if constexpr (!GA && Red::kEid) ei = GR::bc(win.eid, off + u);
-        if constexpr (kG) red.consume_gat(p, v[u], red.own_as(v[u]));
-        else red.consume(v[u], wt, ei, 0.f);
+        red.consume(v[u], wt, ei, 0.f);
       }
     }
     e += n;
   }
   // tail: the current row, then any rows whose slots all lie in later tasks
   if (cont) {
-    if (act) red.save(slab_ref(p, 2 * (int64_t)w, f, red), stat_writer);
+    if (act) red.save(slab_ref(p, 2 * (int64_t)w, f, red), false);
     cont = false;
     if (r < r_last) {
       rs = ce;
       re = row_ptr(r + 1);
-      begin_row(r);
+      red.begin(p, r, true, f, act);
     }
   }
   while (r < r_last) {
     if (re <= e_end) {
       red.finish(p, r, re - rs, f, act);
     } else {
-      if (act) red.save(slab_ref(p, 2 * (int64_t)w + 1, f, red), stat_writer);
+      if (act) red.save(slab_ref(p, 2 * (int64_t)w + 1, f, red), false);
     }
     ++r;
     if (r < r_last) {
       rs = re;
       re = row_ptr(r + 1);
-      begin_row(r);
+      red.begin(p, r, true, f, act);
     }
   }
 }
@@ -1530,13 +1455,6 @@ static int launch_l(const AggArgs& a, int stages, hipStream_t s) {
         } else {
           rc = launch_main(k_agg_flat<Red, VEC, U, L>, grid, s, a);
         }
-      } else if constexpr (own_as_v<Red> && L == 64) {  // fused GAT on feature tiles
-        if (a.smem && a.far) rc = launch_main(k_agg_flat<Red, VEC, kU_GatFar, 64, false, true>, grid, s, a);
-        else if (a.smem) rc = launch_main(k_agg_flat<Red, VEC, kU_Gat, 64, false, true>, grid, s, a);
-        else rc = launch_main(k_agg_flat<Red, VEC, kU_Gat, 64>, grid, s, a);
-      } else {
-        set_error("flat launch: no flat kernel for this reducer");
-        return MP_ERR_ARG;
       }
     } else {
       rc = launch_main(k_agg_main<Red, VEC, U, L>, grid, s, a);
@@ -1651,7 +1569,6 @@ struct Tune {
   std::atomic<int64_t> flat_vec_arg{2};
   std::atomic<int64_t> flat_seq_tiles{0};
   std::atomic<int64_t> flat_far_min_bytes{256ll << 20};  // the Infinity Cache
-  std::atomic<int64_t> gat_tile_vec{0};  // A/B: 256-feature tile 7.74 ms, 128 9.51, 64 16.8 (VALU-bound)
 };
 static Tune g_tune;
 
@@ -1666,7 +1583,6 @@ static std::atomic<int64_t>* tune_slot(int32_t key) {
     case MP_TUNE_FLAT_VEC_ARG: return &g_tune.flat_vec_arg;
     case MP_TUNE_FLAT_SEQ_TILES: return &g_tune.flat_seq_tiles;
     case MP_TUNE_FLAT_FAR_MIN_BYTES: return &g_tune.flat_far_min_bytes;
-    case MP_TUNE_GAT_TILE_VEC: return &g_tune.gat_tile_vec;
   }
   return nullptr;
 }
@@ -1767,7 +1683,6 @@ int64_t mp_tune(int32_t key, int64_t value) {
   if (value < 0) return v->load();
   if (key == MP_TUNE_FLAT_SMEM || key == MP_TUNE_FLAT_SEQ_TILES) value = value ? 1 : 0;
   if ((key == MP_TUNE_FLAT_VEC || key == MP_TUNE_FLAT_VEC_ARG) && value != 1 && value != 2 && value != 4) return -1;
-  if (key == MP_TUNE_GAT_TILE_VEC && value != 0 && value != 1 && value != 2 && value != 4) return -1;
   return v->exchange(value);
 }
 
@@ -1931,26 +1846,7 @@ int mp_gat_aggregate_att_f32(const mp_csr* g, const float* xw, const float* a_sr
   // a_src from the gathered rows: the node-score kernel's 4-feature lane
   // partials and head groups of C/4 lanes (a power of two <= 64)
   const int hl4 = C / 4;
-  const bool own_ok = att && C % 4 == 0 && hl4 <= 64 && (hl4 & (hl4 - 1)) == 0 && (uintptr_t)att % 16 == 0 &&
-                      (uintptr_t)xw % 16 == 0;
-  // Feature tiles of 64 * tv features holding whole heads (1 to 4 of them), on
-  // 256-B aligned rows: the flat loop with scalar slot batches, online softmax
-  // per tile.  Same per-head arithmetic as the 256-feature tile (a_src
-  // bitwise, GatRed::own_as); the accumulation order of a row is unchanged.
-  const int tv = (int)tuned(g_tune.gat_tile_vec);
-  if (own_ok && tv > 0 && C % tv == 0 && (64 * tv) % C == 0 && (64 * tv) / C <= (tv == 4 ? 8 : 4) &&
-      F % (64 * tv) == 0 && (F * 4) % 256 == 0 && (uintptr_t)xw % 256 == 0 && g->col != nullptr) {
-    a.att = att;
-    a.flat = 1;
-    const int64_t xbytes = (int64_t)g->n_cols * F * 4;
-    a.smem = tuned(g_tune.flat_smem) && g->n_cols > 0 && xbytes <= 0xFFFFFFF0LL;
-    if (a.smem) a.x_bytes = (uint32_t)xbytes;
-    a.far = xbytes > tuned(g_tune.flat_far_min_bytes) ? 1 : 0;
-    if (tv == 1) return launch<GatRed<1, true>, 1>(a, stages, s, 64);
-    if (tv == 2) return launch<GatRed<2, true>, 2>(a, stages, s, 64);
-    return launch<GatRed<4, true>, 4>(a, stages, s, 64);
-  }
-  if (own_ok && vec == 4) {
+  if (att && vec == 4 && C % 4 == 0 && hl4 <= 64 && (hl4 & (hl4 - 1)) == 0 && (uintptr_t)att % 16 == 0) {
     a.att = att;
     return launch<GatRed<4, true>, 4>(a, stages, s, F >= 256 ? kGatLanes : 64);
   }

@@ -74,18 +74,6 @@ __device__ __forceinline__ float group_sum(float t, int g) {
   if (g >= 64) t += __shfl_xor(t, 32);
   return t;
 }
-// The upper levels of group_sum over `g` blocks of B lanes (B = 2 or 4), each
-// block holding one value in all its lanes: block pairs at every level, the
-// same tree group_sum builds over g single lanes.
-template <int B>
-__device__ __forceinline__ float group_sum_blocks(float t, int g) {
-  if (B < 4 && g >= 2) t += dpp<0x4E>(t);        // blocks of 2: quad_perm(2,3,0,1)
-  if (g >= 8 / B) t += dpp<0x141>(t);            // row_half_mirror: pairs 4-lane blocks
-  if (g >= 16 / B) t += dpp<0x140>(t);           // row_mirror: pairs 8-lane blocks
-  if (g >= 32 / B) t += __shfl_xor(t, 16);
-  if (g >= 64 / B) t += __shfl_xor(t, 32);
-  return t;
-}
 
 // wave-uniform value helpers
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }

@@ -30,7 +30,6 @@ MP_TUNE_FLAT_VEC = 6
 MP_TUNE_FLAT_VEC_ARG = 7
 MP_TUNE_FLAT_SEQ_TILES = 8
 MP_TUNE_FLAT_FAR_MIN_BYTES = 9
-MP_TUNE_GAT_TILE_VEC = 10
 MP_LOOPS_REMOVE = 0
 MP_LOOPS_ADD = 1
 MP_LOOPS_ADD_REMAINING = 2

@@ -591,47 +591,6 @@ def test_gat_aggregation_on_identical_inputs():
     assert (alpha.cpu() - al).abs().max().item() < 1e-6
 
 
-@pytest.mark.parametrize("H,C,chunk", [(8, 32, 64), (8, 32, 1024), (16, 16, 64), (4, 64, 128), (2, 32, 64),
-                                       (1, 64, 16), (8, 64, 256), (4, 16, 64), (3, 32, 64)])
-@pytest.mark.parametrize("mode", ["scalar", "far", "window"])
-def test_gat_feature_tiles_bitwise_equal_to_full_row_tile(H, C, chunk, mode):
-    """Fused GAT on 64- / 128-feature tiles of whole heads (k_agg_flat, online
-    softmax per tile, a_src rebuilt from the gathered tile in the node-score
-    kernel's reduction order) against the 256-feature tile (VEC=4): output,
-    alpha and row statistics bitwise equal, on a power-law graph whose hub rows
-    split across tasks; plus the bound against the reference formula.  Modes:
-    scalar slot batches (16 rows in flight), the same with 8 (x beyond the
-    Infinity Cache), and the per-lane slot window (no scalar batches).  Shapes
-    that no tile holds whole (F % 128 != 0 for VEC=2, 3 heads of 32) take the
-    256-feature path under every setting."""
-    _, ops, _, Graph, pl = _mods()
-    N, E = 1500, 40000
-    ei = pl(N, E, seed=11)
-    ei = torch.cat([ei, torch.stack([torch.randint(0, N, (6000,)), torch.full((6000,), 7)])], 1)  # a hub row
-    ei = P.add_self_loops(P.remove_self_loops(ei)[0], num_nodes=N)[0]
-    g = torch.Generator().manual_seed(5)
-    xw = torch.randn(N, H * C, generator=g)
-    att = torch.randn(1, H, 2 * C, generator=g) * 0.2
-    graph = Graph(ei.to(DEV), N, N, chunk=chunk)
-    res = {}
-    knobs = {"scalar": {}, "far": {"flat_far_min_bytes": 0}, "window": {"flat_smem": 0}}[mode]
-    for v in (0, 1, 2, 4):
-        with _tuned(gat_tile_vec=v, **knobs):
-            out, alpha = ops.gat_propagate(graph, ei.to(DEV), xw.to(DEV), att.to(DEV), H, C, 0.2, None, True)
-        res[v] = (out.cpu(), alpha.cpu())
-    for v in (1, 2, 4):
-        assert torch.equal(res[v][0], res[0][0]), "tile VEC=%d output differs from the 256-feature tile" % v
-        assert torch.equal(res[v][1], res[0][1]), "tile VEC=%d alpha differs" % v
-    x_i = xw[ei[1]].view(-1, H, C)
-    x_j = xw[ei[0]].view(-1, H, C)
-    a = torch.nn.functional.leaky_relu((torch.cat([x_i, x_j], -1) * att).sum(-1), 0.2)
-    al = P.softmax(a, ei[1], N)
-    want = S.scatter_sum(x_j * al.view(-1, H, 1), ei[1], N).view(N, H * C)
-    terms = S.scatter_sum(x_j.abs() * al.view(-1, H, 1), ei[1], N).view(N, H * C)
-    _bound_ok(res[1][0], want, terms)
-    assert (res[1][1] - al).abs().max().item() < 1e-6
-
-
 @pytest.mark.parametrize("H,C,chunk", [(8, 32, 64), (8, 32, 512), (4, 16, 64), (2, 64, 128), (1, 128, 64),
                                        (3, 32, 64), (16, 16, 64), (5, 64, 1024)])
 def test_gat_two_pass_matches_reference_formula(monkeypatch, H, C, chunk):
