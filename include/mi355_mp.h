@@ -223,6 +223,23 @@ int mp_gat_aggregate_att_f32(const mp_csr* g, const float* xw, const float* a_sr
                              int64_t ldo, float* row_stats, void* slab,
                              size_t slab_bytes, int32_t stages, void* stream);
 
+/* Training forward of the same layer (att given, C % 4 == 0, C/4 a power of two
+ * <= 64: mp_gat_train_ok), no bias (the backward needs the pre-bias output).
+ * Besides out and row_stats it leaves, with the same online rescaling,
+ *   out2[i,h,:]  = sum_j alpha_ij leaky'_ij xw[j,h,:]    ([n_rows, H*C], contiguous)
+ *   row_s2[i,h]  = sum_j alpha_ij leaky'_ij             ([n_rows, H])
+ * with leaky' = 1 where a_src[j,h] + a_dst[i,h] > 0, else slope.  They turn the
+ * backward's d a_dst into a node-wise quantity (mp_gat_backward_prep_train_f32),
+ * so mp_gat_backward_f32 then runs with de = NULL.
+ * Slab: mp_gat_train_slab_bytes(g, H, C). */
+int mp_gat_train_ok(int32_t H, int32_t C);
+size_t mp_gat_train_slab_bytes(const mp_csr* g, int32_t H, int32_t C);
+int mp_gat_aggregate_train_f32(const mp_csr* g, const float* xw, const float* a_src,
+                               const float* a_dst, const float* att, int32_t H, int32_t C,
+                               float slope, float* out, int64_t ldo, float* row_stats,
+                               float* out2, float* row_s2, void* slab, size_t slab_bytes,
+                               int32_t stages, void* stream);
+
 /* Two-pass form of the same layer, in the reference's own arithmetic
  * (utils.softmax [U3] then message x_j * alpha and scatter_add in edge order,
  * GATConv.update + bias [U6]):
@@ -275,8 +292,9 @@ int mp_gat_sddmm_f32(const mp_csr* g, const int32_t* slot_row, const float* grow
  * pack [n_dst, H, 4] = mp_gat_backward_prep_f32 output.  de[gt.eid[k], h]
  * receives slot k's value: pass the destination-CSR slot of each edge in
  * gt.eid to get de in destination-CSR order (then d a_dst is a contiguous
- * segmented sum: mp_aggregate_f32 with col = NULL).  Needs C/4 or C to be a
- * power of two <= 64.
+ * segmented sum: mp_aggregate_f32 with col = NULL).  de = NULL skips it (the
+ * training forward's out2 / row_s2 give d a_dst directly).  Needs C/4 or C to
+ * be a power of two <= 64.
  * Slab: mp_gat_slab_bytes(gt, H, C). */
 int mp_gat_backward_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, const float* xw,
                         const float* a_src, const float* pack, const float* att, int32_t H,
@@ -291,6 +309,15 @@ int mp_gat_backward_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, co
 int mp_gat_backward_prep_f32(const float* grad_out, int64_t ldg, const float* agg, int64_t lda,
                              const float* a_dst, const float* row_stats, int64_t n, int32_t H,
                              int32_t C, float* pack, float* gsum_part, void* stream);
+
+/* The same prologue after mp_gat_aggregate_train_f32 (C % 4 == 0, C/4 a power
+ * of two <= 64, 16-byte aligned rows), which also writes
+ *   grad_a_dst[n,h] = sum_j de_nj = <grad_out[n,h,:], agg2[n,h,:]> - rs[n,h] * row_s2[n,h]
+ * (agg2 / row_s2 = the training forward's out2 / row_s2). */
+int mp_gat_backward_prep_train_f32(const float* grad_out, int64_t ldg, const float* agg, int64_t lda,
+                                   const float* agg2, const float* row_s2, const float* a_dst,
+                                   const float* row_stats, int64_t n, int32_t H, int32_t C,
+                                   float* pack, float* gsum_part, float* grad_a_dst, void* stream);
 
 /* Rows of the per-block partial arrays of the prep/finish kernels for n nodes. */
 int mp_gat_bwd_blocks(int64_t n);

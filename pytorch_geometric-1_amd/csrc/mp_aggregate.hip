@@ -41,6 +41,10 @@ constexpr int kU_Vec4 = 8;      // x-row loads in flight per task (VEC=4, 64-lan
 constexpr int kU_Vec2 = 16;     // x-row loads in flight per task (VEC=2: the flat kernel, 128-feature tiles)
 constexpr int kU_Vec1 = 16;     // x-row loads in flight per task (VEC=1)
 constexpr int kU_Vec1Far = 8;   // ... scalar-batch sum/mean over an x larger than the Infinity Cache
+#ifndef MP_U_GAT_TRAIN
+#define MP_U_GAT_TRAIN 4
+#endif
+constexpr int kU_GatTrain = MP_U_GAT_TRAIN;  // ... the GAT training forward (A/B U=4/6/8: 8.36/8.57/8.52 ms)
 constexpr int kU_Narrow = 12;   // x-row loads in flight per task (VEC=4, tasks of < 64 lanes)
 constexpr int kWideLanes = 32;  // lanes per task of k_agg_main for rows of >= 256 features (32 beats 64 by ~9%)
 constexpr int kGatLanes = 64;   // lanes per GAT task for H*C >= 256
@@ -120,6 +124,12 @@ struct AggArgs {
   float* de;          // [n_edges, H] d score per slot (this CSR's slot order)
   float* ga;          // [n_rows, H]  d a_src = row sums of d score
   const float* att;   // [H, 2C]      (att_dst | att_src)
+  // GAT training forward (GatRed<.., TR>): out2[r, f] = sum_k alpha leaky' xw (ld F),
+  // row_s2[r, h] = sum_k alpha leaky', and their partial slabs
+  float* out2;
+  float* row_s2;
+  float* slab_v2;
+  float* slab_s2;
 };
 
 // ---------------------------------------------------------------------------
@@ -137,6 +147,8 @@ struct PRef {
   float* v;
   int32_t* a;
   float* st;
+  float* v2;  // GAT training forward: second accumulator, and its per-head sum
+  float* s2;
 };
 
 template <int VEC, bool HAS_W, bool MEAN>
@@ -333,7 +345,15 @@ struct ArgRed {
 // order, as k_gat_node_scores_wave, so bitwise the value that kernel stores).
 // It saves the per-slot a_src gather (one 256-B L1-queue segment per slot on
 // top of the row's four).
-template <int VEC, bool OWN = false>
+//
+// TR (training forward): also accumulates, with the same online rescaling,
+//   acc2 = sum_k alpha_k leaky'_k x_k  and  s2 = sum_k alpha_k leaky'_k
+// (leaky' = 1 or slope at the pre-activation a_src + a_dst), written to
+// out2 / row_s2.  They make the backward's d a_dst node-wise:
+//   d a_dst[i,h] = sum_j de_ij = <g_i, acc2_i>_h - rs_i s2_i
+// (de_ij = alpha_ij (<g_i, xw_j> - rs_i) leaky'_ij), so the backward writes no
+// per-edge d score and needs no segmented pass over it.
+template <int VEC, bool OWN = false, bool TR = false>
 struct GatRed {
   static constexpr bool kW = false;
   static constexpr bool kEid = false;
@@ -345,9 +365,13 @@ struct GatRed {
   struct Part {
     float v[VEC];
     float m, s;
+    float v2[TR ? VEC : 1];
+    float s2;
   };
   float acc[VEC];
   float m, s, ad;
+  [[maybe_unused]] float acc2[TR ? VEC : 1];
+  [[maybe_unused]] float s2 = 0.f;
   int h;
   [[maybe_unused]] float y[OWN ? VEC : 1];
   [[maybe_unused]] int hl = 1;
@@ -373,12 +397,18 @@ struct GatRed {
   __device__ __forceinline__ void begin(const AggArgs& p, int64_t row, bool, int, bool) {
 #pragma unroll
     for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
+    if constexpr (TR) {
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) acc2[k] = 0.f;
+      s2 = 0.f;
+    }
     m = -INFINITY;
     s = 0.f;
     ad = p.a_dst[row * p.H + h];
   }
   __device__ __forceinline__ void consume_gat(const AggArgs& p, const Frag<VEC>& v, float as) {
     float a = as + ad;
+    [[maybe_unused]] const bool pos = a > 0.f;  // leaky' = 1 : slope (the backward's test)
     a = a > 0.f ? a : a * p.slope;  // F.leaky_relu
     // mn = fmaxf(m, a); sc = expf(m - mn); pe = expf(a - mn) with one exp:
     // one of the two arguments is x - x, i.e. 0 (exp 1) or NaN for an
@@ -391,6 +421,12 @@ struct GatRed {
     s = s * sc + pe;
 #pragma unroll
     for (int k = 0; k < VEC; ++k) acc[k] = acc[k] * sc + pe * v.v[k];
+    if constexpr (TR) {
+      const float pl = pos ? pe : pe * p.slope;
+      s2 = s2 * sc + pl;
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) acc2[k] = acc2[k] * sc + pl * v.v[k];
+    }
     m = up ? a : m;
   }
   __device__ __forceinline__ void consume(const Frag<VEC>&, float, int, float) {}
@@ -403,6 +439,12 @@ struct GatRed {
       r.st[0] = m;
       r.st[1] = s;
     }
+    if constexpr (TR) {
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) o.v[k] = acc2[k];
+      store_frag<VEC>(r.v2, o);
+      if (stat_writer) *r.s2 = s2;
+    }
   }
   static __device__ __forceinline__ Part load(PRef r) {
     Frag<VEC> o = load_frag<VEC>(r.v);
@@ -411,6 +453,12 @@ struct GatRed {
     for (int k = 0; k < VEC; ++k) q.v[k] = o.v[k];
     q.m = r.st[0];
     q.s = r.st[1];
+    if constexpr (TR) {
+      Frag<VEC> o2 = load_frag<VEC>(r.v2);
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) q.v2[k] = o2.v[k];
+      q.s2 = *r.s2;
+    }
     return q;
   }
   __device__ __forceinline__ void set(const Part& q) {
@@ -418,6 +466,11 @@ struct GatRed {
     for (int k = 0; k < VEC; ++k) acc[k] = q.v[k];
     m = q.m;
     s = q.s;
+    if constexpr (TR) {
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) acc2[k] = q.v2[k];
+      s2 = q.s2;
+    }
   }
   __device__ __forceinline__ void merge(const Part& q) {
     float mn = fmaxf(m, q.m);
@@ -425,6 +478,11 @@ struct GatRed {
     s = s * c0 + q.s * c1;
 #pragma unroll
     for (int k = 0; k < VEC; ++k) acc[k] = acc[k] * c0 + q.v[k] * c1;
+    if constexpr (TR) {
+      s2 = s2 * c0 + q.s2 * c1;
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) acc2[k] = acc2[k] * c0 + q.v2[k] * c1;
+    }
     m = mn;
   }
   __device__ __forceinline__ Part part() const {
@@ -433,6 +491,11 @@ struct GatRed {
     for (int k = 0; k < VEC; ++k) q.v[k] = acc[k];
     q.m = m;
     q.s = s;
+    if constexpr (TR) {
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) q.v2[k] = acc2[k];
+      q.s2 = s2;
+    }
     return q;
   }
   __device__ __forceinline__ void finish(const AggArgs& p, int64_t row, int64_t, int f, bool act) {
@@ -450,6 +513,12 @@ struct GatRed {
     if (p.row_stats && (f % p.C == 0)) {
       p.row_stats[(row * p.H + h) * 2] = m;
       p.row_stats[(row * p.H + h) * 2 + 1] = den;
+    }
+    if constexpr (TR) {
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) o.v[k] = acc2[k] / den;
+      store_out<VEC>(p.out2 + row * (int64_t)p.F + f, o);
+      if (f % p.C == 0) p.row_s2[row * p.H + h] = s2 / den;
     }
   }
 };
@@ -638,7 +707,7 @@ struct GatBwdRed {
 #pragma unroll
     for (int k = 0; k < VEC; ++k) acc[k] = __builtin_fmaf(alpha, v.v[k], acc[k]);
     dacc += de;
-    if (leader) p.de[slot * p.H + h] = de;
+    if (leader && p.de) p.de[slot * p.H + h] = de;  // no de: the training forward made d a_dst node-wise
   }
   __device__ __forceinline__ void consume(const Frag<VEC>&, float, int, float) {}
   __device__ __forceinline__ void save(PRef r, bool stat_writer) const {
@@ -691,6 +760,8 @@ __device__ __forceinline__ PRef slab_ref(const AggArgs& p, int64_t s, int f, con
   r.v = p.slab_v + s * p.slab_ld + f;
   r.a = p.slab_a ? p.slab_a + s * p.slab_ld + f : nullptr;
   r.st = p.slab_s ? p.slab_s + (s * p.H + red.h) * 2 : nullptr;
+  r.v2 = p.slab_v2 ? p.slab_v2 + s * p.slab_ld + f : nullptr;
+  r.s2 = p.slab_s2 ? p.slab_s2 + s * p.H + red.h : nullptr;
   return r;
 }
 
@@ -901,10 +972,14 @@ struct GatAlphaWin {
 // GAT forward: a_src of each 64-slot window staged in LDS (see SlotWin; 8.85 -> 8.66 ms, bitwise the same)
 template <class Red>
 constexpr bool own_as_v = false;
-template <int VEC>
-constexpr bool own_as_v<GatRed<VEC, true>> = true;
+template <int VEC, bool TR>
+constexpr bool own_as_v<GatRed<VEC, true, TR>> = true;
 template <class Red, int L>
 constexpr bool kGatWin = Red::kGat && !own_as_v<Red> && L == 64;
+template <class Red>
+constexpr bool kGatTrain = false;
+template <int VEC, bool OWN>
+constexpr bool kGatTrain<GatRed<VEC, OWN, true>> = true;
 
 template <class Red, int VEC, int U, int L>
 __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p,
@@ -1433,7 +1508,7 @@ static int launch_main(void (*k)(AggArgs), dim3 grid, hipStream_t s, const AggAr
 
 template <class Red, int VEC, int L>
 static int launch_l(const AggArgs& a, int stages, hipStream_t s) {
-  constexpr int U = VEC == 4 ? (L == 64 ? kU_Vec4 : kU_Narrow)
+  constexpr int U = VEC == 4 ? (L == 64 ? (kGatTrain<Red> ? kU_GatTrain : kU_Vec4) : kU_Narrow)
                              : (VEC == 2 ? kU_Vec2 : (L < kU_Vec1 ? L : kU_Vec1));  // VEC=1 groups < 16 lanes: GAT stats
   const int ftiles = (int)ceil_div(a.F, L * VEC);
   if (stages & MP_STAGE_MAIN) {
@@ -1800,6 +1875,19 @@ size_t mp_gat_slab_bytes(const mp_csr* g, int32_t H, int32_t C) {
   return v + st + 256;
 }
 
+size_t mp_gat_train_slab_bytes(const mp_csr* g, int32_t H, int32_t C) {
+  if (!g || H <= 0 || C <= 0) return 256;
+  size_t slots = 2 * (size_t)g->n_waves;
+  size_t v = align_up(slots * (size_t)slab_ld_for(H * C) * 4, 256);
+  size_t s2 = align_up(slots * (size_t)H * 4, 256);
+  return mp_gat_slab_bytes(g, H, C) + v + s2;
+}
+
+int mp_gat_train_ok(int32_t H, int32_t C) {
+  const int hl4 = C / 4;
+  return H > 0 && C > 0 && C % 4 == 0 && hl4 <= 64 && (hl4 & (hl4 - 1)) == 0 ? 1 : 0;
+}
+
 int mp_gat_aggregate_f32(const mp_csr* g, const float* xw, const float* a_src, const float* a_dst,
                          int32_t H, int32_t C, float slope, const float* bias, float* out,
                          int64_t ldo, float* row_stats, void* slab, size_t slab_bytes,
@@ -1855,6 +1943,51 @@ int mp_gat_aggregate_att_f32(const mp_csr* g, const float* xw, const float* a_sr
     case 2: return launch<GatRed<2>, 2>(a, stages, s);
     default: return launch<GatRed<1>, 1>(a, stages, s);
   }
+}
+
+int mp_gat_aggregate_train_f32(const mp_csr* g, const float* xw, const float* a_src, const float* a_dst,
+                               const float* att, int32_t H, int32_t C, float slope, float* out, int64_t ldo,
+                               float* row_stats, float* out2, float* row_s2, void* slab, size_t slab_bytes,
+                               int32_t stages, void* stream) {
+  MP_DEVICE_GUARD(stream);
+  int rc = check_graph(g, "mp_gat_aggregate_train_f32");
+  if (rc) return rc;
+  MP_CHECK_ARG(mp_gat_train_ok(H, C), "mp_gat_aggregate_train_f32: needs C %% 4 == 0 and C/4 a power of two <= 64");
+  MP_CHECK_ARG(xw && a_src && a_dst && att && out && row_stats && out2 && row_s2,
+               "mp_gat_aggregate_train_f32: null input");
+  const int F = H * C;
+  MP_CHECK_ARG(ldo >= F, "mp_gat_aggregate_train_f32: ldo < H*C");
+  MP_CHECK_ARG((uintptr_t)xw % 16 == 0 && (uintptr_t)att % 16 == 0 && (uintptr_t)out % 16 == 0 && ldo % 4 == 0 &&
+                   (uintptr_t)out2 % 16 == 0,
+               "mp_gat_aggregate_train_f32: xw, att, out, out2 must be 16-byte aligned (ldo % 4 == 0)");
+  MP_CHECK_ARG(slab != nullptr && slab_bytes >= mp_gat_train_slab_bytes(g, H, C),
+               "mp_gat_aggregate_train_f32: slab workspace too small");
+  AggArgs a{};
+  fill_graph(a, g);
+  a.F = F;
+  a.x = xw;
+  a.ldx = F;
+  a.out = out;
+  a.ldo = ldo;
+  a.a_src = a_src;
+  a.a_dst = a_dst;
+  a.att = att;
+  a.H = H;
+  a.C = C;
+  a.slope = slope;
+  a.row_stats = row_stats;
+  a.out2 = out2;
+  a.row_s2 = row_s2;
+  a.slab_ld = slab_ld_for(F);
+  const size_t slots = 2 * (size_t)g->n_waves;
+  char* b = (char*)slab;
+  const size_t v = align_up(slots * (size_t)a.slab_ld * 4, 256);
+  a.slab_v = (float*)b;
+  a.slab_s = (float*)(b + v);
+  b += mp_gat_slab_bytes(g, H, C);
+  a.slab_v2 = (float*)b;
+  a.slab_s2 = (float*)(b + v);
+  return launch<GatRed<4, true, true>, 4>(a, stages, as_stream(stream), F >= 256 ? kGatLanes : 64);
 }
 
 int mp_gat_two_pass_ok(int32_t H, int32_t C) {
@@ -1944,7 +2077,7 @@ int mp_gat_backward_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, co
   int rc = check_graph(gt, "mp_gat_backward_f32");
   if (rc) return rc;
   MP_CHECK_ARG(H > 0 && C > 0, "mp_gat_backward_f32: H, C must be positive");
-  MP_CHECK_ARG(grad_out && xw && a_src && pack && att && grad_xw && grad_a_src && (gt->n_edges == 0 || de),
+  MP_CHECK_ARG(grad_out && xw && a_src && pack && att && grad_xw && grad_a_src,
                "mp_gat_backward_f32: null pointer");
   MP_CHECK_ARG((uintptr_t)pack % 16 == 0, "mp_gat_backward_f32: pack must be 16-byte aligned");
   const int F = H * C;

@@ -180,7 +180,10 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep_wave(const float* __restri
                                                            const float* __restrict__ a_dst,
                                                            const float* __restrict__ stats, int64_t n, int32_t H,
                                                            int32_t C, int32_t G, float* __restrict__ pack,
-                                                           float* __restrict__ gsum_part) {
+                                                           float* __restrict__ gsum_part,
+                                                           const float* __restrict__ agg2 = nullptr,
+                                                           const float* __restrict__ s2 = nullptr,
+                                                           float* __restrict__ ga_dst = nullptr) {
   const int lane = lane_id();
   const int wid = (int)(threadIdx.x >> 6);
   const int64_t HC = (int64_t)H * C;
@@ -200,6 +203,15 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep_wave(const float* __restri
       for (int k = 0; k < 4; ++k) t = __fadd_rn(t, __fmul_rn(x.v[k], y.v[k]));
       for (int o = 1; o < G; o <<= 1) t = __fadd_rn(t, __shfl_xor(t, o));
       if (act && (lane & (G - 1)) == 0) write_pack(pack, a_dst, stats, r * H + fs / C, t);
+      if (agg2) {  // d a_dst = <g, agg2>_h - rs s2  (training forward's second accumulator)
+        Frag<4> z = load_frag<4>(agg2 + r * HC + fs);
+        float t2 = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t2 = __builtin_fmaf(x.v[k], z.v[k], t2);
+        for (int o = 1; o < G; o <<= 1) t2 += __shfl_xor(t2, o);
+        const int64_t q = r * H + fs / C;
+        if (act && (lane & (G - 1)) == 0) ga_dst[q] = __builtin_fmaf(-t, s2[q], t2);
+      }
       if (gsum_part && act) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) cs[k] += x.v[k];
@@ -296,6 +308,29 @@ int mp_gat_sddmm_f32(const mp_csr* g, const int32_t* slot_row, const float* grow
     k_gat_sddmm_scalar<<<(unsigned)ceil_div(total, 256), 256, 0, s>>>(g->col, slot_row, g->n_edges, grow, ldg,
                                                                       x, ldx, H, C, out);
   }
+  MP_CHECK_LAUNCH();
+  return MP_OK;
+}
+
+int mp_gat_backward_prep_train_f32(const float* grad_out, int64_t ldg, const float* agg, int64_t lda,
+                                   const float* agg2, const float* row_s2, const float* a_dst,
+                                   const float* row_stats, int64_t n, int32_t H, int32_t C, float* pack,
+                                   float* gsum_part, float* grad_a_dst, void* stream) {
+  MP_DEVICE_GUARD(stream);
+  MP_CHECK_ARG(H > 0 && C > 0 && n >= 0, "mp_gat_backward_prep_train_f32: bad sizes");
+  if (n == 0) return MP_OK;
+  MP_CHECK_ARG(grad_out && agg && agg2 && row_s2 && a_dst && row_stats && pack && grad_a_dst,
+               "mp_gat_backward_prep_train_f32: null pointer");
+  const int64_t F = (int64_t)H * C;
+  const int G = C / 4;
+  MP_CHECK_ARG(C % 4 == 0 && G <= 64 && (G & (G - 1)) == 0, "mp_gat_backward_prep_train_f32: needs C/4 a power of two");
+  MP_CHECK_ARG((uintptr_t)pack % 16 == 0 && (uintptr_t)grad_out % 16 == 0 && (uintptr_t)agg % 16 == 0 &&
+                   (uintptr_t)agg2 % 16 == 0 && ldg % 4 == 0 && lda % 4 == 0,
+               "mp_gat_backward_prep_train_f32: 16-byte alignment required");
+  MP_CHECK_ARG(ldg >= F && lda >= F, "mp_gat_backward_prep_train_f32: leading dimension < H*C");
+  MP_CHECK_ARG(!gsum_part || F <= 256, "mp_gat_backward_prep_train_f32: gsum_part needs H*C <= 256");
+  k_gat_bwd_prep_wave<<<(unsigned)mp_gat_bwd_blocks(n), 256, 0, as_stream(stream)>>>(
+      grad_out, ldg, agg, lda, a_dst, row_stats, n, H, C, G, pack, gsum_part, agg2, row_s2, grad_a_dst);
   MP_CHECK_LAUNCH();
   return MP_OK;
 }

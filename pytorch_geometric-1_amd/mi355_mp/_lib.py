@@ -71,6 +71,10 @@ SIGNATURES = {
                                             c_p, i64, c_p, c_p, sz, i32, c_p]),
     "mp_gat_aggregate_att_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, c_p, c_p, i32, i32, f32, c_p,
                                                 c_p, i64, c_p, c_p, sz, i32, c_p]),
+    "mp_gat_train_ok": (ctypes.c_int, [i32, i32]),
+    "mp_gat_train_slab_bytes": (sz, [ctypes.POINTER(MpCsr), i32, i32]),
+    "mp_gat_aggregate_train_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, c_p, c_p, i32, i32, f32,
+                                                  c_p, i64, c_p, c_p, c_p, c_p, sz, i32, c_p]),
     "mp_gat_two_pass_ok": (ctypes.c_int, [i32, i32]),
     "mp_gat_softmax_aggregate_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, c_p, c_p, i32, i32, f32,
                                                     c_p, c_p, i64, c_p, c_p, sz, i32, c_p]),
@@ -84,6 +88,8 @@ SIGNATURES = {
     "mp_gat_backward_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, i64, c_p, c_p, c_p, c_p, i32, i32,
                                            ctypes.c_float, c_p, c_p, c_p, c_p, sz, i32, c_p]),
     "mp_gat_backward_prep_f32": (ctypes.c_int, [c_p, i64, c_p, i64, c_p, c_p, i64, i32, i32, c_p, c_p, c_p]),
+    "mp_gat_backward_prep_train_f32": (ctypes.c_int, [c_p, i64, c_p, i64, c_p, c_p, c_p, c_p, i64, i32, i32, c_p,
+                                                      c_p, c_p, c_p]),
     "mp_gat_bwd_blocks": (ctypes.c_int, [i64]),
     "mp_gat_backward_finish_f32": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, i64, i32, i32, c_p, c_p]),
     "mp_heads_outer_add_f32": (ctypes.c_int, [c_p, i64, c_p, i64, i32, i32, c_p, i64, c_p]),

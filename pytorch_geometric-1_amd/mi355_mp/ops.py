@@ -386,7 +386,15 @@ def gat_two_pass(csr, H, C):
     return GAT_TWO_PASS and bool(_lib.load().mp_gat_two_pass_ok(H, C))
 
 
-def _gat_forward(graph, edge_index, xw, att, H, C, slope, bias, want_alpha):
+# Training forward: the fused pass also leaves sum_j alpha leaky' xw_j and
+# sum_j alpha leaky' per (row, head) (mp_gat_aggregate_train_f32), which make the
+# backward's d a_dst node-wise: no per-edge d score array, no segmented pass.
+GAT_TRAIN_FWD = True
+
+
+def _gat_forward(graph, edge_index, xw, att, H, C, slope, bias, want_alpha, train2=False):
+    """Returns (out, alpha, a_src, a_dst, stats, extra); extra = (agg2, s2) when
+    train2 and the training forward applies, else None."""
     lib = _lib.load()
     dev = xw.device
     N = xw.shape[0]
@@ -403,19 +411,32 @@ def _gat_forward(graph, edge_index, xw, att, H, C, slope, bias, want_alpha):
     out = torch.empty((graph.n_dst, H * C), dtype=torch.float32, device=dev)
     stats = torch.empty((graph.n_dst, H, 2), dtype=torch.float32, device=dev)
     g = csr.struct("other")
-    sb = lib.mp_gat_slab_bytes(g, H, C)
-    slab = torch.empty(sb, dtype=torch.uint8, device=dev)
-    if gat_two_pass(csr, H, C):
-        _lib.check(lib.mp_gat_softmax_aggregate_f32(g, csr.slot_rows().data_ptr(), xw.data_ptr(), a_src.data_ptr(),
-                                                    a_dst.data_ptr(), H, C, float(slope), _lib.ptr(bias),
-                                                    out.data_ptr(), out.stride(0), stats.data_ptr(), slab.data_ptr(),
-                                                    sb, _lib.MP_STAGE_ALL, st), "mp_gat_softmax_aggregate_f32")
-    else:
-        _lib.check(lib.mp_gat_aggregate_att_f32(g, xw.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(),
-                                                att_c.data_ptr() if GAT_OWN_A_SRC else None, H, C, float(slope),
-                                                _lib.ptr(bias), out.data_ptr(), out.stride(0), stats.data_ptr(),
-                                                slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
-                   "mp_gat_aggregate_att_f32")
+    extra = None
+    if (train2 and bias is None and GAT_TRAIN_FWD and GAT_OWN_A_SRC and lib.mp_gat_train_ok(H, C)
+            and not gat_two_pass(csr, H, C) and xw.data_ptr() % 16 == 0):
+        agg2 = torch.empty((graph.n_dst, H * C), dtype=torch.float32, device=dev)
+        s2 = torch.empty((graph.n_dst, H), dtype=torch.float32, device=dev)
+        sb = lib.mp_gat_train_slab_bytes(g, H, C)
+        slab = torch.empty(sb, dtype=torch.uint8, device=dev)
+        _lib.check(lib.mp_gat_aggregate_train_f32(g, xw.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(),
+                                                  att_c.data_ptr(), H, C, float(slope), out.data_ptr(), out.stride(0),
+                                                  stats.data_ptr(), agg2.data_ptr(), s2.data_ptr(), slab.data_ptr(),
+                                                  sb, _lib.MP_STAGE_ALL, st), "mp_gat_aggregate_train_f32")
+        extra = (agg2, s2)
+    if extra is None:
+        sb = lib.mp_gat_slab_bytes(g, H, C)
+        slab = torch.empty(sb, dtype=torch.uint8, device=dev)
+        if gat_two_pass(csr, H, C):
+            _lib.check(lib.mp_gat_softmax_aggregate_f32(g, csr.slot_rows().data_ptr(), xw.data_ptr(), a_src.data_ptr(),
+                                                        a_dst.data_ptr(), H, C, float(slope), _lib.ptr(bias),
+                                                        out.data_ptr(), out.stride(0), stats.data_ptr(), slab.data_ptr(),
+                                                        sb, _lib.MP_STAGE_ALL, st), "mp_gat_softmax_aggregate_f32")
+        else:
+            _lib.check(lib.mp_gat_aggregate_att_f32(g, xw.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(),
+                                                    att_c.data_ptr() if GAT_OWN_A_SRC else None, H, C, float(slope),
+                                                    _lib.ptr(bias), out.data_ptr(), out.stride(0), stats.data_ptr(),
+                                                    slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
+                       "mp_gat_aggregate_att_f32")
     alpha = None
     if want_alpha:
         E = edge_index.shape[1]
@@ -425,7 +446,7 @@ def _gat_forward(graph, edge_index, xw, att, H, C, slope, bias, want_alpha):
         _lib.check(lib.mp_gat_alpha_f32(src.data_ptr(), dst.data_ptr(), E, H, a_src.data_ptr(),
                                         a_dst.data_ptr(), float(slope), stats.data_ptr(), alpha.data_ptr(), st),
                    "mp_gat_alpha_f32")
-    return out, alpha, a_src, a_dst, stats
+    return out, alpha, a_src, a_dst, stats, extra
 
 
 def _heads_aggregate(csr, gather, w_slot, H, x):
@@ -451,7 +472,8 @@ def _gat_bwd_fused_ok(C):
     return (C % 4 == 0 and pow2(C // 4)) or pow2(C)
 
 
-def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope, want_att, want_bias):
+def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope, want_att, want_bias,
+                        extra=None):
     """GATConv backward: prep (packed destination terms + bias-grad partials),
     one gather pass over the transposed CSR (mp_gat_backward_f32), the d a_dst
     row sums over the dst CSR (reading the per-edge d score through the
@@ -470,9 +492,19 @@ def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope
     nb = int(lib.mp_gat_bwd_blocks(N))
     pack = torch.empty((N, H, 4), dtype=torch.float32, device=dev)
     gpart = torch.empty((nb, F), dtype=torch.float32, device=dev) if (want_bias and epi) else None
-    _lib.check(lib.mp_gat_backward_prep_f32(g.data_ptr(), g.stride(0), agg.data_ptr(), agg.stride(0),
-                                            a_dst.data_ptr(), stats.data_ptr(), N, H, C, pack.data_ptr(),
-                                            _lib.ptr(gpart), st), "mp_gat_backward_prep_f32")
+    ga_dst = None
+    if extra is not None:
+        # d a_dst[n,h] = <g_n, agg2_n>_h - rs_n,h s2_n,h: node-wise, no per-edge d score
+        agg2, s2 = extra
+        ga_dst = torch.empty((N, H), dtype=torch.float32, device=dev)
+        _lib.check(lib.mp_gat_backward_prep_train_f32(g.data_ptr(), g.stride(0), agg.data_ptr(), agg.stride(0),
+                                                      agg2.data_ptr(), s2.data_ptr(), a_dst.data_ptr(),
+                                                      stats.data_ptr(), N, H, C, pack.data_ptr(), _lib.ptr(gpart),
+                                                      ga_dst.data_ptr(), st), "mp_gat_backward_prep_train_f32")
+    else:
+        _lib.check(lib.mp_gat_backward_prep_f32(g.data_ptr(), g.stride(0), agg.data_ptr(), agg.stride(0),
+                                                a_dst.data_ptr(), stats.data_ptr(), N, H, C, pack.data_ptr(),
+                                                _lib.ptr(gpart), st), "mp_gat_backward_prep_f32")
     gb = None
     if want_bias:
         gb = gpart.sum(0) if gpart is not None else g.sum(0)
@@ -480,17 +512,19 @@ def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope
     E = src.n_edges
     gx = torch.empty((N, F), dtype=torch.float32, device=dev)
     ga_src = torch.empty((N, H), dtype=torch.float32, device=dev)
-    de = torch.empty((max(E, 1), H), dtype=torch.float32, device=dev)   # in dst-CSR slot order
+    # per-edge d score in dst-CSR slot order (only without the training forward's extras)
+    de = torch.empty((max(E, 1), H), dtype=torch.float32, device=dev) if ga_dst is None else None
     gs = src.struct("dst_slot")
     sb = lib.mp_gat_slab_bytes(gs, H, C)
     slab = torch.empty(sb, dtype=torch.uint8, device=dev)
     _lib.check(lib.mp_gat_backward_f32(gs, g.data_ptr(), g.stride(0), xw.data_ptr(), a_src.data_ptr(),
                                        pack.data_ptr(), att_c.data_ptr(), H, C, float(slope), gx.data_ptr(),
-                                       ga_src.data_ptr(), de.data_ptr(), slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
+                                       ga_src.data_ptr(), _lib.ptr(de), slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
                "mp_gat_backward_f32")
     del slab, pack
-    ga_dst, _ = _aggregate(graph.dst, "slot", de, None, "sum", 0, None)
-    del de
+    if ga_dst is None:
+        ga_dst, _ = _aggregate(graph.dst, "slot", de, None, "sum", 0, None)
+        del de
     gatt = None
     if epi:
         apart = torch.empty((nb, 2, F), dtype=torch.float32, device=dev)
@@ -515,8 +549,8 @@ class _GatPropagate(torch.autograd.Function):
     def forward(ctx, xw, att, bias, graph, edge_index, H, C, slope, want_alpha, train):
         fused = train and _gat_bwd_fused_ok(C)
         # the fused backward needs the pre-bias aggregate (rs_i = <g_i, agg_i>)
-        out, alpha, a_src, a_dst, stats = _gat_forward(graph, edge_index, xw, att, H, C, slope,
-                                                       None if fused else bias, want_alpha)
+        out, alpha, a_src, a_dst, stats, extra = _gat_forward(graph, edge_index, xw, att, H, C, slope,
+                                                              None if fused else bias, want_alpha, train2=fused)
         agg = None
         if fused:
             agg = out
@@ -524,7 +558,9 @@ class _GatPropagate(torch.autograd.Function):
         ctx.graph, ctx.H, ctx.C, ctx.slope = graph, H, C, slope
         ctx.has_bias = bias is not None
         ctx.fused = fused
-        ctx.save_for_backward(xw, att, edge_index, a_src, a_dst, stats, agg)
+        ctx.has_extra = extra is not None
+        ctx.save_for_backward(xw, att, edge_index, a_src, a_dst, stats, agg,
+                              *(extra if extra is not None else ()))
         if alpha is not None:
             ctx.mark_non_differentiable(alpha)
         return out, alpha
@@ -539,7 +575,8 @@ class _GatPropagate(torch.autograd.Function):
           dxw   += d a_src (x) att_src + d a_dst (x) att_dst;  d att = sum_n d a (x) xw
         Only [E, H]-sized arrays are materialised, never [E, H*C]."""
         lib = _lib.load()
-        xw, att, edge_index, a_src, a_dst, stats, agg = ctx.saved_tensors
+        xw, att, edge_index, a_src, a_dst, stats, agg = ctx.saved_tensors[:7]
+        extra = tuple(ctx.saved_tensors[7:9]) if ctx.has_extra else None
         graph, H, C, slope = ctx.graph, ctx.H, ctx.C, ctx.slope
         dev = xw.device
         st = _lib.stream_ptr(dev)
@@ -547,7 +584,8 @@ class _GatPropagate(torch.autograd.Function):
         N = xw.shape[0]
         if ctx.fused:
             gx, gatt, gb = _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope,
-                                               ctx.needs_input_grad[1], ctx.has_bias and ctx.needs_input_grad[2])
+                                               ctx.needs_input_grad[1], ctx.has_bias and ctx.needs_input_grad[2],
+                                               extra)
             return gx, gatt, gb, None, None, None, None, None, None, None
         gb = g.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
         dst, src = graph.dst, graph.src

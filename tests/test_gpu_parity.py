@@ -609,9 +609,9 @@ def test_gat_two_pass_matches_reference_formula(monkeypatch, H, C, chunk):
     graph = Graph(ei.to(DEV), N, N, chunk=chunk)
     monkeypatch.setattr(ops, "GAT_TWO_PASS", True)
     assert ops.gat_two_pass(graph.dst, H, C)
-    out, alpha, a_src, a_dst, stats = ops._gat_forward(graph, ei.to(DEV), xw.to(DEV), att.to(DEV), H, C, 0.2,
+    out, alpha, a_src, a_dst, stats, _ = ops._gat_forward(graph, ei.to(DEV), xw.to(DEV), att.to(DEV), H, C, 0.2,
                                                        bias.to(DEV), True)
-    out2, _, _, _, stats2 = ops._gat_forward(graph, ei.to(DEV), xw.to(DEV), att.to(DEV), H, C, 0.2,
+    out2, _, _, _, stats2, _ = ops._gat_forward(graph, ei.to(DEV), xw.to(DEV), att.to(DEV), H, C, 0.2,
                                              bias.to(DEV), False)
     assert torch.equal(out, out2) and torch.equal(stats, stats2)  # deterministic
     a_src, a_dst = a_src.cpu(), a_dst.cpu()
@@ -631,7 +631,7 @@ def test_gat_two_pass_matches_reference_formula(monkeypatch, H, C, chunk):
     _bound_ok(out.cpu(), want, terms)
     monkeypatch.setattr(ops, "GAT_TWO_PASS", False)
     assert not ops.gat_two_pass(graph.dst, H, C)
-    one, _, _, _, st1 = ops._gat_forward(graph, ei.to(DEV), xw.to(DEV), att.to(DEV), H, C, 0.2, bias.to(DEV), False)
+    one, _, _, _, st1, _ = ops._gat_forward(graph, ei.to(DEV), xw.to(DEV), att.to(DEV), H, C, 0.2, bias.to(DEV), False)
     _bound_ok(out.cpu(), one.cpu(), 2 * terms)
     assert torch.equal(st1.cpu()[has][..., 0], m[has])
 
@@ -1151,6 +1151,63 @@ def test_gat_fused_backward_hub_rows_split_across_tasks():
     for got, want in ((xd.grad, x64.grad), (conv.weight.grad, W.grad), (conv.att.grad, att.grad),
                       (conv.bias.grad, b.grad)):
         assert torch.allclose(got.cpu().double(), want, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("H,C,chunk", [(8, 32, 64), (4, 16, 16), (2, 64, 256), (1, 256, 64), (3, 4, 16)])
+def test_gat_training_forward_node_wise_d_a_dst(H, C, chunk, monkeypatch):
+    """mp_gat_aggregate_train_f32 leaves agg2 = sum alpha leaky' xw_j and
+    s2 = sum alpha leaky'; the backward then takes d a_dst = <g, agg2> - rs s2
+    per node instead of summing a per-edge d score.  Checks: agg2 / s2 against
+    the reference formula, the forward output bitwise equal to the inference
+    kernel's, and every gradient within the float64-autograd bound for both
+    backward forms (hub rows split across tasks: a star centre plus chunk 16)."""
+    from torch_geometric.nn import GATConv
+    from mi355_mp import ops
+    _, _, _, Graph, pl = _mods()
+    N, Fi = 1200, 12
+    g = torch.Generator().manual_seed(41)
+    ei = pl(N, 20000, seed=41)
+    ei = torch.cat([ei, torch.stack([torch.randint(0, N, (3000,), generator=g), torch.zeros(3000, dtype=torch.long)]),
+                    torch.stack([torch.zeros(3000, dtype=torch.long), torch.randint(0, N, (3000,), generator=g)])], 1)
+    x = torch.randn(N, Fi, generator=g)
+    gout = torch.randn(N, H * C, generator=g)
+    # agg2 / s2 against the reference formula, on the layer's own loops
+    ei_l = P.add_self_loops(P.remove_self_loops(ei)[0], num_nodes=N)[0]
+    xw = torch.randn(N, H * C, generator=g)
+    att = torch.randn(1, H, 2 * C, generator=g) * 0.3
+    graph = Graph(ei_l.to(DEV), N, N, chunk=chunk)
+    out, _, _, _, _, extra = ops._gat_forward(graph, ei_l.to(DEV), xw.to(DEV), att.to(DEV), H, C, 0.2, None, False,
+                                              train2=True)
+    out_inf, _, _, _, _, none = ops._gat_forward(graph, ei_l.to(DEV), xw.to(DEV), att.to(DEV), H, C, 0.2, None, False)
+    assert extra is not None and none is None
+    assert torch.equal(out, out_inf)
+    x_i = xw[ei_l[1]].view(-1, H, C)
+    x_j = xw[ei_l[0]].view(-1, H, C)
+    pre = (torch.cat([x_i, x_j], -1) * att).sum(-1)
+    al = P.softmax(torch.nn.functional.leaky_relu(pre, 0.2), ei_l[1], N)
+    lk = torch.where(pre > 0, torch.ones_like(pre), torch.full_like(pre, 0.2))
+    want2 = S.scatter_sum(x_j * (al * lk).view(-1, H, 1), ei_l[1], N).view(N, H * C)
+    terms2 = S.scatter_sum(x_j.abs() * (al * lk).view(-1, H, 1), ei_l[1], N).view(N, H * C)
+    _bound_ok(extra[0].cpu(), want2, terms2)
+    assert (extra[1].cpu() - S.scatter_sum(al * lk, ei_l[1], N)).abs().max().item() < 1e-5
+    # gradients, both backward forms, against float64 autograd
+    conv = GATConv(Fi, C, heads=H).to(DEV)
+    with torch.no_grad():
+        conv.bias.normal_()
+    W = conv.weight.detach().cpu().double().requires_grad_(True)
+    a64 = conv.att.detach().cpu().double().requires_grad_(True)
+    b = conv.bias.detach().cpu().double().requires_grad_(True)
+    x64 = x.double().requires_grad_(True)
+    P.gat_conv(x64, ei, W, a64, b, H, C).backward(gout.double())
+    grads = {}
+    for mode in (True, False):
+        monkeypatch.setattr(ops, "GAT_TRAIN_FWD", mode)
+        conv.zero_grad()
+        xd = x.to(DEV).requires_grad_(True)
+        conv(xd, ei.to(DEV)).backward(gout.to(DEV))
+        grads[mode] = [xd.grad.cpu(), conv.weight.grad.cpu(), conv.att.grad.cpu(), conv.bias.grad.cpu()]
+        for got, want in zip(grads[mode], (x64.grad, W.grad, a64.grad, b.grad)):
+            assert torch.allclose(got.double(), want, rtol=1e-4, atol=1e-4), mode
 
 
 def test_gat_forward_identical_with_and_without_grad():

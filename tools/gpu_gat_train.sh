@@ -1,0 +1,6 @@
+set -u
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "gat or GAT" -p no:cacheprovider > gpurun_out/pytest_gat.log 2>&1
+rc=$?; tail -15 gpurun_out/pytest_gat.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 400 python -u tools/bench_configs.py --configs c3train,c3 > gpurun_out/c3train.jsonl 2>&1
+rc=$?; grep -v amdgpu.ids gpurun_out/c3train.jsonl | cut -c1-400; exit $rc
