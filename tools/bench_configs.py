@@ -295,9 +295,18 @@ def c5(dev):
 
 
 def _train_step_ms(conv, x, ei):
+    # one training step of the layer as an optimizer loop runs it: gradients
+    # reset to None first (zero_grad(set_to_none=True), so no accumulation
+    # pass), a fixed upstream gradient allocated once
+    gout = [None]
+
     def step():
+        conv.zero_grad(set_to_none=True)
+        x.grad = None
         out = conv(x, ei)
-        out.backward(torch.ones_like(out))
+        if gout[0] is None:
+            gout[0] = torch.ones_like(out)
+        out.backward(gout[0])
     for _ in range(2):
         step()
     torch.cuda.synchronize()
