@@ -1210,6 +1210,38 @@ def test_gat_training_forward_node_wise_d_a_dst(H, C, chunk, monkeypatch):
             assert torch.allclose(got.double(), want, rtol=1e-4, atol=1e-4), mode
 
 
+@pytest.mark.parametrize("concat", [False, True])
+def test_gat_training_mean_heads_and_attention_weights(concat):
+    """Training through the node-wise d a_dst path with concat=False (heads
+    averaged after the fused aggregation) and return_attention_weights=True:
+    gradients within the float64-autograd bound, alpha within 1e-6."""
+    from torch_geometric.nn import GATConv
+    from mi355_mp import ops
+    _, _, _, _, pl = _mods()
+    N, Fi, H, C = 900, 10, 4, 16
+    ei = pl(N, 15000, seed=43)
+    g = torch.Generator().manual_seed(43)
+    x = torch.randn(N, Fi, generator=g)
+    conv = GATConv(Fi, C, heads=H, concat=concat).to(DEV)
+    with torch.no_grad():
+        conv.bias.normal_()
+    assert ops.GAT_TRAIN_FWD and ops._gat_bwd_fused_ok(C)
+    xd = x.to(DEV).requires_grad_(True)
+    out, (ei_a, alpha) = conv(xd, ei.to(DEV), return_attention_weights=True)
+    gout = torch.randn(out.shape, generator=g)
+    out.backward(gout.to(DEV))
+    W = conv.weight.detach().cpu().double().requires_grad_(True)
+    att = conv.att.detach().cpu().double().requires_grad_(True)
+    b = conv.bias.detach().cpu().double().requires_grad_(True)
+    x64 = x.double().requires_grad_(True)
+    o64, _, al64 = P.gat_conv(x64, ei, W, att, b, H, C, concat=concat, return_alpha=True)
+    o64.backward(gout.double())
+    assert (alpha.cpu().double() - al64.detach()).abs().max().item() < 1e-6
+    for got, want in ((xd.grad, x64.grad), (conv.weight.grad, W.grad), (conv.att.grad, att.grad),
+                      (conv.bias.grad, b.grad)):
+        assert torch.allclose(got.cpu().double(), want, rtol=1e-4, atol=1e-4)
+
+
 def test_gat_forward_identical_with_and_without_grad():
     """Training mode adds the bias outside the kernel (the backward keeps the
     pre-bias aggregate): the same fp32 add, so the output is bit-identical."""
