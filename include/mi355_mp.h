@@ -319,6 +319,11 @@ int mp_gat_backward_prep_train_f32(const float* grad_out, int64_t ldg, const flo
                                    const float* row_stats, int64_t n, int32_t H, int32_t C,
                                    float* pack, float* gsum_part, float* grad_a_dst, void* stream);
 
+/* Per-block column sums of x [n, F] (0 < F <= 256, F % 4 == 0, 16-byte aligned
+ * rows): part [mp_gat_bwd_blocks(n), F]; sum_i x[i, :] is their sum over the
+ * blocks (a layer's bias gradient, sum over rows of grad_out). */
+int mp_col_sums_f32(const float* x, int64_t ldx, int64_t n, int32_t F, float* part, void* stream);
+
 /* Rows of the per-block partial arrays of the prep/finish kernels for n nodes. */
 int mp_gat_bwd_blocks(int64_t n);
 

@@ -123,6 +123,37 @@ __device__ __forceinline__ void block_partial_store(const float (&v)[4], float* 
   }
 }
 
+// Column sums of x [n, F] (F <= 256, F % 4 == 0, 16-B rows) as per-block
+// partials [gridDim.x, F]: the bias gradient of a layer whose output adds a
+// bias row, sum_i g[i, :].  One wave per row, four rows in flight; the
+// partials are added in a fixed order (deterministic).
+__global__ __launch_bounds__(256) void k_col_sums(const float* __restrict__ x, int64_t ldx, int64_t n, int32_t F,
+                                                  float* __restrict__ part) {
+  const int lane = lane_id();
+  const int wid = (int)(threadIdx.x >> 6);
+  const int64_t f = (int64_t)lane * 4;
+  const int64_t fs = f < F ? f : 0;
+  const int64_t step = (int64_t)gridDim.x * 4;
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  int64_t r = (int64_t)blockIdx.x * 4 + wid;
+  for (; r + 3 * step < n; r += 4 * step) {
+    Frag<4> v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = load_frag<4>(x + (r + u * step) * ldx + fs);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) cs[k] += v[u].v[k];
+  }
+  for (; r < n; r += step) {
+    Frag<4> v = load_frag<4>(x + r * ldx + fs);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) cs[k] += v.v[k];
+  }
+  if (f >= F) cs[0] = cs[1] = cs[2] = cs[3] = 0.f;
+  block_partial_store(cs, part + (int64_t)blockIdx.x * F, F);
+}
+
 // Backward epilogue, one wave per node n (H*C <= 256, C % 4 == 0):
 //   gx[n, h*C+c] += ga_dst[n,h] * att[h, c]                (the x_i use of xw in the score)
 //   att_part[blk, 0, :] += ga_dst[n,h] * xw[n, :]          (d att_dst, per-block partial)
@@ -331,6 +362,21 @@ int mp_gat_backward_prep_train_f32(const float* grad_out, int64_t ldg, const flo
   MP_CHECK_ARG(!gsum_part || F <= 256, "mp_gat_backward_prep_train_f32: gsum_part needs H*C <= 256");
   k_gat_bwd_prep_wave<<<(unsigned)mp_gat_bwd_blocks(n), 256, 0, as_stream(stream)>>>(
       grad_out, ldg, agg, lda, a_dst, row_stats, n, H, C, G, pack, gsum_part, agg2, row_s2, grad_a_dst);
+  MP_CHECK_LAUNCH();
+  return MP_OK;
+}
+
+int mp_col_sums_f32(const float* x, int64_t ldx, int64_t n, int32_t F, float* part, void* stream) {
+  MP_DEVICE_GUARD(stream);
+  MP_CHECK_ARG(n >= 0 && F > 0 && F <= 256 && F % 4 == 0, "mp_col_sums_f32: needs 0 < F <= 256, F %% 4 == 0");
+  MP_CHECK_ARG(part && (n == 0 || (x && ldx >= F && ldx % 4 == 0 && (uintptr_t)x % 16 == 0)),
+               "mp_col_sums_f32: bad argument (16-byte aligned rows required)");
+  const int nb = mp_gat_bwd_blocks(n);
+  if (n == 0) {
+    MP_CHECK_HIP(hipMemsetAsync(part, 0, (size_t)nb * F * sizeof(float), as_stream(stream)));
+    return MP_OK;
+  }
+  k_col_sums<<<(unsigned)nb, 256, 0, as_stream(stream)>>>(x, ldx, n, F, part);
   MP_CHECK_LAUNCH();
   return MP_OK;
 }

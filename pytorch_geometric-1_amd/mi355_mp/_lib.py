@@ -91,6 +91,7 @@ SIGNATURES = {
     "mp_gat_backward_prep_train_f32": (ctypes.c_int, [c_p, i64, c_p, i64, c_p, c_p, c_p, c_p, i64, i32, i32, c_p,
                                                       c_p, c_p, c_p]),
     "mp_gat_bwd_blocks": (ctypes.c_int, [i64]),
+    "mp_col_sums_f32": (ctypes.c_int, [c_p, i64, i64, i32, c_p, c_p]),
     "mp_gat_backward_finish_f32": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, i64, i32, i32, c_p, c_p]),
     "mp_heads_outer_add_f32": (ctypes.c_int, [c_p, i64, c_p, i64, i32, i32, c_p, i64, c_p]),
     "mp_gather_rows_f32": (ctypes.c_int, [c_p, i64, c_p, i64, i32, c_p, i64, c_p]),

@@ -85,6 +85,21 @@ def gather_rows(x, idx):
     return out
 
 
+def col_sums(g):
+    """sum over rows of a [n, F] fp32 gradient (a bias gradient): native
+    per-block partials (mp_col_sums_f32) where the row fits 256 features,
+    else torch's reduction."""
+    n, F = g.shape
+    if g.is_cuda and 0 < F <= 256 and F % 4 == 0 and g.stride(1) == 1 and g.stride(0) % 4 == 0 \
+            and g.data_ptr() % 16 == 0 and g.dtype == torch.float32:
+        lib = _lib.load()
+        part = torch.empty((int(lib.mp_gat_bwd_blocks(n)), F), dtype=torch.float32, device=g.device)
+        _lib.check(lib.mp_col_sums_f32(g.data_ptr(), g.stride(0), n, F, part.data_ptr(), _lib.stream_ptr(g.device)),
+                   "mp_col_sums_f32")
+        return part.sum(0)
+    return g.sum(0)
+
+
 # ---------------------------------------------------------------------------
 # fused gather -> weight -> reduce over a Graph (MessagePassing fast path)
 # ---------------------------------------------------------------------------
@@ -121,7 +136,7 @@ class _FusedPropagate(torch.autograd.Function):
         grad_out = grad_out.contiguous()
         gx = gw = gb = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            gb = grad_out.sum(0)
+            gb = col_sums(grad_out)
         if reduce in ("max", "min"):
             want_w = ctx.needs_input_grad[1] and edge_weight is not None
             if ctx.needs_input_grad[0] or want_w:
@@ -587,7 +602,7 @@ class _GatPropagate(torch.autograd.Function):
                                                ctx.needs_input_grad[1], ctx.has_bias and ctx.needs_input_grad[2],
                                                extra)
             return gx, gatt, gb, None, None, None, None, None, None, None
-        gb = g.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        gb = col_sums(g) if ctx.has_bias and ctx.needs_input_grad[2] else None
         dst, src = graph.dst, graph.src
         E = dst.n_edges
         sr = dst.slot_rows()

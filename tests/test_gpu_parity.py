@@ -1793,3 +1793,18 @@ def test_self_loop_utilities_bit_exact(seed):
     w64 = w.double().requires_grad_(True)
     P.add_remaining_self_loops(ei, w64, 1, N)[1].backward(gout.double())
     assert torch.equal(wg.grad.cpu().double(), w64.grad)
+
+
+@pytest.mark.parametrize("n,F", [(0, 64), (1, 4), (5, 256), (100003, 256), (70001, 100), (4097, 300)])
+def test_col_sums_bias_gradient(n, F):
+    """ops.col_sums (mp_col_sums_f32 per-block partials, or torch for F > 256 /
+    F % 4 != 0) against a float64 column sum; deterministic across calls."""
+    from mi355_mp import ops
+    g = torch.randn(n, F, generator=torch.Generator().manual_seed(n + F))
+    got = ops.col_sums(g.to(DEV))
+    again = ops.col_sums(g.to(DEV))
+    want = g.double().sum(0)
+    assert got.shape == (F,)
+    assert torch.equal(got, again)
+    tol = 1e-5 * torch.clamp(g.double().abs().sum(0), min=1.0)
+    assert bool(((got.cpu().double() - want).abs() <= tol).all())
