@@ -224,8 +224,10 @@ int mp_gat_aggregate_att_f32(const mp_csr* g, const float* xw, const float* a_sr
                              size_t slab_bytes, int32_t stages, void* stream);
 
 /* Training forward of the same layer (att given, C % 4 == 0, C/4 a power of two
- * <= 64: mp_gat_train_ok), no bias (the backward needs the pre-bias output).
- * Besides out and row_stats it leaves, with the same online rescaling,
+ * <= 64: mp_gat_train_ok).  out = aggregate + bias (bias may be NULL); agg
+ * (NULL allowed without a bias) receives the pre-bias aggregate [n_rows, H*C]
+ * (contiguous) that the backward's rs needs.  Besides these and row_stats it
+ * leaves, with the same online rescaling,
  *   out2[i,h,:]  = sum_j alpha_ij leaky'_ij xw[j,h,:]    ([n_rows, H*C], contiguous)
  *   row_s2[i,h]  = sum_j alpha_ij leaky'_ij             ([n_rows, H])
  * with leaky' = 1 where a_src[j,h] + a_dst[i,h] > 0, else slope.  They turn the
@@ -236,9 +238,9 @@ int mp_gat_train_ok(int32_t H, int32_t C);
 size_t mp_gat_train_slab_bytes(const mp_csr* g, int32_t H, int32_t C);
 int mp_gat_aggregate_train_f32(const mp_csr* g, const float* xw, const float* a_src,
                                const float* a_dst, const float* att, int32_t H, int32_t C,
-                               float slope, float* out, int64_t ldo, float* row_stats,
-                               float* out2, float* row_s2, void* slab, size_t slab_bytes,
-                               int32_t stages, void* stream);
+                               float slope, const float* bias, float* out, int64_t ldo,
+                               float* agg, float* row_stats, float* out2, float* row_s2,
+                               void* slab, size_t slab_bytes, int32_t stages, void* stream);
 
 /* Two-pass form of the same layer, in the reference's own arithmetic
  * (utils.softmax [U3] then message x_j * alpha and scatter_add in edge order,

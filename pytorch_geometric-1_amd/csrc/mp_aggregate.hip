@@ -128,6 +128,7 @@ struct AggArgs {
   // row_s2[r, h] = sum_k alpha leaky', and their partial slabs
   float* out2;
   float* row_s2;
+  float* agg_nb;  // pre-bias output (ld F), when the output carries the bias
   float* slab_v2;
   float* slab_s2;
 };
@@ -504,6 +505,9 @@ struct GatRed {
     float den = s + 1e-16f;
 #pragma unroll
     for (int k = 0; k < VEC; ++k) o.v[k] = acc[k] / den;
+    if constexpr (TR) {  // the pre-bias aggregate the backward's rs needs
+      if (p.agg_nb) store_out<VEC>(p.agg_nb + row * (int64_t)p.F + f, o);
+    }
     if (p.bias) {
       Frag<VEC> b = load_frag<VEC>(p.bias + f);
 #pragma unroll
@@ -1946,9 +1950,9 @@ int mp_gat_aggregate_att_f32(const mp_csr* g, const float* xw, const float* a_sr
 }
 
 int mp_gat_aggregate_train_f32(const mp_csr* g, const float* xw, const float* a_src, const float* a_dst,
-                               const float* att, int32_t H, int32_t C, float slope, float* out, int64_t ldo,
-                               float* row_stats, float* out2, float* row_s2, void* slab, size_t slab_bytes,
-                               int32_t stages, void* stream) {
+                               const float* att, int32_t H, int32_t C, float slope, const float* bias, float* out,
+                               int64_t ldo, float* agg, float* row_stats, float* out2, float* row_s2, void* slab,
+                               size_t slab_bytes, int32_t stages, void* stream) {
   MP_DEVICE_GUARD(stream);
   int rc = check_graph(g, "mp_gat_aggregate_train_f32");
   if (rc) return rc;
@@ -1958,8 +1962,9 @@ int mp_gat_aggregate_train_f32(const mp_csr* g, const float* xw, const float* a_
   const int F = H * C;
   MP_CHECK_ARG(ldo >= F, "mp_gat_aggregate_train_f32: ldo < H*C");
   MP_CHECK_ARG((uintptr_t)xw % 16 == 0 && (uintptr_t)att % 16 == 0 && (uintptr_t)out % 16 == 0 && ldo % 4 == 0 &&
-                   (uintptr_t)out2 % 16 == 0,
-               "mp_gat_aggregate_train_f32: xw, att, out, out2 must be 16-byte aligned (ldo % 4 == 0)");
+                   (uintptr_t)out2 % 16 == 0 && (uintptr_t)agg % 16 == 0 && (uintptr_t)bias % 16 == 0,
+               "mp_gat_aggregate_train_f32: xw, att, bias, out, agg, out2 must be 16-byte aligned (ldo % 4 == 0)");
+  MP_CHECK_ARG(!bias || agg, "mp_gat_aggregate_train_f32: a bias needs agg (the pre-bias output)");
   MP_CHECK_ARG(slab != nullptr && slab_bytes >= mp_gat_train_slab_bytes(g, H, C),
                "mp_gat_aggregate_train_f32: slab workspace too small");
   AggArgs a{};
@@ -1978,6 +1983,8 @@ int mp_gat_aggregate_train_f32(const mp_csr* g, const float* xw, const float* a_
   a.row_stats = row_stats;
   a.out2 = out2;
   a.row_s2 = row_s2;
+  a.bias = bias;
+  a.agg_nb = agg;
   a.slab_ld = slab_ld_for(F);
   const size_t slots = 2 * (size_t)g->n_waves;
   char* b = (char*)slab;

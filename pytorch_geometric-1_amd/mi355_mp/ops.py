@@ -407,9 +407,16 @@ def gat_two_pass(csr, H, C):
 GAT_TRAIN_FWD = True
 
 
+def _gat_train_fwd_ok(graph, xw, H, C):
+    """The training forward (mp_gat_aggregate_train_f32) applies."""
+    return (GAT_TRAIN_FWD and GAT_OWN_A_SRC and bool(_lib.load().mp_gat_train_ok(H, C))
+            and not gat_two_pass(graph.dst, H, C) and xw.data_ptr() % 16 == 0 and graph.n_dst == xw.shape[0])
+
+
 def _gat_forward(graph, edge_index, xw, att, H, C, slope, bias, want_alpha, train2=False):
-    """Returns (out, alpha, a_src, a_dst, stats, extra); extra = (agg2, s2) when
-    train2 and the training forward applies, else None."""
+    """Returns (out, alpha, a_src, a_dst, stats, extra).  train2 (callers check
+    _gat_train_fwd_ok first): the training forward, out = aggregate + bias and
+    extra = (agg2, s2, agg) with agg the pre-bias aggregate; else extra = None."""
     lib = _lib.load()
     dev = xw.device
     N = xw.shape[0]
@@ -427,17 +434,19 @@ def _gat_forward(graph, edge_index, xw, att, H, C, slope, bias, want_alpha, trai
     stats = torch.empty((graph.n_dst, H, 2), dtype=torch.float32, device=dev)
     g = csr.struct("other")
     extra = None
-    if (train2 and bias is None and GAT_TRAIN_FWD and GAT_OWN_A_SRC and lib.mp_gat_train_ok(H, C)
-            and not gat_two_pass(csr, H, C) and xw.data_ptr() % 16 == 0):
+    if train2:
         agg2 = torch.empty((graph.n_dst, H * C), dtype=torch.float32, device=dev)
         s2 = torch.empty((graph.n_dst, H), dtype=torch.float32, device=dev)
+        agg = torch.empty_like(out) if bias is not None else out
         sb = lib.mp_gat_train_slab_bytes(g, H, C)
         slab = torch.empty(sb, dtype=torch.uint8, device=dev)
         _lib.check(lib.mp_gat_aggregate_train_f32(g, xw.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(),
-                                                  att_c.data_ptr(), H, C, float(slope), out.data_ptr(), out.stride(0),
-                                                  stats.data_ptr(), agg2.data_ptr(), s2.data_ptr(), slab.data_ptr(),
-                                                  sb, _lib.MP_STAGE_ALL, st), "mp_gat_aggregate_train_f32")
-        extra = (agg2, s2)
+                                                  att_c.data_ptr(), H, C, float(slope), _lib.ptr(bias),
+                                                  out.data_ptr(), out.stride(0),
+                                                  agg.data_ptr() if bias is not None else None, stats.data_ptr(),
+                                                  agg2.data_ptr(), s2.data_ptr(), slab.data_ptr(), sb,
+                                                  _lib.MP_STAGE_ALL, st), "mp_gat_aggregate_train_f32")
+        extra = (agg2, s2, agg)
     if extra is None:
         sb = lib.mp_gat_slab_bytes(g, H, C)
         slab = torch.empty(sb, dtype=torch.uint8, device=dev)
@@ -563,11 +572,20 @@ class _GatPropagate(torch.autograd.Function):
     @staticmethod
     def forward(ctx, xw, att, bias, graph, edge_index, H, C, slope, want_alpha, train):
         fused = train and _gat_bwd_fused_ok(C)
-        # the fused backward needs the pre-bias aggregate (rs_i = <g_i, agg_i>)
+        # the fused backward needs the pre-bias aggregate (rs_i = <g_i, agg_i>):
+        # the training forward writes it next to the output; otherwise the
+        # bias is added here
+        train2 = fused and _gat_train_fwd_ok(graph, xw, H, C)
         out, alpha, a_src, a_dst, stats, extra = _gat_forward(graph, edge_index, xw, att, H, C, slope,
-                                                              None if fused else bias, want_alpha, train2=fused)
+                                                              bias if (train2 or not fused) else None, want_alpha,
+                                                              train2=train2)
         agg = None
-        if fused:
+        if train2:
+            agg = extra[2]
+            extra = extra[:2]
+            if bias is None:
+                out = agg.clone()
+        elif fused:
             agg = out
             out = agg + bias if bias is not None else agg.clone()
         ctx.graph, ctx.H, ctx.C, ctx.slope = graph, H, C, slope

@@ -1176,11 +1176,16 @@ def test_gat_training_forward_node_wise_d_a_dst(H, C, chunk, monkeypatch):
     xw = torch.randn(N, H * C, generator=g)
     att = torch.randn(1, H, 2 * C, generator=g) * 0.3
     graph = Graph(ei_l.to(DEV), N, N, chunk=chunk)
-    out, _, _, _, _, extra = ops._gat_forward(graph, ei_l.to(DEV), xw.to(DEV), att.to(DEV), H, C, 0.2, None, False,
-                                              train2=True)
-    out_inf, _, _, _, _, none = ops._gat_forward(graph, ei_l.to(DEV), xw.to(DEV), att.to(DEV), H, C, 0.2, None, False)
+    bias = torch.randn(H * C, generator=g).to(DEV)
+    assert ops._gat_train_fwd_ok(graph, xw.to(DEV), H, C)
+    out, _, _, _, st_t, extra = ops._gat_forward(graph, ei_l.to(DEV), xw.to(DEV), att.to(DEV), H, C, 0.2, bias,
+                                                 False, train2=True)
+    out_inf, _, _, _, st_i, none = ops._gat_forward(graph, ei_l.to(DEV), xw.to(DEV), att.to(DEV), H, C, 0.2, bias,
+                                                    False)
+    agg_inf = ops._gat_forward(graph, ei_l.to(DEV), xw.to(DEV), att.to(DEV), H, C, 0.2, None, False)[0]
     assert extra is not None and none is None
-    assert torch.equal(out, out_inf)
+    assert torch.equal(out, out_inf) and torch.equal(st_t, st_i)
+    assert torch.equal(extra[2], agg_inf)  # the pre-bias aggregate
     x_i = xw[ei_l[1]].view(-1, H, C)
     x_j = xw[ei_l[0]].view(-1, H, C)
     pre = (torch.cat([x_i, x_j], -1) * att).sum(-1)

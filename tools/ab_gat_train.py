@@ -59,7 +59,8 @@ def main():
     def launch(n, stages):
         o, s_, o2, s2 = res[n]
         _lib.check(libs[n].mp_gat_aggregate_train_f32(g, xw.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(),
-                                                      att.data_ptr(), H, C, 0.2, o.data_ptr(), H * C, s_.data_ptr(),
+                                                      att.data_ptr(), H, C, 0.2, None, o.data_ptr(), H * C, None,
+                                                      s_.data_ptr(),
                                                       o2.data_ptr(), s2.data_ptr(), slab.data_ptr(), sb, stages, st),
                    "train")
 
