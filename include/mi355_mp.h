@@ -303,6 +303,17 @@ int mp_gat_backward_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, co
                         int32_t C, float slope, float* grad_xw, float* grad_a_src, float* de,
                         void* slab, size_t slab_bytes, int32_t stages, void* stream);
 
+/* The same pass after the training forward: no per-edge d score; grad_a_dst
+ * [n_rows, H] (mp_gat_backward_prep_train_f32) is an input, and each row's
+ * grad_xw also receives grad_a_dst[j,h] * att[h, 0:C] (the term
+ * mp_gat_backward_finish_f32 adds otherwise; call that with grad_xw = NULL for
+ * the att-gradient partials only). */
+int mp_gat_backward_train_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, const float* xw,
+                              const float* a_src, const float* pack, const float* att, int32_t H,
+                              int32_t C, float slope, const float* grad_a_dst, float* grad_xw,
+                              float* grad_a_src, void* slab, size_t slab_bytes, int32_t stages,
+                              void* stream);
+
 /* pack[n,h,:] = (a_dst[n,h], m[n,h], 1/den[n,h], rs[n,h]) with
  * rs[n,h] = sum_c grad_out[n, h*C+c] * agg[n, h*C+c]  (agg = pre-bias GAT output;
  * rs = sum_j alpha_nj <g_n, xw_j>_h, the softmax-backward row term).
@@ -333,7 +344,8 @@ int mp_gat_bwd_blocks(int64_t n);
  *   grad_xw[n, h*C+c] += ga_dst[n,h] * att[h, c]        (att = [H, 2C]: dst half first)
  *   att_part[b, 0, :]  = sum over block b's nodes of ga_dst[n,h] * xw[n, h*C+c]
  *   att_part[b, 1, :]  = ... ga_src[n,h] * xw[n, h*C+c]
- * att_part is [mp_gat_bwd_blocks(n), 2, H*C]; d att = its sum over blocks. */
+ * att_part is [mp_gat_bwd_blocks(n), 2, H*C]; d att = its sum over blocks.
+ * grad_xw = NULL: the att-gradient partials only. */
 int mp_gat_backward_finish_f32(float* grad_xw, const float* xw, const float* ga_dst,
                                const float* ga_src, const float* att, int64_t n, int32_t H,
                                int32_t C, float* att_part, void* stream);

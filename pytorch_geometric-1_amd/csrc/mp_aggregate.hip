@@ -123,6 +123,8 @@ struct AggArgs {
   const f32x4* pack;  // [n_cols, H]  (a_dst, m, 1/den, rs) of the destination, rs = <g_i, agg_i>_h
   float* de;          // [n_edges, H] d score per slot (this CSR's slot order)
   float* ga;          // [n_rows, H]  d a_src = row sums of d score
+  const float* ga_dst_in;  // [n_rows, H] d a_dst of each row (node-wise, training forward): the
+                           // row's d xw also takes d a_dst (x) att_dst at its finish
   const float* att;   // [H, 2C]      (att_dst | att_src)
   // GAT training forward (GatRed<.., TR>): out2[r, f] = sum_k alpha leaky' xw (ld F),
   // row_s2[r, h] = sum_k alpha leaky', and their partial slabs
@@ -680,6 +682,7 @@ struct GatBwdRed {
   float acc[VEC];
   float y[VEC];
   float dacc, as;
+  float gd = 0.f;  // d a_dst of the row (ga_dst_in)
   int h, hl;
   bool leader;
 
@@ -694,6 +697,12 @@ struct GatBwdRed {
 #pragma unroll
     for (int k = 0; k < VEC; ++k) y[k] = act ? o.v[k] : 0.f;
     as = p.a_src[row * p.H + h];
+    row_terms(p, row);
+  }
+  // the row's node-wise terms needed at finish (the fix-up, which finishes a
+  // split row without a begin, calls this itself)
+  __device__ __forceinline__ void row_terms(const AggArgs& p, int64_t row) {
+    if (p.ga_dst_in) gd = p.ga_dst_in[row * p.H + h];
   }
   // head-group dot product <v, y> (all lanes of the head get the sum)
   __device__ __forceinline__ float dot(const Frag<VEC>& v) const {
@@ -752,6 +761,11 @@ struct GatBwdRed {
     Frag<VEC> o;
 #pragma unroll
     for (int k = 0; k < VEC; ++k) o.v[k] = __builtin_fmaf(dacc, at[k], acc[k]);
+    if (p.ga_dst_in) {  // the x_i use of xw in the score: + d a_dst (x) att_dst
+      const float* ad = p.att + (int64_t)h * 2 * p.C + (f % p.C);
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) o.v[k] = __builtin_fmaf(gd, ad[k], o.v[k]);
+    }
     store_out<VEC>(p.out + row * p.ldo + f, o);
     if (leader) p.ga[row * p.H + h] = dacc;
   }
@@ -1446,6 +1460,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_fixup(AggArgs p) {
   if (wid != 0) return;
   for (int q = 1; q < kWavesPerBlock; ++q)
     if (has[q]) red.merge(lds[q - 1][lane]);
+  if constexpr (Red::kGatB) red.row_terms(p, r);
   red.finish(p, r, re - rs, f, act);
 }
 
@@ -2077,9 +2092,10 @@ int mp_gat_softmax_aggregate_f32(const mp_csr* g, const int32_t* slot_row, const
   return MP_OK;
 }
 
-int mp_gat_backward_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, const float* xw, const float* a_src,
+static int gat_backward(const mp_csr* gt, const float* grad_out, int64_t ldg, const float* xw, const float* a_src,
                         const float* pack, const float* att, int32_t H, int32_t C, float slope, float* grad_xw,
-                        float* grad_a_src, float* de, void* slab, size_t slab_bytes, int32_t stages, void* stream) {
+                        float* grad_a_src, float* de, const float* ga_dst_in, void* slab, size_t slab_bytes,
+                        int32_t stages, void* stream) {
   MP_DEVICE_GUARD(stream);
   int rc = check_graph(gt, "mp_gat_backward_f32");
   if (rc) return rc;
@@ -2104,6 +2120,7 @@ int mp_gat_backward_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, co
   a.att = att;
   a.de = de;
   a.ga = grad_a_src;
+  a.ga_dst_in = ga_dst_in;
   a.H = H;
   a.C = C;
   a.slope = slope;
@@ -2122,6 +2139,22 @@ int mp_gat_backward_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, co
   }
   MP_CHECK_ARG(pow2(C), "mp_gat_backward_f32: C=%d needs C/4 or C to be a power of two <= 64", C);
   return launch<GatBwdRed<1>, 1>(a, stages, s);
+}
+
+int mp_gat_backward_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, const float* xw, const float* a_src,
+                        const float* pack, const float* att, int32_t H, int32_t C, float slope, float* grad_xw,
+                        float* grad_a_src, float* de, void* slab, size_t slab_bytes, int32_t stages, void* stream) {
+  return gat_backward(gt, grad_out, ldg, xw, a_src, pack, att, H, C, slope, grad_xw, grad_a_src, de, nullptr, slab,
+                      slab_bytes, stages, stream);
+}
+
+int mp_gat_backward_train_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, const float* xw,
+                              const float* a_src, const float* pack, const float* att, int32_t H, int32_t C,
+                              float slope, const float* grad_a_dst, float* grad_xw, float* grad_a_src, void* slab,
+                              size_t slab_bytes, int32_t stages, void* stream) {
+  MP_CHECK_ARG(grad_a_dst != nullptr, "mp_gat_backward_train_f32: null grad_a_dst");
+  return gat_backward(gt, grad_out, ldg, xw, a_src, pack, att, H, C, slope, grad_xw, grad_a_src, nullptr,
+                      grad_a_dst, slab, slab_bytes, stages, stream);
 }
 
 }  // extern "C"

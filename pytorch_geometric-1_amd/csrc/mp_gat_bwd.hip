@@ -178,13 +178,15 @@ __global__ __launch_bounds__(256) void k_gat_bwd_finish(float* __restrict__ gx, 
     const float gs = ga_src[r * H + h];
     Frag<4> x = load_frag<4>(xw + r * HC + fs);
     if (act) {
-      float* d = gx + r * HC + f;
-      Frag<4> o = load_frag<4>(d);
-      o.v[0] = __builtin_fmaf(gd, ad.x, o.v[0]);
-      o.v[1] = __builtin_fmaf(gd, ad.y, o.v[1]);
-      o.v[2] = __builtin_fmaf(gd, ad.z, o.v[2]);
-      o.v[3] = __builtin_fmaf(gd, ad.w, o.v[3]);
-      store_frag<4>(d, o);
+      if (gx) {  // (NULL: the transposed pass already added it, mp_gat_backward_train_f32)
+        float* d = gx + r * HC + f;
+        Frag<4> o = load_frag<4>(d);
+        o.v[0] = __builtin_fmaf(gd, ad.x, o.v[0]);
+        o.v[1] = __builtin_fmaf(gd, ad.y, o.v[1]);
+        o.v[2] = __builtin_fmaf(gd, ad.z, o.v[2]);
+        o.v[3] = __builtin_fmaf(gd, ad.w, o.v[3]);
+        store_frag<4>(d, o);
+      }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         pd[k] = __builtin_fmaf(gd, x.v[k], pd[k]);
@@ -418,7 +420,7 @@ int mp_gat_backward_finish_f32(float* grad_xw, const float* xw, const float* ga_
   MP_DEVICE_GUARD(stream);
   MP_CHECK_ARG(H > 0 && C > 0 && n >= 0, "mp_gat_backward_finish_f32: bad sizes");
   MP_CHECK_ARG(C % 4 == 0 && H * C <= 256, "mp_gat_backward_finish_f32: needs C %% 4 == 0 and H*C <= 256");
-  MP_CHECK_ARG(grad_xw && xw && ga_dst && ga_src && att && att_part, "mp_gat_backward_finish_f32: null pointer");
+  MP_CHECK_ARG(xw && ga_dst && ga_src && att && att_part, "mp_gat_backward_finish_f32: null pointer");
   MP_CHECK_ARG((uintptr_t)grad_xw % 16 == 0 && (uintptr_t)xw % 16 == 0 && (uintptr_t)att % 16 == 0,
                "mp_gat_backward_finish_f32: 16-byte alignment required");
   k_gat_bwd_finish<<<(unsigned)mp_gat_bwd_blocks(n), 256, 0, as_stream(stream)>>>(grad_xw, xw, ga_dst, ga_src, att, n,

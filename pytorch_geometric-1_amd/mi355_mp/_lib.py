@@ -87,6 +87,8 @@ SIGNATURES = {
     "mp_gat_sddmm_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, i64, c_p, i64, i32, i32, c_p, c_p]),
     "mp_gat_backward_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, i64, c_p, c_p, c_p, c_p, i32, i32,
                                            ctypes.c_float, c_p, c_p, c_p, c_p, sz, i32, c_p]),
+    "mp_gat_backward_train_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, i64, c_p, c_p, c_p, c_p, i32, i32,
+                                                 ctypes.c_float, c_p, c_p, c_p, c_p, sz, i32, c_p]),
     "mp_gat_backward_prep_f32": (ctypes.c_int, [c_p, i64, c_p, i64, c_p, c_p, i64, i32, i32, c_p, c_p, c_p]),
     "mp_gat_backward_prep_train_f32": (ctypes.c_int, [c_p, i64, c_p, i64, c_p, c_p, c_p, c_p, i64, i32, i32, c_p,
                                                       c_p, c_p, c_p]),

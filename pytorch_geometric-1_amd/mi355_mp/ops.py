@@ -541,20 +541,30 @@ def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope
     gs = src.struct("dst_slot")
     sb = lib.mp_gat_slab_bytes(gs, H, C)
     slab = torch.empty(sb, dtype=torch.uint8, device=dev)
-    _lib.check(lib.mp_gat_backward_f32(gs, g.data_ptr(), g.stride(0), xw.data_ptr(), a_src.data_ptr(),
-                                       pack.data_ptr(), att_c.data_ptr(), H, C, float(slope), gx.data_ptr(),
-                                       ga_src.data_ptr(), _lib.ptr(de), slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
-               "mp_gat_backward_f32")
+    fused_dst = ga_dst is not None and epi
+    if fused_dst:
+        # the transposed pass also adds d a_dst (x) att_dst to each row's d xw
+        _lib.check(lib.mp_gat_backward_train_f32(gs, g.data_ptr(), g.stride(0), xw.data_ptr(), a_src.data_ptr(),
+                                                 pack.data_ptr(), att_c.data_ptr(), H, C, float(slope),
+                                                 ga_dst.data_ptr(), gx.data_ptr(), ga_src.data_ptr(), slab.data_ptr(),
+                                                 sb, _lib.MP_STAGE_ALL, st), "mp_gat_backward_train_f32")
+    else:
+        _lib.check(lib.mp_gat_backward_f32(gs, g.data_ptr(), g.stride(0), xw.data_ptr(), a_src.data_ptr(),
+                                           pack.data_ptr(), att_c.data_ptr(), H, C, float(slope), gx.data_ptr(),
+                                           ga_src.data_ptr(), _lib.ptr(de), slab.data_ptr(), sb, _lib.MP_STAGE_ALL,
+                                           st), "mp_gat_backward_f32")
     del slab, pack
     if ga_dst is None:
         ga_dst, _ = _aggregate(graph.dst, "slot", de, None, "sum", 0, None)
         del de
     gatt = None
     if epi:
-        apart = torch.empty((nb, 2, F), dtype=torch.float32, device=dev)
-        _lib.check(lib.mp_gat_backward_finish_f32(gx.data_ptr(), xw.data_ptr(), ga_dst.data_ptr(), ga_src.data_ptr(),
-                                                  att_c.data_ptr(), N, H, C, apart.data_ptr(), st),
-                   "mp_gat_backward_finish_f32")
+        if want_att or not fused_dst:
+            # att_dst term of d xw (unless the transposed pass added it) + d att partials
+            apart = torch.empty((nb, 2, F), dtype=torch.float32, device=dev)
+            _lib.check(lib.mp_gat_backward_finish_f32(None if fused_dst else gx.data_ptr(), xw.data_ptr(),
+                                                      ga_dst.data_ptr(), ga_src.data_ptr(), att_c.data_ptr(), N, H, C,
+                                                      apart.data_ptr(), st), "mp_gat_backward_finish_f32")
         if want_att:
             p = apart.sum(0).view(2, H, C)
             gatt = torch.cat([p[0], p[1]], dim=-1).view_as(att)
