@@ -387,6 +387,30 @@ int mp_self_loops(const int64_t* row, const int64_t* col, int64_t n_edges, int64
 int mp_gather_fill_f32(const float* src, const int64_t* pos, int64_t n, float fill,
                        float* out, void* stream);
 
+/* ---- shard plan (destination-range shards, halo maps) ---------- */
+
+/* The plan of rank `rank` owning the key rows [lo, hi) = [cuts[rank],
+ * cuts[rank + 1]) of a range partition (replaces the torch-op construction in
+ * mi355_mp/dist.py ShardPlan: nonzero / unique / searchsorted):
+ *   edge_pos[k]     positions of the edges with lo <= key < hi, in edge order;
+ *   local_key[k]    key[edge_pos[k]] - lo;
+ *   local_other[k]  other - lo when lo <= other < hi, else n_own + the rank of
+ *                   `other` among halo_nodes;
+ *   halo_nodes      the sorted unique remote `other` values of those edges;
+ *   counts (device, int64 [2 + world]): [0] = selected edges, [1] = halo nodes
+ *                   (-1 when a selected edge's `other` lies outside
+ *                   [0, n_nodes): the outputs are then invalid), [2 + q] = halo
+ *                   nodes owned by rank q.
+ * key = destination, other = source for flow source_to_target (the forward
+ * plan); swapped for the transposed (backward) plan.  cuts: device int64
+ * [world + 1].  Outputs are sized at their upper bounds (n_edges, n_nodes);
+ * the caller reads counts and slices.  Workspace: mp_shard_plan_workspace. */
+size_t mp_shard_plan_workspace(int64_t n_edges, int64_t n_nodes);
+int mp_shard_plan(const int64_t* key, const int64_t* other, int64_t n_edges, int64_t n_nodes,
+                  const int64_t* cuts, int32_t world, int32_t rank, int64_t lo, int64_t hi,
+                  int64_t* edge_pos, int64_t* local_key, int64_t* local_other,
+                  int64_t* halo_nodes, int64_t* counts, void* ws, size_t ws_bytes, void* stream);
+
 /* ---- helpers on the path -------------------------------------------------- */
 
 /* out[k,:] = x[idx[k],:]  (index_select of __collect__, scatter-sum backward,

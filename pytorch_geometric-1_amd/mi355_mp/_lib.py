@@ -103,6 +103,9 @@ SIGNATURES = {
     "mp_self_loops_workspace": (sz, [i64, i64]),
     "mp_self_loops": (ctypes.c_int, [c_p, c_p, i64, i64, i32, i64, c_p, c_p, c_p, c_p, sz, c_p]),
     "mp_gather_fill_f32": (ctypes.c_int, [c_p, c_p, i64, f32, c_p, c_p]),
+    "mp_shard_plan_workspace": (sz, [i64, i64]),
+    "mp_shard_plan": (ctypes.c_int, [c_p, c_p, i64, i64, c_p, i32, i32, i64, i64, c_p, c_p, c_p, c_p, c_p, c_p, sz,
+                                     c_p]),
     "mp_gcn_norm_f32": (ctypes.c_int, [c_p, c_p, c_p, i64, i64, c_p, c_p, c_p]),
 }
 

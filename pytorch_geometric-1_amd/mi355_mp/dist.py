@@ -52,13 +52,63 @@ def edge_balanced_cuts(in_degree, parts):
     return cuts
 
 
+def _plan_torch(key, other, num_nodes, cuts, rank, world):
+    """The plan of rank `rank` in torch ops (host tensors: the gloo tests of the
+    plan logic; on the GPU the checker of mp_shard_plan).  Returns (edge_pos,
+    local key, local other, halo_nodes, recv_counts)."""
+    dev = key.device
+    lo, hi = cuts[rank], cuts[rank + 1]
+    mine = (key >= lo) & (key < hi)
+    edge_pos = torch.nonzero(mine).view(-1)                  # positions in the global edge order
+    k = key[edge_pos] - lo
+    o = other[edge_pos]
+    if o.numel() and (int(o.min()) < 0 or int(o.max()) >= num_nodes):
+        raise IndexError("mi355_mp.dist: an edge endpoint lies outside [0, %d)" % num_nodes)
+    owner = torch.searchsorted(torch.tensor(cuts[1:], device=dev), o, right=True)
+    remote = owner != rank
+    halo_nodes = torch.unique(o[remote])                     # sorted, hence grouped by owner
+    halo_owner = torch.searchsorted(torch.tensor(cuts[1:], device=dev), halo_nodes, right=True)
+    recv_counts = [int((halo_owner == q).sum()) for q in range(world)]
+    # local column ids: own rows first, then halo rows in sorted order
+    local_o = torch.empty_like(o)
+    local_o[~remote] = o[~remote] - lo
+    local_o[remote] = (hi - lo) + torch.searchsorted(halo_nodes, o[remote])
+    return edge_pos, k, local_o, halo_nodes, recv_counts
+
+
+def _plan_native(key, other, num_nodes, cuts, rank, world):
+    """_plan_torch on the device by mp_shard_plan (flag + scan, no sort):
+    bitwise the same outputs."""
+    from . import _lib
+    lib = _lib.load()
+    dev = key.device
+    key = key.to(torch.int64).contiguous()
+    other = other.to(torch.int64).contiguous()
+    E = key.numel()
+    cuts_d = torch.tensor(cuts, dtype=torch.int64, device=dev)
+    edge_pos = torch.empty(E, dtype=torch.int64, device=dev)
+    lkey = torch.empty_like(edge_pos)
+    lother = torch.empty_like(edge_pos)
+    halo = torch.empty(num_nodes, dtype=torch.int64, device=dev)
+    counts = torch.empty(2 + world, dtype=torch.int64, device=dev)
+    ws = torch.empty(lib.mp_shard_plan_workspace(E, num_nodes), dtype=torch.uint8, device=dev)
+    _lib.check(lib.mp_shard_plan(key.data_ptr(), other.data_ptr(), E, num_nodes, cuts_d.data_ptr(), world, rank,
+                                 cuts[rank], cuts[rank + 1], edge_pos.data_ptr(), lkey.data_ptr(),
+                                 lother.data_ptr(), halo.data_ptr(), counts.data_ptr(), ws.data_ptr(),
+                                 ws.numel(), _lib.stream_ptr(dev)), "mp_shard_plan")
+    c = counts.tolist()
+    if c[1] < 0:
+        raise IndexError("mi355_mp.dist: an edge endpoint lies outside [0, %d)" % num_nodes)
+    n = c[0]
+    return edge_pos[:n].clone(), lkey[:n].clone(), lother[:n].clone(), halo[:c[1]].clone(), c[2:]
+
+
 class ShardPlan:
     """Everything rank `rank` needs to aggregate its destination rows."""
 
     def __init__(self, edge_index, num_nodes, rank, world, cuts=None, flow="source_to_target"):
         i, j = (1, 0) if flow == "source_to_target" else (0, 1)
         dst_all, src_all = edge_index[i], edge_index[j]
-        dev = edge_index.device
         if cuts is None:
             deg = torch.bincount(dst_all, minlength=num_nodes)
             cuts = edge_balanced_cuts(deg, world)
@@ -66,20 +116,10 @@ class ShardPlan:
         self.rank, self.world = rank, world
         lo, hi = cuts[rank], cuts[rank + 1]
         self.lo, self.hi, self.n_own = lo, hi, hi - lo
-        mine = (dst_all >= lo) & (dst_all < hi)
-        self.edge_pos = torch.nonzero(mine).view(-1)          # positions in the global edge order
-        dst = dst_all[self.edge_pos] - lo
-        src = src_all[self.edge_pos]
-        owner = torch.searchsorted(torch.tensor(cuts[1:], device=dev), src, right=True)
-        remote = owner != rank
-        halo_nodes = torch.unique(src[remote])                 # sorted, hence grouped by owner
-        halo_owner = torch.searchsorted(torch.tensor(cuts[1:], device=dev), halo_nodes, right=True)
+        plan = _plan_native if edge_index.is_cuda else _plan_torch
+        self.edge_pos, dst, local_src, halo_nodes, self.recv_counts = plan(dst_all, src_all, num_nodes, cuts, rank,
+                                                                           world)
         self.halo_nodes = halo_nodes
-        self.recv_counts = [int((halo_owner == q).sum()) for q in range(world)]
-        # local column ids: own rows first, then halo rows in sorted order
-        local_src = torch.empty_like(src)
-        local_src[~remote] = src[~remote] - lo
-        local_src[remote] = self.n_own + torch.searchsorted(halo_nodes, src[remote])
         self.local_edge_index = torch.stack([local_src, dst]) if i == 1 else torch.stack([dst, local_src])
         self.n_local_src = self.n_own + halo_nodes.numel()
         self.send_idx = None

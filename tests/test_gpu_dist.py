@@ -231,3 +231,51 @@ def test_full_size_products_sharded_rehearsal():
         assert excess <= 0, res
         assert frac > 0.95, res   # rows split across merge-path tasks differ in the last bits
         assert n_halo > 0
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("flow", ["source_to_target", "target_to_source"])
+def test_native_shard_plan_matches_torch_plan(world, flow):
+    """mp_shard_plan (flag + scan on the device) vs the torch-op plan, bitwise:
+    edge positions, local ids, halo nodes and per-owner counts, for every rank
+    of a power-law graph with duplicate edges, self loops, isolated nodes and
+    (world 8) an empty shard."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "pytorch_geometric-1_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from mi355_mp import dist as mdist
+    from mi355_mp.graphgen import powerlaw_edge_index
+    dev = torch.device("cuda", 0)
+    N, E = 5000, 80000
+    ei = powerlaw_edge_index(N - 100, E, seed=41)        # nodes N-100.. are isolated
+    ei = torch.cat([ei, ei[:, :500], torch.arange(7).repeat(2, 1)], 1).to(dev)
+    key = ei[1] if flow == "source_to_target" else ei[0]
+    cuts = mdist.edge_balanced_cuts(torch.bincount(key, minlength=N), world)
+    if world == 8:
+        cuts[3] = cuts[2]                                  # rank 2 owns no rows
+    for rank in range(world):
+        plan = mdist.ShardPlan(ei, N, rank, world, cuts=cuts, flow=flow)
+        i, j = (1, 0) if flow == "source_to_target" else (0, 1)
+        want = mdist._plan_torch(ei[i], ei[j], N, cuts, rank, world)
+        assert torch.equal(plan.edge_pos, want[0])
+        loc = plan.local_edge_index
+        lk, lo_ = (loc[1], loc[0]) if flow == "source_to_target" else (loc[0], loc[1])
+        assert torch.equal(lk, want[1]) and torch.equal(lo_, want[2])
+        assert torch.equal(plan.halo_nodes, want[3])
+        assert plan.recv_counts == want[4]
+        assert plan.n_local_src == plan.n_own + want[3].numel()
+
+
+def test_native_shard_plan_rejects_out_of_range_endpoint():
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "pytorch_geometric-1_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from mi355_mp import dist as mdist
+    dev = torch.device("cuda", 0)
+    ei = torch.tensor([[0, 1, 2, 99], [1, 2, 0, 1]], device=dev)   # source 99 >= N
+    with pytest.raises(IndexError):
+        mdist.ShardPlan(ei, 4, 0, 2, cuts=[0, 2, 4])
