@@ -20,7 +20,9 @@ DEFAULT_CHUNK = None   # auto: see auto_chunk()
 # elements past their end: scalar slot batches may read whole batches there.
 SLOT_PAD = 64
 MIN_CHUNK, MAX_CHUNK = 16, 1024
-TARGET_TASKS = 50_000
+# auto_chunk: the best task size grows like sqrt(units): c with 56 c^2 <= units
+CHUNK_SQRT_K = 56
+# An explicit task-count target (the rule before the sqrt fit; GAT's graphs):
 # GAT's per-slot softmax work favours more, shorter tasks: its fused backward
 # pass over the transposed CSR runs 1.9 ms longer at chunk 1024 than at 512 on
 # RMAT21 (layer forward + backward 32.0 vs 33.9 ms, profiles/r02_ab_chunk_train.log)
@@ -28,17 +30,30 @@ GAT_TARGET_TASKS = 100_000
 
 
 def auto_chunk(n_rows, n_edges, target=None):
-    """Merge-path task size in work units (rows + slots): the largest power of
-    two <= units / 50K, clamped to [16, 1024].  Large graphs get big tasks:
-    fewer hub rows cross a task boundary, so the fix-up shrinks and more rows
-    are summed in one task (bit-identical to the sequential order); RMAT21
-    (64M units) gets 1024 (main + fix-up 6.65 -> 6.61 ms vs 512, 6.79 ms at
-    256; profiles/r02_ab_chunk.log), the Reddit-scale graph (115M units, degree
-    ~490) 1024 (-3..4% vs 256, tools/ab_bench.py).  Small graphs keep enough
-    tasks to spread over 256 CUs (Cora, 13K units: 16 -> 829 tasks)."""
+    """Merge-path task size in work units (rows + slots), a power of two in
+    [16, 1024].
+
+    Default: the largest c with 56 c^2 <= units -- a fit of the measured best
+    chunk on graphs of 1.5M to 128M units (tools/exp_shard_chunk.py,
+    profiles/r02_exp_shard_chunk.log, profiles/r02_ab_chunk.log): the per-rank
+    graphs of the sharded config-2 bench (interior edges at P = 8, 1.5M units:
+    128, 0.231 ms vs 0.323 ms at the old 50K-task rule's 16; boundary edges at
+    P = 4, 11.8M units: 256, 1.160 vs 1.224 ms at 128), RMAT21 (64M units:
+    1024, main + fix-up 6.57 ms vs 6.59 at 512 and 6.65 at 2048), the
+    products-scale (128M) and Reddit-scale (115M) graphs 1024.  Bigger tasks
+    mean fewer rows cut by a task boundary (a smaller fix-up, more rows summed
+    in one task: bit-identical to the sequential order) and less per-task
+    overhead; small graphs keep enough tasks to spread over 256 CUs (Cora, 13K
+    units: 16 -> 829 tasks).
+
+    target: the largest c <= units / target instead (GAT_TARGET_TASKS)."""
     units = int(n_rows) + int(n_edges)
-    target = TARGET_TASKS if target is None else int(target)
     c = MIN_CHUNK
+    if target is None:
+        while c * 2 <= MAX_CHUNK and CHUNK_SQRT_K * (c * 2) ** 2 <= units:
+            c *= 2
+        return c
+    target = int(target)
     while c * 2 <= MAX_CHUNK and units // (c * 2) >= target:
         c *= 2
     return c

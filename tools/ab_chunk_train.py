@@ -1,5 +1,6 @@
-"""GCN / GAT layer forward + backward at two merge-path task targets
-(graph.TARGET_TASKS), one process: python tools/ab_chunk_train.py"""
+"""GCN / GAT layer forward + backward at two merge-path task targets (the
+default auto_chunk rule replaced by a task-count target), one process:
+python tools/ab_chunk_train.py"""
 import os
 import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -15,8 +16,9 @@ def main():
     import bench_configs
     mi355_mp.load_native()
     dev = torch.device("cuda", 0)
+    orig = graph.auto_chunk
     for target in (100_000, 50_000, 100_000, 50_000):
-        graph.TARGET_TASKS = target
+        graph.auto_chunk = lambda r, e, t=None, _T=target: orig(r, e, _T if t is None else t)
         graph.clear_caches()
         print("TARGET_TASKS", target, flush=True)
         for c in ("c3train", "c2train"):
