@@ -154,3 +154,80 @@ def edge_conv_max(x, edge_index, mlp):
     out, _ = S.scatter_max(msg, edge_index[1], x.size(0))
     out[out < -10000] = 0
     return out
+
+
+# --- utils.get_laplacian / ChebConv / AGNNConv [U] ---------------------------
+# callers: ConvexPruning.py:259-264 (ChebConv(..., K=1)), :236-237 (AGNNConv)
+
+def get_laplacian(edge_index, edge_weight=None, normalization=None, dtype=torch.float32, num_nodes=None):
+    edge_index, edge_weight = remove_self_loops(edge_index, edge_weight)
+    if edge_weight is None:
+        edge_weight = torch.ones((edge_index.size(1),), dtype=dtype)
+    row, col = edge_index
+    deg = S.scatter_sum(edge_weight, row, num_nodes)
+    if normalization is None:
+        edge_index, _ = add_self_loops(edge_index, num_nodes=num_nodes)
+        return edge_index, torch.cat([-edge_weight, deg], dim=0)
+    if normalization == "sym":
+        dinv = deg.pow(-0.5)
+        dinv[dinv == float("inf")] = 0
+        edge_weight = dinv[row] * edge_weight * dinv[col]
+    else:
+        dinv = 1.0 / deg
+        dinv[dinv == float("inf")] = 0
+        edge_weight = dinv[row] * edge_weight
+    return add_self_loops(edge_index, -edge_weight, fill_value=1, num_nodes=num_nodes)
+
+
+def cheb_norm(edge_index, num_nodes, edge_weight=None, normalization="sym", lambda_max=2.0,
+              dtype=torch.float32):
+    edge_index, edge_weight = remove_self_loops(edge_index, edge_weight)
+    edge_index, edge_weight = get_laplacian(edge_index, edge_weight, normalization, dtype, num_nodes)
+    edge_weight = (2.0 * edge_weight) / lambda_max
+    edge_weight.masked_fill_(edge_weight == float("inf"), 0)
+    return add_self_loops(edge_index, edge_weight, fill_value=-1, num_nodes=num_nodes)
+
+
+def cheb_conv(x, edge_index, weight, bias=None, edge_weight=None, normalization="sym", lambda_max=None):
+    """ChebConv.forward: weight [K, F_in, F_out]."""
+    N = x.size(0)
+    lambda_max = 2.0 if lambda_max is None else lambda_max
+    ei, norm = cheb_norm(edge_index, N, edge_weight, normalization, lambda_max, x.dtype)
+    Tx_0 = x
+    out = torch.matmul(Tx_0, weight[0])
+    if weight.size(0) > 1:
+        Tx_1 = gcn_aggregate(x, ei, norm, N)
+        out = out + torch.matmul(Tx_1, weight[1])
+    for k in range(2, weight.size(0)):
+        Tx_2 = 2 * gcn_aggregate(Tx_1, ei, norm, N) - Tx_0
+        out = out + torch.matmul(Tx_2, weight[k])
+        Tx_0, Tx_1 = Tx_1, Tx_2
+    return out + bias if bias is not None else out
+
+
+def agnn_conv(x, edge_index, beta):
+    """AGNNConv.forward: softmax over N(i) u {i} of beta * cos(x_i, x_j), sum of alpha * x_j."""
+    N = x.size(0)
+    ei, _ = remove_self_loops(edge_index)
+    ei, _ = add_self_loops(ei, num_nodes=N)
+    x_norm = F.normalize(x, p=2, dim=-1)
+    x_j = x.index_select(0, ei[0])
+    alpha = beta * (x_norm.index_select(0, ei[1]) * x_norm.index_select(0, ei[0])).sum(dim=-1)
+    alpha = softmax(alpha, ei[1], N)
+    return S.scatter_sum(x_j * alpha.view(-1, 1), ei[1], N)
+
+
+# --- SGConv / GINConv [U] (upstream examples/sgc.py, examples/mutag_gin.py) ---
+
+def sg_conv(x, edge_index, K, lin_w, lin_b=None, edge_weight=None):
+    N = x.size(0)
+    ei, norm = gcn_norm(edge_index, N, edge_weight, False, x.dtype)
+    for _ in range(K):
+        x = gcn_aggregate(x, ei, norm, N)
+    return F.linear(x, lin_w, lin_b)
+
+
+def gin_conv(x, edge_index, mlp, eps):
+    ei, _ = remove_self_loops(edge_index)
+    x_j = x.index_select(0, ei[0])
+    return mlp((1 + eps) * x + S.scatter_sum(x_j, ei[1], x.size(0)))

@@ -1813,3 +1813,143 @@ def test_col_sums_bias_gradient(n, F):
     assert torch.equal(got, again)
     tol = 1e-5 * torch.clamp(g.double().abs().sum(0), min=1.0)
     assert bool(((got.cpu().double() - want).abs() <= tol).all())
+
+
+@pytest.mark.parametrize("K,normalization,weighted", [(1, "sym", False), (2, "sym", False), (3, "sym", True),
+                                                      (3, "rw", False), (2, None, True)])
+def test_cheb_conv_forward_backward(K, normalization, weighted):
+    """ChebConv (ConvexPruning.py:259-264) on the fused w * x_j path: the
+    Laplacian rewrite (loops removed, get_laplacian, 2/lambda_max scaling,
+    the -1 loops) and every T_k propagate vs the fp32 oracle and float64
+    autograd, on a power-law graph with duplicate edges and self loops."""
+    from torch_geometric.nn import ChebConv
+    pl = _mods()[4]
+    N, E, Fi, Fo = 500, 8000, 16, 24
+    ei = pl(N, E, seed=11)
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(N, Fi, generator=g)
+    w = torch.rand(E, generator=g) + 0.5 if weighted else None
+    lam = None if normalization == "sym" else 3.0
+    conv = ChebConv(Fi, Fo, K=K, normalization=normalization).to(DEV)
+    with torch.no_grad():
+        conv.bias.normal_()
+    xd = x.to(DEV).requires_grad_(True)
+    out = conv(xd, ei.to(DEV), None if w is None else w.to(DEV), lambda_max=lam)
+    W = conv.weight.detach().cpu()
+    b = conv.bias.detach().cpu()
+    # bound: 1e-5 of the magnitude of every term (the recursion run on |x|,
+    # |W|, |norm|): L = D - A puts the degrees on the diagonal, so rows of hubs
+    # sum large terms of both signs (and hub rows split across tasks sum in a
+    # different grouping than the sequential loop)
+    w64 = None if w is None else w.double()
+    cei, cnorm = P.cheb_norm(ei, N, w64, normalization, 2.0 if lam is None else lam, torch.float64)
+    T = [x.double().abs()]
+    if K > 1:
+        T.append(P.gcn_aggregate(T[0], cei, cnorm.abs(), N))
+    for _ in range(2, K):
+        T.append(2 * P.gcn_aggregate(T[-1], cei, cnorm.abs(), N) + T[-2])
+    scale = sum(T[k] @ W[k].double().abs() for k in range(K)) + b.double().abs()
+    ref32 = P.cheb_conv(x, ei, W, b, w, normalization, lam)
+    assert ((out.detach().cpu().double() - ref32.double()).abs() <= 1e-5 * scale + 1e-6).all()
+    gout = torch.randn(N, Fo, generator=g)
+    out.backward(gout.to(DEV))
+    W64 = W.double().requires_grad_(True)
+    b64 = b.double().requires_grad_(True)
+    x64 = x.double().requires_grad_(True)
+    ref64 = P.cheb_conv(x64, ei, W64, b64, w64, normalization, lam)
+    assert ((out.detach().cpu().double() - ref64.detach()).abs() <= 1e-5 * scale + 1e-6).all()
+    ref64.backward(gout.double())
+    for got, want in ((xd.grad, x64.grad), (conv.weight.grad, W64.grad), (conv.bias.grad, b64.grad)):
+        # large-degree diagonal terms (normalization None): atol follows the tensor's scale
+        assert torch.allclose(got.cpu().double(), want, rtol=1e-4, atol=1e-4 + 1e-6 * float(want.abs().max()))
+
+
+@pytest.mark.parametrize("requires_grad", [True, False])
+def test_agnn_conv_forward_backward(requires_grad):
+    """AGNNConv (ConvexPruning.py:236-237) on the generic path (native gathers
+    of x_j / x_norm_i / x_norm_j, utils.softmax on native segment ops, native
+    segmented sum) vs the fp32 oracle and float64 autograd (x and beta)."""
+    from torch_geometric.nn import AGNNConv
+    pl = _mods()[4]
+    N, E, Fd = 400, 6000, 16
+    ei = pl(N, E, seed=12)
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(N, Fd, generator=g)
+    conv = AGNNConv(requires_grad=requires_grad).to(DEV)
+    if requires_grad:
+        with torch.no_grad():
+            conv.beta.fill_(0.8)
+    beta = torch.tensor([0.8 if requires_grad else 1.0])
+    xd = x.to(DEV).requires_grad_(True)
+    out = conv(xd, ei.to(DEV))
+    assert torch.allclose(out.detach().cpu(), P.agnn_conv(x, ei, beta), rtol=1e-5, atol=1e-5)
+    gout = torch.randn(N, Fd, generator=g)
+    out.backward(gout.to(DEV))
+    x64 = x.double().requires_grad_(True)
+    b64 = beta.double().requires_grad_(requires_grad)
+    ref64 = P.agnn_conv(x64, ei, b64)
+    assert torch.allclose(out.detach().cpu().double(), ref64.detach(), rtol=1e-4, atol=1e-5)
+    ref64.backward(gout.double())
+    assert torch.allclose(xd.grad.cpu().double(), x64.grad, rtol=1e-4, atol=1e-4)
+    if requires_grad:
+        assert torch.allclose(conv.beta.grad.cpu().double(), b64.grad, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("K,cached", [(1, False), (2, False), (3, True)])
+def test_sg_conv_forward_backward(K, cached):
+    """SGConv (upstream examples/sgc.py): K fused GCN-normalised propagates +
+    Linear vs the fp32 oracle and float64 autograd; cached=True reuses S^K X."""
+    from torch_geometric.nn import SGConv
+    pl = _mods()[4]
+    N, E, Fi, Fo = 500, 8000, 16, 7
+    ei = pl(N, E, seed=13)
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(N, Fi, generator=g)
+    conv = SGConv(Fi, Fo, K=K, cached=cached).to(DEV)
+    xd = x.to(DEV).requires_grad_(not cached)
+    out = conv(xd, ei.to(DEV))
+    lw, lb = conv.lin.weight.detach().cpu(), conv.lin.bias.detach().cpu()
+    assert torch.allclose(out.detach().cpu(), P.sg_conv(x, ei, K, lw, lb), rtol=1e-5, atol=1e-5)
+    gout = torch.randn(N, Fo, generator=g)
+    out.backward(gout.to(DEV))
+    x64 = x.double().requires_grad_(True)
+    lw64, lb64 = lw.double().requires_grad_(True), lb.double().requires_grad_(True)
+    ref = P.sg_conv(x64, ei, K, lw64, lb64)
+    ref.backward(gout.double())
+    assert torch.allclose(conv.lin.weight.grad.cpu().double(), lw64.grad, rtol=1e-4, atol=1e-4)
+    if not cached:
+        assert torch.allclose(xd.grad.cpu().double(), x64.grad, rtol=1e-4, atol=1e-4)
+    else:
+        out2 = conv(xd, ei.to(DEV))       # cached S^K X: the same values, no propagate
+        assert torch.equal(out2, out)
+
+
+@pytest.mark.parametrize("train_eps", [False, True])
+def test_gin_conv_forward_backward(train_eps):
+    """GINConv (upstream examples/mutag_gin.py): loops removed, fused sum of
+    x_j, (1 + eps) x + sum, MLP -- vs the fp32 oracle and float64 autograd."""
+    from torch_geometric.nn import GINConv
+    pl = _mods()[4]
+    N, E, Fd = 400, 6000, 32
+    ei = pl(N, E, seed=14)
+    g = torch.Generator().manual_seed(14)
+    x = torch.randn(N, Fd, generator=g)
+    torch.manual_seed(14)
+    mlp = torch.nn.Sequential(torch.nn.Linear(Fd, 24), torch.nn.ReLU(), torch.nn.Linear(24, 24))
+    conv = GINConv(mlp, eps=0.3, train_eps=train_eps).to(DEV)
+    xd = x.to(DEV).requires_grad_(True)
+    out = conv(xd, ei.to(DEV))
+    import copy
+    mlp_cpu = copy.deepcopy(conv.nn).cpu()
+    assert torch.allclose(out.detach().cpu(), P.gin_conv(x, ei, mlp_cpu, 0.3), rtol=1e-5, atol=1e-5)
+    gout = torch.randn(N, 24, generator=g)
+    out.backward(gout.to(DEV))
+    mlp64 = copy.deepcopy(mlp_cpu).double()
+    x64 = x.double().requires_grad_(True)
+    eps64 = torch.tensor([0.3], dtype=torch.float64, requires_grad=True)
+    P.gin_conv(x64, ei, mlp64, eps64).backward(gout.double())
+    assert torch.allclose(xd.grad.cpu().double(), x64.grad, rtol=1e-4, atol=1e-4)
+    for p, q in zip(conv.nn.parameters(), mlp64.parameters()):
+        assert torch.allclose(p.grad.cpu().double(), q.grad, rtol=1e-4, atol=1e-4)
+    if train_eps:
+        assert torch.allclose(conv.eps.grad.cpu().double(), eps64.grad, rtol=1e-4, atol=1e-4)

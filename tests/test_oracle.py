@@ -177,3 +177,104 @@ def test_oracle_torch_scatter_documented_vectors():
     assert S.scatter_sum(src2, index, 4).tolist() == [[4, 6], [21, 24], [0, 0], [11, 12]]
     mx2, amx2 = S.scatter_loop(src2, index, 4, "max")
     assert mx2.tolist() == [[3, 4], [9, 10], [0, 0], [11, 12]] and amx2.tolist() == [[2, 2], [4, 4], [6, 6], [5, 5]]
+
+
+def _dense(ei, w, N):
+    """Operator of propagate(edge_index, norm) as a dense matrix: out = M x,
+    M[i, j] = sum of the weights of edges j -> i (flow source_to_target)."""
+    M = torch.zeros(N, N, dtype=torch.float64)
+    for e in range(ei.shape[1]):
+        M[ei[1, e], ei[0, e]] += w[e]
+    return M
+
+
+def _kat_graph():
+    # 7 nodes: an undirected path 0-1-2-3, a triangle 3-4-5, a duplicate
+    # edge (1->2 twice), a self loop on 4, node 6 isolated
+    und = [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (5, 3)]
+    src = [a for a, b in und] + [b for a, b in und] + [1, 4]
+    dst = [b for a, b in und] + [a for a, b in und] + [2, 4]
+    return torch.tensor([src, dst]), 7
+
+
+@pytest.mark.parametrize("normalization", ["sym", "rw", None])
+def test_kat_get_laplacian_and_cheb_conv(normalization):
+    """The oracle's get_laplacian / ChebConv against the textbook operators
+    built densely: L = D - A, I - D^-1/2 A D^-1/2, I - D^-1 A (degrees over
+    edge_index[0] after removing loops), L_hat = 2 L / lambda_max - I, and
+    the Chebyshev recursion T_0 = X, T_1 = L_hat X, T_k = 2 L_hat T_{k-1} - T_{k-2}."""
+    ei, N = _kat_graph()
+    keep = ei[0] != ei[1]
+    A = torch.zeros(N, N, dtype=torch.float64)
+    for s, d in ei[:, keep].t().tolist():
+        A[d, s] += 1.0                   # message s -> d
+    deg = torch.zeros(N, dtype=torch.float64)
+    for s in ei[0, keep].tolist():
+        deg[s] += 1.0                    # deg = scatter_add(w, row)
+    I = torch.eye(N, dtype=torch.float64)
+    if normalization is None:
+        L = torch.diag(deg) - A
+    elif normalization == "sym":
+        dinv = torch.where(deg > 0, deg.pow(-0.5), torch.zeros_like(deg))
+        L = I - dinv.view(-1, 1) * A * dinv.view(1, -1)
+    else:
+        # edge j -> i carries 1/deg[j] (deg of the source, edge_index[0])
+        dinv = torch.where(deg > 0, 1.0 / deg, torch.zeros_like(deg))
+        L = I - A * dinv.view(1, -1)
+    lei, lw = P.get_laplacian(ei, None, normalization, torch.float64, N)
+    assert torch.allclose(_dense(lei, lw, N), L, atol=1e-12)
+    lam = 2.0 if normalization == "sym" else 3.5
+    L_hat = 2.0 * L / lam - I
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(N, 3, generator=g, dtype=torch.float64)
+    W = torch.randn(3, 3, 2, generator=g, dtype=torch.float64)
+    b = torch.randn(2, generator=g, dtype=torch.float64)
+    T = [x, L_hat @ x]
+    T.append(2 * L_hat @ T[1] - T[0])
+    want = sum(T[k] @ W[k] for k in range(3)) + b
+    got = P.cheb_conv(x, ei, W, b, normalization=normalization, lambda_max=None if normalization == "sym" else lam)
+    assert torch.allclose(got, want, atol=1e-12)
+    # the propagated operator of cheb_norm is L_hat itself (the -I rides as separate loops)
+    cei, cw = P.cheb_norm(ei, N, None, normalization, lam, torch.float64)
+    assert torch.allclose(_dense(cei, cw, N), L_hat, atol=1e-12)
+    assert cei.shape[1] == int(keep.sum()) + 2 * N      # edges, L's diagonal, the -1 loops
+
+
+def test_kat_agnn_conv():
+    """AGNNConv: x'_i = sum_{j in N(i) u {i}} softmax_j(beta cos(x_i, x_j)) x_j,
+    with a duplicate edge counted twice and existing loops replaced by one."""
+    ei, N = _kat_graph()
+    g = torch.Generator().manual_seed(6)
+    x = torch.randn(N, 4, generator=g, dtype=torch.float64)
+    beta = torch.tensor([0.7], dtype=torch.float64)
+    xn = x / x.norm(dim=1, keepdim=True)
+    want = torch.zeros_like(x)
+    keep = ei[0] != ei[1]
+    for i in range(N):
+        srcs = [s for s, d in ei[:, keep].t().tolist() if d == i] + [i]
+        sc = torch.stack([beta[0] * (xn[i] * xn[j]).sum() for j in srcs])
+        p = torch.softmax(sc, 0)
+        want[i] = sum(p[k] * x[j] for k, j in enumerate(srcs))
+    assert torch.allclose(P.agnn_conv(x, ei, beta), want, atol=1e-12)
+
+
+def test_kat_sg_conv_and_gin_conv():
+    """SGConv = Linear(S^K X) with S = D^-1/2 (A + I) D^-1/2 (remaining loops:
+    an existing loop keeps its weight), GINConv = nn((1 + eps) X + A X) with
+    loops removed -- against dense operators."""
+    ei, N = _kat_graph()
+    keep = ei[0] != ei[1]
+    A = torch.zeros(N, N, dtype=torch.float64)
+    for s, d in ei[:, keep].t().tolist():
+        A[d, s] += 1.0
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(N, 3, generator=g, dtype=torch.float64)
+    Ah = A + torch.eye(N, dtype=torch.float64)
+    deg = Ah.sum(0)                 # deg over edge_index[0] = column sums (sources)
+    S_ = Ah / deg.sqrt().view(-1, 1) / deg.sqrt().view(1, -1)
+    lw = torch.randn(2, 3, generator=g, dtype=torch.float64)
+    lb = torch.randn(2, generator=g, dtype=torch.float64)
+    want = (S_ @ (S_ @ x)) @ lw.t() + lb
+    assert torch.allclose(P.sg_conv(x, ei, 2, lw, lb), want, atol=1e-12)
+    mlp = torch.nn.Linear(3, 2).double()
+    assert torch.allclose(P.gin_conv(x, ei, mlp, 0.25), mlp(1.25 * x + A @ x), atol=1e-12)
