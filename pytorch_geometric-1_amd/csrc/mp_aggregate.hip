@@ -40,7 +40,10 @@ namespace mp {
 constexpr int kU_Vec4 = 8;      // x-row loads in flight per task (VEC=4, 64-lane tasks: GAT)
 constexpr int kU_Vec2 = 16;     // x-row loads in flight per task (VEC=2: the flat kernel, 128-feature tiles)
 constexpr int kU_Vec1 = 16;     // x-row loads in flight per task (VEC=1)
-constexpr int kU_Vec1Far = 8;   // ... scalar-batch sum/mean over an x larger than the Infinity Cache
+#ifndef MP_U_VEC1_FAR
+#define MP_U_VEC1_FAR 8
+#endif
+constexpr int kU_Vec1Far = MP_U_VEC1_FAR;  // ... scalar-batch sum/mean over an x larger than the Infinity Cache
 #ifndef MP_U_GAT_TRAIN
 #define MP_U_GAT_TRAIN 4
 #endif
