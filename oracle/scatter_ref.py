@@ -50,11 +50,19 @@ def _addr(a):
     return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
 
 
+def _flat2(src):
+    """[E, ...] -> [E, prod(...)] (also for E = 0, where reshape(E, -1) is ambiguous)."""
+    f = 1
+    for d in src.shape[1:]:
+        f *= int(d)
+    return src.reshape(src.shape[0], f)
+
+
 # --- torch-op forms (the literal upstream calls) ---------------------------
 
 def scatter_sum(src, index, dim_size):
     """zeros(dim_size, F).scatter_add_(0, index broadcast, src) (edge order)."""
-    src2 = src.reshape(src.shape[0], -1)
+    src2 = _flat2(src)
     out = torch.zeros((dim_size, src2.shape[1]), dtype=src.dtype)
     if src2.numel():
         out.scatter_add_(0, index.view(-1, 1).expand_as(src2), src2)
@@ -74,7 +82,7 @@ def scatter_mean(src, index, dim_size):
 def scatter_loop(src, index, dim_size, reduce, out=None):
     """Serial loop in C; returns (out, arg or None).  fp32 only."""
     red = {"sum": R_SUM, "add": R_SUM, "mean": R_MEAN, "max": R_MAX, "min": R_MIN}[reduce]
-    s = _np(src.reshape(src.shape[0], -1), np.float32)
+    s = _np(_flat2(src), np.float32)
     E, F = s.shape
     idx = _np(index, np.int64)
     has_out = out is not None

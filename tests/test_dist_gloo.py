@@ -79,7 +79,7 @@ def _worker(rank, world, port, result_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
 def test_sharded_gcn_aggregation_matches_single_process(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -1953,3 +1953,52 @@ def test_gin_conv_forward_backward(train_eps):
         assert torch.allclose(p.grad.cpu().double(), q.grad, rtol=1e-4, atol=1e-4)
     if train_eps:
         assert torch.allclose(conv.eps.grad.cpu().double(), eps64.grad, rtol=1e-4, atol=1e-4)
+
+
+from hypothesis import HealthCheck, given, settings, strategies as st  # noqa: E402
+
+
+@settings(max_examples=200, deadline=None, derandomize=True, database=None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+@given(N=st.integers(1, 400), deg=st.floats(0.0, 40.0),
+       F=st.sampled_from([1, 2, 3, 4, 5, 7, 8, 16, 31, 33, 64, 100, 128, 130, 256, 300]),
+       reduce=st.sampled_from(["sum", "mean", "max", "min"]), weighted=st.booleans(),
+       chunk=st.sampled_from([16, 32, 64, 256, 1024]), kind=st.sampled_from(["powerlaw", "uniform", "star"]),
+       seed=st.integers(0, 1 << 16))
+def test_fuzz_fused_aggregation_vs_serial_loop(N, deg, F, reduce, weighted, chunk, kind, seed):
+    """Shape / degree fuzzing of the fused gather -> reduce kernel
+    (every dispatch shape: lane tasks, lane groups, flat tiles, split rows)
+    against torch_scatter's serial loop on the materialised messages: max/min
+    values and first-edge args bit-exact (tie-heavy integer data), sum/mean
+    within 1e-5 of the sum of |terms| (bit-exact on rows inside one task)."""
+    _, ops, _, Graph, pl = _mods()
+    g = torch.Generator().manual_seed(seed)
+    E = int(N * deg)
+    if kind == "powerlaw" and N > 1 and E > 0:
+        ei = pl(N, E, seed=seed, symmetric=False)
+    elif kind == "star" and E > 0:
+        hub = torch.zeros(E // 2, dtype=torch.int64)
+        rest = torch.randint(N, (E - E // 2,), generator=g)
+        ei = torch.stack([torch.randint(N, (E,), generator=g), torch.cat([hub, rest])])
+    else:
+        ei = torch.randint(N, (2, E), generator=g)
+    E = ei.shape[1]
+    arg_red = reduce in ("max", "min")
+    x = torch.randint(-3, 4, (N, F), generator=g).float() if arg_red else torch.randn(N, F, generator=g)
+    w = None
+    if weighted:
+        w = (torch.tensor([0.5, 1.0, 2.0])[torch.randint(3, (E,), generator=g)] if arg_red
+             else torch.rand(E, generator=g))
+    csr = Graph(ei.to(DEV), N, N, chunk=chunk).dst
+    w_csr = csr.to_csr_order(w.to(DEV)) if weighted else None
+    out, arg = ops._aggregate(csr, "other", x.to(DEV), w_csr, reduce, 0, None)
+    msg = x[ei[0]] if w is None else w.view(-1, 1) * x[ei[0]]
+    want, warg = S.scatter_loop(msg, ei[1], N, reduce)
+    if arg_red:
+        assert torch.equal(out.cpu(), want)
+        assert torch.equal(arg.cpu(), warg)
+    else:
+        terms = S.scatter_loop(msg.abs(), ei[1], N, "sum")[0]
+        if reduce == "mean":
+            terms = terms / torch.bincount(ei[1], minlength=N).clamp(min=1).view(-1, 1).float()
+        _bound_ok(out.cpu(), want, terms)

@@ -278,3 +278,35 @@ def test_kat_sg_conv_and_gin_conv():
     assert torch.allclose(P.sg_conv(x, ei, 2, lw, lb), want, atol=1e-12)
     mlp = torch.nn.Linear(3, 2).double()
     assert torch.allclose(P.gin_conv(x, ei, mlp, 0.25), mlp(1.25 * x + A @ x), atol=1e-12)
+
+
+from hypothesis import HealthCheck, given, settings, strategies as st  # noqa: E402
+
+
+@settings(max_examples=80, deadline=None, derandomize=True, database=None,
+          suppress_health_check=[HealthCheck.too_slow])
+@given(N=st.integers(1, 200), E=st.integers(0, 2000), F=st.integers(1, 9), ties=st.booleans(),
+       seed=st.integers(0, 1 << 16))
+def test_fuzz_oracle_forms_agree(N, E, F, ties, seed):
+    """Property fuzzing of the oracle's two independent forms:
+    torch's scatter_add_ / amax + first-hit amin vs the serial C loop
+    (scatter_loop.c, torch_scatter's b/e/k loop), on empty inputs, empty
+    rows and tie-heavy integer data."""
+    g = torch.Generator().manual_seed(seed)
+    src = (torch.randint(-2, 3, (E, F), generator=g).float() if ties else torch.randn(E, F, generator=g))
+    idx = torch.randint(N, (E,), generator=g)
+    assert torch.equal(S.scatter_sum(src, idx, N), S.scatter_loop(src, idx, N, "sum")[0])
+    assert torch.equal(S.scatter_mean(src, idx, N), S.scatter_loop(src, idx, N, "mean")[0])
+    for red, amax in (("max", "amax"), ("min", "amin")):
+        out, arg = S.scatter_loop(src, idx, N, red)
+        fill = float("-inf") if red == "max" else float("inf")
+        ref = torch.full((N, F), fill).scatter_reduce(0, idx.view(-1, 1).expand(E, F), src, amax)
+        empty = torch.isinf(ref)
+        ref[empty] = 0
+        assert torch.equal(out, ref)
+        e = torch.arange(E).view(-1, 1).expand(E, F)
+        hit = src == ref[idx]
+        first = torch.full((N, F), E, dtype=torch.int64).scatter_reduce(
+            0, idx.view(-1, 1).expand(E, F), torch.where(hit, e, torch.full_like(e, E)), "amin")
+        first[empty] = E
+        assert torch.equal(arg, first)
