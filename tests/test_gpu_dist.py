@@ -279,3 +279,93 @@ def test_native_shard_plan_rejects_out_of_range_endpoint():
     ei = torch.tensor([[0, 1, 2, 99], [1, 2, 0, 1]], device=dev)   # source 99 >= N
     with pytest.raises(IndexError):
         mdist.ShardPlan(ei, 4, 0, 2, cuts=[0, 2, 4])
+
+
+def _rccl_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "pytorch_geometric-1_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    try:
+        assert dist.get_backend() == "nccl"
+        from mi355_mp import dist as mdist, ops
+        from mi355_mp.graph import Graph
+        from mi355_mp.graphgen import powerlaw_edge_index
+        from torch_geometric.nn import GCNConv
+        N, E, Fi, F = 3000, 60000, 64, 256
+        ei = powerlaw_edge_index(N, E, seed=51).to(dev)
+        gen = torch.Generator().manual_seed(51)
+        x = torch.randn(N, F, generator=gen).to(dev)
+        bias = torch.randn(F, generator=gen).to(dev)
+        ei2, norm = GCNConv.norm(ei, N)
+        g1 = Graph(ei2, N, N, chunk=64)
+        ref = ops._aggregate(g1.dst, "other", x, g1.dst.to_csr_order(norm), "sum", 0, bias)[0]
+        res = {}
+        # the bench's step: async all_to_all_single on the RCCL stream + work.wait()
+        plan = mdist.ShardPlan(ei2, N, rank, world).exchange_requests()
+        ov = mdist.OverlappedAggregation(plan, norm, chunk=64)
+        xl = plan.local_buffer(F)
+        xl[:plan.n_own].copy_(x)
+        out = torch.empty(plan.n_own, F, device=dev)
+        ov.step(xl, out, bias)
+        tiles = plan.local_tiles(F, 128)
+        for t, xt in enumerate(tiles):
+            xt[:plan.n_own].copy_(x[:, 128 * t:128 * t + xt.shape[1]])
+        out_t = torch.empty(plan.n_own, F, device=dev)
+        ov.step_tiled(tiles, out_t, bias)
+        res["step"] = float((out - ref).abs().max())
+        res["tiled_eq_step"] = bool(torch.equal(out_t, out))
+        # sharded GCNConv forward + backward, RCCL broadcast / all_reduce of the weights
+        gout = torch.randn(N, F, generator=gen).to(dev)
+        xi = torch.randn(N, Fi, generator=gen).to(dev)
+        conv_ref = GCNConv(Fi, F).to(dev)
+        with torch.no_grad():
+            conv_ref.bias.normal_()
+        xr = xi.clone().requires_grad_(True)
+        (conv_ref(xr, ei) * gout).sum().backward()
+        sg = mdist.ShardedGraph.for_gcn(ei, N, rank, world)
+        conv = mdist.ShardedGCNConv(Fi, F).to(dev)
+        conv.load_state_dict(conv_ref.state_dict())
+        mdist.broadcast_parameters(conv)
+        xo = xi.clone().requires_grad_(True)
+        o = conv(xo, sg)
+        (o * gout).sum().backward()
+        mdist.allreduce_gradients(conv)
+        res["layer_out"] = float((o.detach() - conv_ref(xi, ei).detach()).abs().max())
+        res["layer_gx"] = float((xo.grad - xr.grad).abs().max())
+        res["layer_gw"] = float((conv.weight.grad - conv_ref.weight.grad).abs().max()
+                                / conv_ref.weight.grad.abs().max())
+        # max / min with global edge ids
+        xm = torch.randint(-3, 4, (N, F), generator=gen).to(torch.float32).to(dev)
+        sgm = mdist.ShardedGraph(ei2, N, rank, world)
+        exact = True
+        for red in ("max", "min"):
+            om, am = sgm.propagate(xm, red)
+            wo, wa = ops._aggregate(g1.dst, "other", xm, None, red, 0, None)
+            exact = exact and bool(torch.equal(om, wo)) and bool(torch.equal(am, wa))
+        res["max_exact"] = exact
+        torch.cuda.synchronize()
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_path_over_rccl_world_one():
+    """The sharded path on the RCCL backend ("nccl" = RCCL on ROCm) itself:
+    one rank on the box's one GPU (two ranks cannot share a device under RCCL,
+    profiles/r02_rccl_one_gpu_probe.log).  Runs every RCCL call the multi-GPU
+    bench makes -- communicator setup with device_id, async all_to_all_single
+    with split sizes on device tensors + work.wait() (OverlappedAggregation
+    step / step_tiled), the blocking exchanges of ShardPlan / ShardedGraph,
+    broadcast and all_reduce of the replicated GCNConv weights -- with empty
+    halo splits, against the single-GPU kernel and GCNConv."""
+    (rank, r), = _spawn(_rccl_worker, world=1, timeout=300)
+    assert r["step"] < 1e-5 and r["tiled_eq_step"], r
+    assert r["layer_out"] < 1e-5 and r["layer_gx"] < 1e-5 and r["layer_gw"] < 1e-5, r
+    assert r["max_exact"], r
