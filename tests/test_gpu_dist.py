@@ -220,12 +220,14 @@ def _products_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_full_size_products_sharded_rehearsal():
+@pytest.mark.parametrize("world", [2, 8])
+def test_full_size_products_sharded_rehearsal(world):
     """Config 5 at full size (N=2,449,029, E=123,718,280 + self loops, F=256),
-    destination-range sharded over 2 ranks sharing the device (gloo staging of
-    the halo rows -- the RCCL call is the one step not exercised): every rank's
-    owned rows within 1e-5 * sum|w x| of the single-GPU kernel."""
-    res = _spawn(_products_worker, timeout=900)
+    destination-range sharded over 2 ranks, and over 8 -- config 5's own
+    partition count -- sharing the device (gloo staging of the halo rows; the
+    RCCL call is covered by test_sharded_path_over_rccl_world_one): every
+    rank's owned rows within 1e-5 * sum|w x| of the single-GPU kernel."""
+    res = _spawn(_products_worker, world=world, timeout=900)
     assert sum(r[3] for r in res) == 2_449_029
     for rank, excess, frac, n_own, n_edges, n_halo in res:
         assert excess <= 0, res
