@@ -42,7 +42,7 @@ def test_ctypes_signatures_cover_the_header():
 
 
 def test_abi_version_and_error_string(lib):
-    assert lib.mp_abi_version() == 2
+    assert lib.mp_abi_version() == 3
     assert isinstance(lib.mp_last_error(), bytes)
 
 
@@ -87,7 +87,7 @@ def test_column_array_requires_n_cols(lib):
     rc = lib.mp_aggregate_f32(g, None, fake, 4, 4, 0, 0, None, fake, 4, None, fake, 1 << 20, 3, None)
     assert rc == 1 and b"n_cols" in lib.mp_last_error()
     buf = __import__("ctypes").create_string_buffer(256)
-    rc = lib.mp_aggregate_kernel_name(g, None, fake, 4, 4, 0, None, fake, 4, buf, 256, None)
+    rc = lib.mp_aggregate_kernel_name(g, None, fake, 4, 4, 0, 0, None, fake, 4, buf, 256, None)
     assert rc == 1 and b"n_cols" in lib.mp_last_error()
     # identity gather (col = NULL) needs no n_cols
     g2 = _lib.MpCsr(fake, None, fake, fake, fake, None, 10, 40, 256, 1, 0, 0, 0)

@@ -70,10 +70,11 @@ def main():
     main_ms = sorted(a.elapsed_time(b) for a, b, _ in ev)
     fix_ms = sorted(b.elapsed_time(c) for _, b, c in ev)
     kernel = _lib.kernel_name(csr.struct("other"), w.data_ptr(), x.data_ptr(), x.stride(0), F, "sum",
-                              bias.data_ptr(), out.data_ptr(), out.stride(0), dev)
+                              bias.data_ptr(), out.data_ptr(), out.stride(0), dev,
+                              flags=ops.hint_flags(csr, "other", x, "sum"))
     print(json.dumps({"graph": args.graph, "num_nodes": N, "num_edges": csr.n_edges,
                       "avg_degree": csr.n_edges / N, "main_ms": main_ms[len(main_ms) // 2],
-                      "fixup_ms": fix_ms[len(fix_ms) // 2], "kernel": kernel}))
+                      "fixup_ms": fix_ms[len(fix_ms) // 2], "hot_share": csr.hot_share(), "kernel": kernel}))
 
 
 if __name__ == "__main__":
