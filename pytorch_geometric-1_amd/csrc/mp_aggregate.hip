@@ -1338,16 +1338,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
       if constexpr (Red::kW) scalar_batch<U>(p.w, p.n_edges, e, wb);
       Frag<VEC> v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-#ifdef MP_COLD_TAG_AUX  // A/B variant: sign-tagged columns (cold sources) load with these cache-policy bits
-        const int c = c_nxt[u];
-        const uint32_t so = (uint32_t)(c & 0x7fffffff) * (uint32_t)ldxb;
-        if (c < 0) v[u] = load_frag_buf<VEC, MP_COLD_TAG_AUX>(xr, foff, so);
-        else v[u] = load_frag_buf<VEC>(xr, foff, so);
-#else
-        v[u] = load_frag_buf<VEC>(xr, foff, (uint32_t)c_nxt[u] * (uint32_t)ldxb);
-#endif
-      }
+      for (int u = 0; u < U; ++u) v[u] = load_frag_buf<VEC>(xr, foff, (uint32_t)c_nxt[u] * (uint32_t)ldxb);
       // the columns are dead once the gathers are issued: the next batch's
       // land in the same SGPRs while this batch's rows are in flight
       if (e + U < e_end) scalar_batch<U>(p.col, p.n_edges, e + U, c_nxt);

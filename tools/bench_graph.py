@@ -48,19 +48,6 @@ def main():
     ei2, norm = GCNConv.norm(ei, N)
     csr = Graph(ei2, N, N).dst
     w = csr.to_csr_order(norm)
-    cold_t = int(os.environ.get("MP_COLD_TAG_T", "0"))
-    csr.hot_share()   # cached before any tagging
-    if cold_t > 0:
-        # A/B of a tools/variants library built with -DMP_COLD_TAG_AUX: columns of
-        # sources with out-degree <= cold_t carry the sign bit (the default
-        # library must not see them)
-        E = csr.n_edges
-        col = csr.col[:E]
-        outdeg = torch.bincount(col, minlength=N)
-        cold = outdeg[col.long()] <= cold_t
-        col[cold] = col[cold] | torch.iinfo(torch.int32).min
-        print("cold tag: out-degree <= %d, %.1f%% of slots" % (cold_t, 100.0 * float(cold.float().mean())),
-              file=sys.stderr)
     x = torch.randn(N, F, device=dev, generator=torch.Generator(device=dev).manual_seed(1))
     bias = torch.randn(F, device=dev, generator=torch.Generator(device=dev).manual_seed(7)) * 0.1
     out = torch.empty(N, F, device=dev)
