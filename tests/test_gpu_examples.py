@@ -18,9 +18,12 @@ def _load(name):
 
 
 def test_example_gcn_cora_shaped():
-    losses = _load("gcn").main(["--epochs", "60"])
-    # the Cora-shaped graph has random labels: the model can only fit the training split
-    assert all(math.isfinite(v) for v in losses) and losses[-1] < 0.9 * losses[0]
+    import torch
+    torch.manual_seed(0)   # weights and dropout masks (the example itself is unseeded, as the reference's)
+    losses = _load("gcn").main(["--epochs", "100"])
+    # the Cora-shaped graph has random labels: the model can only fit the training
+    # split, and dropout keeps the per-epoch loss noisy -- judge the last 10 epochs
+    assert all(math.isfinite(v) for v in losses) and min(losses[-10:]) < 0.85 * losses[0], losses[::10]
 
 
 def test_example_ppi_gat():
