@@ -27,10 +27,14 @@ def test_example_gcn_cora_shaped():
 
 
 def test_example_ppi_gat():
+    import torch
+    torch.manual_seed(0)
     losses = _load("ppi").main(["--epochs", "2", "--train-graphs", "3"])
     assert all(math.isfinite(v) for v in losses) and losses[-1] < losses[0]
 
 
 def test_example_data_parallel():
+    import torch
+    torch.manual_seed(0)
     losses = _load("data_parallel").main(["--epochs", "3", "--graphs", "512"])
     assert all(math.isfinite(v) for v in losses) and losses[-1] < losses[0]
