@@ -22,6 +22,9 @@ GRAPHS = {
     "rmat20_deg58": ("rmat", dict(scale=20, n_samples=30_000_000)),
     "rmat21_deg45": ("rmat", dict(scale=21, n_samples=45_000_000)),
     "products": ("powerlaw", dict(num_nodes=2_449_029, num_edges=123_718_280)),
+    "products_deg25": ("powerlaw", dict(num_nodes=2_449_029, num_edges=61_859_140)),
+    "rmat22": ("rmat", dict(scale=22, n_samples=30_000_000)),
+    "rmat22_deg30": ("rmat", dict(scale=22, n_samples=60_000_000)),
 }
 
 
@@ -29,6 +32,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--graph", default="rmat21", choices=sorted(GRAPHS))
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--force-u", type=int, choices=(6, 8), default=None,
+                    help="pin the far-x batch depth: 6 (hint on) or 8 (hint off) whatever the hot-source share")
     args = ap.parse_args()
     import mi355_mp
     from mi355_mp import _lib, ops
@@ -48,6 +53,9 @@ def main():
     ei2, norm = GCNConv.norm(ei, N)
     csr = Graph(ei2, N, N).dst
     w = csr.to_csr_order(norm)
+    share = csr.hot_share()
+    if args.force_u is not None:
+        csr._hot_share = 0.0 if args.force_u == 6 else 1.0
     x = torch.randn(N, F, device=dev, generator=torch.Generator(device=dev).manual_seed(1))
     bias = torch.randn(F, device=dev, generator=torch.Generator(device=dev).manual_seed(7)) * 0.1
     out = torch.empty(N, F, device=dev)
@@ -74,7 +82,7 @@ def main():
                               flags=ops.hint_flags(csr, "other", x, "sum"))
     print(json.dumps({"graph": args.graph, "num_nodes": N, "num_edges": csr.n_edges,
                       "avg_degree": csr.n_edges / N, "main_ms": main_ms[len(main_ms) // 2],
-                      "fixup_ms": fix_ms[len(fix_ms) // 2], "hot_share": csr.hot_share(), "kernel": kernel}))
+                      "fixup_ms": fix_ms[len(fix_ms) // 2], "hot_share": share, "force_u": args.force_u, "kernel": kernel}))
 
 
 if __name__ == "__main__":
