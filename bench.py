@@ -280,8 +280,7 @@ def main():
         timing_src = "HIP events over back-to-back launches on the rank's local graph (after the timed region)"
     # the kernel the library dispatches for exactly these arguments (no heuristic copy)
     kernel = _lib.kernel_name(st_main, w_csr.data_ptr(), x_src.data_ptr(), x_src.stride(0), F_DIM, "sum",
-                              bias.data_ptr(), out_buf.data_ptr(), out_buf.stride(0), dev,
-                              flags=ops.hint_flags(csr, "other", x_src, "sum"))
+                              bias.data_ptr(), out_buf.data_ptr(), out_buf.stride(0), dev)
     main_avg = sum(main_ms) / len(main_ms)
     fix_avg = sum(fix_ms) / len(fix_ms)
     alg_bytes = E_local * BYTES_PER_EDGE + n_rows * BYTES_PER_NODE

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MP_ABI_VERSION 3
+#define MP_ABI_VERSION 2
 
 /* status codes */
 #define MP_OK 0
@@ -51,11 +51,6 @@ extern "C" {
 #define MP_FLAG_INIT_FROM_OUT 1 /* torch_scatter `out=` given: reduce into out's values */
 #define MP_FLAG_PYG_MASK 2      /* torch_geometric.utils.scatter_: max -> out<-10000 := 0,
                                    min -> out>10000 := 0 */
-#define MP_FLAG_COLD_SOURCES 4  /* hint (results unchanged): under 44 % of the slots gather the
-                                   16384 most-gathered source rows (mi355_mp CSR.hot_share), so an
-                                   XCD's L2 serves few gathers; the scalar-batch sum/mean kernel
-                                   over an x beyond the Infinity Cache then keeps 6 rows in flight
-                                   per wave instead of 8 */
 
 /* aggregate stages (bench times the main kernel on its own) */
 #define MP_STAGE_MAIN 1
@@ -197,7 +192,7 @@ int mp_aggregate_f32(const mp_csr* g, const float* w, const float* x,
  * profile summary be matched to the dispatched kernel (bench.py).  Needs a
  * HIP device for the name lookup; MP_ERR_ARG when none is available. */
 int mp_aggregate_kernel_name(const mp_csr* g, const float* w, const float* x,
-                             int64_t ldx, int32_t F, int32_t reduce, int32_t flags,
+                             int64_t ldx, int32_t F, int32_t reduce,
                              const float* bias, const float* out, int64_t ldo,
                              char* buf, size_t buf_len, void* stream);
 

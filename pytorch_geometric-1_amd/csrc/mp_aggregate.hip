@@ -44,7 +44,6 @@ constexpr int kU_Vec1 = 16;     // x-row loads in flight per task (VEC=1)
 #define MP_U_VEC1_FAR 8
 #endif
 constexpr int kU_Vec1Far = MP_U_VEC1_FAR;  // ... scalar-batch sum/mean over an x larger than the Infinity Cache
-constexpr int kU_Vec1FarCold = 6;  // ... the same with MP_FLAG_COLD_SOURCES (products-scale 14.50 -> 13.99 ms)
 #ifndef MP_U_GAT_TRAIN
 #define MP_U_GAT_TRAIN 4
 #endif
@@ -1545,10 +1544,7 @@ static int launch_l(const AggArgs& a, int stages, hipStream_t s) {
           bool far = false;
           if constexpr (VEC == 1) {
             far = a.smem && a.far;
-            if (far && (a.flags & MP_FLAG_COLD_SOURCES))
-              rc = launch_main(k_agg_flat<Red, 1, kU_Vec1FarCold, 64, false, true>, grid, s, a);
-            else if (far)
-              rc = launch_main(k_agg_flat<Red, 1, kU_Vec1Far, 64, false, true>, grid, s, a);
+            if (far) rc = launch_main(k_agg_flat<Red, 1, kU_Vec1Far, 64, false, true>, grid, s, a);
           }
           if (far) {
           } else if (a.smem) rc = launch_main(k_agg_flat<Red, VEC, U, 64, false, true>, grid, s, a);
@@ -1829,7 +1825,7 @@ int mp_aggregate_f32(const mp_csr* g, const float* w, const float* x, int64_t ld
 }
 
 int mp_aggregate_kernel_name(const mp_csr* g, const float* w, const float* x, int64_t ldx, int32_t F,
-                             int32_t reduce, int32_t flags, const float* bias, const float* out, int64_t ldo, char* buf,
+                             int32_t reduce, const float* bias, const float* out, int64_t ldo, char* buf,
                              size_t buf_len, void* stream) {
   int rc = check_graph(g, "mp_aggregate_kernel_name");
   if (rc) return rc;
@@ -1843,7 +1839,6 @@ int mp_aggregate_kernel_name(const mp_csr* g, const float* w, const float* x, in
   a.w = w;
   a.x = x;
   a.ldx = ldx;
-  a.flags = flags;
   a.bias = bias;
   a.out = const_cast<float*>(out);
   a.ldo = ldo;

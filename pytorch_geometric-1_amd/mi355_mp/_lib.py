@@ -17,7 +17,6 @@ MP_OK = 0
 MP_REDUCE = {"sum": 0, "add": 0, "mean": 1, "max": 2, "min": 3}
 MP_FLAG_INIT_FROM_OUT = 1
 MP_FLAG_PYG_MASK = 2
-MP_FLAG_COLD_SOURCES = 4
 MP_STAGE_MAIN = 1
 MP_STAGE_FIXUP = 2
 MP_STAGE_STATS = 4
@@ -64,7 +63,7 @@ SIGNATURES = {
     "mp_aggregate_slab_bytes": (sz, [ctypes.POINTER(MpCsr), i32, i32]),
     "mp_aggregate_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, i64, i32, i32, i32, c_p,
                                         c_p, i64, c_p, c_p, sz, i32, c_p]),
-    "mp_aggregate_kernel_name": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, i64, i32, i32, i32, c_p, c_p, i64,
+    "mp_aggregate_kernel_name": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, i64, i32, i32, c_p, c_p, i64,
                                                 ctypes.c_char_p, sz, c_p]),
     "mp_gat_node_scores_f32": (ctypes.c_int, [c_p, i64, i32, i32, c_p, c_p, c_p, c_p]),
     "mp_gat_slab_bytes": (sz, [ctypes.POINTER(MpCsr), i32, i32]),
@@ -159,12 +158,12 @@ def source_hash():
     return h.hexdigest()[:16]
 
 
-def kernel_name(csr_struct, w, x, ldx, F, reduce, bias, out, ldo, device=None, flags=0):
+def kernel_name(csr_struct, w, x, ldx, F, reduce, bias, out, ldo, device=None):
     """Demangled name of the main kernel mp_aggregate_f32 dispatches for these
     arguments (mp_aggregate_kernel_name)."""
     buf = ctypes.create_string_buffer(1024)
-    check(load().mp_aggregate_kernel_name(csr_struct, w, x, ldx, F, MP_REDUCE[reduce], flags, bias, out, ldo, buf,
-                                          1024, stream_ptr(device)), "mp_aggregate_kernel_name")
+    check(load().mp_aggregate_kernel_name(csr_struct, w, x, ldx, F, MP_REDUCE[reduce], bias, out, ldo, buf, 1024,
+                                          stream_ptr(device)), "mp_aggregate_kernel_name")
     return buf.value.decode()
 
 

@@ -120,29 +120,6 @@ class CSR:
         self._structs = {}
         self._deg = None
 
-    HOT_ROWS = 16384        # 256-B row tiles one XCD's 4 MiB L2 holds
-    COLD_BELOW = 0.44       # hot_share under which MP_FLAG_COLD_SOURCES is passed
-
-    def hot_share(self):
-        """Fraction of the slots whose column is one of the HOT_ROWS most
-        gathered columns (one bincount + top-k, once per CSR; None while a
-        stream is being captured).  Six synthetic graphs:
-        0.18 and 0.41 favour 6 rows in flight in the far-x sum kernel, 0.47-0.58
-        favour 8."""
-        h = getattr(self, "_hot_share", None)
-        if h is None:
-            if torch.cuda.is_current_stream_capturing():
-                return None
-            E = self.n_edges
-            if E == 0:
-                h = 1.0
-            else:
-                cnt = torch.bincount(self.col[:E], minlength=self.n_other)
-                k = min(self.HOT_ROWS, cnt.numel())
-                h = float(cnt.topk(k, sorted=False).values.sum().item()) / E
-            self._hot_share = h
-        return h
-
     @classmethod
     def from_slots(cls, rowptr, col, eid, n_rows, n_other, chunk=DEFAULT_CHUNK):
         """A CSR over explicit int32 arrays (rowptr [n_rows+1], col / eid [E])."""

@@ -45,22 +45,6 @@ def _max_csr(csr):
     return csr.first_occurrences() if n > FIRST_OCCURRENCE_AFTER else csr
 
 
-# the cold-sources hint only matters to the far-x kernel (x beyond the Infinity Cache)
-COLD_HINT_MIN_BYTES = 256 << 20
-
-
-def hint_flags(csr, gather, x, reduce, flags=0):
-    """flags | MP_FLAG_COLD_SOURCES for a sum/mean gather of an x beyond the
-    Infinity Cache over a graph with a low hot-source share (a dispatch hint;
-    results are bitwise the same either way)."""
-    if (reduce in ("sum", "mean") and gather == "other" and csr.n_edges
-            and x.shape[0] * x.stride(0) * 4 > COLD_HINT_MIN_BYTES):
-        h = csr.hot_share()
-        if h is not None and h < csr.COLD_BELOW:
-            flags |= _lib.MP_FLAG_COLD_SOURCES
-    return flags
-
-
 def _aggregate(csr, gather, x, w_csr, reduce, flags, bias, out=None, stages=_lib.MP_STAGE_ALL, slab=None,
                arg=None):
     """Launch mp_aggregate_f32; returns (out, arg_or_None)."""
@@ -78,7 +62,6 @@ def _aggregate(csr, gather, x, w_csr, reduce, flags, bias, out=None, stages=_lib
         return out, arg
     g = csr.struct(gather)
     red = _lib.MP_REDUCE[reduce]
-    flags = hint_flags(csr, gather, x, reduce, flags)
     sb = lib.mp_aggregate_slab_bytes(g, F, red)
     if slab is None or slab.numel() < sb:
         slab = torch.empty(sb, dtype=torch.uint8, device=dev)

@@ -234,7 +234,7 @@ def test_unaligned_rows_widest_vector_bitwise_equal(F, reduce):
             out = torch.empty(N, F, device=DEV)
             buf = __import__("ctypes").create_string_buffer(512)
             _lib.check(lib.mp_aggregate_kernel_name(graph.dst.struct("other"), 0, xx.data_ptr(), xx.stride(0), F,
-                                                    _lib.MP_REDUCE[reduce], 0, 0, out.data_ptr(), out.stride(0), buf,
+                                                    _lib.MP_REDUCE[reduce], 0, out.data_ptr(), out.stride(0), buf,
                                                     512, torch.cuda.current_stream().cuda_stream), "kernel_name")
             names.append(buf.value.decode())
         assert names[0] != names[1] and "k_agg_flat" in names[1] and ", 1, 16, 64" in names[1], names
@@ -2003,48 +2003,3 @@ def test_fuzz_fused_aggregation_vs_serial_loop(N, deg, F, reduce, weighted, chun
             terms = terms / torch.bincount(ei[1], minlength=N).clamp(min=1).view(-1, 1).float()
         _bound_ok(out.cpu(), want, terms)
 
-
-def test_cold_sources_hint_dispatch_bitwise_equal():
-    """MP_FLAG_COLD_SOURCES (6 rows in flight in the far-x scalar-batch sum
-    kernel) is a dispatch hint only: sum and mean bitwise equal to the default
-    kernel over an x beyond the Infinity Cache; ops.hint_flags sets it for a
-    uniform graph (low hot-source share) and not for a hub-heavy one; the
-    kernel query reports the U=6 instance."""
-    _, ops, _, Graph, pl = _mods()
-    from mi355_mp import _lib
-    N, F = 300_000, 256                      # x = 307 MB > 256 MiB: the far-x kernel
-    g = torch.Generator(device=DEV).manual_seed(5)
-    E = 2_000_000
-    ei_u = torch.randint(0, N, (2, E), device=DEV, generator=g)
-    ei_h = pl(N, E, seed=5).to(DEV)
-    x = torch.randn(N, F, device=DEV, generator=g)
-    w = torch.rand(E, device=DEV, generator=g)
-    gu, gh = Graph(ei_u, N, N), Graph(ei_h, N, N)
-    assert gu.dst.hot_share() < gu.dst.COLD_BELOW <= gh.dst.hot_share()
-    assert ops.hint_flags(gu.dst, "other", x, "sum") & _lib.MP_FLAG_COLD_SOURCES
-    assert not ops.hint_flags(gh.dst, "other", x, "sum") & _lib.MP_FLAG_COLD_SOURCES
-    assert ops.hint_flags(gu.dst, "other", x[:1000], "sum") == 0      # x in the Infinity Cache
-    assert ops.hint_flags(gu.dst, "other", x, "max") == 0
-    wc = gu.dst.to_csr_order(w)
-    bias = torch.randn(F, device=DEV, generator=g)
-    names = []
-    for fl in (0, _lib.MP_FLAG_COLD_SOURCES):
-        names.append(_lib.kernel_name(gu.dst.struct("other"), wc.data_ptr(), x.data_ptr(), x.stride(0), F, "sum",
-                                      bias.data_ptr(), x.data_ptr(), F, flags=fl))
-    assert ", 1, 8, 64, false, true>" in names[0] and ", 1, 6, 64, false, true>" in names[1], names
-    for red in ("sum", "mean"):
-        lib = _lib.load()
-        st = gu.dst.struct("other")
-        outs = []
-        for fl in (0, _lib.MP_FLAG_COLD_SOURCES):
-            out = torch.empty(N, F, device=DEV)
-            sb = lib.mp_aggregate_slab_bytes(st, F, _lib.MP_REDUCE[red])
-            slab = torch.empty(sb, dtype=torch.uint8, device=DEV)
-            _lib.check(lib.mp_aggregate_f32(st, wc.data_ptr(), x.data_ptr(), F, F, _lib.MP_REDUCE[red], fl,
-                                            bias.data_ptr(), out.data_ptr(), F, None, slab.data_ptr(), sb,
-                                            _lib.MP_STAGE_ALL, _lib.stream_ptr()), "mp_aggregate_f32")
-            outs.append(out)
-        assert torch.equal(outs[0], outs[1]), red
-        # and the hinted path through ops equals the oracle-checked default path
-        got = ops._aggregate(gu.dst, "other", x, wc, red, 0, bias)[0]
-        assert torch.equal(got, outs[0]), red

@@ -42,7 +42,7 @@ def test_ctypes_signatures_cover_the_header():
 
 
 def test_abi_version_and_error_string(lib):
-    assert lib.mp_abi_version() == 3
+    assert lib.mp_abi_version() == 2
     assert isinstance(lib.mp_last_error(), bytes)
 
 
@@ -87,7 +87,7 @@ def test_column_array_requires_n_cols(lib):
     rc = lib.mp_aggregate_f32(g, None, fake, 4, 4, 0, 0, None, fake, 4, None, fake, 1 << 20, 3, None)
     assert rc == 1 and b"n_cols" in lib.mp_last_error()
     buf = __import__("ctypes").create_string_buffer(256)
-    rc = lib.mp_aggregate_kernel_name(g, None, fake, 4, 4, 0, 0, None, fake, 4, buf, 256, None)
+    rc = lib.mp_aggregate_kernel_name(g, None, fake, 4, 4, 0, None, fake, 4, buf, 256, None)
     assert rc == 1 and b"n_cols" in lib.mp_last_error()
     # identity gather (col = NULL) needs no n_cols
     g2 = _lib.MpCsr(fake, None, fake, fake, fake, None, 10, 40, 256, 1, 0, 0, 0)
@@ -246,33 +246,3 @@ def test_torch_scatter_dispatcher_ops_registered():
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         torch.ops.torch_scatter.segment_sum_csr(torch.ones(3, 2), torch.tensor([0, 2, 3]), None)
 
-
-def test_cold_sources_hint_host_logic():
-    """ops.hint_flags (the MP_FLAG_COLD_SOURCES dispatch hint) on a stand-in
-    CSR: only sum/mean over the 'other' gather of an x beyond 256 MiB with a
-    hot-source share under CSR.COLD_BELOW; a share of None (stream capture)
-    leaves the flags alone; other flag bits are kept."""
-    from mi355_mp import _lib, ops
-    from mi355_mp.graph import CSR
-
-    class Fake:
-        COLD_BELOW = CSR.COLD_BELOW
-
-        def __init__(self, share, n_edges=10):
-            self.share, self.n_edges = share, n_edges
-
-        def hot_share(self):
-            return self.share
-
-    big = torch.empty((300_000, 256), device="meta")      # 307 MB
-    small = torch.empty((1000, 256), device="meta")
-    cold = _lib.MP_FLAG_COLD_SOURCES
-    assert ops.hint_flags(Fake(0.2), "other", big, "sum") == cold
-    assert ops.hint_flags(Fake(0.2), "other", big, "mean", _lib.MP_FLAG_INIT_FROM_OUT) == \
-        cold | _lib.MP_FLAG_INIT_FROM_OUT
-    assert ops.hint_flags(Fake(0.5), "other", big, "sum") == 0
-    assert ops.hint_flags(Fake(None), "other", big, "sum") == 0
-    assert ops.hint_flags(Fake(0.2), "other", small, "sum") == 0
-    assert ops.hint_flags(Fake(0.2), "other", big, "max") == 0
-    assert ops.hint_flags(Fake(0.2), "eid", big, "sum") == 0
-    assert ops.hint_flags(Fake(0.2, n_edges=0), "other", big, "sum") == 0

@@ -116,7 +116,7 @@ def main():
         with_keys(libs[name], keys, lambda: launch(name, keys, _lib.MP_STAGE_ALL))
         buf = __import__("ctypes").create_string_buffer(1024)
         with_keys(libs[name], keys, lambda: libs[name].mp_aggregate_kernel_name(
-            g, _lib.ptr(w), x.data_ptr(), x.stride(0), args.F, red, 0, bias.data_ptr(), outs[name].data_ptr(),
+            g, _lib.ptr(w), x.data_ptr(), x.stride(0), args.F, red, bias.data_ptr(), outs[name].data_ptr(),
             outs[name].stride(0), buf, 1024, st))
         kernel[name] = buf.value.decode()
     torch.cuda.synchronize()
