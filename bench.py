@@ -41,7 +41,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md chip table)
 # Cache, so it can exceed 1).
 BYTES_PER_EDGE = 4 * F_DIM + 4 + 4   # x_j row + col + norm
 BYTES_PER_NODE = 4 * F_DIM + 4       # out row + rowptr
-PMC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r03_pmc_traffic.json")
 
 
 def parse():
@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ref-paths", action="store_true",
+                    help="skip timing the reference's ATen device path and the vendor SpMM")
     ap.add_argument("--cpu-sample-edges", type=int, default=48_000_000)
     ap.add_argument("--chunk", type=int, default=0, help="merge-path task size (0: auto_chunk)")
     ap.add_argument("--no-overlap", action="store_true", help="N>1: exchange, then aggregate (no overlap)")
@@ -136,6 +138,94 @@ def cpu_baseline(ei_loops, norm, x, sample_edges):
             "sample": "first %d of the %d edges (original order), F=%d, torch CPU index_select+mul+"
                       "scatter_add_ in 4M-edge chunks, %d threads (the CPUs this job may use; the machine "
                       "has %d), %.1f s" % (E, ei_loops.shape[1], N and F_DIM, threads, machine, dt)}
+
+
+def _ev_ms(fn, reps):
+    """Average ms of fn() over `reps` runs, HIP events on the current stream
+    (one warm-up run first)."""
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def device_reference_paths(ei, norm, x, csr, w_csr, bias, fused_out, terms, reps=3):
+    """The same GCNConv propagate + bias on the same MI355X by two other routes,
+    timed beside the fused kernel and checked against its output:
+
+      reference_path: what the reference runs on a GPU (examples/gcn.py:31-32
+        moves the model and data to CUDA): PyG 1.4.3 __collect__'s
+        x.index_select(0, edge_index[0]) -> GCNConv.message norm.view(-1, 1) * x_j
+        -> torch_scatter 2.0.4 scatter_sum = zeros.scatter_add_(0, broadcast
+        index, msg) (ATen atomics) -> update + bias.  The [E', 256] x_j and
+        message tensors are materialised at full size (63.6 GB each).
+      vendor_spmm: torch.sparse_csr_tensor(rowptr, col, norm) @ x on the same
+        CSR and weights (rocSPARSE / hipSPARSE SpMM) + bias.
+
+    Each output is compared with the fused kernel's: within
+    1e-5 * max(1, sum_e |w_e x_j|) (terms), plus the bitwise-equal fraction."""
+    res = {}
+    N, F = x.shape
+    E = ei.shape[1]
+
+    def check(out):
+        d = (out - fused_out).abs()
+        excess = float((d - 1e-5 * terms.clamp(min=1.0)).max())
+        return {"max_abs_diff": float(d.max()), "bound_excess": excess, "within_1e-5_bound": excess <= 0,
+                "bitwise_equal_frac": float((out == fused_out).float().mean())}
+    try:
+        idx = ei[1].view(-1, 1).expand(E, F)
+        bufs = {}
+
+        # (each piece frees its previous output first: x_j and msg are 63.6 GB apiece)
+        def gather():
+            bufs.pop("x_j", None)
+            bufs["x_j"] = x.index_select(0, ei[0])
+
+        def message():
+            bufs.pop("msg", None)
+            bufs["msg"] = norm.view(-1, 1) * bufs["x_j"]
+
+        def scatter():
+            bufs.pop("out", None)
+            bufs["out"] = torch.zeros(N, F, device=x.device).scatter_add_(0, idx, bufs["msg"]) + bias
+
+        def whole():
+            bufs.clear()
+            gather()
+            message()
+            scatter()
+        ms = _ev_ms(whole, reps)
+        piece = {"index_select_ms": _ev_ms(gather, reps), "mul_ms": _ev_ms(message, reps),
+                 "scatter_add_plus_bias_ms": _ev_ms(scatter, reps)}
+        res["reference_path"] = dict(ms=ms, **piece, **check(bufs["out"]),
+                                     desc="ATen index_select -> norm*x_j -> zeros.scatter_add_ -> +bias, fp32, "
+                                          "full size (x_j and msg materialised)")
+        bufs.clear()
+        del idx
+    except RuntimeError as exc:   # e.g. out of memory on a smaller part
+        res["reference_path"] = {"error": str(exc)[:200]}
+    torch.cuda.empty_cache()
+    try:
+        A = torch.sparse_csr_tensor(csr.rowptr, csr.col[:csr.n_edges], w_csr[:csr.n_edges], size=(N, N))
+        box = {}
+
+        def spmm():
+            box["out"] = torch.mm(A, x) + bias
+        ms = _ev_ms(spmm, reps)
+        res["vendor_spmm"] = dict(ms=ms, **check(box["out"]),
+                                  desc="torch.sparse_csr_tensor(rowptr, col, norm; int32 indices) @ x "
+                                       "(rocSPARSE/hipSPARSE SpMM) + bias")
+        del A, box
+    except RuntimeError as exc:
+        res["vendor_spmm"] = {"error": str(exc)[:200]}
+    torch.cuda.empty_cache()
+    return res
 
 
 def main():
@@ -308,7 +398,7 @@ def main():
     # dispatched kernel, from the committed profile summary -- used only when the
     # summary names the same kernel and the same native source hash
     traffic, traffic_src = None, "no profile for this build"
-    src_hash = _lib.source_hash()
+    src_hash = lib.mp_source_hash().decode()   # the LOADED library's build (load() checks it against the tree)
     if os.path.exists(PMC_FILE) and world == 1:
         try:
             with open(PMC_FILE) as f:
@@ -321,6 +411,18 @@ def main():
                 traffic_src = "%s is for another build (kernel/source hash differ)" % os.path.relpath(PMC_FILE, ROOT)
         except (OSError, ValueError):
             traffic = None
+
+    # the reference's own device path and a vendor SpMM on the same GPU, same
+    # CSR / weights (outside the timed region; checked against the fused output)
+    ref_paths = None
+    if world == 1 and not args.no_ref_paths:
+        aggregate(x, out=out_buf)
+        fused_out = out_buf.clone()
+        terms = ops._aggregate(csr, "other", x.abs(), w_csr.abs(), "sum", 0, None)[0]
+        ref_paths = device_reference_paths(ei2, norm, x, csr, w_csr, bias, fused_out, terms)
+        ref_paths["fused_ms"] = main_avg + fix_avg
+        del fused_out, terms
+        torch.cuda.empty_cache()
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -366,6 +468,9 @@ def main():
                       "overlap": world > 1 and not args.no_overlap,
                       "halo_tile": args.halo_tile if world > 1 and not args.no_overlap else None,
                       "n_wave_tasks": csr.n_waves,
+                      "gpu_reference_path_ms": ((ref_paths or {}).get("reference_path") or {}).get("ms"),
+                      "hipsparse_spmm_ms": ((ref_paths or {}).get("vendor_spmm") or {}).get("ms"),
+                      "same_gpu_paths": ref_paths,
                       "agg_only_GBps_incl_fixup": alg_bytes / ((main_avg + fix_avg) * 1e-3) / 1e9},
         }
         print(json.dumps(line))

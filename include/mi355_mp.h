@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MP_ABI_VERSION 2
+#define MP_ABI_VERSION 3
 
 /* status codes */
 #define MP_OK 0
@@ -97,6 +97,11 @@ typedef struct mp_csr {
 
 const char* mp_last_error(void);
 int mp_abi_version(void);
+/* First 16 hex digits of the sha256 of the native sources this library was
+ * compiled from (csrc/Makefile computes it; mi355_mp._lib.source_hash() is the
+ * same scheme over the tree).  The Python loader refuses a library whose hash
+ * differs from the sources beside it: a stale prebuilt .so never runs.  (ABI 3) */
+const char* mp_source_hash(void);
 
 /* Process-wide dispatch table (tests and in-process A/B runs).  Sets `key`
  * to `value` and returns the previous value; value < 0 only queries.
@@ -377,8 +382,13 @@ int mp_gat_alpha_f32(const int64_t* src_idx, const int64_t* dst_idx,
 #define MP_LOOPS_REMOVE 0
 #define MP_LOOPS_ADD 1
 #define MP_LOOPS_ADD_REMAINING 2
+/* count_dev: device int64[2]; [0] = number of self loops, [1] = self loops (r, r)
+ * with r outside [0, n_nodes) -- upstream's `loop_weight[row[inv_mask]]` raises
+ * an IndexError for those, and the caller must reject them before
+ * mp_self_loops (whose loop bookkeeping ignores them).  (ABI 3: n_nodes and the
+ * second counter.) */
 int mp_self_loop_count(const int64_t* row, const int64_t* col, int64_t n_edges,
-                       int64_t* count_dev, void* stream);
+                       int64_t n_nodes, int64_t* count_dev, void* stream);
 size_t mp_self_loops_workspace(int64_t n_edges, int64_t n_nodes);
 int mp_self_loops(const int64_t* row, const int64_t* col, int64_t n_edges, int64_t n_nodes,
                   int32_t mode, int64_t n_kept, int64_t* out_row, int64_t* out_col,
@@ -423,9 +433,57 @@ int mp_gather_rows_f32(const float* x, int64_t ldx, const int64_t* idx,
 int mp_permute_f32(const float* src, const int32_t* perm, int64_t n,
                    float* dst, void* stream);
 
+/* ---- deterministic source-side reductions (csrc/mp_segment.hip) ----------- */
+
+/* out[r] = ((0 + v[id(k0)]) + v[id(k0+1)]) + ... over the slots k of row r in
+ * slot order, id(k) = eid[k] (eid NULL: k).  Bit-identical to the serial CPU
+ * loop.  Over the transposed CSR (rows = edge_index[0]) with v = the edge
+ * weights in original order it is GCNConv.norm's deg = scatter_add(w, row) [U5]
+ * in the reference's edge order (replaces the float atomics of mp_gcn_norm_f32
+ * for real-valued weights). */
+int mp_segment_sum_serial_f32(const int32_t* rowptr, const int32_t* eid, const float* v,
+                              int64_t n_rows, float* out, void* stream);
+
+/* GCNConv.norm steps 2-3 from a given degree: deg is overwritten with
+ * deg^-1/2 (inf -> 0), norm[e] = dinv[row[e]] * w[e] * dinv[col[e]]. */
+int mp_gcn_norm_from_deg_f32(const int64_t* row, const int64_t* col, const float* w,
+                             int64_t n_edges, int64_t n_nodes, float* deg, float* norm,
+                             void* stream);
+
+/* inv[eid[k]] = k for every slot k of g (the slot of each edge id). */
+int mp_csr_inverse_eid(const mp_csr* g, int32_t* inv, void* stream);
+
+/* Deterministic ScatterMax/ScatterMin backward of a fused message w_e * x[src_e]
+ * ([U8] ScatterMax.backward, then the message's and index_select's backward:
+ * an index_add_ by source in edge order).  Three steps over the TRANSPOSED CSR
+ * gt (rows = source nodes, slots = out-edges in original order, col = the
+ * destination row, eid = the edge id):
+ *   1. mp_arg_winner_mask: mask [gt.n_edges, mp_arg_mask_words(F)] uint32 in gt
+ *      slot order, bit f of slot inv[e] set when arg[r, f] = e (inv =
+ *      mp_csr_inverse_eid(gt)); ids outside [0, n_edges) (empty rows) set nothing.
+ *   2. mp_scatter_arg_backward_csr_f32: grad[j, f] = sum over the slots of row j
+ *      in order of w_e * grad_out[dst, f] where the slot won (j, f) -- the
+ *      reference's edge-order sum, bit for bit; every row of grad is written.
+ *      w: per-edge weights in ORIGINAL edge order, or NULL (= 1).
+ *   3. (optional) mp_scatter_arg_grad_w_f32: grad_w[e] = sum over the features
+ *      e won of grad_out[dst_map[e], f] * x[src_map[e], f] (fixed reduction tree),
+ *      0 for edges that won nothing; every entry written.
+ * The mask must be 8-byte aligned. */
+int32_t mp_arg_mask_words(int32_t F);
+int mp_arg_winner_mask(const int64_t* arg, int64_t n_rows, int32_t F, int64_t n_edges,
+                       const int32_t* inv, uint32_t* mask, void* stream);
+int mp_scatter_arg_backward_csr_f32(const mp_csr* gt, const uint32_t* mask,
+                                    const float* grad_out, int64_t ldg, int32_t F,
+                                    const float* w, float* grad, int64_t ldgx, void* stream);
+int mp_scatter_arg_grad_w_f32(const int64_t* src_map, const int64_t* dst_map, int64_t n_edges,
+                              const int32_t* inv, const uint32_t* mask, int32_t F,
+                              const float* grad_out, int64_t ldg, const float* x, int64_t ldx,
+                              float* grad_w, void* stream);
+
 /* ScatterMax/ScatterMin backward [U8]: for every (r,f) with arg[r,f] = e != n_edges
  *   src_map == NULL: grad[e, f]            = grad_out[r,f]          (plain store)
- *   src_map != NULL: grad[src_map[e], f]  += grad_out[r,f] * w[e]   (atomic; w NULL = 1)
+ *   src_map != NULL: grad[src_map[e], f]  += grad_out[r,f] * w[e]   (atomic; w NULL = 1 --
+ *                    NOT deterministic; the Python layer uses the CSR form above)
  *   grad_w != NULL:  grad_w[e]            += grad_out[r,f] * x[src_map[e], f]
  * (the message of a weighted max/min aggregation is w[e] * x[src_map[e]];
  * grad_w is d w).  grad / grad_w must be zero-initialised by the caller; either
@@ -438,7 +496,10 @@ int mp_scatter_arg_backward_f32(const float* grad_out, const int64_t* arg,
 
 /* GCNConv.norm [U5]: deg = scatter_add(w, row); dinv = deg^-1/2 (inf -> 0);
  * norm[e] = dinv[row[e]] * w[e] * dinv[col[e]] (original edge order).
- * w == NULL means all ones.  deg_ws: n_nodes floats of workspace. */
+ * w == NULL means all ones.  deg_ws: n_nodes floats of workspace.  The degree
+ * is summed with float atomics: exact (hence deterministic) only for
+ * integer-valued weights (self-loop fills 1 / 2, unweighted graphs); for real
+ * weights use mp_segment_sum_serial_f32 + mp_gcn_norm_from_deg_f32. */
 int mp_gcn_norm_f32(const int64_t* row, const int64_t* col, const float* w,
                     int64_t n_edges, int64_t n_nodes, float* deg_ws,
                     float* norm, void* stream);

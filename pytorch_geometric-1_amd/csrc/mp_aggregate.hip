@@ -2147,6 +2147,10 @@ static int gat_backward(const mp_csr* gt, const float* grad_out, int64_t ldg, co
 int mp_gat_backward_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, const float* xw, const float* a_src,
                         const float* pack, const float* att, int32_t H, int32_t C, float slope, float* grad_xw,
                         float* grad_a_src, float* de, void* slab, size_t slab_bytes, int32_t stages, void* stream) {
+  // without the training forward's node-wise d a_dst the per-edge d score is the
+  // only way d a_dst comes out: it is required (mp_gat_backward_train_f32 otherwise)
+  MP_CHECK_ARG(de != nullptr || !gt || gt->n_edges == 0,
+               "mp_gat_backward_f32: de is required (use mp_gat_backward_train_f32 after the training forward)");
   return gat_backward(gt, grad_out, ldg, xw, a_src, pack, att, H, C, slope, grad_xw, grad_a_src, de, nullptr, slab,
                       slab_bytes, stages, stream);
 }

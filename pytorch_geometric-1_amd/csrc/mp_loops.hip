@@ -17,22 +17,29 @@
 
 namespace mp {
 
+// count[0] = self loops; count[1] = self loops (r, r) with r outside [0, n_nodes)
+// (upstream's `loop_weight[row[inv_mask]]` raises an IndexError for those)
 __global__ void k_loop_count(const int64_t* __restrict__ row, const int64_t* __restrict__ col, int64_t n,
-                             unsigned long long* __restrict__ count) {
+                             int64_t n_nodes, unsigned long long* __restrict__ count) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool loop = e < n && row[e] == col[e];
+  const int64_t r = e < n ? row[e] : 0;
+  const bool loop = e < n && r == col[e];
   const unsigned long long m = __ballot(loop);
+  const unsigned long long bad = __ballot(loop && (r < 0 || r >= n_nodes));
   if (lane_id() == 0 && m) atomicAdd(count, (unsigned long long)__popcll(m));
+  if (lane_id() == 0 && bad) atomicAdd(count + 1, (unsigned long long)__popcll(bad));
 }
 
 __global__ void k_loop_flags(const int64_t* __restrict__ row, const int64_t* __restrict__ col, int64_t n,
-                             uint8_t* __restrict__ keep, int32_t* __restrict__ last) {
+                             int64_t n_nodes, uint8_t* __restrict__ keep, int32_t* __restrict__ last) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   const int64_t r = row[e];
   const bool loop = r == col[e];
   keep[e] = loop ? 0 : 1;
-  if (loop && last) atomicMax(last + r, (int32_t)e);
+  // the range guard keeps a bad index from writing outside `last`; the caller has
+  // already rejected it through mp_self_loop_count's out-of-range count
+  if (loop && last && r >= 0 && r < n_nodes) atomicMax(last + r, (int32_t)e);
 }
 
 // out[k] = edge pos[k] for k < n_kept (pos == nullptr: identity), then the
@@ -76,15 +83,17 @@ using namespace mp;
 
 extern "C" {
 
-int mp_self_loop_count(const int64_t* row, const int64_t* col, int64_t n_edges, int64_t* count_dev,
+int mp_self_loop_count(const int64_t* row, const int64_t* col, int64_t n_edges, int64_t n_nodes, int64_t* count_dev,
                        void* stream) {
   MP_DEVICE_GUARD(stream);
-  MP_CHECK_ARG(n_edges >= 0 && count_dev && (n_edges == 0 || (row && col)), "mp_self_loop_count: bad arguments");
+  MP_CHECK_ARG(n_edges >= 0 && n_nodes >= 0 && count_dev && (n_edges == 0 || (row && col)),
+               "mp_self_loop_count: bad arguments");
   hipStream_t s = as_stream(stream);
-  MP_CHECK_HIP(hipMemsetAsync(count_dev, 0, sizeof(int64_t), s));
+  MP_CHECK_HIP(hipMemsetAsync(count_dev, 0, 2 * sizeof(int64_t), s));
   if (n_edges == 0) return MP_OK;
   const int B = 256;
-  k_loop_count<<<ceil_div(n_edges, B), B, 0, s>>>(row, col, n_edges, reinterpret_cast<unsigned long long*>(count_dev));
+  k_loop_count<<<ceil_div(n_edges, B), B, 0, s>>>(row, col, n_edges, n_nodes,
+                                                  reinterpret_cast<unsigned long long*>(count_dev));
   MP_CHECK_LAUNCH();
   return MP_OK;
 }
@@ -126,7 +135,7 @@ int mp_self_loops(const int64_t* row, const int64_t* col, int64_t n_edges, int64
   const bool identity = mode == MP_LOOPS_ADD || n_kept == n_edges;
   if (remaining && n_nodes > 0) MP_CHECK_HIP(hipMemsetAsync(last, 0xff, (size_t)n_nodes * 4, s));  // -1
   if (n_edges > 0 && (remaining || !identity)) {
-    k_loop_flags<<<ceil_div(n_edges, B), B, 0, s>>>(row, col, n_edges, keep, remaining ? last : nullptr);
+    k_loop_flags<<<ceil_div(n_edges, B), B, 0, s>>>(row, col, n_edges, n_nodes, keep, remaining ? last : nullptr);
     MP_CHECK_LAUNCH();
   }
   if (!identity) {

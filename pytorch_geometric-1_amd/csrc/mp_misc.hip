@@ -221,6 +221,23 @@ int mp_gcn_norm_f32(const int64_t* row, const int64_t* col, const float* w, int6
   return MP_OK;
 }
 
+int mp_gcn_norm_from_deg_f32(const int64_t* row, const int64_t* col, const float* w, int64_t n_edges,
+                             int64_t n_nodes, float* deg, float* norm, void* stream) {
+  MP_DEVICE_GUARD(stream);
+  MP_CHECK_ARG(n_edges >= 0 && n_nodes >= 0, "mp_gcn_norm_from_deg_f32: negative size");
+  MP_CHECK_ARG((n_nodes == 0 || deg) && (n_edges == 0 || (row && col && norm)), "mp_gcn_norm_from_deg_f32: null pointer");
+  hipStream_t s = as_stream(stream);
+  if (n_nodes > 0) {
+    k_gcn_dinv<<<(unsigned)ceil_div(n_nodes, 256), 256, 0, s>>>(deg, n_nodes);
+    MP_CHECK_LAUNCH();
+  }
+  if (n_edges > 0) {
+    k_gcn_norm<<<(unsigned)ceil_div(n_edges, 256), 256, 0, s>>>(row, col, w, n_edges, deg, norm);
+    MP_CHECK_LAUNCH();
+  }
+  return MP_OK;
+}
+
 int mp_gat_node_scores_f32(const float* xw, int64_t n_nodes, int32_t H, int32_t C, const float* att,
                            float* a_src, float* a_dst, void* stream) {
   MP_DEVICE_GUARD(stream);

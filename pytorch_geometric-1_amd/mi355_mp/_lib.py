@@ -11,7 +11,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("MI355_MP_LIB", os.path.join(_HERE, "libmi355_mp.so"))
+DEFAULT_LIB_PATH = os.path.join(_HERE, "libmi355_mp.so")
+LIB_PATH = os.environ.get("MI355_MP_LIB", DEFAULT_LIB_PATH)
 
 MP_OK = 0
 MP_REDUCE = {"sum": 0, "add": 0, "mean": 1, "max": 2, "min": 3}
@@ -54,6 +55,7 @@ class MpCsr(ctypes.Structure):
 SIGNATURES = {
     "mp_last_error": (ctypes.c_char_p, []),
     "mp_abi_version": (ctypes.c_int, []),
+    "mp_source_hash": (ctypes.c_char_p, []),
     "mp_tune": (i64, [i32, i64]),
     "mp_csr_build_workspace": (sz, [i64, i64]),
     "mp_csr_build": (ctypes.c_int, [c_p, c_p, i64, i64, i64, c_p, c_p, c_p, c_p, c_p, sz, c_p]),
@@ -99,7 +101,7 @@ SIGNATURES = {
     "mp_gather_rows_f32": (ctypes.c_int, [c_p, i64, c_p, i64, i32, c_p, i64, c_p]),
     "mp_permute_f32": (ctypes.c_int, [c_p, c_p, i64, c_p, c_p]),
     "mp_scatter_arg_backward_f32": (ctypes.c_int, [c_p, c_p, i64, i32, i64, c_p, c_p, c_p, i64, c_p, i64, c_p, c_p]),
-    "mp_self_loop_count": (ctypes.c_int, [c_p, c_p, i64, c_p, c_p]),
+    "mp_self_loop_count": (ctypes.c_int, [c_p, c_p, i64, i64, c_p, c_p]),
     "mp_self_loops_workspace": (sz, [i64, i64]),
     "mp_self_loops": (ctypes.c_int, [c_p, c_p, i64, i64, i32, i64, c_p, c_p, c_p, c_p, sz, c_p]),
     "mp_gather_fill_f32": (ctypes.c_int, [c_p, c_p, i64, f32, c_p, c_p]),
@@ -107,6 +109,13 @@ SIGNATURES = {
     "mp_shard_plan": (ctypes.c_int, [c_p, c_p, i64, i64, c_p, i32, i32, i64, i64, c_p, c_p, c_p, c_p, c_p, c_p, sz,
                                      c_p]),
     "mp_gcn_norm_f32": (ctypes.c_int, [c_p, c_p, c_p, i64, i64, c_p, c_p, c_p]),
+    "mp_gcn_norm_from_deg_f32": (ctypes.c_int, [c_p, c_p, c_p, i64, i64, c_p, c_p, c_p]),
+    "mp_segment_sum_serial_f32": (ctypes.c_int, [c_p, c_p, c_p, i64, c_p, c_p]),
+    "mp_csr_inverse_eid": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p]),
+    "mp_arg_mask_words": (i32, [i32]),
+    "mp_arg_winner_mask": (ctypes.c_int, [c_p, i64, i32, i64, c_p, c_p, c_p]),
+    "mp_scatter_arg_backward_csr_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, i64, i32, c_p, c_p, i64, c_p]),
+    "mp_scatter_arg_grad_w_f32": (ctypes.c_int, [c_p, c_p, i64, c_p, c_p, i32, c_p, i64, c_p, i64, c_p, c_p]),
 }
 
 _lib = None
@@ -116,8 +125,14 @@ class NativeLibraryMissing(RuntimeError):
     pass
 
 
+class NativeLibraryStale(RuntimeError):
+    pass
+
+
 def load(path=None):
-    """Load (once) and return the native library; raise if it is absent."""
+    """Load (once) and return the native library; raise if it is absent, or
+    (the in-tree library) if it was built from other sources than the ones
+    beside it -- the library carries its source hash (mp_source_hash)."""
     global _lib
     if _lib is not None and path is None:
         return _lib
@@ -127,6 +142,13 @@ def load(path=None):
             "mi355_mp: native library %s not found; build it with "
             "`python -c 'import __graft_entry__ as g; g.build()'` "
             "(there is no CPU fallback)" % p)
+    if path is None and os.path.abspath(p) == os.path.abspath(DEFAULT_LIB_PATH):
+        built = library_hash(p)
+        want = source_hash()
+        if built != want:
+            raise NativeLibraryStale(
+                "mi355_mp: %s was built from sources %s, the tree holds %s; rebuild it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'`" % (p, built, want))
     # RTLD_LOCAL: every build keeps its own kernels.  With RTLD_GLOBAL a second build
     # loaded into the process (an A/B variant) binds its template kernel stubs to the
     # first build's same-named definitions and silently runs the first build's code.
@@ -140,14 +162,29 @@ def load(path=None):
     return lib
 
 
+def library_hash(path=None):
+    """The source hash compiled into a library file (mp_source_hash); needs no
+    GPU.  'unknown' for a library built without it."""
+    lib = ctypes.CDLL(path or LIB_PATH, mode=ctypes.RTLD_LOCAL)
+    try:
+        fn = lib.mp_source_hash
+    except AttributeError:
+        return "unknown"
+    fn.restype = ctypes.c_char_p
+    fn.argtypes = []
+    return fn().decode()
+
+
 def source_hash():
     """sha256 over the native sources the library is built from (csrc/*.hip,
-    csrc/*.h, csrc/Makefile, include/mi355_mp.h).  Profile summaries record it,
-    so a committed counter profile is only used for the build it measured."""
+    csrc/*.h, csrc/*.cpp, csrc/Makefile, include/mi355_mp.h); the Makefile
+    compiles the same hash into the library.  Profile summaries record it, so a
+    committed counter profile is only used for the build it measured."""
     import glob
     import hashlib
     csrc = os.path.join(os.path.dirname(_HERE), "csrc")
-    files = sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.h")))
+    files = sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.h"))
+                   + glob.glob(os.path.join(csrc, "*.cpp")))
     files += [os.path.join(csrc, "Makefile"),
               os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "mi355_mp.h")]
     h = hashlib.sha256()

@@ -16,9 +16,10 @@ examples/data_parallel.py:35-49).  One large graph is sharded here instead:
     on its own link), then the local fused aggregation runs on
     [own rows ; halo rows].
 
-The plan logic is host/torch code (tested with gloo on CPU); the data path
-calls the native kernels through `local_aggregate`, which tests replace with
-the CPU oracle.
+The plan is built natively on the device (mp_shard_plan: flag + scan, no
+sort); host tensors take its torch-op form (_plan_torch), which the gloo tests
+run on CPU.  The data path calls the native kernels (sharded_propagate takes
+the local aggregation as a callable, so the CPU tests can pass a host one).
 """
 import torch
 import torch.distributed as dist
@@ -207,6 +208,9 @@ def sharded_propagate(plan, x_own, local_aggregate, gather_rows, edge_weight=Non
     res = local_aggregate(x_local, plan.local_edge_index, plan.n_own, plan.n_local_src, w)
     if isinstance(res, tuple):
         out, arg = res
+        if n_edges_global is None:
+            raise ValueError("sharded_propagate: a max/min aggregation needs n_edges_global "
+                             "(the global edge count, the empty-row argmax sentinel)")
         return out, plan.global_edge_ids(arg, n_edges_global)
     return res
 
@@ -400,28 +404,28 @@ class _ShardedAggregate(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad_out, _grad_arg=None):
-        from . import _lib, ops
+        from . import ops
         sg, reduce = ctx.sg, ctx.reduce
         g = grad_out.contiguous()
         F = g.shape[1]
         if reduce in ("max", "min"):
             # gradient lands on the argmax edge's source, which may live in the halo:
             # accumulate per local column, then return the halo rows to their owners
+            # (deterministic: the local transposed CSR adds each column's winning
+            # terms in local = global edge order; the rows returned by several
+            # peers are summed by a segmented sum keyed on send_idx, in peer order)
             (arg,) = ctx.saved_tensors
             plan = sg.fwd
-            lib = _lib.load()
-            gl = torch.zeros((plan.n_local_src, F), dtype=torch.float32, device=g.device)
-            src_map = plan.local_edge_index[0].contiguous()
             w = sg._w[2] if sg._w is not None else None  # local edge order: the arg's positions
-            _lib.check(lib.mp_scatter_arg_backward_f32(g.data_ptr(), arg.data_ptr(), g.shape[0], F,
-                                                       int(plan.edge_pos.numel()), src_map.data_ptr(), _lib.ptr(w),
-                                                       None, 0, gl.data_ptr(), gl.stride(0), None,
-                                                       _lib.stream_ptr(g.device)), "mp_scatter_arg_backward_f32")
-            gx = gl[:plan.n_own].clone()
+            gl, _ = ops.arg_backward(sg.g_fwd, arg, g, plan.n_local_src, w)
+            gx = gl[:plan.n_own]
             back = plan.return_halo(gl[plan.n_own:], sg.group)
             if back.shape[0]:
-                gx.index_add_(0, plan.send_idx, back)
-            return gx, None, None
+                from .graph import csr_for_index
+                ret, _ = ops._aggregate(csr_for_index(plan.send_idx, plan.n_own), "eid", back.contiguous(), None,
+                                        "sum", 0, None)
+                gx = gx + ret
+            return gx.contiguous(), None, None
         if reduce == "mean":
             g = g / sg.g_fwd.dst.degree().clamp(min=1).to(torch.float32).view(-1, 1)
         plan = sg.bwd

@@ -217,6 +217,15 @@ class CSR:
             self._slot_rows = sr
         return self._slot_rows
 
+    def inverse_eid(self):
+        """int32 [E]: inv[e] = the slot of edge id e in this CSR (cached)."""
+        if getattr(self, "_inv", None) is None:
+            inv = torch.empty(max(self.n_edges, 1), dtype=torch.int32, device=self.device)
+            _lib.check(_lib.load().mp_csr_inverse_eid(self.struct("other"), inv.data_ptr(),
+                                                      _lib.stream_ptr(self.device)), "mp_csr_inverse_eid")
+            self._inv = inv
+        return self._inv
+
     def degree(self):
         """In-degree per row (int64), from rowptr."""
         if self._deg is None:

@@ -100,6 +100,44 @@ def col_sums(g):
     return g.sum(0)
 
 
+def arg_backward(graph, arg, g, n_src, edge_weight=None, x=None, want_gx=True, want_gw=False):
+    """ScatterMax / ScatterMin backward of the fused message w_e * x[src_e]
+    (torch_scatter 2.0.4 [U8]: grad_msg = zeros(E+1, F).scatter_(0, arg, g)[:E],
+    then the message's backward and index_select's backward, an index_add_ by
+    source in edge order), deterministic and in the reference's order: a winner
+    bit mask in the transposed CSR's slot order, then one pass over the
+    transposed CSR that adds each source row's winning terms slot by slot
+    (mp_scatter_arg_backward_csr_f32) -- no float atomics.  `arg` holds original
+    edge ids of graph.dst's edges (E = no edge).  Returns (gx or None, gw or None)."""
+    lib = _lib.load()
+    dev = g.device
+    st = _lib.stream_ptr(dev)
+    src = graph.src
+    E = src.n_edges
+    F = g.shape[1]
+    inv = src.inverse_eid()
+    W = int(lib.mp_arg_mask_words(F))
+    mask = torch.empty(max(E * W, 2), dtype=torch.int32, device=dev)
+    _lib.check(lib.mp_arg_winner_mask(arg.data_ptr(), g.shape[0], F, E, inv.data_ptr(), mask.data_ptr(), st),
+               "mp_arg_winner_mask")
+    w = edge_weight.to(torch.float32).contiguous() if edge_weight is not None else None
+    gx = gw = None
+    if want_gx:
+        gx = torch.empty((int(n_src), F), dtype=torch.float32, device=dev)
+        _lib.check(lib.mp_scatter_arg_backward_csr_f32(src.struct("other"), mask.data_ptr(), g.data_ptr(), g.stride(0),
+                                                       F, _lib.ptr(w), gx.data_ptr(), gx.stride(0), st),
+                   "mp_scatter_arg_backward_csr_f32")
+    if want_gw:
+        ei = graph._edge_index()
+        srcs = ei[graph.j].contiguous()
+        dsts = ei[graph.i].contiguous()
+        gw = torch.empty(max(E, 1), dtype=torch.float32, device=dev)[:E]
+        _lib.check(lib.mp_scatter_arg_grad_w_f32(srcs.data_ptr(), dsts.data_ptr(), E, inv.data_ptr(), mask.data_ptr(),
+                                                 F, g.data_ptr(), g.stride(0), x.data_ptr(), x.stride(0),
+                                                 gw.data_ptr(), st), "mp_scatter_arg_grad_w_f32")
+    return gx, gw
+
+
 # ---------------------------------------------------------------------------
 # fused gather -> weight -> reduce over a Graph (MessagePassing fast path)
 # ---------------------------------------------------------------------------
@@ -143,20 +181,7 @@ class _FusedPropagate(torch.autograd.Function):
                 # message = w_e * x[src_e] at the argmax edge e: d x[src_e] += w_e g,
                 # d w_e += <g, x[src_e]> over the features whose argmax is e
                 g = (grad_out * keep if keep is not None else grad_out).contiguous()
-                dev = x.device
-                if ctx.needs_input_grad[0]:
-                    gx = torch.zeros((ctx.n_src, x.shape[1]), dtype=torch.float32, device=dev)
-                if want_w:
-                    gw = torch.zeros(edge_weight.shape[0], dtype=torch.float32, device=dev)
-                w = edge_weight.to(torch.float32).contiguous() if edge_weight is not None else None
-                other = edge_index[graph.j].contiguous()
-                lib = _lib.load()
-                _lib.check(lib.mp_scatter_arg_backward_f32(g.data_ptr(), arg.data_ptr(), g.shape[0],
-                                                           g.shape[1], graph.dst.n_edges, other.data_ptr(),
-                                                           _lib.ptr(w), x.data_ptr(), x.stride(0), _lib.ptr(gx),
-                                                           gx.stride(0) if gx is not None else 0, _lib.ptr(gw),
-                                                           _lib.stream_ptr(dev)),
-                           "mp_scatter_arg_backward_f32")
+                gx, gw = arg_backward(graph, arg, g, ctx.n_src, edge_weight, x, ctx.needs_input_grad[0], want_w)
                 if gw is not None and gw.dtype != edge_weight.dtype:
                     gw = gw.to(edge_weight.dtype)
             return gx, gw, gb, None, None, None, None, None
@@ -312,10 +337,14 @@ def self_loops(edge_index, num_nodes, mode):
     m = _LOOP_MODES[mode]
     n_kept = E
     if m != _lib.MP_LOOPS_ADD and E:
-        cnt = torch.empty(1, dtype=torch.int64, device=dev)
-        _lib.check(lib.mp_self_loop_count(row.data_ptr(), col.data_ptr(), E, cnt.data_ptr(), st),
+        cnt = torch.empty(2, dtype=torch.int64, device=dev)
+        _lib.check(lib.mp_self_loop_count(row.data_ptr(), col.data_ptr(), E, N, cnt.data_ptr(), st),
                    "mp_self_loop_count")
-        n_kept = E - int(cnt.item())
+        n_loops, n_bad = cnt.tolist()
+        if n_bad and m == _lib.MP_LOOPS_ADD_REMAINING:
+            # upstream: loop_weight[row[inv_mask]] = ... raises for these
+            raise IndexError("mi355_mp: %d self loops name a node outside [0, %d)" % (n_bad, N))
+        n_kept = E - n_loops
     n_out = n_kept + (0 if m == _lib.MP_LOOPS_REMOVE else N)
     out = torch.empty((2, n_out), dtype=torch.int64, device=dev)
     pos = torch.empty(max(n_out, 1), dtype=torch.int64, device=dev)
@@ -361,22 +390,38 @@ def gather_fill(w, pos, fill):
 # GCN normalisation (GCNConv.norm [U5])
 # ---------------------------------------------------------------------------
 
-def gcn_norm_weights(edge_index, num_nodes, edge_weight=None):
+def gcn_norm_weights(edge_index, num_nodes, edge_weight=None, integer_weights=False):
     """norm[e] = deg^-1/2[row] * w[e] * deg^-1/2[col], deg = scatter_add(w, row).
 
     edge_index must already carry the self loops (add_remaining_self_loops).
+    integer_weights: the caller guarantees integer-valued weights (GCNConv's
+    structure-only norm: ones and the loop fill 1 / 2): the degree is then
+    exact in any order and mp_gcn_norm_f32 sums it with atomics.  Otherwise the
+    degree is the transposed CSR's serial segment sum
+    (mp_segment_sum_serial_f32): the reference's edge-order sum bit for bit,
+    deterministic; that CSR is the one the layer's backward uses anyway.
     """
     _lib.require_device(edge_index, edge_weight)
     lib = _lib.load()
     E = edge_index.shape[1]
+    N = int(num_nodes)
     dev = edge_index.device
+    st = _lib.stream_ptr(dev)
     row = edge_index[0].contiguous()
     col = edge_index[1].contiguous()
     w = edge_weight.to(torch.float32).contiguous() if edge_weight is not None else None
-    deg = torch.empty(max(int(num_nodes), 1), dtype=torch.float32, device=dev)
+    deg = torch.empty(max(N, 1), dtype=torch.float32, device=dev)
     norm = torch.empty(E, dtype=torch.float32, device=dev)
-    _lib.check(lib.mp_gcn_norm_f32(row.data_ptr(), col.data_ptr(), _lib.ptr(w), E, int(num_nodes),
-                                   deg.data_ptr(), norm.data_ptr(), _lib.stream_ptr(dev)), "mp_gcn_norm_f32")
+    if w is None or integer_weights or E == 0:
+        _lib.check(lib.mp_gcn_norm_f32(row.data_ptr(), col.data_ptr(), _lib.ptr(w), E, N,
+                                       deg.data_ptr(), norm.data_ptr(), st), "mp_gcn_norm_f32")
+        return norm
+    from .graph import graph_for
+    rows = graph_for(edge_index, N, N, "source_to_target").src   # CSR keyed on edge_index[0]
+    _lib.check(lib.mp_segment_sum_serial_f32(rows.rowptr.data_ptr(), rows.eid.data_ptr(), w.data_ptr(), N,
+                                             deg.data_ptr(), st), "mp_segment_sum_serial_f32")
+    _lib.check(lib.mp_gcn_norm_from_deg_f32(row.data_ptr(), col.data_ptr(), w.data_ptr(), E, N, deg.data_ptr(),
+                                            norm.data_ptr(), st), "mp_gcn_norm_from_deg_f32")
     return norm
 
 
@@ -541,7 +586,7 @@ def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope
     gs = src.struct("dst_slot")
     sb = lib.mp_gat_slab_bytes(gs, H, C)
     slab = torch.empty(sb, dtype=torch.uint8, device=dev)
-    fused_dst = ga_dst is not None and epi
+    fused_dst = ga_dst is not None
     if fused_dst:
         # the transposed pass also adds d a_dst (x) att_dst to each row's d xw
         _lib.check(lib.mp_gat_backward_train_f32(gs, g.data_ptr(), g.stride(0), xw.data_ptr(), a_src.data_ptr(),
@@ -569,8 +614,9 @@ def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope
             p = apart.sum(0).view(2, H, C)
             gatt = torch.cat([p[0], p[1]], dim=-1).view_as(att)
     else:
-        _lib.check(lib.mp_heads_outer_add_f32(gx.data_ptr(), gx.stride(0), ga_dst.data_ptr(), N, H, C,
-                                              att_c.data_ptr(), 2 * C, st), "mp_heads_outer_add_f32")
+        if not fused_dst:
+            _lib.check(lib.mp_heads_outer_add_f32(gx.data_ptr(), gx.stride(0), ga_dst.data_ptr(), N, H, C,
+                                                  att_c.data_ptr(), 2 * C, st), "mp_heads_outer_add_f32")
         if want_att:
             x3 = xw.view(N, H, C)
             gatt = torch.cat([torch.einsum("nh,nhc->hc", ga_dst, x3), torch.einsum("nh,nhc->hc", ga_src, x3)],

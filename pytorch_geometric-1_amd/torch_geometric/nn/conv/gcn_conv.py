@@ -72,7 +72,7 @@ class GCNConv(MessagePassing):
             def build():
                 ones = torch.ones((edge_index.size(1),), dtype=torch.float32, device=edge_index.device)
                 w = remaining_loops_weight(ones, pos, fill_value)
-                return _ops.gcn_norm_weights(ei, num_nodes, w)
+                return _ops.gcn_norm_weights(ei, num_nodes, w, integer_weights=True)
             norm = cached_value(edge_index, ("gcn_norm", int(num_nodes), fill_value), build)
             return ei, norm
         w = remaining_loops_weight(edge_weight, pos, fill_value)

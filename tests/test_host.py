@@ -42,8 +42,25 @@ def test_ctypes_signatures_cover_the_header():
 
 
 def test_abi_version_and_error_string(lib):
-    assert lib.mp_abi_version() == 2
+    assert lib.mp_abi_version() == 3
     assert isinstance(lib.mp_last_error(), bytes)
+
+
+def test_library_is_bound_to_its_sources(lib, monkeypatch):
+    """The library carries the hash of the sources it was compiled from
+    (Makefile -> mp_source_hash), equal to the tree's (_lib.source_hash: same
+    scheme); a library built from other sources is refused, whatever its
+    timestamp says."""
+    from mi355_mp import _lib
+    assert _lib.library_hash(_lib.DEFAULT_LIB_PATH) == _lib.source_hash()
+    assert lib.mp_source_hash().decode() == _lib.source_hash()
+    out = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "pytorch_geometric-1_amd", "csrc"), "hash"],
+                         capture_output=True, text=True, check=True).stdout.strip()
+    assert out == _lib.source_hash()
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "source_hash", lambda: "0123456789abcdef")
+    with pytest.raises(_lib.NativeLibraryStale, match="0123456789abcdef"):
+        _lib.load()
 
 
 def test_tuning_knob_set_query_restore(lib):
@@ -188,20 +205,35 @@ def test_graph_generators_deterministic_and_shaped():
     assert int(d["train_mask"].sum()) == 140
 
 
-def test_loop_utilities_have_no_cpu_fallback():
-    """utils.loop runs on the native engine (mp_self_loops); host tensors raise
-    instead of silently taking a CPU path (GPU parity: test_gpu_parity.py
-    test_self_loop_utilities_bit_exact)."""
+def test_loop_utilities_host_tensors_match_oracle():
+    """utils.loop on host tensors (CPU preprocessing, e.g. a dataset transform)
+    takes the torch form of the rewrite: order, loop weights (last duplicate
+    loop wins) and fills equal to the oracle's sequential restatement.  Device
+    tensors run mp_self_loops (GPU parity: test_gpu_parity.py
+    test_self_loop_utilities_bit_exact); the aggregation itself still has no CPU
+    path (test_no_cpu_fallback)."""
     from torch_geometric.utils import add_remaining_self_loops, add_self_loops, remove_self_loops
-    ei = torch.tensor([[0, 1, 1, 2, 2, 1], [1, 1, 2, 0, 2, 1]])
-    for fn in (add_remaining_self_loops, add_self_loops, remove_self_loops):
-        with pytest.raises(RuntimeError, match="no CPU fallback"):
-            fn(ei)
-    # the oracle's own KAT: node 1 has two self loops (weights 2 and 6), the last wins
     from oracle import pyg_ref as P
-    r_ei, r_w = P.add_remaining_self_loops(ei, torch.tensor([1., 2., 3., 4., 5., 6.]), 2, 4)
+    ei = torch.tensor([[0, 1, 1, 2, 2, 1], [1, 1, 2, 0, 2, 1]])
+    w = torch.tensor([1., 2., 3., 4., 5., 6.])
+    r_ei, r_w = P.add_remaining_self_loops(ei, w, 2, 4)
     assert r_w.tolist()[-4:] == [2., 6., 5., 2.]
     assert r_ei[:, :3].tolist() == [[0, 1, 2], [1, 2, 0]]
+    g = torch.Generator().manual_seed(3)
+    for ei_, w_ in ((ei, w), (torch.randint(40, (2, 500), generator=g), torch.rand(500, generator=g))):
+        N = int(ei_.max()) + 3
+        for fill in (1, 2):
+            a = add_remaining_self_loops(ei_, w_, fill, N)
+            b = P.add_remaining_self_loops(ei_, w_, fill, N)
+            assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+        a = add_self_loops(ei_, w_, 3.0, N)
+        b = P.add_self_loops(ei_, w_, 3.0, N)
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+        a = remove_self_loops(ei_, w_)
+        b = P.remove_self_loops(ei_, w_)
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    with pytest.raises(IndexError):
+        add_remaining_self_loops(torch.tensor([[0, 7], [1, 7]]), num_nodes=3)
 
 
 def test_data_batch_semantics():
