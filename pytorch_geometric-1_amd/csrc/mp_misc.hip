@@ -59,12 +59,57 @@ __global__ void k_gcn_degree(const int64_t* __restrict__ row, const float* __res
   if (e < n_edges) atomicAdd(deg + row[e], w ? w[e] : 1.f);
 }
 
-// step 2: deg^-0.5 computed as 1/sqrt(deg) with correctly rounded sqrt and
-// division (== torch CPU pow(-0.5) bit for bit); inf -> 0.
+// Correctly rounded fp32 sqrt and reciprocal, exact on any hardware sqrt / div
+// accuracy: a double-precision estimate rounded to float, then checked against
+// the rounding midpoints with products that are exact in double (a 26-bit
+// midpoint squared, or times a 24-bit float, fits 53 bits) and moved by one ulp
+// if needed.  (gfx950's fp32 __fsqrt_rn is not correctly rounded: 426 of 3000
+// real-valued degrees came out one ulp off torch's CPU pow(-0.5).)
+__device__ __forceinline__ float f_next(float v) { return __int_as_float(__float_as_int(v) + 1); }
+__device__ __forceinline__ float f_prev(float v) { return __int_as_float(__float_as_int(v) - 1); }
+// half the distance to the next float above / below a positive normal v
+__device__ __forceinline__ double half_ulp_up(float v) {
+  const int e = (__float_as_int(v) >> 23) & 0xff;
+  return ldexp(1.0, (e ? e : 1) - 127 - 24);
+}
+__device__ __forceinline__ double half_ulp_down(float v) {
+  const int b = __float_as_int(v);
+  const int e = (b >> 23) & 0xff;
+  return ldexp(1.0, (e ? e : 1) - 127 - 24 - ((b & 0x7fffff) == 0 && e > 1 ? 1 : 0));
+}
+
+__device__ float sqrt_rn_exact(float x) {
+  if (!(x > 0.f) || isinf(x)) return sqrtf(x);  // 0, negative, NaN, inf: the IEEE special cases
+  const double xd = x;
+  float s = (float)sqrt(xd);
+  for (int it = 0; it < 3; ++it) {
+    const double sd = s, lo = sd - half_ulp_down(s), hi = sd + half_ulp_up(s);
+    if (lo * lo > xd) s = f_prev(s);
+    else if (hi * hi < xd) s = f_next(s);
+    else break;
+  }
+  return s;
+}
+
+__device__ float rcp_rn_exact(float s) {
+  if (!(s > 0.f) || isinf(s)) return 1.f / s;  // 0 -> inf, inf -> 0, NaN, negatives (not a degree)
+  const double sd = s;
+  float q = (float)(1.0 / sd);
+  for (int it = 0; it < 3; ++it) {
+    const double qd = q, lo = qd - half_ulp_down(q), hi = qd + half_ulp_up(q);
+    if (lo * sd > 1.0) q = f_prev(q);
+    else if (hi * sd < 1.0) q = f_next(q);
+    else break;
+  }
+  return q;
+}
+
+// step 2: deg^-0.5 as torch's CPU pow(-0.5) computes it, 1 / sqrt(deg) with a
+// correctly rounded sqrt, then a correctly rounded division; inf -> 0.
 __global__ void k_gcn_dinv(float* __restrict__ deg, int64_t n) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  float d = __fdiv_rn(1.f, __fsqrt_rn(deg[i]));
+  float d = rcp_rn_exact(sqrt_rn_exact(deg[i]));
   deg[i] = isinf(d) ? 0.f : d;
 }
 

@@ -390,6 +390,35 @@ def gather_fill(w, pos, fill):
 # GCN normalisation (GCNConv.norm [U5])
 # ---------------------------------------------------------------------------
 
+def segment_sum_serial(csr, values, out=None):
+    """out[r] = sum over the slots of row r, in slot order, of values[eid[k]]
+    (mp_segment_sum_serial_f32): a 1-D scatter_add_ in the reference's edge
+    order, bit for bit (csr keyed on the scatter index; values in original
+    edge order, fp32)."""
+    _lib.require_device(values)
+    v = values.to(torch.float32).contiguous()
+    if out is None:
+        out = torch.empty(max(csr.n_rows, 1), dtype=torch.float32, device=v.device)[:csr.n_rows]
+    _lib.check(_lib.load().mp_segment_sum_serial_f32(csr.rowptr.data_ptr(), csr.eid.data_ptr(), v.data_ptr(),
+                                                     csr.n_rows, out.data_ptr(), _lib.stream_ptr(v.device)),
+               "mp_segment_sum_serial_f32")
+    return out
+
+
+def norm_from_degree(row, col, deg, edge_weight):
+    """dinv = deg^-1/2 (inf -> 0, torch's CPU pow(-0.5) rounding), then
+    dinv[row] * w * dinv[col] (mp_gcn_norm_from_deg_f32).  deg is consumed."""
+    _lib.require_device(row, col, deg, edge_weight)
+    E = row.numel()
+    w = edge_weight.to(torch.float32).contiguous() if edge_weight is not None else None
+    norm = torch.empty(E, dtype=torch.float32, device=row.device)
+    d = deg.to(torch.float32).contiguous()
+    _lib.check(_lib.load().mp_gcn_norm_from_deg_f32(row.contiguous().data_ptr(), col.contiguous().data_ptr(),
+                                                    _lib.ptr(w), E, d.numel(), d.data_ptr(), norm.data_ptr(),
+                                                    _lib.stream_ptr(row.device)), "mp_gcn_norm_from_deg_f32")
+    return norm
+
+
 def gcn_norm_weights(edge_index, num_nodes, edge_weight=None, integer_weights=False):
     """norm[e] = deg^-1/2[row] * w[e] * deg^-1/2[col], deg = scatter_add(w, row).
 
@@ -418,8 +447,7 @@ def gcn_norm_weights(edge_index, num_nodes, edge_weight=None, integer_weights=Fa
         return norm
     from .graph import graph_for
     rows = graph_for(edge_index, N, N, "source_to_target").src   # CSR keyed on edge_index[0]
-    _lib.check(lib.mp_segment_sum_serial_f32(rows.rowptr.data_ptr(), rows.eid.data_ptr(), w.data_ptr(), N,
-                                             deg.data_ptr(), st), "mp_segment_sum_serial_f32")
+    segment_sum_serial(rows, w, out=deg[:N])
     _lib.check(lib.mp_gcn_norm_from_deg_f32(row.data_ptr(), col.data_ptr(), w.data_ptr(), E, N, deg.data_ptr(),
                                             norm.data_ptr(), st), "mp_gcn_norm_from_deg_f32")
     return norm
