@@ -421,6 +421,39 @@ int mp_shard_plan(const int64_t* key, const int64_t* other, int64_t n_edges, int
                   int64_t* edge_pos, int64_t* local_key, int64_t* local_other,
                   int64_t* halo_nodes, int64_t* counts, void* ws, size_t ws_bytes, void* stream);
 
+/* ---- other dtypes (csrc/mp_dtype.hip) -------------------------------------
+ * torch_scatter 2.0.4 reduces any dtype ([U8/U9]); the fp32 hot path is
+ * mp_aggregate_f32, these are the breadth path for the rest. */
+#define MP_DTYPE_F32 0
+#define MP_DTYPE_F64 1
+#define MP_DTYPE_F16 2
+#define MP_DTYPE_BF16 3
+#define MP_DTYPE_I64 4
+
+/* out[r, :] = REDUCE_{k in row r} src[col[k], :] (col NULL: src row k), rows
+ * of `dtype` with leading dimensions lds / ldo in elements.  Every row is
+ * reduced by one wave per 64-feature tile in slot (= original edge) order,
+ * never split: float64 / int64 follow the reference's arithmetic bit for bit
+ * (int64 sums wrap); float16 / bfloat16 accumulate in fp32 and round once.
+ * max / min: strict compare (first edge wins), start at the type's lowest() /
+ * max(); a row that keeps it reports 0 and arg = n_ids (n_edges when 0); arg_out
+ * int64 [n_rows, F] (contiguous).  mean: (sum [+ out]) / max(count, 1), integer
+ * division truncating toward zero.  flags: MP_FLAG_INIT_FROM_OUT (torch_scatter
+ * `out=`), MP_FLAG_PYG_MASK (utils.scatter_'s +-10000 masks). */
+int mp_segment_reduce(const mp_csr* g, int32_t dtype, const void* src, int64_t lds,
+                      int32_t F, int32_t reduce, int32_t flags, void* out, int64_t ldo,
+                      int64_t* arg_out, void* stream);
+
+/* out[k, :] = x[idx[k], :] for elements of elem_bytes (2, 4 or 8) bytes. */
+int mp_gather_rows_any(int32_t elem_bytes, const void* x, int64_t ldx, const int64_t* idx,
+                       int64_t n, int32_t F, void* out, int64_t ldo, void* stream);
+
+/* grad[arg[r, f], f] = grad_out[r, f] for arg in [0, n_edges) (ScatterMax
+ * backward on materialised messages; grad zero-initialised by the caller). */
+int mp_scatter_arg_any(int32_t elem_bytes, const void* grad_out, const int64_t* arg,
+                       int64_t n_rows, int32_t F, int64_t n_edges, void* grad, int64_t ldg,
+                       void* stream);
+
 /* ---- helpers on the path -------------------------------------------------- */
 
 /* out[k,:] = x[idx[k],:]  (index_select of __collect__, scatter-sum backward,

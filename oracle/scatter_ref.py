@@ -126,3 +126,61 @@ def gather_max(x, other, index, dim_size):
     _c().oracle_gather_max_f32(_addr(xs), _addr(oth), _addr(idx), idx.shape[0], F, dim_size, _addr(o),
                                _addr(a))
     return torch.from_numpy(o), torch.from_numpy(a)
+
+
+# --- any dtype (scatter_cpu.cpp's loop for float64 / float16 / int64) -------
+
+_LOWEST = {np.dtype(np.float64): np.finfo(np.float64).min, np.dtype(np.float32): np.finfo(np.float32).min,
+           np.dtype(np.float16): np.finfo(np.float16).min, np.dtype(np.int64): np.iinfo(np.int64).min}
+_HIGHEST = {np.dtype(np.float64): np.finfo(np.float64).max, np.dtype(np.float32): np.finfo(np.float32).max,
+            np.dtype(np.float16): np.finfo(np.float16).max, np.dtype(np.int64): np.iinfo(np.int64).max}
+
+
+def scatter_loop_any(src, index, dim_size, reduce, out=None):
+    """scatter_cpu.cpp's serial loop (torch_scatter 2.0.4 [U9]) in numpy for
+    any of float64 / float32 / float16 / int64, sequential over edges,
+    vectorised over features: sums in the source dtype in edge order (numpy
+    float16 rounds after every add, as the CPU Half kernel does), max / min with
+    a strict compare from lowest() / max() (first edge wins; rows that keep the
+    init value -> 0, arg = E unless `out` was given), mean = sum / max(count, 1)
+    with integer division truncating toward zero.  Returns (out, arg or None)
+    as torch tensors.  Small inputs only (a Python loop over edges)."""
+    s = src.detach().cpu().numpy()
+    s2 = s.reshape(s.shape[0], -1)
+    E, F = s2.shape
+    idx = index.cpu().numpy().astype(np.int64)
+    dt = s2.dtype
+    has_out = out is not None
+    if has_out:
+        o = out.detach().cpu().numpy().reshape(dim_size, F).copy()
+    elif reduce == "max":
+        o = np.full((dim_size, F), _LOWEST[dt], dt)
+    elif reduce == "min":
+        o = np.full((dim_size, F), _HIGHEST[dt], dt)
+    else:
+        o = np.zeros((dim_size, F), dt)
+    a = np.full((dim_size, F), E, np.int64) if reduce in ("max", "min") else None
+    cnt = np.zeros(dim_size, np.int64)
+    with np.errstate(over="ignore"):
+        for e in range(E):
+            r = idx[e]
+            cnt[r] += 1
+            if reduce in ("sum", "add", "mean"):
+                o[r] = o[r] + s2[e]
+            else:
+                better = s2[e] > o[r] if reduce == "max" else s2[e] < o[r]
+                o[r] = np.where(better, s2[e], o[r])
+                a[r] = np.where(better, e, a[r])
+    if reduce == "mean":
+        c = np.maximum(cnt, 1).reshape(-1, 1)
+        if np.issubdtype(dt, np.integer):
+            o = (np.abs(o) // c) * np.sign(o)
+        else:
+            o = (o / c.astype(dt)).astype(dt)
+    if reduce in ("max", "min") and not has_out:
+        init = _LOWEST[dt] if reduce == "max" else _HIGHEST[dt]
+        o = np.where(o == init, np.zeros_like(o), o)
+    shape = (dim_size,) + tuple(src.shape[1:])
+    ot = torch.from_numpy(np.ascontiguousarray(o)).reshape(shape)
+    at = torch.from_numpy(a).reshape(shape) if a is not None else None
+    return ot, at

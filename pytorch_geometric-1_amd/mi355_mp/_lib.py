@@ -31,6 +31,7 @@ MP_TUNE_FLAT_VEC = 6
 MP_TUNE_FLAT_VEC_ARG = 7
 MP_TUNE_FLAT_SEQ_TILES = 8
 MP_TUNE_FLAT_FAR_MIN_BYTES = 9
+MP_DTYPE = {torch.float32: 0, torch.float64: 1, torch.float16: 2, torch.bfloat16: 3, torch.int64: 4}
 MP_LOOPS_REMOVE = 0
 MP_LOOPS_ADD = 1
 MP_LOOPS_ADD_REMAINING = 2
@@ -116,6 +117,9 @@ SIGNATURES = {
     "mp_arg_winner_mask": (ctypes.c_int, [c_p, i64, i32, i64, c_p, c_p, c_p]),
     "mp_scatter_arg_backward_csr_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, i64, i32, c_p, c_p, i64, c_p]),
     "mp_scatter_arg_grad_w_f32": (ctypes.c_int, [c_p, c_p, i64, c_p, c_p, i32, c_p, i64, c_p, i64, c_p, c_p]),
+    "mp_segment_reduce": (ctypes.c_int, [ctypes.POINTER(MpCsr), i32, c_p, i64, i32, i32, i32, c_p, i64, c_p, c_p]),
+    "mp_gather_rows_any": (ctypes.c_int, [i32, c_p, i64, c_p, i64, i32, c_p, i64, c_p]),
+    "mp_scatter_arg_any": (ctypes.c_int, [i32, c_p, c_p, i64, i32, i64, c_p, i64, c_p]),
 }
 
 _lib = None

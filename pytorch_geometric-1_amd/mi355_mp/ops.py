@@ -19,6 +19,36 @@ from .graph import csr_for_index, in_csr_order
 _REDUCES = ("sum", "add", "mean", "max", "min")
 
 
+def _any_2d(x, what):
+    """A 2-D row-major tensor of a dtype the native reductions take (fp32 hot
+    path; float64 / float16 / bfloat16 / int64 breadth path, mp_segment_reduce)."""
+    if x.dtype not in _lib.MP_DTYPE:
+        raise TypeError("mi355_mp: %s dtype %s is not supported (float32, float64, float16, bfloat16, int64)"
+                        % (what, x.dtype))
+    if x.dim() != 2:
+        raise ValueError("mi355_mp: %s must be 2-D [rows, features]" % what)
+    if x.stride(1) != 1 or x.stride(0) < max(x.shape[1], 1):
+        x = x.contiguous()
+    return x
+
+
+def _aggregate_any(csr, gather, src, reduce, flags, out=None):
+    """mp_segment_reduce: any supported dtype, every row in edge order (not
+    split).  Returns (out, arg_or_None)."""
+    lib = _lib.load()
+    F = src.shape[1]
+    dev = src.device
+    if out is None:
+        out = torch.empty((csr.n_rows, F), dtype=src.dtype, device=dev)
+    arg = torch.empty((csr.n_rows, F), dtype=torch.int64, device=dev) if reduce in ("max", "min") else None
+    if csr.n_rows == 0 or F == 0:
+        return out, arg
+    _lib.check(lib.mp_segment_reduce(csr.struct(gather), _lib.MP_DTYPE[src.dtype], src.data_ptr(), src.stride(0), F,
+                                     _lib.MP_REDUCE[reduce], flags, out.data_ptr(), out.stride(0), _lib.ptr(arg),
+                                     _lib.stream_ptr(dev)), "mp_segment_reduce")
+    return out, arg
+
+
 def _f32_2d(x, what):
     if x.dtype != torch.float32:
         raise TypeError("mi355_mp: %s must be float32 (got %s)" % (what, x.dtype))
@@ -75,13 +105,18 @@ def _aggregate(csr, gather, x, w_csr, reduce, flags, bias, out=None, stages=_lib
 def gather_rows(x, idx):
     """out = x[idx] via the native row gather (no autograd; see GatherRows)."""
     lib = _lib.load()
-    x = _f32_2d(x, "x")
+    x = _any_2d(x, "x")
     idx = idx.to(torch.int64).contiguous()
-    out = torch.empty((idx.numel(), x.shape[1]), dtype=torch.float32, device=x.device)
+    out = torch.empty((idx.numel(), x.shape[1]), dtype=x.dtype, device=x.device)
     if idx.numel() and x.shape[1]:
-        _lib.check(lib.mp_gather_rows_f32(x.data_ptr(), x.stride(0), idx.data_ptr(), idx.numel(),
-                                          x.shape[1], out.data_ptr(), out.stride(0),
-                                          _lib.stream_ptr(x.device)), "mp_gather_rows_f32")
+        if x.dtype == torch.float32:
+            _lib.check(lib.mp_gather_rows_f32(x.data_ptr(), x.stride(0), idx.data_ptr(), idx.numel(),
+                                              x.shape[1], out.data_ptr(), out.stride(0),
+                                              _lib.stream_ptr(x.device)), "mp_gather_rows_f32")
+        else:
+            _lib.check(lib.mp_gather_rows_any(x.element_size(), x.data_ptr(), x.stride(0), idx.data_ptr(),
+                                              idx.numel(), x.shape[1], out.data_ptr(), out.stride(0),
+                                              _lib.stream_ptr(x.device)), "mp_gather_rows_any")
     return out
 
 
@@ -225,7 +260,10 @@ class _SegmentReduce(torch.autograd.Function):
         csr = csr_for_index(index, dim_size)
         need_mask_grad = pyg_mask and reduce in ("max", "min") and ctx.needs_input_grad[0]
         flags = _lib.MP_FLAG_PYG_MASK if (pyg_mask and not need_mask_grad) else 0
-        out, arg = _aggregate(csr, "eid", src, None, reduce, flags, None)
+        if src.dtype == torch.float32:
+            out, arg = _aggregate(csr, "eid", src, None, reduce, flags, None)
+        else:
+            out, arg = _aggregate_any(csr, "eid", src, reduce, flags)
         ctx.reduce = reduce
         ctx.csr = csr
         ctx.n_src = src.shape[0]
@@ -245,16 +283,21 @@ class _SegmentReduce(torch.autograd.Function):
         reduce = ctx.reduce
         if reduce in ("max", "min"):
             lib = _lib.load()
-            g = grad_out * keep if keep is not None else grad_out
-            gs = torch.zeros((ctx.n_src, g.shape[1]), dtype=torch.float32, device=g.device)
-            _lib.check(lib.mp_scatter_arg_backward_f32(g.data_ptr(), arg.data_ptr(), g.shape[0], g.shape[1],
-                                                       ctx.n_src, None, None, None, 0, gs.data_ptr(), gs.stride(0),
-                                                       None, _lib.stream_ptr(g.device)),
-                       "mp_scatter_arg_backward_f32")
+            g = (grad_out * keep if keep is not None else grad_out).contiguous()
+            gs = torch.zeros((ctx.n_src, g.shape[1]), dtype=g.dtype, device=g.device)
+            if g.dtype == torch.float32:
+                _lib.check(lib.mp_scatter_arg_backward_f32(g.data_ptr(), arg.data_ptr(), g.shape[0], g.shape[1],
+                                                           ctx.n_src, None, None, None, 0, gs.data_ptr(),
+                                                           gs.stride(0), None, _lib.stream_ptr(g.device)),
+                           "mp_scatter_arg_backward_f32")
+            else:
+                _lib.check(lib.mp_scatter_arg_any(g.element_size(), g.data_ptr(), arg.data_ptr(), g.shape[0],
+                                                  g.shape[1], ctx.n_src, gs.data_ptr(), gs.stride(0),
+                                                  _lib.stream_ptr(g.device)), "mp_scatter_arg_any")
             return gs, None, None, None, None
         g = grad_out
         if reduce == "mean":
-            g = g / ctx.csr.degree().clamp(min=1).to(torch.float32).view(-1, 1)
+            g = g / ctx.csr.degree().clamp(min=1).to(g.dtype).view(-1, 1)
         return gather_rows(g, index), None, None, None, None
 
 
@@ -267,7 +310,7 @@ def segment_reduce(src, index, dim_size, reduce="sum", pyg_mask=False):
         raise ValueError("unknown reduce %r" % (reduce,))
     reduce = "sum" if reduce == "add" else reduce
     _lib.require_device(src, index)
-    src = _f32_2d(src, "src")
+    src = _any_2d(src, "src")
     if index.dim() != 1 or index.numel() != src.shape[0]:
         raise ValueError("mi355_mp: index must be 1-D with src.size(0) entries")
     return _SegmentReduce.apply(src, index, int(dim_size), reduce, pyg_mask)
@@ -277,14 +320,15 @@ def segment_reduce_into(src, index, out, reduce="sum"):
     """torch_scatter ``out=`` semantics: reduce into (and return) the given out tensor."""
     reduce = "sum" if reduce == "add" else reduce
     _lib.require_device(src, index, out)
-    src = _f32_2d(src, "src")
-    if out.dtype != torch.float32 or out.dim() != 2 or out.stride(1) != 1:
-        raise ValueError("mi355_mp: out must be a row-major float32 [dim_size, F] tensor")
+    src = _any_2d(src, "src")
+    if out.dtype != src.dtype or out.dim() != 2 or out.stride(1) != 1:
+        raise ValueError("mi355_mp: out must be a row-major [dim_size, F] tensor of src's dtype")
     if torch.is_grad_enabled() and (src.requires_grad or out.requires_grad):
         raise NotImplementedError("mi355_mp: autograd through torch_scatter `out=` is not supported")
     csr = csr_for_index(index, out.shape[0])
-    out, arg = _aggregate(csr, "eid", src, None, reduce, _lib.MP_FLAG_INIT_FROM_OUT, None, out=out)
-    return out, arg
+    if src.dtype == torch.float32:
+        return _aggregate(csr, "eid", src, None, reduce, _lib.MP_FLAG_INIT_FROM_OUT, None, out=out)
+    return _aggregate_any(csr, "eid", src, reduce, _lib.MP_FLAG_INIT_FROM_OUT, out=out)
 
 
 class GatherRows(torch.autograd.Function):
@@ -300,14 +344,19 @@ class GatherRows(torch.autograd.Function):
     def backward(ctx, g):
         (idx,) = ctx.saved_tensors
         csr = csr_for_index(idx, ctx.n)
-        gx, _ = _aggregate(csr, "eid", g.contiguous(), None, "sum", 0, None)
+        g = g.contiguous()
+        if g.dtype == torch.float32:
+            gx, _ = _aggregate(csr, "eid", g, None, "sum", 0, None)
+        else:
+            gx, _ = _aggregate_any(csr, "eid", g, "sum", 0)
         return gx, None
 
 
 def index_select_rows(x, idx):
-    """Differentiable native replacement of x.index_select(0, idx) for 2-D fp32 x."""
+    """Differentiable native replacement of x.index_select(0, idx) for 2-D x
+    (fp32 / fp64 / fp16 / bf16 / int64)."""
     _lib.require_device(x, idx)
-    return GatherRows.apply(_f32_2d(x, "x"), idx)
+    return GatherRows.apply(_any_2d(x, "x"), idx)
 
 
 # ---------------------------------------------------------------------------

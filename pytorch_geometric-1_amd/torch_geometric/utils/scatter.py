@@ -3,7 +3,7 @@
 Dispatches to torch_scatter.scatter_{add,mean,min,max}, keeps the first
 element of tuple results, and masks max -> out < -10000 := 0,
 min -> out > 10000 := 0.  Here the mask is fused into the native reduction
-(MP_FLAG_PYG_MASK) whenever src is a float32 device tensor.
+(MP_FLAG_PYG_MASK) for every device dtype the engine takes.
 """
 import torch_scatter
 

@@ -16,7 +16,10 @@ scatter_max/min, segment_{sum,mean,min,max}_{csr,coo}, gather_{csr,coo}; the
 schemas of torch_scatter 2.0.4's csrc), so TorchScript-visible callers resolve.
 
 All reductions run as destination-sorted segmented reductions in HIP
-(mi355_mp.ops); fp32 on a ROCm device only -- there is no CPU path.
+(mi355_mp.ops) on a ROCm device -- there is no CPU path.  float32 takes the
+fused hot-path kernels; float64 / float16 / bfloat16 / int64 the
+mp_segment_reduce kernels (every row in edge order: float64 and int64 bit for
+bit, the half types accumulated in fp32).
 """
 import torch
 
@@ -65,10 +68,14 @@ def _index_1d(src, index, dim):
     return None
 
 
+def _check_dtype(src):
+    if src.dtype not in _lib.MP_DTYPE:
+        raise TypeError("mi355_mp: scatter ops take float32, float64, float16, bfloat16 or int64 (got %s)" % src.dtype)
+
+
 def _prepare(src, index, dim, dim_size):
     _lib.require_device(src, index)
-    if src.dtype != torch.float32:
-        raise TypeError("mi355_mp: scatter ops are implemented for float32 (got %s)" % src.dtype)
+    _check_dtype(src)
     dim = dim % src.dim() if src.dim() else 0
     idx = _index_1d(src, index, dim).to(torch.int64)
     if dim_size is None:
@@ -119,8 +126,7 @@ def _reduce_general(src, index, dim, out, dim_size, reduce):
 
 def _reduce(src, index, dim, out, dim_size, reduce):
     _lib.require_device(src, index)
-    if src.dtype != torch.float32:
-        raise TypeError("mi355_mp: scatter ops are implemented for float32 (got %s)" % src.dtype)
+    _check_dtype(src)
     d = dim % src.dim() if src.dim() else 0
     if _index_1d(src, index, d) is None:
         if out is not None:

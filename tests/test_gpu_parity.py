@@ -2122,3 +2122,110 @@ def test_self_loop_out_of_range_raises_without_writing():
                                                   _lib.stream_ptr()), "count")
         assert cnt.cpu().tolist() == [2, 1]
     torch.cuda.synchronize()
+
+
+# --------------------------------------------------------------------------
+# round 3: the torch_scatter replacement for float64 / float16 / bfloat16 / int64
+# --------------------------------------------------------------------------
+
+def _dtype_case(dtype, seed, E=6000, N=300, F=37):
+    """Index with a hub row (1/3 of the edges), empty rows and duplicates; data
+    with ties (small integers, scaled for the float types)."""
+    g = torch.Generator().manual_seed(seed)
+    idx = torch.cat([torch.full((E // 3,), 7, dtype=torch.int64), torch.randint(N - 20, (E - E // 3,), generator=g)])
+    idx = idx[torch.randperm(E, generator=g)]
+    if dtype == torch.int64:
+        src = torch.randint(-50, 50, (E, F), generator=g)
+        src[::97, 0] = torch.iinfo(torch.int64).min
+        src[::89, 1] = torch.iinfo(torch.int64).max // 3
+    elif dtype == torch.float64:
+        src = torch.randint(-40, 40, (E, F), generator=g).double() * 0.37 + torch.rand(E, F, generator=g).double()
+    else:
+        # multiples of 1/4 up to 10: exact in float16 / bfloat16 and every fp32 partial sum exact,
+        # so the single rounding of the fp32 accumulator is that of the exact result
+        src = (torch.randint(-40, 41, (E, F), generator=g).double() * 0.25).to(dtype)
+    return src, idx, N
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.int64, torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("reduce", ["sum", "mean", "max", "min"])
+def test_torch_scatter_dtypes_vs_oracle(dtype, reduce):
+    """torch_scatter.scatter_* for the non-fp32 dtypes (mp_segment_reduce) vs the
+    serial-loop oracle: float64 and int64 bit for bit on EVERY row (rows are
+    never split: the 2000-edge hub too), max / min values and first-edge args
+    bit-exact for every dtype; float16 / bfloat16 sums and means (fp32
+    accumulation, one rounding) within half an output ulp of the float64 sum."""
+    import torch_scatter
+    src, idx, N = _dtype_case(dtype, 31)
+    fn = getattr(torch_scatter, "scatter_" + reduce)
+    res = fn(src.to(DEV), idx.to(DEV), 0, dim_size=N)
+    out, arg = (res if isinstance(res, tuple) else (res, None))
+    assert out.dtype == dtype
+    if dtype in (torch.float16, torch.bfloat16):
+        ref, rarg = S.scatter_loop_any(src.double(), idx, N, reduce)
+        got = out.cpu()
+        if reduce in ("max", "min"):
+            assert torch.equal(got.double(), ref) and torch.equal(arg.cpu(), rarg)
+        else:
+            want = ref.to(dtype)                       # the float64 result rounded once
+            assert torch.equal(got, want), float((got.double() - ref).abs().max())
+    else:
+        ref, rarg = S.scatter_loop_any(src, idx, N, reduce)
+        assert torch.equal(out.cpu(), ref), float((out.cpu().double() - ref.double()).abs().max())
+        if arg is not None:
+            assert torch.equal(arg.cpu(), rarg)
+    # scatter_ (PyG) masks and the out= form
+    if reduce in ("max", "min") and dtype != torch.int64:
+        from torch_geometric.utils import scatter_
+        m = scatter_(reduce, src.to(DEV) * 1000, idx.to(DEV), dim_size=N).cpu()
+        r, _ = S.scatter_loop_any((src.double() * 1000).to(dtype).double(), idx, N, reduce)
+        r = r.masked_fill(r < -10000, 0) if reduce == "max" else r.masked_fill(r > 10000, 0)
+        assert torch.equal(m.double(), r)
+    if dtype in (torch.float64, torch.int64):
+        base = (torch.arange(N * src.shape[1]).view(N, -1) % 5).to(dtype)
+        o = base.clone().to(DEV)
+        res = fn(src.to(DEV), idx.to(DEV), 0, out=o)
+        ref, rarg = S.scatter_loop_any(src, idx, N, reduce, out=base)
+        assert torch.equal(o.cpu(), ref)
+
+
+def test_torch_scatter_dtype_gradcheck_float64():
+    """torch.autograd.gradcheck of scatter_max / scatter_min / scatter_mean /
+    scatter_sum and the gather_csr round trip in float64 (continuous data: no
+    ties), through the native float64 kernels and their backward."""
+    import torch_scatter
+    g = torch.Generator().manual_seed(3)
+    E, N, F = 120, 15, 4
+    idx = torch.randint(N - 3, (E,), generator=g).to(DEV)
+    src = torch.randn(E, F, generator=g, dtype=torch.float64).to(DEV).requires_grad_(True)
+    for fn in (lambda s: torch_scatter.scatter_max(s, idx, 0, dim_size=N)[0],
+               lambda s: torch_scatter.scatter_min(s, idx, 0, dim_size=N)[0],
+               lambda s: torch_scatter.scatter_mean(s, idx, 0, dim_size=N),
+               lambda s: torch_scatter.scatter_sum(s, idx, 0, dim_size=N),
+               lambda s: torch_scatter.gather_coo(torch_scatter.scatter_sum(s, idx, 0, dim_size=N), idx)):
+        assert torch.autograd.gradcheck(fn, (src,), eps=1e-6, atol=1e-7)
+
+
+def test_torch_scatter_dtype_elementwise_index_and_segment_ops():
+    """The element-wise-index path and segment_csr / segment_coo / gather_csr in
+    float64 and int64 against torch's own ops (sum exact for int64; float64
+    max / min exact)."""
+    import torch_scatter
+    g = torch.Generator().manual_seed(8)
+    for dtype in (torch.float64, torch.int64):
+        src = (torch.randn(6, 50, generator=g) * 10).to(dtype)
+        index = torch.randint(9, (6, 50), generator=g)
+        out = torch_scatter.scatter_add(src.to(DEV), index.to(DEV), dim=1, dim_size=9).cpu()
+        ref = torch.zeros(6, 9, dtype=dtype).scatter_add_(1, index, src)
+        assert torch.equal(out, ref)
+        mx, am = torch_scatter.scatter_max(src.to(DEV), index.to(DEV), dim=1, dim_size=9)
+        ref = torch.zeros(6, 9, dtype=dtype).scatter_reduce(1, index, src, "amax", include_self=False)
+        assert torch.equal(mx.cpu(), ref)
+        counts = torch.tensor([3, 0, 5, 2])
+        indptr = torch.cat([torch.zeros(1, dtype=torch.int64), counts.cumsum(0)])
+        s2 = (torch.randn(10, 3, generator=g) * 10).to(dtype)
+        seg = torch_scatter.segment_csr(s2.to(DEV), indptr.to(DEV), reduce="sum").cpu()
+        ref = torch.stack([s2[int(indptr[i]):int(indptr[i + 1])].sum(0) for i in range(4)])
+        assert torch.equal(seg, ref) if dtype == torch.int64 else torch.allclose(seg, ref)
+        gat = torch_scatter.gather_csr(seg.to(DEV), indptr.to(DEV)).cpu()
+        assert torch.equal(gat, seg.repeat_interleave(counts, 0))

@@ -310,3 +310,26 @@ def test_fuzz_oracle_forms_agree(N, E, F, ties, seed):
             0, idx.view(-1, 1).expand(E, F), torch.where(hit, e, torch.full_like(e, E)), "amin")
         first[empty] = E
         assert torch.equal(arg, first)
+
+
+@pytest.mark.parametrize("reduce", ["sum", "mean", "max", "min"])
+def test_any_dtype_loop_matches_c_loop_and_kats(reduce):
+    """scatter_loop_any (the numpy restatement used for float64 / float16 /
+    int64) equals the C serial loop on float32, tie-heavy data included, and
+    hand-computed int64 KATs (truncating mean, lowest() -> 0, first-index arg)."""
+    g = torch.Generator().manual_seed(11)
+    src = torch.randint(-3, 4, (700, 6), generator=g).float()
+    idx = torch.randint(60, (700,), generator=g)
+    a, b = S.scatter_loop(src, idx, 64, reduce)
+    c, d = S.scatter_loop_any(src, idx, 64, reduce)
+    assert torch.equal(a, c) and (b is None or torch.equal(b, d))
+    lo = torch.iinfo(torch.int64).min
+    s = torch.tensor([[-7], [2], [lo], [5], [5]], dtype=torch.int64)
+    i = torch.tensor([0, 0, 1, 2, 2])
+    o, arg = S.scatter_loop_any(s, i, 4, reduce)
+    want = {"sum": ([-5], [lo], [10], [0]), "mean": ([-2], [lo], [5], [0]),
+            "max": ([2], [0], [5], [0]), "min": ([-7], [lo], [5], [0])}[reduce]
+    assert o.view(-1).tolist() == [w[0] for w in want]
+    if arg is not None:
+        # max: lowest() itself never beats the init value (arg stays E = 5, value -> 0)
+        assert arg.view(-1).tolist() == ([1, 5, 3, 5] if reduce == "max" else [0, 2, 3, 5])
