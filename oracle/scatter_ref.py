@@ -174,7 +174,8 @@ def scatter_loop_any(src, index, dim_size, reduce, out=None):
     if reduce == "mean":
         c = np.maximum(cnt, 1).reshape(-1, 1)
         if np.issubdtype(dt, np.integer):
-            o = (np.abs(o) // c) * np.sign(o)
+            q = o // c                                   # floor; then toward zero (no abs: INT64_MIN)
+            o = q + ((q * c != o) & (o < 0))
         else:
             o = (o / c.astype(dt)).astype(dt)
     if reduce in ("max", "min") and not has_out:
