@@ -11,9 +11,12 @@ One step = one GCNConv propagate: the fused gather * norm -> segment-sum
 schedule / norm build (one-time, cached=True semantics) and the x @ W GEMM
 are timed separately and reported beside the metric.
 
-N > 1: the same graph is sharded by destination range (edge balanced); a
-step is halo all_to_all (RCCL) + local fused aggregation on every rank;
-value = E' / max-over-ranks step time (strong scaling).
+N > 1: the same graph is sharded by destination range (edge balanced), built
+from per-rank slices of the edge list (ShardedGraph.for_gcn_from_slices: no
+rank holds the whole list); a step is the halo all_to_all (RCCL) overlapped
+with the interior edges, then the boundary edges, on every rank; value = E' /
+max-over-ranks step time (strong scaling).  extra.per_rank carries each rank's
+halo bytes and the interior / exposed-exchange / boundary split of its steps.
 
 Prints ONE JSON line on rank 0.
 """
@@ -243,16 +246,25 @@ def main():
     N = 1 << SCALE
     t0 = time.perf_counter()
     ei = rmat_edge_index(scale=SCALE, n_samples=SAMPLES, seed=1, device=dev)
+    if world > 1:
+        # each rank keeps only its contiguous 1/world slice of the edge list (the
+        # generator, deterministic on every rank, stands in for reading the rank's
+        # shard of an edge file): loops, norm, cuts and plans are built from the
+        # slices with all_to_alls -- no rank holds or sorts the whole list
+        E_raw = ei.shape[1]
+        s0, s1 = rank * E_raw // world, (rank + 1) * E_raw // world
+        ei_slice = ei[:, s0:s1].clone()
+        del ei
     torch.cuda.synchronize()
     t_gen = time.perf_counter() - t0
 
     # one-time build: loops + norm (GCNConv.norm), CSR + schedule
     t0 = time.perf_counter()
-    ei2, norm = GCNConv.norm(ei, N)
-    E2 = ei2.shape[1]
     bias = torch.randn(F_DIM, device=dev, generator=torch.Generator(device=dev).manual_seed(7)) * 0.1
     g = torch.Generator(device=dev).manual_seed(1)
     if world == 1:
+        ei2, norm = GCNConv.norm(ei, N)
+        E2 = ei2.shape[1]
         graph = Graph(ei2, N, N, chunk=args.chunk or None)
         csr = graph.dst
         w_csr = csr.to_csr_order(norm)
@@ -261,7 +273,10 @@ def main():
         E_local = E2
     else:
         from mi355_mp import dist as mdist
-        plan = mdist.ShardPlan(ei2, N, rank, world).exchange_requests()
+        sg = mdist.ShardedGraph.for_gcn_from_slices(ei_slice, s0, N, rank, world, chunk=args.chunk or None)
+        del ei_slice
+        E2 = sg.n_edges
+        plan = sg.fwd
         x_full = torch.randn(N, F_DIM, device=dev, generator=g)
         x_local = plan.local_buffer(F_DIM)
         x_local[:plan.n_own].copy_(x_full[plan.lo:plan.hi])
@@ -275,10 +290,10 @@ def main():
                 c0 += xt.shape[1]
         del x_full
         lei = plan.local_edge_index
-        graph = Graph(lei, plan.n_own, plan.n_local_src, chunk=args.chunk or None)
+        graph = sg.g_fwd
         csr = graph.dst
-        w_csr = csr.to_csr_order(norm[plan.edge_pos])
-        overlap = mdist.OverlappedAggregation(plan, norm, chunk=args.chunk or None)
+        w_csr = sg._w[0]
+        overlap = mdist.OverlappedAggregation(plan, sg.norm_fwd, chunk=args.chunk or None, local_weights=True)
         n_rows = plan.n_own
         E_local = lei.shape[1]
     torch.cuda.synchronize()
@@ -314,10 +329,11 @@ def main():
         elif args.no_overlap:
             aggregate(plan.exchange_into(x_local, ops.gather_rows), out=out_buf)
         elif x_tiles is not None:
-            overlap.step_tiled(x_tiles, out_buf, bias)
+            overlap.step_tiled(x_tiles, out_buf, bias, events=None if i is None else step_events[i])
         else:
             overlap.step(x_local, out_buf, bias)
 
+    step_events = [dict() for _ in range(args.steps)]
     for _ in range(args.warmup):
         step()
     if world == 1:
@@ -424,6 +440,29 @@ def main():
         del fused_out, terms
         torch.cuda.empty_cache()
 
+    # per-rank exchange / compute split of the timed steps (N > 1, tiled overlap):
+    # HIP events on the compute stream around the interior passes, around each
+    # tile's work.wait() (exchange time the compute stream is exposed to) and
+    # around each boundary pass; gathered to rank 0
+    ranks = None
+    if world > 1:
+        def span(evs, k):
+            lst = evs.get(k, [])
+            return sum(lst[j].elapsed_time(lst[j + 1]) for j in range(0, len(lst) - 1, 2))
+        torch.cuda.synchronize()
+        mine = {"rank": rank, "rows": plan.n_own, "edges": E_local, "interior_edges": overlap.n_interior,
+                "boundary_edges": overlap.n_boundary, "halo_rows": plan.n_local_src - plan.n_own,
+                "halo_bytes_in": (plan.n_local_src - plan.n_own) * F_DIM * 4,
+                "halo_bytes_out": int(plan.send_idx.numel()) * F_DIM * 4,
+                "peers_in": [int(c) for c in plan.recv_counts]}
+        if x_tiles is not None:
+            n = max(1, len(step_events))
+            mine.update({"interior_ms": sum(span(e, "interior") for e in step_events) / n,
+                         "exchange_exposed_ms": sum(span(e, "wait") for e in step_events) / n,
+                         "boundary_ms": sum(span(e, "boundary") for e in step_events) / n})
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(ei2, norm, x, args.cpu_sample_edges)
@@ -468,6 +507,7 @@ def main():
                       "overlap": world > 1 and not args.no_overlap,
                       "halo_tile": args.halo_tile if world > 1 and not args.no_overlap else None,
                       "n_wave_tasks": csr.n_waves,
+                      "per_rank": ranks,
                       "gpu_reference_path_ms": ((ref_paths or {}).get("reference_path") or {}).get("ms"),
                       "hipsparse_spmm_ms": ((ref_paths or {}).get("vendor_spmm") or {}).get("ms"),
                       "same_gpu_paths": ref_paths,

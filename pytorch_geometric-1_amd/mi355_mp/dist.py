@@ -107,7 +107,11 @@ def _plan_native(key, other, num_nodes, cuts, rank, world):
 class ShardPlan:
     """Everything rank `rank` needs to aggregate its destination rows."""
 
-    def __init__(self, edge_index, num_nodes, rank, world, cuts=None, flow="source_to_target"):
+    def __init__(self, edge_index, num_nodes, rank, world, cuts=None, flow="source_to_target", edge_ids=None):
+        """edge_index: the global edge list, or any list holding (at least) this
+        rank's edges in global order -- e.g. the rank's own in-edges from
+        scatter_edges_by_owner; edge_ids then gives each listed edge's GLOBAL id
+        (argmax ids stay global).  edge_pos indexes the list passed in."""
         i, j = (1, 0) if flow == "source_to_target" else (0, 1)
         dst_all, src_all = edge_index[i], edge_index[j]
         if cuts is None:
@@ -121,6 +125,7 @@ class ShardPlan:
         self.edge_pos, dst, local_src, halo_nodes, self.recv_counts = plan(dst_all, src_all, num_nodes, cuts, rank,
                                                                            world)
         self.halo_nodes = halo_nodes
+        self.edge_gid = edge_ids[self.edge_pos] if edge_ids is not None else self.edge_pos
         self.local_edge_index = torch.stack([local_src, dst]) if i == 1 else torch.stack([dst, local_src])
         self.n_local_src = self.n_own + halo_nodes.numel()
         self.send_idx = None
@@ -188,7 +193,7 @@ class ShardPlan:
         n_local = int(self.edge_pos.numel())
         if n_local == 0:
             return torch.full_like(arg_local, n_edges_global)
-        ids = self.edge_pos[arg_local.clamp(max=n_local - 1)]
+        ids = self.edge_gid[arg_local.clamp(max=n_local - 1)]
         return torch.where(arg_local >= n_local, torch.full_like(ids, n_edges_global), ids)
 
 
@@ -215,6 +220,149 @@ def sharded_propagate(plan, x_own, local_aggregate, gather_rows, edge_weight=Non
     return res
 
 
+# ---------------------------------------------------------------------------
+# building the shards from per-rank slices of the edge list (no rank holds it all)
+# ---------------------------------------------------------------------------
+
+def scatter_edges_by_owner(key, cuts, payloads, group=None):
+    """Route the entries of `payloads` (1-D tensors aligned with `key`) to the
+    rank owning key (range partition `cuts`): one all_to_all per payload.  The
+    result is the concatenation over sender ranks in rank order, each sender's
+    entries in their original order -- so when every rank holds a contiguous
+    slice of the global edge list (rank r before rank r + 1), each rank receives
+    its edges in GLOBAL order."""
+    world = len(cuts) - 1
+    dev = key.device
+    owner = torch.searchsorted(torch.tensor(cuts[1:], dtype=key.dtype, device=dev), key, right=True)
+    order = torch.sort(owner, stable=True).indices
+    send = torch.bincount(owner, minlength=world)
+    recv = torch.empty_like(send)
+    _a2a(recv, send, group=group)
+    sc, rc = send.tolist(), recv.tolist()
+    out = []
+    for p in payloads:
+        buf = p.new_empty(sum(rc))
+        _a2a(buf, p[order].contiguous(), rc, sc, group)
+        out.append(buf)
+    return out
+
+
+def _all_gather_ints(vals, group=None):
+    """[[vals of rank 0], [vals of rank 1], ...] for a few host ints."""
+    got = [None] * dist.get_world_size(group)
+    dist.all_gather_object(got, list(vals), group=group)
+    return got
+
+
+def _segment_sum_in_order(index, values, n, device_native):
+    """out[k] = sum of values[index == k] left to right (the CPU scatter_add_'s
+    order): torch's serial CPU scatter_add_ on host tensors, the transposed
+    CSR's serial segment sum (mp_segment_sum_serial_f32) on the device."""
+    if not device_native:
+        return torch.zeros(n, dtype=values.dtype).scatter_add_(0, index, values)
+    from . import ops
+    from .graph import CSR
+    return ops.segment_sum_serial(CSR(index, None, n, index.numel()), values)
+
+
+def gcn_shards_from_slices(edge_slice, slice_offset, num_nodes, rank, world, group=None, edge_weight=None,
+                           improved=False):
+    """GCNConv's graph (add_remaining_self_loops + deg over row + norm, PyG 1.4.3
+    [U5]) for a graph held as per-rank slices: rank r holds the global edges
+    [slice_offset, slice_offset + n_r) (slices contiguous, in rank order).  No
+    rank ever holds the whole edge list:
+
+      1. self loops are dropped locally; kept-edge global ids follow from the
+         kept counts of the earlier ranks (one all_gather of two ints);
+      2. cuts: the in-degree (integer, so exact under any reduction order; +1
+         for the appended loops) is all-reduced, then edge-balanced;
+      3. a node's pre-existing loops go to its owner, the LAST one's weight wins
+         (upstream's sequential index_put_);
+      4. the out-edges of each rank's rows come to it in global order
+         (scatter_edges_by_owner by source): the degree is their edge-order sum,
+         then + the loop weight -- the reference's scatter_add arithmetic;
+      5. the in-edges of each rank's rows come to it in global order (by
+         destination); the N loops are appended last with ids E_kept + v;
+      6. the norm needs deg of remote endpoints: it travels over each plan's
+         halo exchange (ShardedGraph.for_gcn_from_slices).
+
+    Returns a dict: cuts, E (total edges after the loops), deg (own rows),
+    fwd = (edge_index [2, m] global ids, global edge ids, weights) of the
+    in-edges, bwd = the same for the out-edges."""
+    row, col = edge_slice[0].to(torch.int64), edge_slice[1].to(torch.int64)
+    dev = row.device
+    N = int(num_nodes)
+    n = row.numel()
+    w = (edge_weight.to(torch.float32) if edge_weight is not None
+         else torch.ones(n, dtype=torch.float32, device=dev))
+    fill = 2.0 if improved else 1.0
+    keep = row != col
+    kept = torch.nonzero(keep).view(-1)
+    sizes = _all_gather_ints([n, kept.numel()], group)
+    if slice_offset != sum(sz[0] for sz in sizes[:rank]):
+        raise ValueError("gcn_shards_from_slices: rank %d's slice offset %d does not follow the earlier slices"
+                         % (rank, slice_offset))
+    k_off = sum(sz[1] for sz in sizes[:rank])
+    E_kept = sum(sz[1] for sz in sizes)
+    kr, kc, kw = row[kept], col[kept], w[kept]
+    kgid = k_off + torch.arange(kept.numel(), dtype=torch.int64, device=dev)
+    # 2. cuts from the global in-degree (+1: every node gets its loop)
+    deg_in = torch.bincount(kc, minlength=N)
+    deg_in = deg_in.to(dev)
+    if dev.type != "cpu" and dist.get_backend(group) == "gloo":
+        h = deg_in.cpu()
+        dist.all_reduce(h, group=group)
+        deg_in = h.to(dev)
+    else:
+        dist.all_reduce(deg_in, group=group)
+    cuts = edge_balanced_cuts(deg_in + 1, world)
+    lo, hi = cuts[rank], cuts[rank + 1]
+    own = torch.arange(lo, hi, dtype=torch.int64, device=dev)
+    # 3. pre-existing loops -> the node's owner; the last one (largest position) wins
+    lidx = torch.nonzero(~keep).view(-1)
+    lv, lw = row[lidx], w[lidx]
+    if lv.numel() and (int(lv.min()) < 0 or int(lv.max()) >= N):
+        raise IndexError("self loops name a node outside [0, %d)" % N)
+    rv, rpos, rw = scatter_edges_by_owner(lv, cuts, [lv, lidx + slice_offset, lw], group)
+    loop_w = torch.full((hi - lo,), fill, dtype=torch.float32, device=dev)
+    if rv.numel():
+        best = torch.full((hi - lo,), -1, dtype=torch.int64, device=dev)
+        best.scatter_reduce_(0, rv - lo, rpos, "amax")
+        last = rpos == best[rv - lo]
+        loop_w[rv[last] - lo] = rw[last]
+    # 4. out-edges of my rows, global order -> deg = scatter_add(w, row) in edge order, then the loop
+    b_row, b_col, b_gid, b_w = scatter_edges_by_owner(kr, cuts, [kr, kc, kgid, kw], group)
+    deg = _segment_sum_in_order(b_row - lo, b_w, hi - lo, dev.type != "cpu")
+    deg = deg + loop_w
+    # 5. in-edges of my rows, global order; the loops last
+    f_row, f_col, f_gid, f_w = scatter_edges_by_owner(kc, cuts, [kr, kc, kgid, kw], group)
+    loop_gid = E_kept + own
+    fwd = (torch.stack([torch.cat([f_row, own]), torch.cat([f_col, own])]), torch.cat([f_gid, loop_gid]),
+           torch.cat([f_w, loop_w]))
+    bwd = (torch.stack([torch.cat([b_row, own]), torch.cat([b_col, own])]), torch.cat([b_gid, loop_gid]),
+           torch.cat([b_w, loop_w]))
+    return {"cuts": cuts, "E": E_kept + N, "deg": deg, "fwd": fwd, "bwd": bwd}
+
+
+def _norm_over_plan(plan, deg_own, w_local, group=None):
+    """GCN norm dinv[row] * w * dinv[col] of a plan's local edges: the degrees of
+    the halo endpoints come over the plan's own exchange (one float per halo
+    node), dinv = deg^-1/2 with inf -> 0 (torch's CPU pow(-0.5) rounding: the
+    native mp_gcn_norm_from_deg_f32 on the device)."""
+    degl = deg_own.new_empty((plan.n_local_src, 1))
+    degl[:plan.n_own, 0] = deg_own
+    if deg_own.is_cuda:
+        from . import ops
+        plan.exchange_into(degl, ops.gather_rows, group)
+        lei = plan.local_edge_index
+        return ops.norm_from_degree(lei[0], lei[1], degl.view(-1).clone(), w_local)
+    plan.exchange_into(degl, lambda t, idx: t[idx], group)
+    dinv = degl.view(-1).pow(-0.5)
+    dinv[dinv == float("inf")] = 0
+    lei = plan.local_edge_index
+    return dinv[lei[0]] * w_local * dinv[lei[1]]
+
+
 class OverlappedAggregation:
     """GCN-style sharded aggregation with the halo exchange hidden behind the
     interior edges.
@@ -231,13 +379,18 @@ class OverlappedAggregation:
     1e-5 bound of the single-GPU order, not bit-identical to it.
     """
 
-    def __init__(self, plan, edge_weight=None, chunk=None):
+    def __init__(self, plan, edge_weight=None, chunk=None, local_weights=False):
+        """edge_weight: per-edge weights of the list the plan was built from
+        (indexed by plan.edge_pos); local_weights=True: already in the plan's
+        local edge order."""
         from .graph import Graph
         self.plan = plan
         lei = plan.local_edge_index
         src_local = lei[0]
         interior = src_local < plan.n_own
-        w = edge_weight[plan.edge_pos] if edge_weight is not None else None
+        w = None
+        if edge_weight is not None:
+            w = edge_weight if local_weights else edge_weight[plan.edge_pos]
         ei_int = lei[:, interior]
         ei_bnd = lei[:, ~interior]
         self.g_int = Graph(ei_int, plan.n_own, plan.n_own, chunk=chunk)
@@ -267,7 +420,7 @@ class OverlappedAggregation:
                        out=out)
         return out
 
-    def step_tiled(self, x_tiles, out, bias=None, group=None):
+    def step_tiled(self, x_tiles, out, bias=None, group=None, events=None):
         """step() pipelined over feature tiles (x_tiles from plan.local_tiles):
           1. pack every tile's requested rows and start its all_to_all (RCCL
              runs them back to back on its stream while the compute stream
@@ -276,7 +429,18 @@ class OverlappedAggregation:
           3. per tile, wait for ITS halo only, then aggregate its boundary
              edges on top (MP_FLAG_INIT_FROM_OUT) plus that tile's bias.
         Tile t's boundary pass overlaps tile t+1's exchange.  Per row and
-        feature the arithmetic is that of step(): bitwise the same output."""
+        feature the arithmetic is that of step(): bitwise the same output.
+        events (optional dict of lists): HIP events recorded on the compute
+        stream -- 'interior' (start, end) of the interior passes, 'wait'
+        (before, after) around each tile's wait (the exchange time the compute
+        stream is exposed to), 'boundary' (start, end) of each boundary pass."""
+        def rec(name):
+            if events is None:
+                return None
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            events.setdefault(name, []).append(e)
+            return e
         from . import _lib, ops
         plan = self.plan
         gloo = out.is_cuda and dist.get_backend(group) == "gloo"
@@ -298,16 +462,22 @@ class OverlappedAggregation:
                 work = dist.all_to_all_single(halo, send, output_split_sizes=plan.recv_counts,
                                               input_split_sizes=plan.send_counts, group=group, async_op=True)
                 pending.append((work, send))
+        rec("interior")
         for t, xt in enumerate(x_tiles):
             ops._aggregate(self.g_int.dst, "other", xt[:plan.n_own], self.w_int, "sum", 0, None,
                            out=out[:, offs[t]:offs[t + 1]])
+        rec("interior")
         for t, xt in enumerate(x_tiles):
             work, _send = pending[t]
+            rec("wait")
             if work is not None:
                 work.wait()
+            rec("wait")
+            rec("boundary")
             b = bias[offs[t]:offs[t + 1]] if bias is not None else None
             ops._aggregate(self.g_bnd.dst, "other", xt, self.w_bnd, "sum", _lib.MP_FLAG_INIT_FROM_OUT, b,
                            out=out[:, offs[t]:offs[t + 1]])
+            rec("boundary")
         return out
 
 
@@ -354,6 +524,44 @@ class ShardedGraph:
         ei2, norm = GCNConv.norm(edge_index, num_nodes, edge_weight, improved)
         return cls(ei2, num_nodes, rank, world, group=group, chunk=chunk).set_edge_weight(norm)
 
+    @classmethod
+    def for_gcn_from_slices(cls, edge_slice, slice_offset, num_nodes, rank, world, group=None, improved=False,
+                            edge_weight=None, chunk=None):
+        """for_gcn() for a graph held as per-rank slices of its edge list (rank r:
+        the global edges [slice_offset, slice_offset + n_r), slices contiguous in
+        rank order; edge_weight aligned with the slice): the loops, degrees and
+        both plans are built from the slices with all_to_alls (gcn_shards_from_slices);
+        the local edge lists, global edge ids and norms are those of for_gcn()
+        bit for bit."""
+        from .graph import Graph
+        d = gcn_shards_from_slices(edge_slice, slice_offset, num_nodes, rank, world, group, edge_weight, improved)
+        self = cls.__new__(cls)
+        self.group = group
+        self.num_nodes = int(num_nodes)
+        self.n_edges = int(d["E"])
+        f_ei, f_gid, f_w = d["fwd"]
+        b_ei, b_gid, b_w = d["bwd"]
+        self.fwd = ShardPlan(f_ei, num_nodes, rank, world, cuts=d["cuts"], edge_ids=f_gid).exchange_requests(group)
+        self.bwd = ShardPlan(b_ei, num_nodes, rank, world, cuts=d["cuts"], flow="target_to_source",
+                             edge_ids=b_gid).exchange_requests(group)
+        self.lo, self.hi, self.n_own = self.fwd.lo, self.fwd.hi, self.fwd.n_own
+        self.g_fwd = Graph(self.fwd.local_edge_index, self.n_own, self.fwd.n_local_src, chunk=chunk)
+        self.g_bwd = Graph(self.bwd.local_edge_index, self.n_own, self.bwd.n_local_src,
+                           flow="target_to_source", chunk=chunk)
+        self.deg = d["deg"]
+        self.norm_fwd = _norm_over_plan(self.fwd, d["deg"], f_w[self.fwd.edge_pos], group)
+        self.norm_bwd = _norm_over_plan(self.bwd, d["deg"], b_w[self.bwd.edge_pos], group)
+        self._w = None
+        if self.norm_fwd.is_cuda:
+            self._set_local_weights(self.norm_fwd, self.norm_bwd)
+        return self
+
+    def _set_local_weights(self, w_fwd, w_bwd):
+        """Per-edge weights already in each plan's local edge order."""
+        self._w = (self.g_fwd.dst.to_csr_order(w_fwd.contiguous()), self.g_bwd.dst.to_csr_order(w_bwd.contiguous()),
+                   w_fwd.contiguous())
+        return self
+
     def set_edge_weight(self, edge_weight):
         """Per-edge weights in GLOBAL edge order (e.g. the GCN norm), permuted
         once into both local CSR orders."""
@@ -363,10 +571,7 @@ class ShardedGraph:
         if edge_weight.requires_grad:
             raise NotImplementedError("mi355_mp.dist: edge weights of a sharded graph carry no gradient")
         w = edge_weight.to(torch.float32)
-        w_fwd = w[self.fwd.edge_pos].contiguous()
-        self._w = (self.g_fwd.dst.to_csr_order(w_fwd), self.g_bwd.dst.to_csr_order(w[self.bwd.edge_pos].contiguous()),
-                   w_fwd)
-        return self
+        return self._set_local_weights(w[self.fwd.edge_pos], w[self.bwd.edge_pos])
 
     def propagate(self, x_own, reduce="sum"):
         """Sharded MessagePassing.propagate for message = w * x_j: this rank's

@@ -107,3 +107,79 @@ def test_edge_balanced_cuts():
     assert cuts[1] in (1, 2, 7)
     cuts = edge_balanced_cuts(torch.ones(10, dtype=torch.long), 5)
     assert cuts == [0, 2, 4, 6, 8, 10]
+
+
+def _slices_worker(rank, world, port, result_q):
+    """gcn_shards_from_slices / ShardedGraph.for_gcn_from_slices: every rank
+    holds only its contiguous slice of the edge list; the cuts, the rank's local
+    edge lists (in-edges and out-edges, global order), their global ids and the
+    GCN norms must equal the plans built from the full list and the oracle's
+    norm bit for bit -- weighted, with duplicate pre-existing self loops (the
+    last one's weight wins) -- and the sharded propagate must equal the
+    single-process oracle."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "pytorch_geometric-1_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mi355_mp import dist as mdist
+        from mi355_mp.graphgen import powerlaw_edge_index
+        from oracle import pyg_ref as P, scatter_ref as S
+        N, E, F = 700, 9000, 5
+        ei = powerlaw_edge_index(N, E, seed=23)
+        g = torch.Generator().manual_seed(23)
+        loops = torch.randint(N, (40,), generator=g)
+        loops = torch.cat([loops, loops[:10]])                       # duplicate loops of some nodes
+        ei = torch.cat([ei, torch.stack([loops, loops])], 1)
+        ei = ei[:, torch.randperm(ei.shape[1], generator=g)]
+        E = ei.shape[1]
+        w = torch.rand(E, generator=g) * 2
+        ok = {}
+        for improved, weighted in ((False, False), (True, True), (False, True)):
+            ww = w if weighted else None
+            s0, s1 = rank * E // world, (rank + 1) * E // world
+            sg = mdist.ShardedGraph.for_gcn_from_slices(ei[:, s0:s1].clone(), s0, N, rank, world, improved=improved,
+                                                         edge_weight=None if ww is None else ww[s0:s1].clone())
+            ei2, norm = P.gcn_norm(ei, N, ww, improved)
+            cuts = mdist.edge_balanced_cuts(torch.bincount(ei2[1], minlength=N), world)
+            rf = mdist.ShardPlan(ei2, N, rank, world, cuts=cuts)
+            rb = mdist.ShardPlan(ei2, N, rank, world, cuts=cuts, flow="target_to_source")
+            key = (improved, weighted)
+            ok[key] = (sg.fwd.cuts == cuts and sg.n_edges == ei2.shape[1]
+                       and torch.equal(sg.fwd.local_edge_index, rf.local_edge_index)
+                       and torch.equal(sg.fwd.edge_gid, rf.edge_pos)
+                       and torch.equal(sg.bwd.local_edge_index, rb.local_edge_index)
+                       and torch.equal(sg.bwd.edge_gid, rb.edge_pos)
+                       and torch.equal(sg.norm_fwd, norm[rf.edge_pos])
+                       and torch.equal(sg.norm_bwd, norm[rb.edge_pos]))
+            # the sharded propagate over the slice-built plan == the single-process oracle
+            x = torch.randn(N, F, generator=torch.Generator().manual_seed(5))
+
+            def local_aggregate(xl, lei, n_dst, n_src, wl):
+                return S.gather_sum(xl, lei[0], lei[1], wl, n_dst)
+            out = mdist.sharded_propagate(sg.fwd, x[sg.lo:sg.hi].contiguous(), local_aggregate,
+                                          lambda t, idx: t[idx], edge_weight=sg.norm_fwd)
+            want = S.gather_sum(x, ei2[0], ei2[1], norm, N)[sg.lo:sg.hi]
+            ok[key] = ok[key] and torch.equal(out, want)
+        result_q.put((rank, all(ok.values()), {str(k): v for k, v in ok.items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4])
+def test_gcn_shards_from_edge_slices_match_full_list(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_slices_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+        assert p.exitcode == 0
+    res = sorted(q.get(timeout=10) for _ in range(world))
+    assert all(r[1] for r in res), res

@@ -113,6 +113,15 @@ def _layer_worker(rank, world, port, q):
         out_ref = ref(xr, ei)
         (out_ref * gout).sum().backward()
         sg = mdist.ShardedGraph.for_gcn(ei, N, rank, world)
+        # the same shards built from per-rank slices of the edge list (native
+        # serial degree, exact deg^-1/2, degree halo exchange): bit-equal plans and norms
+        s0, s1 = rank * ei.shape[1] // world, (rank + 1) * ei.shape[1] // world
+        sgs = mdist.ShardedGraph.for_gcn_from_slices(ei[:, s0:s1].clone(), s0, N, rank, world)
+        slices_equal = (sgs.fwd.cuts == sg.fwd.cuts and sgs.n_edges == sg.n_edges
+                        and torch.equal(sgs.fwd.local_edge_index, sg.fwd.local_edge_index)
+                        and torch.equal(sgs.fwd.edge_gid, sg.fwd.edge_pos)
+                        and torch.equal(sgs.bwd.local_edge_index, sg.bwd.local_edge_index)
+                        and torch.equal(sgs._w[0], sg._w[0]) and torch.equal(sgs._w[1], sg._w[1]))
         conv = mdist.ShardedGCNConv(Fi, Fo).to(dev)
         conv.load_state_dict(ref.state_dict())
         lo, hi = sg.lo, sg.hi
@@ -157,6 +166,7 @@ def _layer_worker(rank, world, port, q):
         res["gmax_exact"] = bool(torch.equal(grads[0], xf.grad[lo:hi]))
         res["gmax_repeat"] = bool(torch.equal(grads[0], grads[1])) and bool(torch.equal(grads[2], grads[3]))
         res["max_exact"] = exact
+        res["slices_equal"] = bool(slices_equal)
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -190,6 +200,7 @@ def test_sharded_gcnconv_forward_backward_on_one_gpu():
         assert r["out"] < 1e-5 and r["gx"] < 1e-5, r
         assert r["gw"] < 1e-5 and r["gb"] < 1e-5, r
         assert r["max_exact"], r
+        assert r["slices_equal"], r
         assert r["gmax_exact"] and r["gmax_repeat"], r   # deterministic on both sides (round 3)
 
 
@@ -340,6 +351,10 @@ def _rccl_worker(rank, world, port, q):
         xr = xi.clone().requires_grad_(True)
         (conv_ref(xr, ei) * gout).sum().backward()
         sg = mdist.ShardedGraph.for_gcn(ei, N, rank, world)
+        # the slice-built shards over RCCL (all_gather_object, all_reduce, all_to_all of edges)
+        sgs = mdist.ShardedGraph.for_gcn_from_slices(ei.clone(), 0, N, rank, world)
+        slices_equal = (sgs.n_edges == sg.n_edges and torch.equal(sgs.fwd.local_edge_index, sg.fwd.local_edge_index)
+                        and torch.equal(sgs._w[0], sg._w[0]) and torch.equal(sgs._w[1], sg._w[1]))
         conv = mdist.ShardedGCNConv(Fi, F).to(dev)
         conv.load_state_dict(conv_ref.state_dict())
         mdist.broadcast_parameters(conv)
@@ -360,6 +375,7 @@ def _rccl_worker(rank, world, port, q):
             wo, wa = ops._aggregate(g1.dst, "other", xm, None, red, 0, None)
             exact = exact and bool(torch.equal(om, wo)) and bool(torch.equal(am, wa))
         res["max_exact"] = exact
+        res["slices_equal"] = bool(slices_equal)
         torch.cuda.synchronize()
         q.put((rank, res))
     finally:
@@ -379,6 +395,7 @@ def test_sharded_path_over_rccl_world_one():
     assert r["step"] < 1e-5 and r["tiled_eq_step"], r
     assert r["layer_out"] < 1e-5 and r["layer_gx"] < 1e-5 and r["layer_gw"] < 1e-5, r
     assert r["max_exact"], r
+    assert r["slices_equal"], r
 
 
 def test_bench_multi_rank_path_end_to_end():
@@ -406,3 +423,8 @@ def test_bench_multi_rank_path_end_to_end():
     ex = d["extra"]
     assert ex["overlap"] and ex["halo_tile"] == 128 and ex["halo_rows_rank0"] > 0
     assert 0 < ex["interior_edges_rank0"] < ex["edges_local_rank0"] < d["config"]["num_edges"]
+    pr = ex["per_rank"]
+    assert [p["rank"] for p in pr] == [0, 1] and sum(p["edges"] for p in pr) == d["config"]["num_edges"]
+    for p in pr:
+        assert p["halo_bytes_in"] == p["halo_rows"] * 256 * 4 and p["halo_bytes_out"] > 0
+        assert p["interior_ms"] > 0 and p["boundary_ms"] > 0 and p["exchange_exposed_ms"] >= 0
