@@ -228,6 +228,18 @@ int mp_gat_aggregate_att_f32(const mp_csr* g, const float* xw, const float* a_sr
                              int64_t ldo, float* row_stats, void* slab,
                              size_t slab_bytes, int32_t stages, void* stream);
 
+/* The same forward with the node scores computed in-kernel (C % 4 == 0 and
+ * C/4 a power of two <= 64: mp_gat_train_ok; xw, att, bias, out 16-byte
+ * aligned; the graph square -- row i's own xw is row i of xw): a_src / a_dst
+ * [n_rows, H] are OUTPUTS, each destination row's scores reduced from its own
+ * xw row with mp_gat_node_scores_f32's arithmetic (bitwise its values), so no
+ * separate node-score pass over xw runs.  a_src is also recomputed from every
+ * gathered row (as mp_gat_aggregate_att_f32).  (ABI 3) */
+int mp_gat_forward_f32(const mp_csr* g, const float* xw, const float* att, int32_t H,
+                       int32_t C, float slope, const float* bias, float* out, int64_t ldo,
+                       float* a_src, float* a_dst, float* row_stats, void* slab,
+                       size_t slab_bytes, int32_t stages, void* stream);
+
 /* Training forward of the same layer (att given, C % 4 == 0, C/4 a power of two
  * <= 64: mp_gat_train_ok).  out = aggregate + bias (bias may be NULL); agg
  * (NULL allowed without a bias) receives the pre-bias aggregate [n_rows, H*C]
@@ -246,6 +258,13 @@ int mp_gat_aggregate_train_f32(const mp_csr* g, const float* xw, const float* a_
                                float slope, const float* bias, float* out, int64_t ldo,
                                float* agg, float* row_stats, float* out2, float* row_s2,
                                void* slab, size_t slab_bytes, int32_t stages, void* stream);
+/* mp_gat_aggregate_train_f32 with the node scores computed in-kernel (the
+ * outputs a_src / a_dst, as mp_gat_forward_f32). */
+int mp_gat_forward_train_f32(const mp_csr* g, const float* xw, const float* att, int32_t H,
+                             int32_t C, float slope, const float* bias, float* out, int64_t ldo,
+                             float* agg, float* row_stats, float* out2, float* row_s2,
+                             float* a_src, float* a_dst, void* slab, size_t slab_bytes,
+                             int32_t stages, void* stream);
 
 /* Two-pass form of the same layer, in the reference's own arithmetic
  * (utils.softmax [U3] then message x_j * alpha and scatter_add in edge order,

@@ -114,6 +114,8 @@ struct AggArgs {
   // GAT
   const float* a_src;
   const float* a_dst;
+  float* a_src_out;   // GAT forward with in-kernel node scores (GatRed ND): written per owned row
+  float* a_dst_out;
   int32_t H;
   int32_t C;
   float slope;
@@ -359,12 +361,21 @@ struct ArgRed {
 //   d a_dst[i,h] = sum_j de_ij = <g_i, acc2_i>_h - rs_i s2_i
 // (de_ij = alpha_ij (<g_i, xw_j> - rs_i) leaky'_ij), so the backward writes no
 // per-edge d score and needs no segmented pass over it.
-template <int VEC, bool OWN = false, bool TR = false>
+//
+// ND (node scores, needs OWN): a_dst[i, h] and a_src[i, h] of each destination
+// row come from the row's own xw, loaded at begin() and reduced at the first
+// slot (its load completes before the first gathered row's, so the wait is
+// hidden) with the node-score kernel's arithmetic -- bitwise its values; the
+// row's owner task writes both to a_src_out / a_dst_out, so no separate
+// node-score pass over xw is needed.
+template <int VEC, bool OWN = false, bool TR = false, bool ND = false>
 struct GatRed {
+  static_assert(!ND || OWN, "in-kernel node scores reuse the own-a_src reduction");
   static constexpr bool kW = false;
   static constexpr bool kEid = false;
   static constexpr bool kGat = true;
   static constexpr bool kOwnAs = OWN;
+  static constexpr bool kNodeScores = ND;
   static constexpr bool kHW = false;
   static constexpr bool kGatB = false;
   static constexpr bool kStat = true;
@@ -381,6 +392,10 @@ struct GatRed {
   int h;
   [[maybe_unused]] float y[OWN ? VEC : 1];
   [[maybe_unused]] int hl = 1;
+  [[maybe_unused]] Frag<ND ? VEC : 1> rowv;  // the destination row's own xw (ND)
+  [[maybe_unused]] bool need_ad = false, own_row = false, lead = false;
+  [[maybe_unused]] int c_ = 0;               // this lane's first feature within its head (ND)
+  [[maybe_unused]] int64_t row_ = 0;
 
   __device__ GatRed(const AggArgs& p, int f, bool act) : h(act ? f / p.C : 0) {
     if constexpr (OWN) {
@@ -389,6 +404,36 @@ struct GatRed {
       Frag<VEC> o = load_frag<VEC>(p.att + (int64_t)h * 2 * p.C + p.C + c);
 #pragma unroll
       for (int k = 0; k < VEC; ++k) y[k] = act ? o.v[k] : 0.f;
+      if constexpr (ND) {
+        c_ = c;
+        lead = act && c == 0;
+      }
+    }
+  }
+  // the row's scores from rowv; the owner writes them (every lane of the
+  // wave runs this together: the group sums are cross-lane)
+  __device__ __forceinline__ void node_scores(const AggArgs& p) {
+    if constexpr (ND) {
+      // att_dst slice: an L1-resident 16-B load per row rather than 4 VGPRs held
+      // through the slot loop (keeps the kernel at the OWN path's occupancy)
+      const Frag<VEC> yd = load_frag<VEC>(p.att + (int64_t)h * 2 * p.C + c_);
+      float t = rowv.v[0] * yd.v[0];
+#pragma unroll
+      for (int k = 1; k < VEC; ++k) t = t + rowv.v[k] * yd.v[k];
+      ad = group_sum(t, hl);
+      const float as_own = own_as(rowv);
+      need_ad = false;
+      if (own_row && lead) {
+        p.a_dst_out[row_ * p.H + h] = ad;
+        p.a_src_out[row_ * p.H + h] = as_own;
+      }
+    }
+  }
+  // before a partial of an owned row is saved (its task may have seen none of
+  // its slots): make sure the row's scores were written
+  __device__ __forceinline__ void flush_scores(const AggArgs& p) {
+    if constexpr (ND) {
+      if (need_ad) node_scores(p);
     }
   }
   // <row, att_src> over the head's lanes: v.x*y.x + v.y*y.y + ... separately
@@ -400,7 +445,7 @@ struct GatRed {
     return group_sum(t, hl);
   }
 
-  __device__ __forceinline__ void begin(const AggArgs& p, int64_t row, bool, int, bool) {
+  __device__ __forceinline__ void begin(const AggArgs& p, int64_t row, bool owned, int f, bool act) {
 #pragma unroll
     for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
     if constexpr (TR) {
@@ -410,9 +455,19 @@ struct GatRed {
     }
     m = -INFINITY;
     s = 0.f;
-    ad = p.a_dst[row * p.H + h];
+    if constexpr (ND) {
+      rowv = load_frag<VEC>(p.x + row * p.ldx + (act ? f : 0));
+      need_ad = true;
+      own_row = owned;
+      row_ = row;
+    } else {
+      ad = p.a_dst[row * p.H + h];
+    }
   }
   __device__ __forceinline__ void consume_gat(const AggArgs& p, const Frag<VEC>& v, float as) {
+    if constexpr (ND) {
+      if (need_ad) node_scores(p);
+    }
     float a = as + ad;
     [[maybe_unused]] const bool pos = a > 0.f;  // leaky' = 1 : slope (the backward's test)
     a = a > 0.f ? a : a * p.slope;  // F.leaky_relu
@@ -505,6 +560,9 @@ struct GatRed {
     return q;
   }
   __device__ __forceinline__ void finish(const AggArgs& p, int64_t row, int64_t, int f, bool act) {
+    if constexpr (ND) {
+      if (need_ad) node_scores(p);  // a row without slots (the fix-up never begins a row: need_ad false)
+    }
     if (!act) return;
     Frag<VEC> o;
     float den = s + 1e-16f;
@@ -993,14 +1051,18 @@ struct GatAlphaWin {
 // GAT forward: a_src of each 64-slot window staged in LDS (see SlotWin; 8.85 -> 8.66 ms, bitwise the same)
 template <class Red>
 constexpr bool own_as_v = false;
-template <int VEC, bool TR>
-constexpr bool own_as_v<GatRed<VEC, true, TR>> = true;
+template <int VEC, bool TR, bool ND>
+constexpr bool own_as_v<GatRed<VEC, true, TR, ND>> = true;
 template <class Red, int L>
 constexpr bool kGatWin = Red::kGat && !own_as_v<Red> && L == 64;
 template <class Red>
 constexpr bool kGatTrain = false;
-template <int VEC, bool OWN>
-constexpr bool kGatTrain<GatRed<VEC, OWN, true>> = true;
+template <int VEC, bool OWN, bool ND>
+constexpr bool kGatTrain<GatRed<VEC, OWN, true, ND>> = true;
+template <class Red>
+constexpr bool kNodeScoresV = false;
+template <int VEC, bool OWN, bool TR, bool ND>
+constexpr bool kNodeScoresV<GatRed<VEC, OWN, TR, ND>> = ND;
 
 template <class Red, int VEC, int U, int L>
 __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p,
@@ -1121,6 +1183,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_main(AggArgs p) {
       red.finish(p, r, re - rs, f, act);
     } else {
       run_slots<Red, VEC, U, L>(red, p, win, rs, e_end, foff, gl);
+      if constexpr (kNodeScoresV<Red>) red.flush_scores(p);
       if (act) red.save(slab_ref(p, 2 * (int64_t)w + 1, f, red), Red::kStat && (f % p.C == 0));
     }
   }
@@ -1967,16 +2030,53 @@ int mp_gat_aggregate_att_f32(const mp_csr* g, const float* xw, const float* a_sr
   }
 }
 
-int mp_gat_aggregate_train_f32(const mp_csr* g, const float* xw, const float* a_src, const float* a_dst,
-                               const float* att, int32_t H, int32_t C, float slope, const float* bias, float* out,
-                               int64_t ldo, float* agg, float* row_stats, float* out2, float* row_s2, void* slab,
-                               size_t slab_bytes, int32_t stages, void* stream) {
+int mp_gat_forward_f32(const mp_csr* g, const float* xw, const float* att, int32_t H, int32_t C, float slope,
+                       const float* bias, float* out, int64_t ldo, float* a_src, float* a_dst, float* row_stats,
+                       void* slab, size_t slab_bytes, int32_t stages, void* stream) {
+  MP_DEVICE_GUARD(stream);
+  int rc = check_graph(g, "mp_gat_forward_f32");
+  if (rc) return rc;
+  MP_CHECK_ARG(mp_gat_train_ok(H, C), "mp_gat_forward_f32: needs C %% 4 == 0 and C/4 a power of two <= 64");
+  MP_CHECK_ARG(xw && att && out && a_src && a_dst, "mp_gat_forward_f32: null pointer");
+  MP_CHECK_ARG(g->n_cols == g->n_rows, "mp_gat_forward_f32: the graph must be square (row i's own xw is row i)");
+  const int F = H * C;
+  MP_CHECK_ARG(ldo >= F && ldo % 4 == 0, "mp_gat_forward_f32: ldo < H*C or not a multiple of 4");
+  MP_CHECK_ARG((uintptr_t)xw % 16 == 0 && (uintptr_t)att % 16 == 0 && (uintptr_t)out % 16 == 0 &&
+                   (uintptr_t)bias % 16 == 0,
+               "mp_gat_forward_f32: xw, att, bias, out must be 16-byte aligned");
+  MP_CHECK_ARG(slab != nullptr && slab_bytes >= mp_gat_slab_bytes(g, H, C),
+               "mp_gat_forward_f32: slab workspace too small");
+  AggArgs a{};
+  fill_graph(a, g);
+  a.F = F;
+  a.x = xw;
+  a.ldx = F;
+  a.out = out;
+  a.ldo = ldo;
+  a.bias = bias;
+  a.a_src_out = a_src;
+  a.a_dst_out = a_dst;
+  a.att = att;
+  a.H = H;
+  a.C = C;
+  a.slope = slope;
+  a.row_stats = row_stats;
+  a.slab_ld = slab_ld_for(F);
+  size_t v = align_up(2 * (size_t)g->n_waves * (size_t)a.slab_ld * 4, 256);
+  a.slab_v = (float*)slab;
+  a.slab_s = (float*)((char*)slab + v);
+  return launch<GatRed<4, true, false, true>, 4>(a, stages, as_stream(stream), F >= 256 ? kGatLanes : 64);
+}
+
+static int gat_train(const mp_csr* g, const float* xw, const float* a_src, const float* a_dst, const float* att,
+                     int32_t H, int32_t C, float slope, const float* bias, float* out, int64_t ldo, float* agg,
+                     float* row_stats, float* out2, float* row_s2, void* slab, size_t slab_bytes, int32_t stages,
+                     void* stream, float* as_out, float* ad_out) {
   MP_DEVICE_GUARD(stream);
   int rc = check_graph(g, "mp_gat_aggregate_train_f32");
   if (rc) return rc;
   MP_CHECK_ARG(mp_gat_train_ok(H, C), "mp_gat_aggregate_train_f32: needs C %% 4 == 0 and C/4 a power of two <= 64");
-  MP_CHECK_ARG(xw && a_src && a_dst && att && out && row_stats && out2 && row_s2,
-               "mp_gat_aggregate_train_f32: null input");
+  MP_CHECK_ARG(xw && att && out && row_stats && out2 && row_s2, "mp_gat_aggregate_train_f32: null input");
   const int F = H * C;
   MP_CHECK_ARG(ldo >= F, "mp_gat_aggregate_train_f32: ldo < H*C");
   MP_CHECK_ARG((uintptr_t)xw % 16 == 0 && (uintptr_t)att % 16 == 0 && (uintptr_t)out % 16 == 0 && ldo % 4 == 0 &&
@@ -2003,6 +2103,8 @@ int mp_gat_aggregate_train_f32(const mp_csr* g, const float* xw, const float* a_
   a.row_s2 = row_s2;
   a.bias = bias;
   a.agg_nb = agg;
+  a.a_src_out = as_out;  // mp_gat_forward_train_f32: node scores in-kernel
+  a.a_dst_out = ad_out;
   a.slab_ld = slab_ld_for(F);
   const size_t slots = 2 * (size_t)g->n_waves;
   char* b = (char*)slab;
@@ -2012,7 +2114,27 @@ int mp_gat_aggregate_train_f32(const mp_csr* g, const float* xw, const float* a_
   b += mp_gat_slab_bytes(g, H, C);
   a.slab_v2 = (float*)b;
   a.slab_s2 = (float*)(b + v);
+  if (a.a_src_out) return launch<GatRed<4, true, true, true>, 4>(a, stages, as_stream(stream), F >= 256 ? kGatLanes : 64);
   return launch<GatRed<4, true, true>, 4>(a, stages, as_stream(stream), F >= 256 ? kGatLanes : 64);
+}
+
+int mp_gat_aggregate_train_f32(const mp_csr* g, const float* xw, const float* a_src, const float* a_dst,
+                               const float* att, int32_t H, int32_t C, float slope, const float* bias, float* out,
+                               int64_t ldo, float* agg, float* row_stats, float* out2, float* row_s2, void* slab,
+                               size_t slab_bytes, int32_t stages, void* stream) {
+  MP_CHECK_ARG(a_src && a_dst, "mp_gat_aggregate_train_f32: null input");
+  return gat_train(g, xw, a_src, a_dst, att, H, C, slope, bias, out, ldo, agg, row_stats, out2, row_s2, slab,
+                   slab_bytes, stages, stream, nullptr, nullptr);
+}
+
+int mp_gat_forward_train_f32(const mp_csr* g, const float* xw, const float* att, int32_t H, int32_t C, float slope,
+                             const float* bias, float* out, int64_t ldo, float* agg, float* row_stats, float* out2,
+                             float* row_s2, float* a_src, float* a_dst, void* slab, size_t slab_bytes,
+                             int32_t stages, void* stream) {
+  MP_CHECK_ARG(a_src && a_dst, "mp_gat_forward_train_f32: null a_src / a_dst");
+  MP_CHECK_ARG(!g || g->n_cols == g->n_rows, "mp_gat_forward_train_f32: the graph must be square");
+  return gat_train(g, xw, a_src, a_dst, att, H, C, slope, bias, out, ldo, agg, row_stats, out2, row_s2, slab,
+                   slab_bytes, stages, stream, a_src, a_dst);
 }
 
 int mp_gat_two_pass_ok(int32_t H, int32_t C) {

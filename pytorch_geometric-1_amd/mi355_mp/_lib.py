@@ -74,6 +74,10 @@ SIGNATURES = {
                                             c_p, i64, c_p, c_p, sz, i32, c_p]),
     "mp_gat_aggregate_att_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, c_p, c_p, i32, i32, f32, c_p,
                                                 c_p, i64, c_p, c_p, sz, i32, c_p]),
+    "mp_gat_forward_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, i32, i32, f32, c_p, c_p, i64, c_p, c_p,
+                                          c_p, c_p, sz, i32, c_p]),
+    "mp_gat_forward_train_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, i32, i32, f32, c_p, c_p, i64, c_p,
+                                                c_p, c_p, c_p, c_p, c_p, c_p, sz, i32, c_p]),
     "mp_gat_train_ok": (ctypes.c_int, [i32, i32]),
     "mp_gat_train_slab_bytes": (sz, [ctypes.POINTER(MpCsr), i32, i32]),
     "mp_gat_aggregate_train_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, c_p, c_p, i32, i32, f32,

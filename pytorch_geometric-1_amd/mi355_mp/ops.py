@@ -11,6 +11,8 @@ torch_geometric 1.4.3; see oracle/ for the CPU restatement used as checker):
   * max/min   : (out, arg); strict compare, first edge wins ties, empty row
                 -> (0, src.size(0)); scatter_(...) also masks <-10000 / >10000
 """
+import os
+
 import torch
 
 from . import _lib
@@ -527,6 +529,16 @@ def gat_two_pass(csr, H, C):
 # sum_j alpha leaky' per (row, head) (mp_gat_aggregate_train_f32), which make the
 # backward's d a_dst node-wise: no per-edge d score array, no segmented pass.
 GAT_TRAIN_FWD = True
+# The fused forward computes each row's node scores (a_src, a_dst) from the
+# row's own xw (mp_gat_forward_f32 / mp_gat_forward_train_f32, bitwise the
+# node-score kernel's values) instead of running mp_gat_node_scores_f32 first.
+GAT_NODE_SCORES_IN_KERNEL = os.environ.get("MP_GAT_ND", "1") != "0"   # MP_GAT_ND=0: A/B runs
+
+
+def _gat_nd_ok(graph, xw, H, C, bias):
+    return (GAT_NODE_SCORES_IN_KERNEL and GAT_OWN_A_SRC and bool(_lib.load().mp_gat_train_ok(H, C))
+            and not gat_two_pass(graph.dst, H, C) and xw.data_ptr() % 16 == 0 and graph.n_dst == xw.shape[0]
+            and graph.n_src == xw.shape[0] and (bias is None or bias.data_ptr() % 16 == 0))
 
 
 def _gat_train_fwd_ok(graph, xw, H, C):
@@ -549,14 +561,27 @@ def _gat_forward(graph, edge_index, xw, att, H, C, slope, bias, want_alpha, trai
     att_c = att.reshape(H, 2 * C).contiguous().to(torch.float32)
     a_src = torch.empty((N, H), dtype=torch.float32, device=dev)
     a_dst = torch.empty((N, H), dtype=torch.float32, device=dev)
-    if N:
+    nd = _gat_nd_ok(graph, xw, H, C, bias)
+    if N and not nd:
         _lib.check(lib.mp_gat_node_scores_f32(xw.data_ptr(), N, H, C, att_c.data_ptr(), a_src.data_ptr(),
                                               a_dst.data_ptr(), st), "mp_gat_node_scores_f32")
     out = torch.empty((graph.n_dst, H * C), dtype=torch.float32, device=dev)
     stats = torch.empty((graph.n_dst, H, 2), dtype=torch.float32, device=dev)
     g = csr.struct("other")
     extra = None
-    if train2:
+    if train2 and nd:
+        agg2 = torch.empty((graph.n_dst, H * C), dtype=torch.float32, device=dev)
+        s2 = torch.empty((graph.n_dst, H), dtype=torch.float32, device=dev)
+        agg = torch.empty_like(out) if bias is not None else out
+        sb = lib.mp_gat_train_slab_bytes(g, H, C)
+        slab = torch.empty(sb, dtype=torch.uint8, device=dev)
+        _lib.check(lib.mp_gat_forward_train_f32(g, xw.data_ptr(), att_c.data_ptr(), H, C, float(slope), _lib.ptr(bias),
+                                                out.data_ptr(), out.stride(0),
+                                                agg.data_ptr() if bias is not None else None, stats.data_ptr(),
+                                                agg2.data_ptr(), s2.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(),
+                                                slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st), "mp_gat_forward_train_f32")
+        extra = (agg2, s2, agg)
+    elif train2:
         agg2 = torch.empty((graph.n_dst, H * C), dtype=torch.float32, device=dev)
         s2 = torch.empty((graph.n_dst, H), dtype=torch.float32, device=dev)
         agg = torch.empty_like(out) if bias is not None else out
@@ -572,7 +597,12 @@ def _gat_forward(graph, edge_index, xw, att, H, C, slope, bias, want_alpha, trai
     if extra is None:
         sb = lib.mp_gat_slab_bytes(g, H, C)
         slab = torch.empty(sb, dtype=torch.uint8, device=dev)
-        if gat_two_pass(csr, H, C):
+        if nd:
+            _lib.check(lib.mp_gat_forward_f32(g, xw.data_ptr(), att_c.data_ptr(), H, C, float(slope), _lib.ptr(bias),
+                                              out.data_ptr(), out.stride(0), a_src.data_ptr(), a_dst.data_ptr(),
+                                              stats.data_ptr(), slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
+                       "mp_gat_forward_f32")
+        elif gat_two_pass(csr, H, C):
             _lib.check(lib.mp_gat_softmax_aggregate_f32(g, csr.slot_rows().data_ptr(), xw.data_ptr(), a_src.data_ptr(),
                                                         a_dst.data_ptr(), H, C, float(slope), _lib.ptr(bias),
                                                         out.data_ptr(), out.stride(0), stats.data_ptr(), slab.data_ptr(),

@@ -2229,3 +2229,51 @@ def test_torch_scatter_dtype_elementwise_index_and_segment_ops():
         assert torch.equal(seg, ref) if dtype == torch.int64 else torch.allclose(seg, ref)
         gat = torch_scatter.gather_csr(seg.to(DEV), indptr.to(DEV)).cpu()
         assert torch.equal(gat, seg.repeat_interleave(counts, 0))
+
+
+@pytest.mark.parametrize("H,C,chunk", [(8, 32, 64), (4, 16, 16), (2, 64, 256), (1, 256, 64), (16, 32, 16),
+                                       (8, 32, 1024)])
+def test_gat_node_scores_in_kernel_bitwise(H, C, chunk, monkeypatch):
+    """mp_gat_forward_f32 / mp_gat_forward_train_f32 reduce each destination
+    row's a_src / a_dst from its own xw row inside the fused pass: the score
+    arrays, the outputs, the row statistics, alpha, the training extras and
+    every gradient bitwise equal to the path with the separate node-score
+    kernel (hub rows split across tasks; rows that start at a task boundary)."""
+    from torch_geometric.nn import GATConv
+    from mi355_mp import ops
+    _, _, _, Graph, pl = _mods()
+    N, Fi = 1500, 12
+    g = torch.Generator().manual_seed(53)
+    ei = pl(N, 20000, seed=53)
+    ei = torch.cat([ei, torch.stack([torch.randint(0, N, (4000,), generator=g), torch.zeros(4000, dtype=torch.long)])],
+                   1)
+    ei_l = P.add_self_loops(P.remove_self_loops(ei)[0], num_nodes=N)[0].to(DEV)
+    xw = torch.randn(N, H * C, generator=g).to(DEV)
+    att = (torch.randn(1, H, 2 * C, generator=g) * 0.3).to(DEV)
+    bias = torch.randn(H * C, generator=g).to(DEV)
+    graph = Graph(ei_l, N, N, chunk=chunk)
+    assert ops._gat_nd_ok(graph, xw, H, C, bias)
+    res = {}
+    for nd in (True, False):
+        monkeypatch.setattr(ops, "GAT_NODE_SCORES_IN_KERNEL", nd)
+        inf = ops._gat_forward(graph, ei_l, xw, att, H, C, 0.2, bias, True)
+        tr = ops._gat_forward(graph, ei_l, xw, att, H, C, 0.2, bias, True, train2=True)
+        res[nd] = (inf[:5], tr[:5], tr[5])
+    for a, b in zip(res[True][0] + res[True][1] + res[True][2], res[False][0] + res[False][1] + res[False][2]):
+        assert torch.equal(a, b)
+    # the layer, forward + backward, both paths bitwise equal
+    conv = GATConv(Fi, C, heads=H).to(DEV)
+    with torch.no_grad():
+        conv.bias.normal_()
+    x = torch.randn(N, Fi, generator=g).to(DEV)
+    gout = torch.randn(N, H * C, generator=g).to(DEV)
+    grads = {}
+    for nd in (True, False):
+        monkeypatch.setattr(ops, "GAT_NODE_SCORES_IN_KERNEL", nd)
+        conv.zero_grad()
+        xd = x.clone().requires_grad_(True)
+        out = conv(xd, ei.to(DEV))
+        out.backward(gout)
+        grads[nd] = [out.detach(), xd.grad, conv.weight.grad, conv.att.grad, conv.bias.grad]
+    for a, b in zip(grads[True], grads[False]):
+        assert torch.equal(a, b)

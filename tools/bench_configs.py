@@ -185,6 +185,14 @@ def c3(dev):
                                                     a_dst.data_ptr(), H, C, 0.2, bias.data_ptr(), out.data_ptr(),
                                                     H * C, stats.data_ptr(), slab.data_ptr(), sb, stages, st),
                    "gat2")
+    a_src2 = torch.empty(N, H, device=dev)
+    a_dst2 = torch.empty(N, H, device=dev)
+
+    def agg_nd(stages):
+        # the node scores reduced in-kernel from each row's own xw (mp_gat_forward_f32, ops.GAT_NODE_SCORES_IN_KERNEL)
+        _lib.check(lib.mp_gat_forward_f32(s, xw.data_ptr(), att_c.data_ptr(), H, C, 0.2, bias.data_ptr(),
+                                          out.data_ptr(), H * C, a_src2.data_ptr(), a_dst2.data_ptr(), None,
+                                          slab.data_ptr(), sb, stages, st), "gat_nd")
     scores()
     ms_scores = timed(scores)
     E = csr.n_edges
@@ -193,6 +201,10 @@ def c3(dev):
     ms_fix1 = timed(lambda: agg(_lib.MP_STAGE_FIXUP))
     agg(_lib.MP_STAGE_ALL)
     one = out.clone()
+    ms_main_nd = timed(lambda: agg_nd(_lib.MP_STAGE_MAIN))
+    ms_fix_nd = timed(lambda: agg_nd(_lib.MP_STAGE_FIXUP))
+    agg_nd(_lib.MP_STAGE_ALL)
+    nd_equal = bool(torch.equal(out, one)) and bool(torch.equal(a_src2, a_src)) and bool(torch.equal(a_dst2, a_dst))
     # two pass (row statistics, then 64-feature tiles with the reference's alpha)
     ms_stats = timed(lambda: agg2(_lib.MP_STAGE_STATS))
     ms_main = timed(lambda: agg2(_lib.MP_STAGE_MAIN))
@@ -203,6 +215,9 @@ def c3(dev):
     path = "two_pass" if ops.gat_two_pass(csr, H, C) else "one_pass"
     tot1 = ms_main1 + ms_fix1 + ms_scores
     tot2 = ms_stats + ms_main + ms_fix + ms_scores
+    tot_nd = ms_main_nd + ms_fix_nd
+    nd_info = {"main_kernel_ms": ms_main_nd, "fixup_ms": ms_fix_nd, "aggregate_ms": tot_nd,
+               "bitwise_equal_to_separate_scores": nd_equal}
     # compulsory: xw read once + a_src/a_dst + col + rowptr + out written once
     comp = N * H * C * 4 * 2 + N * H * 8 + E * 4 + (N + 1) * 4
     cpu = cpu_gat_baseline(ei, xw, att, H, C, 3_000_000) if CPU_BASELINE else None
@@ -213,10 +228,20 @@ def c3(dev):
                {"stats_ms": ms_stats, "fixup_ms": ms_fix, "node_scores_ms": ms_scores, "n_split": csr.n_split,
                 "one_pass": {"main_kernel_ms": ms_main1, "fixup_ms": ms_fix1, "aggregate_ms": tot1},
                 "max_rel_diff_two_vs_one_pass": diff}, comp, cpu)
+    elif ops.GAT_NODE_SCORES_IN_KERNEL:
+        report("c3", "RMAT21 GATConv heads=8 C=32, fused node scores + leaky_relu+softmax(+1e-16)+aggregate+bias "
+               "(mp_gat_forward_f32, the GATConv forward path)",
+               E, N, 4 * H * C + 4 + 4 * H, 4 * H * C + 4 * H + 4, ms_main_nd, tot_nd,
+               {"fixup_ms": ms_fix_nd, "n_split": csr.n_split, "bitwise_equal_to_separate_scores": nd_equal,
+                "separate_node_scores": {"node_scores_ms": ms_scores, "main_kernel_ms": ms_main1, "fixup_ms": ms_fix1,
+                                         "aggregate_ms": tot1},
+                "two_pass": {"stats_ms": ms_stats, "main_kernel_ms": ms_main, "fixup_ms": ms_fix,
+                             "aggregate_ms": tot2}}, comp, cpu)
     else:
         report("c3", "RMAT21 GATConv heads=8 C=32, fused leaky_relu+softmax(+1e-16)+aggregate+bias",
                E, N, 4 * H * C + 4 + 4 * H, 4 * H * C + 4 * H + 4, ms_main1, tot1,
                {"fixup_ms": ms_fix1, "node_scores_ms": ms_scores, "n_split": csr.n_split,
+                "node_scores_in_kernel": nd_info,
                 "two_pass": {"stats_ms": ms_stats, "main_kernel_ms": ms_main, "fixup_ms": ms_fix,
                              "aggregate_ms": tot2}}, comp, cpu)
     # parity spot check against the generic PyG formula on identical inputs (one row block)
