@@ -465,9 +465,6 @@ struct GatRed {
     }
   }
   __device__ __forceinline__ void consume_gat(const AggArgs& p, const Frag<VEC>& v, float as) {
-    if constexpr (ND) {
-      if (need_ad) node_scores(p);
-    }
     float a = as + ad;
     [[maybe_unused]] const bool pos = a > 0.f;  // leaky' = 1 : slope (the backward's test)
     a = a > 0.f ? a : a * p.slope;  // F.leaky_relu
@@ -1096,6 +1093,10 @@ __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p,
     if constexpr (Red::kGatB) {
 #pragma unroll
       for (int u = 0; u < U; ++u) as[u] = red.dot(v[u]);
+    }
+    if constexpr (kNodeScoresV<Red>) {
+      // the row's own scores, once, after this batch's loads are in flight
+      if (red.need_ad) red.node_scores(p);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {

@@ -532,7 +532,12 @@ GAT_TRAIN_FWD = True
 # The fused forward computes each row's node scores (a_src, a_dst) from the
 # row's own xw (mp_gat_forward_f32 / mp_gat_forward_train_f32, bitwise the
 # node-score kernel's values) instead of running mp_gat_node_scores_f32 first.
+# Config 3 (inference): main 7.78 ms, no 0.50 ms node-score pass -> 7.85 vs 8.30 ms.
 GAT_NODE_SCORES_IN_KERNEL = os.environ.get("MP_GAT_ND", "1") != "0"   # MP_GAT_ND=0: A/B runs
+# The training forward with in-kernel scores needs 92 VGPRs (5 waves / SIMD
+# instead of 6): GATConv forward + backward 26.49 vs 26.28 ms on config 3, so
+# training keeps the separate node-score pass (MP_GAT_ND_TRAIN=1 selects it).
+GAT_NODE_SCORES_IN_KERNEL_TRAIN = os.environ.get("MP_GAT_ND_TRAIN", "0") == "1"
 
 
 def _gat_nd_ok(graph, xw, H, C, bias):
@@ -561,7 +566,7 @@ def _gat_forward(graph, edge_index, xw, att, H, C, slope, bias, want_alpha, trai
     att_c = att.reshape(H, 2 * C).contiguous().to(torch.float32)
     a_src = torch.empty((N, H), dtype=torch.float32, device=dev)
     a_dst = torch.empty((N, H), dtype=torch.float32, device=dev)
-    nd = _gat_nd_ok(graph, xw, H, C, bias)
+    nd = _gat_nd_ok(graph, xw, H, C, bias) and (GAT_NODE_SCORES_IN_KERNEL_TRAIN or not train2)
     if N and not nd:
         _lib.check(lib.mp_gat_node_scores_f32(xw.data_ptr(), N, H, C, att_c.data_ptr(), a_src.data_ptr(),
                                               a_dst.data_ptr(), st), "mp_gat_node_scores_f32")

@@ -2254,6 +2254,7 @@ def test_gat_node_scores_in_kernel_bitwise(H, C, chunk, monkeypatch):
     graph = Graph(ei_l, N, N, chunk=chunk)
     assert ops._gat_nd_ok(graph, xw, H, C, bias)
     res = {}
+    monkeypatch.setattr(ops, "GAT_NODE_SCORES_IN_KERNEL_TRAIN", True)
     for nd in (True, False):
         monkeypatch.setattr(ops, "GAT_NODE_SCORES_IN_KERNEL", nd)
         inf = ops._gat_forward(graph, ei_l, xw, att, H, C, 0.2, bias, True)
