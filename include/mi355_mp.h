@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MP_ABI_VERSION 3
+#define MP_ABI_VERSION 4
 
 /* status codes */
 #define MP_OK 0
@@ -355,6 +355,38 @@ int mp_gat_backward_prep_train_f32(const float* grad_out, int64_t ldg, const flo
                                    const float* agg2, const float* row_s2, const float* a_dst,
                                    const float* row_stats, int64_t n, int32_t H, int32_t C,
                                    float* pack, float* gsum_part, float* grad_a_dst, void* stream);
+
+/* ---- GATConv attention dropout (training) --------------------------------
+ * GATConv.message applies `F.dropout(alpha, p, training)` to the softmax output
+ * (PyG 1.4.3 [U6]; the reference's generic path materialises alpha [E, H] and
+ * the [E, H*C] messages for it).  Here the mask is a function of the edge's
+ * destination-CSR slot s and the head h:
+ *   keep(s, h) = hash(seed, s*H + h) >= floor(p * 2^32),  kept alpha * 1/(1-p)
+ * (hash: two rounds of the murmur3 32-bit finaliser, oracle/pyg_ref.py
+ * restates it), so the forward and the transposed backward evaluate the same
+ * mask without storing one.  0 < p < 1, H <= 32.
+ *
+ * mp_gat_aggregate_train_drop_f32: mp_gat_aggregate_train_f32 with the dropped
+ *   alpha on the messages: out / agg / out2 use alpha * keep / (1-p); the
+ *   softmax statistics (row_stats, row_s2) are those of the undropped alpha.
+ * mp_gat_backward_train_drop_f32: mp_gat_backward_train_f32 for that forward
+ *   (the transposed CSR's eid channel must hold each edge's dst-CSR slot);
+ *   needs C/4 a power of two <= 64 and 16-byte aligned rows.
+ * mp_gat_dropout_keep: bits[s] = keep bits of slot s (bit h), s < n_slots. */
+int mp_gat_aggregate_train_drop_f32(const mp_csr* g, const float* xw, const float* a_src,
+                                    const float* a_dst, const float* att, int32_t H, int32_t C,
+                                    float slope, const float* bias, float* out, int64_t ldo,
+                                    float* agg, float* row_stats, float* out2, float* row_s2,
+                                    uint64_t seed, float p_drop, void* slab, size_t slab_bytes,
+                                    int32_t stages, void* stream);
+int mp_gat_backward_train_drop_f32(const mp_csr* gt, const float* grad_out, int64_t ldg,
+                                   const float* xw, const float* a_src, const float* pack,
+                                   const float* att, int32_t H, int32_t C, float slope,
+                                   const float* grad_a_dst, uint64_t seed, float p_drop,
+                                   float* grad_xw, float* grad_a_src, void* slab, size_t slab_bytes,
+                                   int32_t stages, void* stream);
+int mp_gat_dropout_keep(uint64_t seed, float p_drop, int32_t H, int64_t n_slots, uint32_t* bits,
+                        void* stream);
 
 /* Per-block column sums of x [n, F] (0 < F <= 256, F % 4 == 0, 16-byte aligned
  * rows): part [mp_gat_bwd_blocks(n), F]; sum_i x[i, :] is their sum over the

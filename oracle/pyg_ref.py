@@ -110,8 +110,36 @@ def gcn_conv(x, edge_index, weight, bias=None, edge_weight=None, improved=False)
 
 # --- GATConv [U6] -----------------------------------------------------------
 
+def gat_dropout_keep_slots(seed, p, H, n_slots, start=0):
+    """The fused kernels' attention-dropout keep mask (csrc/mp_aggregate.hip
+    drop_hash / drop_bits), restated in numpy: bool [n_slots, H], slot s of the
+    destination CSR (s from `start`), head h kept iff hash(seed, s*H + h) >= floor(p * 2^32).
+    The reference draws its mask from torch's RNG (GATConv.message:
+    F.dropout(alpha, p)); parity is checked for a given mask, not a given draw."""
+    import numpy as np
+    M = np.uint64(0xFFFFFFFF)
+
+    def mix(h):
+        h = h ^ (h >> np.uint64(16))
+        h = (h * np.uint64(0x85EBCA6B)) & M
+        h = h ^ (h >> np.uint64(13))
+        h = (h * np.uint64(0xC2B2AE35)) & M
+        return h ^ (h >> np.uint64(16))
+
+    seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    idx = np.arange(start * H, (start + n_slots) * H, dtype=np.uint64)  # slots [start, start + n_slots)
+    a = mix((idx & M) ^ np.uint64(seed & 0xFFFFFFFF))
+    hi = (idx >> np.uint64(32)) ^ np.uint64(seed >> 32)
+    b = mix((a + ((np.uint64(0x9E3779B9) * hi) & M) + np.uint64(0x632BE5AB)) & M)
+    thr = min(int(np.floor(float(np.float32(p)) * 4294967296.0)), 0xFFFFFFFF)
+    return torch.from_numpy((b >= np.uint64(thr)).reshape(n_slots, H))
+
+
 def gat_conv(x, edge_index, weight, att, bias, heads, out_channels, concat=True, negative_slope=0.2,
-             return_alpha=False):
+             return_alpha=False, drop_keep=None, drop_p=0.0):
+    """drop_keep (bool [E', H] over the layer's edges incl. its self loops) and
+    drop_p: training-mode attention dropout, alpha * keep / (1 - p) on the
+    messages (F.dropout's scale); the returned alpha is the undropped one."""
     N = x.size(0)
     ei, _ = remove_self_loops(edge_index)
     ei, _ = add_self_loops(ei, num_nodes=N)
@@ -121,7 +149,11 @@ def gat_conv(x, edge_index, weight, att, bias, heads, out_channels, concat=True,
     alpha = (torch.cat([x_i, x_j], dim=-1) * att).sum(dim=-1)
     alpha = F.leaky_relu(alpha, negative_slope)
     alpha = softmax(alpha, ei[1], N)
-    msg = x_j * alpha.view(-1, heads, 1)
+    a_msg = alpha
+    if drop_keep is not None:
+        scale = float(1.0 / (1.0 - float(torch.tensor(drop_p, dtype=torch.float32))))
+        a_msg = alpha * drop_keep.to(alpha.dtype) * scale
+    msg = x_j * a_msg.view(-1, heads, 1)
     out = S.scatter_sum(msg, ei[1], N)
     out = out.view(-1, heads * out_channels) if concat else out.mean(dim=1)
     if bias is not None:

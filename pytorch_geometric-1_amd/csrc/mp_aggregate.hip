@@ -26,6 +26,7 @@
 //     `norm*x_j` followed by CPU scatter_add_: rows that fit in one task are
 //     bit-identical to the oracle.
 #include <atomic>
+#include <cmath>
 #include <cxxabi.h>
 #include <stdlib.h>
 #include <type_traits>
@@ -138,7 +139,42 @@ struct AggArgs {
   float* agg_nb;  // pre-bias output (ld F), when the output carries the bias
   float* slab_v2;
   float* slab_s2;
+  // GAT attention dropout (training: F.dropout on alpha, see drop_bits)
+  uint64_t drop_seed;
+  uint32_t drop_thr;
+  float drop_scale;
 };
+
+// ---------------------------------------------------------------------------
+// GAT attention dropout (GATConv training: `F.dropout(alpha, p)` after the
+// softmax [U6]).  The keep bit of (s, h) -- s the edge's slot in the forward's
+// destination CSR, h the head -- is a counter-based hash of (seed, s * H + h)
+// compared with p * 2^32, so the forward (slot s) and the transposed backward
+// (the edge's dst-slot channel) evaluate the same mask without storing it; a
+// kept alpha is scaled by 1 / (1 - p).  oracle/pyg_ref.py restates the hash.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t drop_mix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, uint64_t idx) {
+  const uint32_t a = drop_mix32((uint32_t)idx ^ (uint32_t)seed);
+  return drop_mix32(a + 0x9E3779B9u * ((uint32_t)(idx >> 32) ^ (uint32_t)(seed >> 32)) + 0x632BE5ABu);
+}
+// keep bits of slot s, bit h for head h (H <= 32)
+__device__ __forceinline__ uint32_t drop_bits(const AggArgs& p, int64_t s) {
+  const uint64_t base = (uint64_t)s * (uint64_t)p.H;
+  uint32_t b = 0;
+  for (int h = 0; h < p.H; ++h) b |= (uint32_t)(drop_hash(p.drop_seed, base + (uint64_t)h) >= p.drop_thr) << h;
+  return b;
+}
+__device__ __forceinline__ float drop_factor(const AggArgs& p, uint32_t bits, int h) {
+  return ((bits >> h) & 1u) ? p.drop_scale : 0.f;
+}
 
 // ---------------------------------------------------------------------------
 // Reducers: per-lane state for VEC features of one (partial) row.
@@ -368,9 +404,12 @@ struct ArgRed {
 // hidden) with the node-score kernel's arithmetic -- bitwise its values; the
 // row's owner task writes both to a_src_out / a_dst_out, so no separate
 // node-score pass over xw is needed.
-template <int VEC, bool OWN = false, bool TR = false, bool ND = false>
+// DR (attention dropout, training): slot weight pe * keep / (1 - p) on the
+// aggregates (acc, acc2), the softmax sums (s, s2) unchanged.
+template <int VEC, bool OWN = false, bool TR = false, bool ND = false, bool DR = false>
 struct GatRed {
   static_assert(!ND || OWN, "in-kernel node scores reuse the own-a_src reduction");
+  static constexpr bool kDrop = DR;
   static constexpr bool kW = false;
   static constexpr bool kEid = false;
   static constexpr bool kGat = true;
@@ -464,7 +503,8 @@ struct GatRed {
       ad = p.a_dst[row * p.H + h];
     }
   }
-  __device__ __forceinline__ void consume_gat(const AggArgs& p, const Frag<VEC>& v, float as) {
+  __device__ __forceinline__ void consume_gat(const AggArgs& p, const Frag<VEC>& v, float as,
+                                              [[maybe_unused]] uint32_t dbits = 0) {
     float a = as + ad;
     [[maybe_unused]] const bool pos = a > 0.f;  // leaky' = 1 : slope (the backward's test)
     a = a > 0.f ? a : a * p.slope;  // F.leaky_relu
@@ -477,13 +517,22 @@ struct GatRed {
     const float sc = up ? e : (m - m) + 1.f;
     const float pe = up ? (a - a) + 1.f : e;
     s = s * sc + pe;
+    [[maybe_unused]] float dsc = 1.f;
+    if constexpr (DR) {
+      dsc = drop_factor(p, dbits, h);
+      const float pd = pe * dsc;
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) acc[k] = acc[k] * sc + pe * v.v[k];
+      for (int k = 0; k < VEC; ++k) acc[k] = acc[k] * sc + pd * v.v[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) acc[k] = acc[k] * sc + pe * v.v[k];
+    }
     if constexpr (TR) {
       const float pl = pos ? pe : pe * p.slope;
       s2 = s2 * sc + pl;
+      const float pld = DR ? pl * dsc : pl;
 #pragma unroll
-      for (int k = 0; k < VEC; ++k) acc2[k] = acc2[k] * sc + pl * v.v[k];
+      for (int k = 0; k < VEC; ++k) acc2[k] = acc2[k] * sc + pld * v.v[k];
     }
     m = up ? a : m;
   }
@@ -725,8 +774,9 @@ struct HeadSumRed : SumRed<VEC, true, false> {
 // A head spans HL = C/VEC lanes (power of two); its dot product is reduced
 // with DPP adds inside the head group.  Gradients are checked to a
 // tolerance, so this pass uses FMA and the hardware exp.
-template <int VEC>
+template <int VEC, bool DR = false>
 struct GatBwdRed {
+  static constexpr bool kDrop = DR;
   static constexpr bool kW = false;
   static constexpr bool kEid = true;
   static constexpr bool kGat = false;
@@ -769,14 +819,22 @@ struct GatBwdRed {
     for (int k = 1; k < VEC; ++k) t = __builtin_fmaf(v.v[k], y[k], t);
     return group_sum(t, hl);
   }
+  // DR: the message used alpha * keep / (1 - p), so d xw_j takes that weight and
+  // d alpha = keep / (1 - p) <g_i, xw_j>
   __device__ __forceinline__ void consume_gatb(const AggArgs& p, const Frag<VEC>& v, float dal, f32x4 q,
-                                               int64_t slot) {
+                                               int64_t slot, [[maybe_unused]] uint32_t dbits = 0) {
     const float sc = as + q.x;
     const float lk = sc > 0.f ? 1.f : p.slope;
     const float alpha = __expf(sc * lk - q.y) * q.z;
+    float aw = alpha;
+    if constexpr (DR) {
+      const float dsc = drop_factor(p, dbits, h);
+      aw = alpha * dsc;
+      dal = dal * dsc;
+    }
     const float de = alpha * (dal - q.w) * lk;
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) acc[k] = __builtin_fmaf(alpha, v.v[k], acc[k]);
+    for (int k = 0; k < VEC; ++k) acc[k] = __builtin_fmaf(aw, v.v[k], acc[k]);
     dacc += de;
     if (leader && p.de) p.de[slot * p.H + h] = de;  // no de: the training forward made d a_dst node-wise
   }
@@ -868,13 +926,16 @@ struct Grp {
 
 // ---------------------------------------------------------------------------
 // Per-group slot window: col / weight / eid of L consecutive CSR slots held one
-// per lane, the next L prefetched.
+// per lane, the next L prefetched.  DR: the lane's slot's dropout keep bits,
+// computed when its window becomes current (key: the eid channel when EID --
+// the transposed backward's dst slot -- else the slot itself).
 // ---------------------------------------------------------------------------
-template <bool W, bool EID, int L, bool GW = false>
+template <bool W, bool EID, int L, bool GW = false, bool DR = false>
 struct SlotWin {
   int64_t base, limit;
   int col, col_n, eid, eid_n;
   float w, w_n;
+  uint32_t dr = 0;
   // GAT (GW, 64-lane tasks, H a power of two <= 8): a_src rows of the current
   // window staged in the wave's LDS (one load per lane per window instead of
   // one gather per slot); the column window runs two windows ahead so the
@@ -922,6 +983,7 @@ struct SlotWin {
     limit = lim;
     fetch(p, base, gl, col, w, eid);
     fetch(p, base + L, gl, col_n, w_n, eid_n);
+    if constexpr (DR) dr = drop_bits(p, EID ? (int64_t)eid : base + gl);
     if constexpr (GW) {
       lds = wave_lds;
       gw = p.H <= 8 && (p.H & (p.H - 1)) == 0;
@@ -941,6 +1003,7 @@ struct SlotWin {
       col = col_n;
       w = w_n;
       eid = eid_n;
+      if constexpr (DR) dr = drop_bits(p, EID ? (int64_t)eid : base + gl);  // eid_n was loaded a window ago
       if constexpr (GW) {
         if (gw) {
           col_n = col_nn;
@@ -1048,22 +1111,28 @@ struct GatAlphaWin {
 // GAT forward: a_src of each 64-slot window staged in LDS (see SlotWin; 8.85 -> 8.66 ms, bitwise the same)
 template <class Red>
 constexpr bool own_as_v = false;
-template <int VEC, bool TR, bool ND>
-constexpr bool own_as_v<GatRed<VEC, true, TR, ND>> = true;
+template <int VEC, bool TR, bool ND, bool DR>
+constexpr bool own_as_v<GatRed<VEC, true, TR, ND, DR>> = true;
 template <class Red, int L>
 constexpr bool kGatWin = Red::kGat && !own_as_v<Red> && L == 64;
 template <class Red>
 constexpr bool kGatTrain = false;
-template <int VEC, bool OWN, bool ND>
-constexpr bool kGatTrain<GatRed<VEC, OWN, true, ND>> = true;
+template <int VEC, bool OWN, bool ND, bool DR>
+constexpr bool kGatTrain<GatRed<VEC, OWN, true, ND, DR>> = true;
 template <class Red>
 constexpr bool kNodeScoresV = false;
-template <int VEC, bool OWN, bool TR, bool ND>
-constexpr bool kNodeScoresV<GatRed<VEC, OWN, TR, ND>> = ND;
+template <int VEC, bool OWN, bool TR, bool ND, bool DR>
+constexpr bool kNodeScoresV<GatRed<VEC, OWN, TR, ND, DR>> = ND;
+template <class Red>
+constexpr bool kDropV = false;
+template <int VEC, bool OWN, bool TR, bool ND, bool DR>
+constexpr bool kDropV<GatRed<VEC, OWN, TR, ND, DR>> = DR;
+template <int VEC, bool DR>
+constexpr bool kDropV<GatBwdRed<VEC, DR>> = DR;
 
 template <class Red, int VEC, int U, int L>
 __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p,
-                                          SlotWin<Red::kW, Red::kEid, L, kGatWin<Red, L>>& win,
+                                          SlotWin<Red::kW, Red::kEid, L, kGatWin<Red, L>, kDropV<Red>>& win,
                                           int64_t s, int64_t t, uint32_t foff, int gl) {
   using GR = Grp<L>;
   const char* xb = reinterpret_cast<const char*>(p.x);
@@ -1101,12 +1170,14 @@ __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p,
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (u < n) {
+        [[maybe_unused]] uint32_t db = 0;
+        if constexpr (kDropV<Red>) db = (uint32_t)GR::bc((int)win.dr, off + u);
         if constexpr (Red::kGat) {
           // own_as next to its consume: slot u waits only for its own row
-          if constexpr (own_as_v<Red>) red.consume_gat(p, v[u], red.own_as(v[u]));
-          else red.consume_gat(p, v[u], as[u]);
+          if constexpr (own_as_v<Red>) red.consume_gat(p, v[u], red.own_as(v[u]), db);
+          else red.consume_gat(p, v[u], as[u], db);
         } else if constexpr (Red::kGatB) {
-          red.consume_gatb(p, v[u], as[u], pk[u], GR::bc(win.eid, off + u));
+          red.consume_gatb(p, v[u], as[u], pk[u], GR::bc(win.eid, off + u), db);
         } else {
           const float wt = Red::kHW ? hw[u] : (Red::kW ? GR::bc(win.w, off + u) : 1.f);
           const int ei = Red::kEid ? GR::bc(win.eid, off + u) : 0;
@@ -1149,7 +1220,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_main(AggArgs p) {
   const int64_t e_end = GR::un(p.wave_slot[w + 1]);
 
   Red red(p, f, act);
-  SlotWin<Red::kW, Red::kEid, L, kGatWin<Red, L>> win;
+  SlotWin<Red::kW, Red::kEid, L, kGatWin<Red, L>, kDropV<Red>> win;
   [[maybe_unused]] float* wave_lds = nullptr;
   if constexpr (kGatWin<Red, L>) {
     __shared__ float gat_as[kWavesPerBlock][64 * 8];
@@ -1832,6 +1903,12 @@ static int aggregate_dispatch(AggArgs& a, const mp_csr* g, int reduce, int stage
   }
 }
 
+// the dropout keep bits of slots [0, n) (mp_gat_dropout_keep: tests, host-side masks)
+__global__ void k_gat_dropout_keep(AggArgs p, int64_t n, uint32_t* bits) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) bits[i] = drop_bits(p, i);
+}
+
 }  // namespace mp
 
 using namespace mp;
@@ -2069,10 +2146,24 @@ int mp_gat_forward_f32(const mp_csr* g, const float* xw, const float* att, int32
   return launch<GatRed<4, true, false, true>, 4>(a, stages, as_stream(stream), F >= 256 ? kGatLanes : 64);
 }
 
+// keep threshold p * 2^32 and scale 1 / (1 - p) (in double, then rounded: F.dropout's scale)
+static void set_drop(AggArgs& a, uint64_t seed, float p_drop) {
+  const double t = std::floor((double)p_drop * 4294967296.0);
+  a.drop_seed = seed;
+  a.drop_thr = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+  a.drop_scale = (float)(1.0 / (1.0 - (double)p_drop));
+}
+
+static int drop_check(float p_drop, int32_t H, const char* who) {
+  MP_CHECK_ARG(p_drop > 0.f && p_drop < 1.f, "%s: dropout p must be in (0, 1) (got %g)", who, (double)p_drop);
+  MP_CHECK_ARG(H >= 1 && H <= 32, "%s: attention dropout needs H <= 32 (got %d)", who, H);
+  return MP_OK;
+}
+
 static int gat_train(const mp_csr* g, const float* xw, const float* a_src, const float* a_dst, const float* att,
                      int32_t H, int32_t C, float slope, const float* bias, float* out, int64_t ldo, float* agg,
                      float* row_stats, float* out2, float* row_s2, void* slab, size_t slab_bytes, int32_t stages,
-                     void* stream, float* as_out, float* ad_out) {
+                     void* stream, float* as_out, float* ad_out, uint64_t drop_seed = 0, float p_drop = 0.f) {
   MP_DEVICE_GUARD(stream);
   int rc = check_graph(g, "mp_gat_aggregate_train_f32");
   if (rc) return rc;
@@ -2115,6 +2206,10 @@ static int gat_train(const mp_csr* g, const float* xw, const float* a_src, const
   b += mp_gat_slab_bytes(g, H, C);
   a.slab_v2 = (float*)b;
   a.slab_s2 = (float*)(b + v);
+  if (p_drop > 0.f) {
+    set_drop(a, drop_seed, p_drop);
+    return launch<GatRed<4, true, true, false, true>, 4>(a, stages, as_stream(stream), F >= 256 ? kGatLanes : 64);
+  }
   if (a.a_src_out) return launch<GatRed<4, true, true, true>, 4>(a, stages, as_stream(stream), F >= 256 ? kGatLanes : 64);
   return launch<GatRed<4, true, true>, 4>(a, stages, as_stream(stream), F >= 256 ? kGatLanes : 64);
 }
@@ -2221,7 +2316,7 @@ int mp_gat_softmax_aggregate_f32(const mp_csr* g, const int32_t* slot_row, const
 static int gat_backward(const mp_csr* gt, const float* grad_out, int64_t ldg, const float* xw, const float* a_src,
                         const float* pack, const float* att, int32_t H, int32_t C, float slope, float* grad_xw,
                         float* grad_a_src, float* de, const float* ga_dst_in, void* slab, size_t slab_bytes,
-                        int32_t stages, void* stream) {
+                        int32_t stages, void* stream, uint64_t drop_seed = 0, float p_drop = 0.f) {
   MP_DEVICE_GUARD(stream);
   int rc = check_graph(gt, "mp_gat_backward_f32");
   if (rc) return rc;
@@ -2261,8 +2356,13 @@ static int gat_backward(const mp_csr* gt, const float* grad_out, int64_t ldg, co
   if (v4) {
     int lanes = F >= 256 ? kGatLanes : pick_shape(F, ldg, grad_out, F, grad_xw).lanes;
     if (lanes < C / 4) lanes = C / 4;
+    if (p_drop > 0.f) {
+      set_drop(a, drop_seed, p_drop);
+      return launch<GatBwdRed<4, true>, 4>(a, stages, s, lanes);
+    }
     return launch<GatBwdRed<4>, 4>(a, stages, s, lanes);
   }
+  MP_CHECK_ARG(p_drop <= 0.f, "mp_gat_backward_train_drop_f32: needs C/4 a power of two <= 64, 16-byte aligned rows");
   MP_CHECK_ARG(pow2(C), "mp_gat_backward_f32: C=%d needs C/4 or C to be a power of two <= 64", C);
   return launch<GatBwdRed<1>, 1>(a, stages, s);
 }
@@ -2285,6 +2385,46 @@ int mp_gat_backward_train_f32(const mp_csr* gt, const float* grad_out, int64_t l
   MP_CHECK_ARG(grad_a_dst != nullptr, "mp_gat_backward_train_f32: null grad_a_dst");
   return gat_backward(gt, grad_out, ldg, xw, a_src, pack, att, H, C, slope, grad_xw, grad_a_src, nullptr,
                       grad_a_dst, slab, slab_bytes, stages, stream);
+}
+
+int mp_gat_aggregate_train_drop_f32(const mp_csr* g, const float* xw, const float* a_src, const float* a_dst,
+                                    const float* att, int32_t H, int32_t C, float slope, const float* bias,
+                                    float* out, int64_t ldo, float* agg, float* row_stats, float* out2,
+                                    float* row_s2, uint64_t seed, float p_drop, void* slab, size_t slab_bytes,
+                                    int32_t stages, void* stream) {
+  int rc = drop_check(p_drop, H, "mp_gat_aggregate_train_drop_f32");
+  if (rc) return rc;
+  MP_CHECK_ARG(a_src && a_dst, "mp_gat_aggregate_train_drop_f32: null input");
+  return gat_train(g, xw, a_src, a_dst, att, H, C, slope, bias, out, ldo, agg, row_stats, out2, row_s2, slab,
+                   slab_bytes, stages, stream, nullptr, nullptr, seed, p_drop);
+}
+
+int mp_gat_backward_train_drop_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, const float* xw,
+                                   const float* a_src, const float* pack, const float* att, int32_t H, int32_t C,
+                                   float slope, const float* grad_a_dst, uint64_t seed, float p_drop,
+                                   float* grad_xw, float* grad_a_src, void* slab, size_t slab_bytes, int32_t stages,
+                                   void* stream) {
+  int rc = drop_check(p_drop, H, "mp_gat_backward_train_drop_f32");
+  if (rc) return rc;
+  MP_CHECK_ARG(grad_a_dst != nullptr, "mp_gat_backward_train_drop_f32: null grad_a_dst");
+  return gat_backward(gt, grad_out, ldg, xw, a_src, pack, att, H, C, slope, grad_xw, grad_a_src, nullptr,
+                      grad_a_dst, slab, slab_bytes, stages, stream, seed, p_drop);
+}
+
+int mp_gat_dropout_keep(uint64_t seed, float p_drop, int32_t H, int64_t n_slots, uint32_t* bits, void* stream) {
+  MP_DEVICE_GUARD(stream);
+  int rc = drop_check(p_drop, H, "mp_gat_dropout_keep");
+  if (rc) return rc;
+  MP_CHECK_ARG(n_slots >= 0, "mp_gat_dropout_keep: negative n_slots");
+  if (n_slots == 0) return MP_OK;
+  MP_CHECK_ARG(bits != nullptr, "mp_gat_dropout_keep: null bits");
+  AggArgs a{};
+  a.H = H;
+  set_drop(a, seed, p_drop);
+  hipLaunchKernelGGL(k_gat_dropout_keep, dim3((unsigned)ceil_div(n_slots, 256)), dim3(256), 0, as_stream(stream), a,
+                     n_slots, bits);
+  MP_CHECK_LAUNCH();
+  return MP_OK;
 }
 
 }  // extern "C"

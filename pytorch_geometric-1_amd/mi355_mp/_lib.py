@@ -38,6 +38,7 @@ MP_LOOPS_ADD_REMAINING = 2
 
 c_p = ctypes.c_void_p
 i64 = ctypes.c_int64
+u64 = ctypes.c_uint64
 i32 = ctypes.c_int32
 f32 = ctypes.c_float
 sz = ctypes.c_size_t
@@ -96,6 +97,12 @@ SIGNATURES = {
                                            ctypes.c_float, c_p, c_p, c_p, c_p, sz, i32, c_p]),
     "mp_gat_backward_train_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, i64, c_p, c_p, c_p, c_p, i32, i32,
                                                  ctypes.c_float, c_p, c_p, c_p, c_p, sz, i32, c_p]),
+    "mp_gat_aggregate_train_drop_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, c_p, c_p, i32, i32, f32,
+                                                       c_p, c_p, i64, c_p, c_p, c_p, c_p, u64, f32, c_p, sz, i32,
+                                                       c_p]),
+    "mp_gat_backward_train_drop_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, i64, c_p, c_p, c_p, c_p, i32,
+                                                      i32, f32, c_p, u64, f32, c_p, c_p, c_p, sz, i32, c_p]),
+    "mp_gat_dropout_keep": (ctypes.c_int, [u64, f32, i32, i64, c_p, c_p]),
     "mp_gat_backward_prep_f32": (ctypes.c_int, [c_p, i64, c_p, i64, c_p, c_p, i64, i32, i32, c_p, c_p, c_p]),
     "mp_gat_backward_prep_train_f32": (ctypes.c_int, [c_p, i64, c_p, i64, c_p, c_p, c_p, c_p, i64, i32, i32, c_p,
                                                       c_p, c_p, c_p]),

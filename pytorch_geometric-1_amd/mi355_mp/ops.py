@@ -552,10 +552,37 @@ def _gat_train_fwd_ok(graph, xw, H, C):
             and not gat_two_pass(graph.dst, H, C) and xw.data_ptr() % 16 == 0 and graph.n_dst == xw.shape[0])
 
 
-def _gat_forward(graph, edge_index, xw, att, H, C, slope, bias, want_alpha, train2=False):
+def gat_dropout_ok(H, C, p):
+    """The fused path carries GATConv's attention dropout (training, 0 < p < 1):
+    the training forward and its transposed backward evaluate one hashed keep
+    mask per (destination-CSR slot, head) (mp_gat_aggregate_train_drop_f32)."""
+    return (0.0 < float(p) < 1.0 and GAT_TRAIN_FWD and GAT_OWN_A_SRC and 1 <= H <= 32
+            and bool(_lib.load().mp_gat_train_ok(H, C)))
+
+
+def gat_dropout_keep(graph, seed, p, H):
+    """The attention-dropout keep mask [E, H] (bool, the graph's edge order) that
+    the fused GAT kernels apply for (seed, p): mp_gat_dropout_keep over the
+    destination-CSR slots, mapped back through the CSR's edge ids."""
+    lib = _lib.load()
+    csr = graph.dst
+    E = csr.n_edges
+    dev = csr.rowptr.device
+    bits = torch.empty(max(E, 1), dtype=torch.int32, device=dev)
+    _lib.check(lib.mp_gat_dropout_keep(int(seed) & 0xFFFFFFFFFFFFFFFF, float(p), int(H), E, bits.data_ptr(),
+                                       _lib.stream_ptr(dev)), "mp_gat_dropout_keep")
+    shifts = torch.arange(H, dtype=torch.int32, device=dev)
+    keep_slot = ((bits[:E].unsqueeze(1) >> shifts) & 1).bool()
+    keep = torch.empty_like(keep_slot)
+    keep[csr.eid[:E].long()] = keep_slot
+    return keep
+
+
+def _gat_forward(graph, edge_index, xw, att, H, C, slope, bias, want_alpha, train2=False, drop=None):
     """Returns (out, alpha, a_src, a_dst, stats, extra).  train2 (callers check
     _gat_train_fwd_ok first): the training forward, out = aggregate + bias and
-    extra = (agg2, s2, agg) with agg the pre-bias aggregate; else extra = None."""
+    extra = (agg2, s2, agg) with agg the pre-bias aggregate; else extra = None.
+    drop = (seed, p): attention dropout on the messages (train2 only)."""
     lib = _lib.load()
     dev = xw.device
     N = xw.shape[0]
@@ -566,7 +593,10 @@ def _gat_forward(graph, edge_index, xw, att, H, C, slope, bias, want_alpha, trai
     att_c = att.reshape(H, 2 * C).contiguous().to(torch.float32)
     a_src = torch.empty((N, H), dtype=torch.float32, device=dev)
     a_dst = torch.empty((N, H), dtype=torch.float32, device=dev)
-    nd = _gat_nd_ok(graph, xw, H, C, bias) and (GAT_NODE_SCORES_IN_KERNEL_TRAIN or not train2)
+    if drop is not None and not train2:
+        raise ValueError("mi355_mp: fused attention dropout runs in the training forward only")
+    nd = (_gat_nd_ok(graph, xw, H, C, bias) and (GAT_NODE_SCORES_IN_KERNEL_TRAIN or not train2)
+          and drop is None)
     if N and not nd:
         _lib.check(lib.mp_gat_node_scores_f32(xw.data_ptr(), N, H, C, att_c.data_ptr(), a_src.data_ptr(),
                                               a_dst.data_ptr(), st), "mp_gat_node_scores_f32")
@@ -592,12 +622,21 @@ def _gat_forward(graph, edge_index, xw, att, H, C, slope, bias, want_alpha, trai
         agg = torch.empty_like(out) if bias is not None else out
         sb = lib.mp_gat_train_slab_bytes(g, H, C)
         slab = torch.empty(sb, dtype=torch.uint8, device=dev)
-        _lib.check(lib.mp_gat_aggregate_train_f32(g, xw.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(),
-                                                  att_c.data_ptr(), H, C, float(slope), _lib.ptr(bias),
-                                                  out.data_ptr(), out.stride(0),
-                                                  agg.data_ptr() if bias is not None else None, stats.data_ptr(),
-                                                  agg2.data_ptr(), s2.data_ptr(), slab.data_ptr(), sb,
-                                                  _lib.MP_STAGE_ALL, st), "mp_gat_aggregate_train_f32")
+        if drop is not None:
+            _lib.check(lib.mp_gat_aggregate_train_drop_f32(g, xw.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(),
+                                                           att_c.data_ptr(), H, C, float(slope), _lib.ptr(bias),
+                                                           out.data_ptr(), out.stride(0),
+                                                           agg.data_ptr() if bias is not None else None,
+                                                           stats.data_ptr(), agg2.data_ptr(), s2.data_ptr(),
+                                                           int(drop[0]), float(drop[1]), slab.data_ptr(), sb,
+                                                           _lib.MP_STAGE_ALL, st), "mp_gat_aggregate_train_drop_f32")
+        else:
+            _lib.check(lib.mp_gat_aggregate_train_f32(g, xw.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(),
+                                                      att_c.data_ptr(), H, C, float(slope), _lib.ptr(bias),
+                                                      out.data_ptr(), out.stride(0),
+                                                      agg.data_ptr() if bias is not None else None, stats.data_ptr(),
+                                                      agg2.data_ptr(), s2.data_ptr(), slab.data_ptr(), sb,
+                                                      _lib.MP_STAGE_ALL, st), "mp_gat_aggregate_train_f32")
         extra = (agg2, s2, agg)
     if extra is None:
         sb = lib.mp_gat_slab_bytes(g, H, C)
@@ -654,7 +693,7 @@ def _gat_bwd_fused_ok(C):
 
 
 def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope, want_att, want_bias,
-                        extra=None):
+                        extra=None, drop=None):
     """GATConv backward: prep (packed destination terms + bias-grad partials),
     one gather pass over the transposed CSR (mp_gat_backward_f32), the d a_dst
     row sums over the dst CSR (reading the per-edge d score through the
@@ -699,7 +738,15 @@ def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope
     sb = lib.mp_gat_slab_bytes(gs, H, C)
     slab = torch.empty(sb, dtype=torch.uint8, device=dev)
     fused_dst = ga_dst is not None
-    if fused_dst:
+    if drop is not None:
+        if not fused_dst:
+            raise ValueError("mi355_mp: the attention-dropout backward needs the training forward's extras")
+        _lib.check(lib.mp_gat_backward_train_drop_f32(gs, g.data_ptr(), g.stride(0), xw.data_ptr(), a_src.data_ptr(),
+                                                      pack.data_ptr(), att_c.data_ptr(), H, C, float(slope),
+                                                      ga_dst.data_ptr(), int(drop[0]), float(drop[1]), gx.data_ptr(),
+                                                      ga_src.data_ptr(), slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
+                   "mp_gat_backward_train_drop_f32")
+    elif fused_dst:
         # the transposed pass also adds d a_dst (x) att_dst to each row's d xw
         _lib.check(lib.mp_gat_backward_train_f32(gs, g.data_ptr(), g.stride(0), xw.data_ptr(), a_src.data_ptr(),
                                                  pack.data_ptr(), att_c.data_ptr(), H, C, float(slope),
@@ -738,15 +785,19 @@ def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope
 
 class _GatPropagate(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, xw, att, bias, graph, edge_index, H, C, slope, want_alpha, train):
-        fused = train and _gat_bwd_fused_ok(C)
+    def forward(ctx, xw, att, bias, graph, edge_index, H, C, slope, want_alpha, train, drop=None):
+        # attention dropout (drop = (seed, p)) runs in the training forward, with
+        # or without a backward to follow (training mode under no_grad)
+        fused = (train or drop is not None) and _gat_bwd_fused_ok(C)
         # the fused backward needs the pre-bias aggregate (rs_i = <g_i, agg_i>):
         # the training forward writes it next to the output; otherwise the
         # bias is added here
         train2 = fused and _gat_train_fwd_ok(graph, xw, H, C)
+        if drop is not None and not train2:
+            raise ValueError("mi355_mp: fused attention dropout needs the training forward (gat_dropout_ok)")
         out, alpha, a_src, a_dst, stats, extra = _gat_forward(graph, edge_index, xw, att, H, C, slope,
                                                               bias if (train2 or not fused) else None, want_alpha,
-                                                              train2=train2)
+                                                              train2=train2, drop=drop)
         agg = None
         if train2:
             agg = extra[2]
@@ -756,7 +807,7 @@ class _GatPropagate(torch.autograd.Function):
         elif fused:
             agg = out
             out = agg + bias if bias is not None else agg.clone()
-        ctx.graph, ctx.H, ctx.C, ctx.slope = graph, H, C, slope
+        ctx.graph, ctx.H, ctx.C, ctx.slope, ctx.drop = graph, H, C, slope, drop
         ctx.has_bias = bias is not None
         ctx.fused = fused
         ctx.has_extra = extra is not None
@@ -786,8 +837,8 @@ class _GatPropagate(torch.autograd.Function):
         if ctx.fused:
             gx, gatt, gb = _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope,
                                                ctx.needs_input_grad[1], ctx.has_bias and ctx.needs_input_grad[2],
-                                               extra)
-            return gx, gatt, gb, None, None, None, None, None, None, None
+                                               extra, ctx.drop)
+            return gx, gatt, gb, None, None, None, None, None, None, None, None
         gb = col_sums(g) if ctx.has_bias and ctx.needs_input_grad[2] else None
         dst, src = graph.dst, graph.src
         E = dst.n_edges
@@ -824,19 +875,32 @@ class _GatPropagate(torch.autograd.Function):
             gd = torch.einsum("nh,nhc->hc", ga_dst, x3)
             gs = torch.einsum("nh,nhc->hc", ga_src, x3)
             gatt = torch.cat([gd, gs], dim=-1).view_as(att)
-        return gx.reshape(N, H * C), gatt, gb, None, None, None, None, None, None, None
+        return gx.reshape(N, H * C), gatt, gb, None, None, None, None, None, None, None, None
 
 
 def gat_propagate(graph, edge_index, xw, att, heads, out_channels, negative_slope=0.2, bias=None,
-                  return_alpha=False):
-    """Fused GATConv aggregation: returns (out [N, H*C], alpha [E, H] or None)."""
+                  return_alpha=False, dropout=0.0, seed=None):
+    """Fused GATConv aggregation: returns (out [N, H*C], alpha [E, H] or None).
+    dropout > 0: GATConv's training-mode attention dropout on the messages
+    (callers check gat_dropout_ok); the keep mask is a hash of (seed, slot, head),
+    seed drawn from torch's default generator unless given (gat_dropout_keep
+    returns the mask).  alpha is the undropped softmax, as upstream's."""
     _lib.require_device(xw, edge_index, att, bias)
     xw = _f32_2d(xw, "x@W").contiguous()
+    H, C = int(heads), int(out_channels)
+    drop = None
+    if dropout > 0:
+        if not (gat_dropout_ok(H, C, dropout) and _gat_train_fwd_ok(graph, xw, H, C)):
+            raise ValueError("mi355_mp: fused attention dropout needs 0 < p < 1, H <= 32, C %% 4 == 0 and C/4 a "
+                             "power of two <= 64 (got p=%g, H=%d, C=%d)" % (dropout, H, C))
+        if seed is None:
+            seed = int(torch.randint(-2 ** 63, 2 ** 63 - 1, (), dtype=torch.int64))
+        drop = (int(seed) & 0xFFFFFFFFFFFFFFFF, float(dropout))
     # autograd.Function.forward always runs with grad disabled: decide here whether
     # a backward can follow (then the forward keeps the pre-bias aggregate)
     train = torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in (xw, att, bias))
-    return _GatPropagate.apply(xw, att, bias, graph, edge_index, int(heads), int(out_channels),
-                               float(negative_slope), bool(return_alpha), train)
+    return _GatPropagate.apply(xw, att, bias, graph, edge_index, H, C, float(negative_slope), bool(return_alpha),
+                               train, drop)
 
 
 class _FeatureTransform(torch.autograd.Function):

@@ -8,8 +8,11 @@ forward: x W on hipBLASLt; per-node scores a_dst = <Wx, att[:C]>,
 a_src = <Wx, att[C:]> (a split of the reference's (cat[x_i,x_j]*att).sum(-1));
 then leaky_relu + segment softmax (+1e-16) + weighted aggregation + bias in
 ONE online-softmax HIP kernel (mp_gat_aggregate_f32).  Attention dropout in
-training mode (dropout > 0) needs torch's RNG on alpha, so that case runs the
-generic message path (still native gathers / scatters).
+training mode (dropout > 0) runs in the same fused training kernels: the keep
+mask of (edge, head) is a hash of a seed drawn from torch's generator and the
+edge's CSR slot, evaluated again by the backward, never stored
+(mp_gat_aggregate_train_drop_f32; shapes outside mi355_mp.ops.gat_dropout_ok
+take the generic message path).
 """
 import torch
 import torch.nn.functional as F
@@ -63,7 +66,8 @@ class GATConv(MessagePassing):
         return (size is None and torch.is_tensor(x) and x.is_cuda and x.dtype == torch.float32
                 and type(self).message is GATConv.message and type(self).update is GATConv.update
                 and type(self).aggregate is MessagePassing.aggregate and self.node_dim == 0
-                and (self.dropout == 0 or not self.training))
+                and (self.dropout == 0 or not self.training
+                     or _ops.gat_dropout_ok(self.heads, self.out_channels, self.dropout)))
 
     def forward(self, x, edge_index, size=None, return_attention_weights=False):
         """"""
@@ -75,8 +79,9 @@ class GATConv(MessagePassing):
             N = xw.size(0)
             graph = graph_for(edge_index, N, N, self.flow, target_tasks=GAT_TARGET_TASKS)
             fused_bias = self.bias if self.concat else None
+            drop = self.dropout if self.training else 0.0
             out, alpha = _ops.gat_propagate(graph, edge_index, xw, self.att, self.heads, self.out_channels,
-                                            self.negative_slope, fused_bias, return_attention_weights)
+                                            self.negative_slope, fused_bias, return_attention_weights, dropout=drop)
             if not self.concat:
                 out = out.view(-1, self.heads, self.out_channels).mean(dim=1)
                 if self.bias is not None:

@@ -1063,20 +1063,91 @@ def test_sage_concat_and_gat_mean_heads():
     assert (out - want).abs().max().item() < 1e-5
 
 
-def test_gat_dropout_training_uses_generic_path():
+def test_gat_dropout_training_shapes_and_eval_deterministic():
+    """GATConv(dropout=0.5): training mode runs (fused for C = 4, generic for
+    C = 6, which mp_gat_train_ok rejects); eval mode is deterministic."""
     from torch_geometric.nn import GATConv
+    from mi355_mp import ops
     _, _, _, _, pl = _mods()
     N, E, F = 200, 2000, 8
     ei = pl(N, E, seed=55)
     x = torch.randn(N, F, generator=torch.Generator().manual_seed(55)).to(DEV)
-    gat = GATConv(F, 4, heads=2, dropout=0.5).to(DEV)
-    gat.train()
-    out = gat(x, ei.to(DEV))
-    assert out.shape == (N, 8) and torch.isfinite(out).all()
-    gat.eval()
-    a = gat(x, ei.to(DEV))
-    b = gat(x, ei.to(DEV))
-    assert torch.equal(a, b)
+    for C, fused in ((4, True), (6, False)):
+        assert ops.gat_dropout_ok(2, C, 0.5) == fused
+        gat = GATConv(F, C, heads=2, dropout=0.5).to(DEV)
+        gat.train()
+        out = gat(x, ei.to(DEV))
+        assert out.shape == (N, 2 * C) and torch.isfinite(out).all()
+        gat.eval()
+        a = gat(x, ei.to(DEV))
+        b = gat(x, ei.to(DEV))
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("H,C", [(8, 32), (4, 16), (2, 64), (3, 4)])
+def test_gat_attention_dropout_fused_vs_masked_reference(H, C):
+    """Training-mode attention dropout in the fused kernels (SURVEY 8a GATConv,
+    `F.dropout(alpha, p)` in GATConv.message): the keep mask the kernels apply
+    (mp_gat_dropout_keep) equals the oracle's numpy restatement of the hash,
+    keeps ~1-p, and the layer's output and every gradient match float64
+    autograd of the reference formula with that mask on the messages (hub rows
+    split across tasks: a star centre plus small chunks)."""
+    from torch_geometric.nn import GATConv
+    from torch_geometric.nn.conv._structure import gat_loops
+    from mi355_mp import ops
+    from mi355_mp.graph import graph_for, GAT_TARGET_TASKS
+    _, _, _, _, pl = _mods()
+    N, Fi, p = 1200, 12, 0.3
+    g = torch.Generator().manual_seed(7 + H * C)
+    ei = pl(N, 20000, seed=43)
+    ei = torch.cat([ei, torch.stack([torch.randint(0, N, (3000,), generator=g), torch.zeros(3000, dtype=torch.long)]),
+                    torch.stack([torch.zeros(3000, dtype=torch.long), torch.randint(0, N, (3000,), generator=g)])], 1)
+    x = torch.randn(N, Fi, generator=g)
+    gout = torch.randn(N, H * C, generator=g)
+    assert ops.gat_dropout_ok(H, C, p)
+    conv = GATConv(Fi, C, heads=H, dropout=p).to(DEV)
+    with torch.no_grad():
+        conv.bias.normal_()
+    conv.train()
+    xd = x.to(DEV).requires_grad_(True)
+    eid = ei.to(DEV)
+    torch.manual_seed(1234)
+    out = conv(xd, eid)
+    out.backward(gout.to(DEV))
+    torch.manual_seed(1234)  # the seed gat_propagate drew
+    seed = int(torch.randint(-2 ** 63, 2 ** 63 - 1, (), dtype=torch.int64)) & 0xFFFFFFFFFFFFFFFF
+    ei_l = gat_loops(eid, N)
+    graph = graph_for(ei_l, N, N, conv.flow, target_tasks=GAT_TARGET_TASKS)
+    keep = ops.gat_dropout_keep(graph, seed, p, H).cpu()
+    # the device mask == the oracle's restatement of the hash (slot order -> edge order)
+    E = ei_l.shape[1]
+    ks = P.gat_dropout_keep_slots(seed, p, H, E)
+    want_keep = torch.empty_like(ks)
+    want_keep[graph.dst.eid[:E].long().cpu()] = ks
+    assert torch.equal(keep, want_keep)
+    frac = keep.float().mean().item()
+    assert abs(frac - (1 - p)) < 0.01, frac
+    # the oracle's edge list is the layer's (loops removed, then appended)
+    ei_ref = P.add_self_loops(P.remove_self_loops(ei)[0], num_nodes=N)[0]
+    assert torch.equal(ei_l.cpu(), ei_ref)
+    W = conv.weight.detach().cpu().double().requires_grad_(True)
+    a64 = conv.att.detach().cpu().double().requires_grad_(True)
+    b = conv.bias.detach().cpu().double().requires_grad_(True)
+    x64 = x.double().requires_grad_(True)
+    want = P.gat_conv(x64, ei, W, a64, b, H, C, drop_keep=keep, drop_p=p)
+    assert torch.allclose(out.detach().cpu().double(), want.detach(), rtol=1e-5, atol=1e-5)
+    want.backward(gout.double())
+    for got, ref in ((xd.grad, x64.grad), (conv.weight.grad, W.grad), (conv.att.grad, a64.grad),
+                     (conv.bias.grad, b.grad)):
+        assert torch.allclose(got.cpu().double(), ref, rtol=1e-4, atol=1e-4)
+    # the no-dropout output differs; training mode under no_grad applies the same mask
+    with torch.no_grad():
+        torch.manual_seed(1234)
+        again = conv(x.to(DEV), eid)
+        conv.eval()
+        plain = conv(x.to(DEV), eid)
+    assert torch.equal(again, out.detach())
+    assert not torch.allclose(plain, out.detach(), atol=1e-3)
 
 
 @pytest.mark.parametrize("H,C", [(8, 32), (3, 5), (1, 64), (4, 100), (2, 16), (4, 8), (1, 256), (2, 2), (8, 64)])

@@ -42,7 +42,7 @@ def test_ctypes_signatures_cover_the_header():
 
 
 def test_abi_version_and_error_string(lib):
-    assert lib.mp_abi_version() == 3
+    assert lib.mp_abi_version() == 4
     assert isinstance(lib.mp_last_error(), bytes)
 
 

@@ -333,3 +333,46 @@ def test_any_dtype_loop_matches_c_loop_and_kats(reduce):
     if arg is not None:
         # max: lowest() itself never beats the init value (arg stays E = 5, value -> 0)
         assert arg.view(-1).tolist() == ([1, 5, 3, 5] if reduce == "max" else [0, 2, 3, 5])
+
+
+def test_gat_dropout_keep_hash_restatement():
+    """oracle.pyg_ref.gat_dropout_keep_slots (numpy, vectorised) against a
+    plain-int restatement of csrc/mp_aggregate.hip drop_hash, including a seed
+    with high bits and slot*H + h past 2^32; keep fraction ~ 1 - p; the oracle
+    layer with an all-keep mask scales the messages by 1/(1-p)."""
+    M = 0xFFFFFFFF
+
+    def mix(h):
+        h ^= h >> 16
+        h = (h * 0x85EBCA6B) & M
+        h ^= h >> 13
+        h = (h * 0xC2B2AE35) & M
+        return h ^ (h >> 16)
+
+    def keep(seed, p, idx):
+        a = mix((idx & M) ^ (seed & M))
+        b = mix((a + 0x9E3779B9 * (((idx >> 32) ^ (seed >> 32)) & M) + 0x632BE5AB) & M)
+        return b >= min(int(np.floor(float(np.float32(p)) * 4294967296.0)), M)
+
+    for seed, p, H, n in ((0, 0.5, 1, 300), (0xDEADBEEF12345678, 0.3, 8, 200), (2 ** 64 - 1, 0.9, 3, 100)):
+        got = P.gat_dropout_keep_slots(seed, p, H, n)
+        want = torch.tensor([[keep(seed, p, s * H + h) for h in range(H)] for s in range(n)])
+        assert torch.equal(got, want)
+    # indices past 2^32 (the high word enters the second round)
+    seed, H = 99, 8
+    big = (1 << 32) // H + 5
+    got = P.gat_dropout_keep_slots(seed, 0.4, H, 3, start=big - 3)
+    want = torch.tensor([[keep(seed, 0.4, s * H + h) for h in range(H)] for s in range(big - 3, big)])
+    assert torch.equal(got, want)
+    frac = P.gat_dropout_keep_slots(5, 0.3, 4, 50000).float().mean().item()
+    assert abs(frac - 0.7) < 0.005
+    g = torch.Generator().manual_seed(3)
+    N, H, C = 30, 2, 4
+    x = torch.randn(N, 5, generator=g, dtype=torch.float64)
+    ei = torch.randint(0, N, (2, 120), generator=g)
+    W = torch.randn(5, H * C, generator=g, dtype=torch.float64)
+    att = torch.randn(1, H, 2 * C, generator=g, dtype=torch.float64)
+    E = P.add_self_loops(P.remove_self_loops(ei)[0], num_nodes=N)[0].shape[1]
+    a = P.gat_conv(x, ei, W, att, None, H, C)
+    b = P.gat_conv(x, ei, W, att, None, H, C, drop_keep=torch.ones(E, H, dtype=torch.bool), drop_p=0.25)
+    assert torch.allclose(b, a / (1 - float(np.float32(0.25))), rtol=1e-12, atol=1e-12)
