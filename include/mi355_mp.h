@@ -356,6 +356,21 @@ int mp_gat_backward_prep_train_f32(const float* grad_out, int64_t ldg, const flo
                                    const float* row_stats, int64_t n, int32_t H, int32_t C,
                                    float* pack, float* gsum_part, float* grad_a_dst, void* stream);
 
+/* ---- Batch.from_data_list on the replica's device ------------------------
+ * torch_geometric.data.Batch.from_data_list (PyG 1.4.3 [U8]; the replica path
+ * of DataParallel, /root/reference/ConvexPruning.py:530) collates a graph list
+ * on the host: per graph `item + cumsum[key]` for index keys and
+ * `torch.full((n_g,), g)` for the batch vector.  With the raw items
+ * concatenated and copied to the device once, these apply the same per-graph
+ * terms on the device.  Segments: starts[0..G] (int64, starts[0] = 0,
+ * starts[G] = n, non-decreasing; empty graphs allowed), device arrays.
+ *   mp_segment_offset_i64: data[r*ld + i] += inc[g(i)], r < rows, i < n
+ *   mp_segment_ids_i64:    ids[i] = g(i)
+ * g(i) = the graph whose segment holds element i.  Bit-exact (integers). */
+int mp_segment_offset_i64(int64_t* data, int64_t ld, int32_t rows, int64_t n, const int64_t* starts,
+                          const int64_t* inc, int64_t n_graphs, void* stream);
+int mp_segment_ids_i64(int64_t* ids, int64_t n, const int64_t* starts, int64_t n_graphs, void* stream);
+
 /* ---- GATConv attention dropout (training) --------------------------------
  * GATConv.message applies `F.dropout(alpha, p, training)` to the softmax output
  * (PyG 1.4.3 [U6]; the reference's generic path materialises alpha [E, H] and

@@ -464,7 +464,8 @@ def norm_from_degree(row, col, deg, edge_weight):
     w = edge_weight.to(torch.float32).contiguous() if edge_weight is not None else None
     norm = torch.empty(E, dtype=torch.float32, device=row.device)
     d = deg.to(torch.float32).contiguous()
-    _lib.check(_lib.load().mp_gcn_norm_from_deg_f32(row.contiguous().data_ptr(), col.contiguous().data_ptr(),
+    row, col = row.contiguous(), col.contiguous()  # named: a temporary copy could be freed before the launch
+    _lib.check(_lib.load().mp_gcn_norm_from_deg_f32(row.data_ptr(), col.data_ptr(),
                                                     _lib.ptr(w), E, d.numel(), d.data_ptr(), norm.data_ptr(),
                                                     _lib.stream_ptr(row.device)), "mp_gcn_norm_from_deg_f32")
     return norm

@@ -168,13 +168,20 @@ class Batch(Data):
         self.batch = batch
 
     @staticmethod
-    def from_data_list(data_list, follow_batch=()):
+    def from_data_list(data_list, follow_batch=(), device=None):
+        """device (extension, e.g. a replica's ``cuda:k``): collate straight onto
+        that device -- each key's raw items concatenated and copied once, the
+        per-graph index offsets and the batch vectors applied there by
+        ``mp_segment_offset_i64`` / ``mp_segment_ids_i64`` -- with the same
+        result as ``from_data_list(data_list, follow_batch).to(device)``."""
         keys = []
         for data in data_list:
             for k in data.keys:
                 if k not in keys:
                     keys.append(k)
         assert "batch" not in keys
+        if device is not None and torch.device(device).type == "cuda":
+            return _collate_on_device(data_list, keys, follow_batch, torch.device(device))
         batch = Batch()
         parts = {k: [] for k in keys}
         for k in follow_batch:
@@ -217,6 +224,98 @@ class Batch(Data):
 
     def to_data_list(self):
         raise NotImplementedError("mi355_mp: Batch.to_data_list is not part of the replica path")
+
+
+def _seg_starts(sizes, dev):
+    starts = torch.zeros(len(sizes) + 1, dtype=torch.int64)
+    if sizes:
+        starts[1:] = torch.tensor(sizes, dtype=torch.int64).cumsum(0)
+    # a blocking copy: an asynchronous one from this pageable temporary could
+    # read it after it is freed
+    return starts.to(dev)
+
+
+def _graph_ids(sizes, dev, lib, st):
+    """torch.cat([torch.full((n_g,), g) for g, n_g in enumerate(sizes)]) on dev."""
+    from mi355_mp import _lib
+    n = int(sum(sizes))
+    ids = torch.empty(n, dtype=torch.long, device=dev)
+    if n:
+        starts = _seg_starts(sizes, dev)
+        _lib.check(lib.mp_segment_ids_i64(ids.data_ptr(), n, starts.data_ptr(), len(sizes), st), "mp_segment_ids_i64")
+    return ids
+
+
+def _to_dev(t, dev):
+    if t.device == dev:
+        return t.contiguous()
+    if t.device.type == "cpu" and t.numel():
+        return t.contiguous().pin_memory().to(dev, non_blocking=True)
+    return t.to(dev)
+
+
+def _collate_on_device(data_list, keys, follow_batch, dev):
+    """Batch.from_data_list(data_list, follow_batch).to(dev), collated on dev
+    (see Batch.from_data_list)."""
+    from mi355_mp import _lib
+    lib = _lib.load()
+    st = _lib.stream_ptr(dev)
+    batch = Batch()
+    ref = data_list[0] if data_list else Data()
+    for k in keys:
+        items, incs, gids = [], [], []
+        inc = 0
+        for i, data in enumerate(data_list):
+            item = data[k]
+            if item is None:
+                continue
+            items.append(item)
+            incs.append(inc)
+            gids.append(i)
+            inc = inc + data.__inc__(k, item)
+        if not items:
+            continue
+        first = items[0]
+        if not torch.is_tensor(first):
+            batch[k] = torch.tensor(items, device=dev) if isinstance(first, (int, float)) else items
+            continue
+        dim = ref.__cat_dim__(k, first)
+        d = _to_dev(torch.cat([t if t.device == items[0].device else t.to(items[0].device) for t in items], dim=dim),
+                    dev)
+        dim = dim % d.dim() if d.dim() else 0
+        sizes = [int(t.size(dim)) if t.dim() else 1 for t in items]
+        if first.dtype != torch.bool:
+            if any(incs):
+                if d.dtype == torch.int64 and d.dim() in (1, 2) and dim == d.dim() - 1 and d.is_contiguous():
+                    # item + cumsum[key] per graph, on the device
+                    rows = 1 if d.dim() == 1 else d.shape[0]
+                    n = d.shape[-1]
+                    # both held in names until the launch is queued (a temporary's block
+                    # would go back to the caching allocator before the next allocation)
+                    starts = _seg_starts(sizes, dev)
+                    inc_d = torch.tensor(incs, dtype=torch.int64).to(dev)
+                    _lib.check(lib.mp_segment_offset_i64(d.data_ptr(), n, rows, n, starts.data_ptr(), inc_d.data_ptr(),
+                                                         len(items), st), "mp_segment_offset_i64")
+                else:
+                    offs = torch.repeat_interleave(torch.tensor(incs, device=dev), torch.tensor(sizes, device=dev))
+                    shape = [1] * d.dim()
+                    shape[dim] = -1
+                    d = d + offs.view(shape).to(d.dtype)
+            elif d.is_floating_point() or d.is_complex():
+                d = d + 0  # the reference's item + 0 (-0.0 becomes +0.0)
+        batch[k] = d
+        if k in follow_batch:
+            fb = [0] * len(data_list)
+            for g, sz in zip(gids, sizes):
+                fb[g] = sz
+            # graphs without the key contribute no entries (as upstream's per-item torch.full)
+            batch["{}_batch".format(k)] = _graph_ids(fb, dev, lib, st)
+    counts = [0] * len(data_list)
+    for i, data in enumerate(data_list):
+        n = data.num_nodes
+        counts[i] = 0 if n is None else int(n)
+    batch.batch = _graph_ids(counts, dev, lib, st)
+    return batch.contiguous()
 
 
 class DataLoader(torch.utils.data.DataLoader):

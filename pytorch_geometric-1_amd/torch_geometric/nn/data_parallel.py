@@ -4,7 +4,8 @@
 
 Same contract as PyG 1.4.3: ``model(data_list)`` splits the list into one
 contiguous chunk per device, balanced by node count, batches each chunk with
-``Batch.from_data_list`` on that device, runs the replicas
+``Batch.from_data_list`` on that device (collated there: one copy per key,
+index offsets and batch vectors by device kernels), runs the replicas
 (``torch.nn.DataParallel`` machinery: parameters broadcast over RCCL, one host
 thread per device) and gathers the outputs on ``output_device``.  Every
 replica's aggregations run on the native kernels of its own device.
@@ -31,7 +32,7 @@ class DataParallel(_TorchDataParallel):
             raise ValueError("DataParallel received an empty data list")
         if not self.device_ids or len(self.device_ids) == 1:
             dev = self.src_device if self.src_device is not None else torch.device("cpu")
-            return self.module(Batch.from_data_list(data_list).to(dev))
+            return self.module(Batch.from_data_list(data_list, device=dev))
         for t in self.module.parameters():
             if t.device != self.src_device:
                 raise RuntimeError("module must have its parameters on device {} (device_ids[0]) but found one "
@@ -50,7 +51,7 @@ class DataParallel(_TorchDataParallel):
             lo, hi = split[k], split[k + 1]
             if hi > lo:  # non-empty chunks take consecutive devices (replicas live on device_ids[:len])
                 dev = torch.device("cuda:{}".format(device_ids[len(chunks)]))
-                chunks.append((Batch.from_data_list(data_list[lo:hi]).to(dev),))
+                chunks.append((Batch.from_data_list(data_list[lo:hi], device=dev),))
         return chunks
 
 

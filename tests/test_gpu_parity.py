@@ -1402,6 +1402,44 @@ def test_data_parallel_replicas_match_batched_model():
     assert torch.equal(DataParallel(net)(graphs), ref)
 
 
+def test_batch_from_data_list_on_device_matches_host_collation():
+    """Batch.from_data_list(..., device=cuda) (mp_segment_offset_i64 /
+    mp_segment_ids_i64 on the device) == the reference's host collation moved
+    to the device, key for key, bitwise and dtype for dtype: graphs without
+    edges or without a key, a [3, F] face key, an int32 index key (torch path),
+    follow_batch, scalar attributes, -0.0 features, and a 1000-graph list."""
+    from torch_geometric.data import Batch, Data
+    g = torch.Generator().manual_seed(8)
+    for n_graphs in (1, 7, 1000):
+        graphs = []
+        for i in range(n_graphs):
+            n = int(torch.randint(1, 30, (1,), generator=g))
+            e = 0 if i % 5 == 3 else int(torch.randint(1, 4 * n, (1,), generator=g))
+            x = torch.randn(n, 3, generator=g)
+            x[0, 0] = -0.0
+            d = Data(x=x, edge_index=torch.randint(0, n, (2, e), generator=g), y=torch.tensor([i % 3]))
+            if i % 4 != 1:
+                d.edge_attr = torch.rand(e, 2, generator=g)
+            d.face = torch.randint(0, n, (3, 2 + i % 3), generator=g)
+            d.my_index = torch.randint(0, n, (e,), generator=g, dtype=torch.int64).to(torch.int32)
+            d.mask = torch.rand(n, generator=g) > 0.5
+            d.scale = float(i) * 0.5
+            graphs.append(d)
+        want = Batch.from_data_list(graphs, follow_batch=["x", "edge_attr"]).to(DEV)
+        got = Batch.from_data_list(graphs, follow_batch=["x", "edge_attr"], device=DEV)
+        assert sorted(got.keys) == sorted(want.keys)
+        for k in want.keys:
+            a, b = got[k], want[k]
+            if torch.is_tensor(b):
+                assert a.device == b.device and a.dtype == b.dtype and a.shape == b.shape, k
+                assert torch.equal(a, b), k
+                if b.is_floating_point():  # -0.0 became +0.0 in both (item + 0)
+                    assert torch.equal(torch.signbit(a), torch.signbit(b)), k
+            else:
+                assert a == b, k
+        assert got.num_graphs == n_graphs
+
+
 def test_gcn_aggregate_first_matches_reference_order():
     """GCNConv(aggregate_first=True) computes (A X) W + b when F_in < F_out:
     equal to the reference order within fp32 rounding, forward and backward."""
