@@ -403,6 +403,20 @@ def c3train(dev):
                       "forward_ms": fwd, "forward_backward_ms": step}), flush=True)
 
 
+def c3train_drop(dev):
+    """GATConv(256, 32, heads=8, dropout=0.6) training step on config 3: the
+    attention dropout runs in the fused kernels (hashed keep mask)."""
+    from mi355_mp.graphgen import rmat_edge_index
+    from torch_geometric.nn import GATConv
+    N = 1 << 21
+    ei = rmat_edge_index(scale=21, n_samples=30_000_000, seed=1, device=dev)
+    x = torch.randn(N, 256, device=dev).requires_grad_(True)
+    conv = GATConv(256, 32, heads=8, dropout=0.6).to(dev).train()
+    _, step = _train_step_ms(conv, x, ei)
+    print(json.dumps({"config": "c3train_drop", "desc": "GATConv(256, 32, heads=8, dropout=0.6) training step "
+                      "on RMAT21, attention dropout fused", "forward_backward_ms": step}), flush=True)
+
+
 def c5reorder(dev):
     """ogbn-products-shaped first layer GCNConv(100, 256): reference order
     A (X W) vs aggregate_first (A X) W, forward + backward."""
