@@ -834,6 +834,8 @@ class _GatPropagate(torch.autograd.Function):
         dev = xw.device
         st = _lib.stream_ptr(dev)
         g = grad_out.contiguous()
+        if g.data_ptr() % 16:
+            g = g.clone()  # a view at an odd offset: the 4-wide transposed pass (the dropout form has no other) needs 16-B rows
         N = xw.shape[0]
         if ctx.fused:
             gx, gatt, gb = _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope,

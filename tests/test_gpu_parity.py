@@ -1140,6 +1140,16 @@ def test_gat_attention_dropout_fused_vs_masked_reference(H, C):
     for got, ref in ((xd.grad, x64.grad), (conv.weight.grad, W.grad), (conv.att.grad, a64.grad),
                      (conv.bias.grad, b.grad)):
         assert torch.allclose(got.cpu().double(), ref, rtol=1e-4, atol=1e-4)
+    # an upstream gradient that is a view at a 4-byte offset (realigned before the 4-wide pass)
+    if H * C == 256:
+        conv.zero_grad()
+        xd.grad = None
+        torch.manual_seed(1234)
+        out2 = conv(xd, eid)
+        big = torch.zeros(N * H * C + 1, device=DEV)
+        big[1:] = gout.to(DEV).reshape(-1)
+        out2.backward(big[1:].view(N, H * C))
+        assert torch.allclose(xd.grad.cpu().double(), x64.grad, rtol=1e-4, atol=1e-4)
     # the no-dropout output differs; training mode under no_grad applies the same mask
     with torch.no_grad():
         torch.manual_seed(1234)
