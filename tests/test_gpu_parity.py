@@ -2397,3 +2397,43 @@ def test_gat_node_scores_in_kernel_bitwise(H, C, chunk, monkeypatch):
         grads[nd] = [out.detach(), xd.grad, conv.weight.grad, conv.att.grad, conv.bias.grad]
     for a, b in zip(grads[True], grads[False]):
         assert torch.equal(a, b)
+
+
+@settings(max_examples=40, deadline=None, derandomize=True, database=None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+@given(N=st.integers(1, 300), deg=st.floats(0.0, 30.0), H=st.sampled_from([1, 2, 3, 4, 8]),
+       C=st.sampled_from([4, 8, 16, 32, 64]), p=st.sampled_from([0.0, 0.1, 0.5, 0.9]),
+       chunk=st.sampled_from([16, 64, 256]), star=st.booleans(), seed=st.integers(0, 1 << 16))
+def test_fuzz_gat_training_with_attention_dropout(N, deg, H, C, p, chunk, star, seed):
+    """Shape fuzzing of the fused GAT training forward + transposed backward,
+    with and without attention dropout: output and the gradients of xw, att and
+    bias against float64 autograd of the reference formula (loops removed and
+    re-added, the kernels' keep mask on the messages)."""
+    _, ops, _, Graph, _ = _mods()
+    g = torch.Generator().manual_seed(seed)
+    E = int(N * deg)
+    dst = torch.zeros(E, dtype=torch.int64) if star else torch.randint(N, (E,), generator=g)
+    if star:
+        dst[E // 2:] = torch.randint(N, (E - E // 2,), generator=g)
+    ei = torch.stack([torch.randint(N, (E,), generator=g), dst])
+    ei_l = P.add_self_loops(P.remove_self_loops(ei)[0], num_nodes=N)[0]
+    xw = torch.randn(N, H * C, generator=g)
+    att = torch.randn(1, H, 2 * C, generator=g) * 0.3
+    bias = torch.randn(H * C, generator=g)
+    gout = torch.randn(N, H * C, generator=g)
+    graph = Graph(ei_l.to(DEV), N, N, chunk=chunk)
+    xd = xw.to(DEV).requires_grad_(True)
+    ad = att.to(DEV).requires_grad_(True)
+    bd = bias.to(DEV).requires_grad_(True)
+    seed_d = seed * 7919 + 13
+    out, _ = ops.gat_propagate(graph, ei_l.to(DEV), xd, ad, H, C, 0.2, bd, False, dropout=p, seed=seed_d)
+    out.backward(gout.to(DEV))
+    keep = ops.gat_dropout_keep(graph, seed_d, p, H).cpu() if p > 0 else None
+    x64 = xw.double().requires_grad_(True)
+    a64 = att.double().requires_grad_(True)
+    b64 = bias.double().requires_grad_(True)
+    want = P.gat_conv(x64, ei_l, torch.eye(H * C, dtype=torch.float64), a64, b64, H, C, drop_keep=keep, drop_p=p)
+    assert torch.allclose(out.detach().cpu().double(), want.detach(), rtol=1e-5, atol=1e-5)
+    want.backward(gout.double())
+    for got, ref in ((xd.grad, x64.grad), (ad.grad, a64.grad), (bd.grad, b64.grad)):
+        assert torch.allclose(got.cpu().double(), ref, rtol=1e-4, atol=1e-4)
