@@ -240,8 +240,9 @@ int mp_gat_forward_f32(const mp_csr* g, const float* xw, const float* att, int32
                        float* a_src, float* a_dst, float* row_stats, void* slab,
                        size_t slab_bytes, int32_t stages, void* stream);
 
-/* Training forward of the same layer (att given, C % 4 == 0, C/4 a power of two
- * <= 64: mp_gat_train_ok).  out = aggregate + bias (bias may be NULL); agg
+/* Training forward of the same layer (C % 4 == 0; with att given and C/4 a power
+ * of two <= 64 -- mp_gat_train_ok -- a_src comes from each gathered row, else
+ * from the a_src array).  out = aggregate + bias (bias may be NULL); agg
  * (NULL allowed without a bias) receives the pre-bias aggregate [n_rows, H*C]
  * (contiguous) that the backward's rs needs.  Besides these and row_stats it
  * leaves, with the same online rescaling,
@@ -355,6 +356,40 @@ int mp_gat_backward_prep_train_f32(const float* grad_out, int64_t ldg, const flo
                                    const float* agg2, const float* row_s2, const float* a_dst,
                                    const float* row_stats, int64_t n, int32_t H, int32_t C,
                                    float* pack, float* gsum_part, float* grad_a_dst, void* stream);
+
+/* ---- GATConv with heads of any width (C % 4 == 0) --------------------------
+ * The reference's own GAT stacks (ConvexPruning.py:209-214) use heads = 1 and
+ * out_channels drawn at random (:106-114), so a head is often wider than one
+ * 256-feature tile or C/4 is not a power of two.  For those shapes:
+ *   forward: mp_gat_node_scores_wide_f32 (one wave per node, per-head dot
+ *     products in 256-feature chunks), then mp_gat_aggregate_f32 (inference)
+ *     or mp_gat_aggregate_train_f32 / _drop_f32 (training; these now take any
+ *     C % 4 == 0: a_src is read from the node-score array when C/4 is not a
+ *     power of two <= 64 or att is NULL);
+ *   backward: mp_gat_backward_prep_wide_f32 (pack + node-wise d a_dst, as
+ *     mp_gat_backward_prep_train_f32), mp_gat_backward_wide_f32 over the
+ *     transposed CSR (no per-slot dot product:
+ *       grad_xw[j] = sum_i alpha d g_i,  acc2[j] = sum_i lk alpha d g_i,
+ *       sc[j,h] = sum_i lk alpha rs_i,   lk = leaky'(score), d = dropout factor
+ *     (p_drop = 0: none; else the eid channel must hold each edge's dst-CSR
+ *     slot), slab mp_gat_train_slab_bytes(gt, H, C)), then
+ *     mp_gat_backward_epilogue_wide_f32: grad_a_src = <acc2, xw>_h - sc (written
+ *     over sc) and grad_xw += grad_a_src att[h, C:] + grad_a_dst att[h, :C].
+ * Rows contiguous [n, H*C] unless an ld is given; 16-byte aligned. */
+int mp_gat_wide_ok(int32_t H, int32_t C);
+int mp_gat_node_scores_wide_f32(const float* xw, int64_t n_nodes, int32_t H, int32_t C, const float* att,
+                                float* a_src, float* a_dst, void* stream);
+int mp_gat_backward_prep_wide_f32(const float* grad_out, int64_t ldg, const float* agg, int64_t lda,
+                                  const float* agg2, const float* row_s2, const float* a_dst,
+                                  const float* row_stats, int64_t n, int32_t H, int32_t C, float* pack,
+                                  float* grad_a_dst, void* stream);
+int mp_gat_backward_wide_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, const float* a_src,
+                             const float* pack, int32_t H, int32_t C, float slope, uint64_t seed, float p_drop,
+                             float* grad_xw, float* acc2, float* sc, void* slab, size_t slab_bytes,
+                             int32_t stages, void* stream);
+int mp_gat_backward_epilogue_wide_f32(float* grad_xw, const float* acc2, const float* xw, const float* att,
+                                      const float* grad_a_dst, float* sc_grad_a_src, int64_t n, int32_t H,
+                                      int32_t C, void* stream);
 
 /* ---- Batch.from_data_list on the replica's device ------------------------
  * torch_geometric.data.Batch.from_data_list (PyG 1.4.3 [U8]; the replica path

@@ -887,6 +887,121 @@ struct GatBwdRed {
   }
 };
 
+// GATConv backward for heads of any width (C % 4 == 0; a head may span several
+// feature tiles, so no per-slot dot product is possible): over the TRANSPOSED
+// CSR (row j = source), with alpha_ij rebuilt from the destination's pack
+// (a_dst, m, 1/den, rs) and the row's own a_src[j,h], lk = leaky'(score):
+//   acc_j  += alpha d g_i              (message part of d xw_j; d = dropout factor)
+//   acc2_j += lk alpha d g_i
+//   sc_j   += lk alpha rs_i            (per head)
+// The per-edge d score never forms: d a_src_j = sum_i lk alpha (d <g_i, xw_j> - rs_i)
+// = <acc2_j, xw_j>_h - sc_j, a node-wise dot product taken after this pass
+// (mp_gat_backward_epilogue_wide_f32).  Rows write acc to out, acc2 to out2 and
+// sc to ga; every lane of a head holds the same sc.  Elementwise per slot:
+// FMA and the hardware exp (gradients are tolerance-checked).
+template <int VEC, bool DR = false>
+struct GatBwdWideRed {
+  static constexpr bool kDrop = DR;
+  static constexpr bool kW = false;
+  static constexpr bool kEid = DR;  // the dropout key: each edge's dst-CSR slot
+  static constexpr bool kGat = false;
+  static constexpr bool kHW = false;
+  static constexpr bool kGatB = false;
+  static constexpr bool kStat = true;
+  struct Part {
+    float v[VEC];
+    float v2[VEC];
+    float s;
+  };
+  float acc[VEC], acc2[VEC];
+  float sc, as;
+  int h;
+
+  __device__ GatBwdWideRed(const AggArgs& p, int f, bool act) : h(act ? f / p.C : 0) {}
+
+  __device__ __forceinline__ void begin(const AggArgs& p, int64_t row, bool, int, bool) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = acc2[k] = 0.f;
+    sc = 0.f;
+    as = p.a_src[row * p.H + h];
+  }
+  __device__ __forceinline__ void consume_gatw(const AggArgs& p, const Frag<VEC>& v, f32x4 q,
+                                               [[maybe_unused]] uint32_t dbits) {
+    const float score = as + q.x;
+    const float lk = score > 0.f ? 1.f : p.slope;
+    const float alpha = __expf(score * lk - q.y) * q.z;
+    sc = __builtin_fmaf(lk * alpha, q.w, sc);
+    float aw = alpha;
+    if constexpr (DR) aw = alpha * drop_factor(p, dbits, h);
+    const float law = lk * aw;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      acc[k] = __builtin_fmaf(aw, v.v[k], acc[k]);
+      acc2[k] = __builtin_fmaf(law, v.v[k], acc2[k]);
+    }
+  }
+  __device__ __forceinline__ void consume(const Frag<VEC>&, float, int, float) {}
+  __device__ __forceinline__ void save(PRef r, bool stat_writer) const {
+    Frag<VEC> o;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) o.v[k] = acc[k];
+    store_frag<VEC>(r.v, o);
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) o.v[k] = acc2[k];
+    store_frag<VEC>(r.v2, o);
+    if (stat_writer) r.st[0] = sc;
+  }
+  static __device__ __forceinline__ Part load(PRef r) {
+    Frag<VEC> o = load_frag<VEC>(r.v);
+    Frag<VEC> o2 = load_frag<VEC>(r.v2);
+    Part q;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      q.v[k] = o.v[k];
+      q.v2[k] = o2.v[k];
+    }
+    q.s = r.st[0];
+    return q;
+  }
+  __device__ __forceinline__ void set(const Part& q) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      acc[k] = q.v[k];
+      acc2[k] = q.v2[k];
+    }
+    sc = q.s;
+  }
+  __device__ __forceinline__ void merge(const Part& q) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      acc[k] += q.v[k];
+      acc2[k] += q.v2[k];
+    }
+    sc += q.s;
+  }
+  __device__ __forceinline__ Part part() const {
+    Part q;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      q.v[k] = acc[k];
+      q.v2[k] = acc2[k];
+    }
+    q.s = sc;
+    return q;
+  }
+  __device__ __forceinline__ void finish(const AggArgs& p, int64_t row, int64_t, int f, bool act) {
+    if (!act) return;
+    Frag<VEC> o;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) o.v[k] = acc[k];
+    store_out<VEC>(p.out + row * p.ldo + f, o);
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) o.v[k] = acc2[k];
+    store_out<VEC>(p.out2 + row * (int64_t)p.F + f, o);
+    if (f % p.C == 0) p.ga[row * p.H + h] = sc;
+  }
+};
+
 // this lane's share of slab slot s (2*task + kind)
 template <class Red>
 __device__ __forceinline__ PRef slab_ref(const AggArgs& p, int64_t s, int f, const Red& red) {
@@ -1129,6 +1244,12 @@ template <int VEC, bool OWN, bool TR, bool ND, bool DR>
 constexpr bool kDropV<GatRed<VEC, OWN, TR, ND, DR>> = DR;
 template <int VEC, bool DR>
 constexpr bool kDropV<GatBwdRed<VEC, DR>> = DR;
+template <int VEC, bool DR>
+constexpr bool kDropV<GatBwdWideRed<VEC, DR>> = DR;
+template <class Red>
+constexpr bool kGatWideV = false;
+template <int VEC, bool DR>
+constexpr bool kGatWideV<GatBwdWideRed<VEC, DR>> = true;
 
 template <class Red, int VEC, int U, int L>
 __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p,
@@ -1157,7 +1278,7 @@ __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p,
       const int c = GR::bc(win.col, off + uu);
       v[u] = load_frag<VEC>(reinterpret_cast<const float*>(xb + (int64_t)c * ldxb + foff));
       if constexpr (Red::kGat && !own_as_v<Red>) as[u] = win.a_src_of(p, off + uu, c, red.h);
-      if constexpr (Red::kGatB) pk[u] = p.pack[(int64_t)c * p.H + red.h];
+      if constexpr (Red::kGatB || kGatWideV<Red>) pk[u] = p.pack[(int64_t)c * p.H + red.h];
     }
     if constexpr (Red::kGatB) {
 #pragma unroll
@@ -1176,6 +1297,8 @@ __device__ __forceinline__ void run_slots(Red& red, const AggArgs& p,
           // own_as next to its consume: slot u waits only for its own row
           if constexpr (own_as_v<Red>) red.consume_gat(p, v[u], red.own_as(v[u]), db);
           else red.consume_gat(p, v[u], as[u], db);
+        } else if constexpr (kGatWideV<Red>) {
+          red.consume_gatw(p, v[u], pk[u], db);
         } else if constexpr (Red::kGatB) {
           red.consume_gatb(p, v[u], as[u], pk[u], GR::bc(win.eid, off + u), db);
         } else {
@@ -1674,7 +1797,7 @@ static int launch_l(const AggArgs& a, int stages, hipStream_t s) {
     dim3 grid((unsigned)nb, (unsigned)ftiles);
     int rc = MP_OK;
     if (a.flat) {
-      if constexpr (!Red::kGat && !Red::kGatB && !Red::kHW) {
+      if constexpr (!Red::kGat && !Red::kGatB && !Red::kHW && !kGatWideV<Red>) {
         if constexpr (L == 64 && !Red::kEid) {
           bool far = false;
           if constexpr (VEC == 1) {
@@ -1694,7 +1817,7 @@ static int launch_l(const AggArgs& a, int stages, hipStream_t s) {
     if (rc) return rc;
   }
   if ((stages & MP_STAGE_FIXUP) && a.n_split > 0) {
-    if constexpr (VEC != 4 && !Red::kGat && !Red::kGatB && !Red::kHW) {
+    if constexpr (VEC != 4 && !Red::kGat && !Red::kGatB && !Red::kHW && !kGatWideV<Red>) {
       if (a.fix4) {
         dim3 grid4((unsigned)a.n_split, (unsigned)ceil_div(a.F, 64 * 4));
         hipLaunchKernelGGL((k_agg_fixup<typename Rebind<Red, 4>::type, 4>), grid4, dim3(kBlock), 0, s, a);
@@ -2167,13 +2290,18 @@ static int gat_train(const mp_csr* g, const float* xw, const float* a_src, const
   MP_DEVICE_GUARD(stream);
   int rc = check_graph(g, "mp_gat_aggregate_train_f32");
   if (rc) return rc;
-  MP_CHECK_ARG(mp_gat_train_ok(H, C), "mp_gat_aggregate_train_f32: needs C %% 4 == 0 and C/4 a power of two <= 64");
-  MP_CHECK_ARG(xw && att && out && row_stats && out2 && row_s2, "mp_gat_aggregate_train_f32: null input");
+  // a_src from each gathered row (OWN) when a head fits one lane group (C/4 a
+  // power of two <= 64); any other C % 4 == 0 reads the node-score arrays
+  const bool own = mp_gat_train_ok(H, C) && att != nullptr;
+  MP_CHECK_ARG(H > 0 && C > 0 && C % 4 == 0, "mp_gat_aggregate_train_f32: needs C %% 4 == 0");
+  MP_CHECK_ARG(own || (!as_out && a_src && a_dst),
+               "mp_gat_aggregate_train_f32: heads with C/4 not a power of two <= 64 need a_src / a_dst inputs");
+  MP_CHECK_ARG(xw && out && row_stats && out2 && row_s2, "mp_gat_aggregate_train_f32: null input");
   const int F = H * C;
   MP_CHECK_ARG(ldo >= F, "mp_gat_aggregate_train_f32: ldo < H*C");
   MP_CHECK_ARG((uintptr_t)xw % 16 == 0 && (uintptr_t)att % 16 == 0 && (uintptr_t)out % 16 == 0 && ldo % 4 == 0 &&
                    (uintptr_t)out2 % 16 == 0 && (uintptr_t)agg % 16 == 0 && (uintptr_t)bias % 16 == 0,
-               "mp_gat_aggregate_train_f32: xw, att, bias, out, agg, out2 must be 16-byte aligned (ldo % 4 == 0)");
+               "mp_gat_aggregate_train_f32: xw, att, bias, out, agg, out2 must be 16-byte aligned (ldo %% 4 == 0)");
   MP_CHECK_ARG(!bias || agg, "mp_gat_aggregate_train_f32: a bias needs agg (the pre-bias output)");
   MP_CHECK_ARG(slab != nullptr && slab_bytes >= mp_gat_train_slab_bytes(g, H, C),
                "mp_gat_aggregate_train_f32: slab workspace too small");
@@ -2206,11 +2334,20 @@ static int gat_train(const mp_csr* g, const float* xw, const float* a_src, const
   b += mp_gat_slab_bytes(g, H, C);
   a.slab_v2 = (float*)b;
   a.slab_s2 = (float*)(b + v);
+  const int lanes = F >= 256 ? kGatLanes : 64;
+  if (!own) {
+    a.att = nullptr;
+    if (p_drop > 0.f) {
+      set_drop(a, drop_seed, p_drop);
+      return launch<GatRed<4, false, true, false, true>, 4>(a, stages, as_stream(stream), lanes);
+    }
+    return launch<GatRed<4, false, true>, 4>(a, stages, as_stream(stream), lanes);
+  }
   if (p_drop > 0.f) {
     set_drop(a, drop_seed, p_drop);
-    return launch<GatRed<4, true, true, false, true>, 4>(a, stages, as_stream(stream), F >= 256 ? kGatLanes : 64);
+    return launch<GatRed<4, true, true, false, true>, 4>(a, stages, as_stream(stream), lanes);
   }
-  if (a.a_src_out) return launch<GatRed<4, true, true, true>, 4>(a, stages, as_stream(stream), F >= 256 ? kGatLanes : 64);
+  if (a.a_src_out) return launch<GatRed<4, true, true, true>, 4>(a, stages, as_stream(stream), lanes);
   return launch<GatRed<4, true, true>, 4>(a, stages, as_stream(stream), F >= 256 ? kGatLanes : 64);
 }
 
@@ -2409,6 +2546,57 @@ int mp_gat_backward_train_drop_f32(const mp_csr* gt, const float* grad_out, int6
   MP_CHECK_ARG(grad_a_dst != nullptr, "mp_gat_backward_train_drop_f32: null grad_a_dst");
   return gat_backward(gt, grad_out, ldg, xw, a_src, pack, att, H, C, slope, grad_xw, grad_a_src, nullptr,
                       grad_a_dst, slab, slab_bytes, stages, stream, seed, p_drop);
+}
+
+int mp_gat_backward_wide_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, const float* a_src,
+                             const float* pack, int32_t H, int32_t C, float slope, uint64_t seed, float p_drop,
+                             float* grad_xw, float* acc2, float* sc, void* slab, size_t slab_bytes, int32_t stages,
+                             void* stream) {
+  MP_DEVICE_GUARD(stream);
+  int rc = check_graph(gt, "mp_gat_backward_wide_f32");
+  if (rc) return rc;
+  MP_CHECK_ARG(H > 0 && C > 0 && C % 4 == 0, "mp_gat_backward_wide_f32: needs C %% 4 == 0");
+  if (p_drop > 0.f) {
+    rc = drop_check(p_drop, H, "mp_gat_backward_wide_f32");
+    if (rc) return rc;
+  }
+  MP_CHECK_ARG(grad_out && a_src && pack && grad_xw && acc2 && sc, "mp_gat_backward_wide_f32: null pointer");
+  const int F = H * C;
+  MP_CHECK_ARG(ldg >= F && ldg % 4 == 0, "mp_gat_backward_wide_f32: ldg < H*C or not a multiple of 4");
+  MP_CHECK_ARG((uintptr_t)grad_out % 16 == 0 && (uintptr_t)grad_xw % 16 == 0 && (uintptr_t)acc2 % 16 == 0 &&
+                   (uintptr_t)pack % 16 == 0,
+               "mp_gat_backward_wide_f32: grad_out, grad_xw, acc2, pack must be 16-byte aligned");
+  MP_CHECK_ARG(slab && slab_bytes >= mp_gat_train_slab_bytes(gt, H, C),
+               "mp_gat_backward_wide_f32: slab workspace too small (mp_gat_train_slab_bytes)");
+  AggArgs a{};
+  fill_graph(a, gt);
+  a.F = F;
+  a.x = grad_out;
+  a.ldx = ldg;
+  a.out = grad_xw;
+  a.ldo = F;
+  a.out2 = acc2;
+  a.ga = sc;
+  a.a_src = a_src;
+  a.pack = reinterpret_cast<const f32x4*>(pack);
+  a.H = H;
+  a.C = C;
+  a.slope = slope;
+  a.slab_ld = slab_ld_for(F);
+  const size_t slots = 2 * (size_t)gt->n_waves;
+  char* b = (char*)slab;
+  const size_t v = align_up(slots * (size_t)a.slab_ld * 4, 256);
+  a.slab_v = (float*)b;
+  a.slab_s = (float*)(b + v);
+  b += mp_gat_slab_bytes(gt, H, C);
+  a.slab_v2 = (float*)b;
+  hipStream_t s = as_stream(stream);
+  const int lanes = F >= 256 ? 64 : (F / 4 <= 4 ? 4 : next_pow2(F / 4));
+  if (p_drop > 0.f) {
+    set_drop(a, seed, p_drop);
+    return launch<GatBwdWideRed<4, true>, 4>(a, stages, s, lanes);
+  }
+  return launch<GatBwdWideRed<4>, 4>(a, stages, s, lanes);
 }
 
 int mp_gat_dropout_keep(uint64_t seed, float p_drop, int32_t H, int64_t n_slots, uint32_t* bits, void* stream) {

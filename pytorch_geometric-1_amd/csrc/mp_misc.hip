@@ -297,6 +297,9 @@ int mp_gat_node_scores_f32(const float* xw, int64_t n_nodes, int32_t H, int32_t 
     if (blocks > 16384) blocks = 16384;
     k_gat_node_scores_wave<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(xw, n_nodes, H, C, G, att, a_src,
                                                                             a_dst);
+  } else if (C % 4 == 0 && (uintptr_t)xw % 16 == 0 && (uintptr_t)att % 16 == 0) {
+    // heads of any other width: one wave per node, 256-feature chunks (mp_gat_wide.hip)
+    return mp_gat_node_scores_wide_f32(xw, n_nodes, H, C, att, a_src, a_dst, stream);
   } else {
     int64_t total = n_nodes * (int64_t)H;
     k_gat_node_scores<<<(unsigned)ceil_div(total, 256), 256, 0, as_stream(stream)>>>(xw, n_nodes, H, C, att,

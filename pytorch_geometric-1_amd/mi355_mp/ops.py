@@ -548,17 +548,25 @@ def _gat_nd_ok(graph, xw, H, C, bias):
 
 
 def _gat_train_fwd_ok(graph, xw, H, C):
-    """The training forward (mp_gat_aggregate_train_f32) applies."""
-    return (GAT_TRAIN_FWD and GAT_OWN_A_SRC and bool(_lib.load().mp_gat_train_ok(H, C))
+    """The training forward (mp_gat_aggregate_train_f32) applies: C % 4 == 0
+    (a_src from the gathered rows when C/4 is a power of two <= 64, else from
+    the node-score array)."""
+    return (GAT_TRAIN_FWD and GAT_OWN_A_SRC and gat_wide_ok(H, C)
             and not gat_two_pass(graph.dst, H, C) and xw.data_ptr() % 16 == 0 and graph.n_dst == xw.shape[0])
+
+
+def gat_wide_ok(H, C):
+    """Heads of any width with C % 4 == 0 (GATConv pads C to it): the fused
+    training forward reads a_src from the node-score array when C/4 is not a
+    power of two <= 64, and the backward runs the wide form (mp_gat_backward_wide_f32)."""
+    return bool(_lib.load().mp_gat_wide_ok(H, C))
 
 
 def gat_dropout_ok(H, C, p):
     """The fused path carries GATConv's attention dropout (training, 0 < p < 1):
     the training forward and its transposed backward evaluate one hashed keep
     mask per (destination-CSR slot, head) (mp_gat_aggregate_train_drop_f32)."""
-    return (0.0 < float(p) < 1.0 and GAT_TRAIN_FWD and GAT_OWN_A_SRC and 1 <= H <= 32
-            and bool(_lib.load().mp_gat_train_ok(H, C)))
+    return (0.0 < float(p) < 1.0 and GAT_TRAIN_FWD and GAT_OWN_A_SRC and 1 <= H <= 32 and gat_wide_ok(H, C))
 
 
 def gat_dropout_keep(graph, seed, p, H):
@@ -693,6 +701,56 @@ def _gat_bwd_fused_ok(C):
     return (C % 4 == 0 and pow2(C // 4)) or pow2(C)
 
 
+def _gat_backward_wide(graph, g, xw, att, a_src, a_dst, stats, agg, extra, H, C, slope, want_att, want_bias,
+                       drop=None):
+    """GATConv backward for heads of any width (C % 4 == 0), after the training
+    forward: prep (pack + node-wise d a_dst), one pass over the transposed CSR
+    with no per-slot dot product (mp_gat_backward_wide_f32: sum alpha g_i,
+    sum lk alpha g_i, sum lk alpha rs_i per source row), then the node-wise
+    epilogue (d a_src = <acc2, xw> - sc, the att terms of d xw).
+    Returns (d xw, d att or None, d bias or None)."""
+    lib = _lib.load()
+    dev = xw.device
+    st = _lib.stream_ptr(dev)
+    N = xw.shape[0]
+    F = H * C
+    att_c = att.reshape(H, 2 * C).contiguous()
+    if N == 0:
+        return (torch.zeros_like(xw), torch.zeros_like(att) if want_att else None,
+                g.new_zeros(F) if want_bias else None)
+    agg2, s2 = extra
+    pack = torch.empty((N, H, 4), dtype=torch.float32, device=dev)
+    ga_dst = torch.empty((N, H), dtype=torch.float32, device=dev)
+    _lib.check(lib.mp_gat_backward_prep_wide_f32(g.data_ptr(), g.stride(0), agg.data_ptr(), agg.stride(0),
+                                                 agg2.data_ptr(), s2.data_ptr(), a_dst.data_ptr(), stats.data_ptr(),
+                                                 N, H, C, pack.data_ptr(), ga_dst.data_ptr(), st),
+               "mp_gat_backward_prep_wide_f32")
+    src = graph.src_with_dst_slots()
+    gs = src.struct("dst_slot")
+    gx = torch.empty((N, F), dtype=torch.float32, device=dev)
+    acc2 = torch.empty((N, F), dtype=torch.float32, device=dev)
+    sc = torch.empty((N, H), dtype=torch.float32, device=dev)
+    sb = lib.mp_gat_train_slab_bytes(gs, H, C)
+    slab = torch.empty(sb, dtype=torch.uint8, device=dev)
+    seed, p = (0, 0.0) if drop is None else (int(drop[0]), float(drop[1]))
+    _lib.check(lib.mp_gat_backward_wide_f32(gs, g.data_ptr(), g.stride(0), a_src.data_ptr(), pack.data_ptr(), H, C,
+                                            float(slope), seed, p, gx.data_ptr(), acc2.data_ptr(), sc.data_ptr(),
+                                            slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st), "mp_gat_backward_wide_f32")
+    del slab, pack
+    _lib.check(lib.mp_gat_backward_epilogue_wide_f32(gx.data_ptr(), acc2.data_ptr(), xw.data_ptr(), att_c.data_ptr(),
+                                                     ga_dst.data_ptr(), sc.data_ptr(), N, H, C, st),
+               "mp_gat_backward_epilogue_wide_f32")
+    del acc2
+    ga_src = sc
+    gatt = None
+    if want_att:
+        x3 = xw.view(N, H, C)
+        gatt = torch.cat([torch.einsum("nh,nhc->hc", ga_dst, x3), torch.einsum("nh,nhc->hc", ga_src, x3)],
+                         dim=-1).view_as(att)
+    gb = col_sums(g) if want_bias else None
+    return gx, gatt, gb
+
+
 def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope, want_att, want_bias,
                         extra=None, drop=None):
     """GATConv backward: prep (packed destination terms + bias-grad partials),
@@ -789,11 +847,14 @@ class _GatPropagate(torch.autograd.Function):
     def forward(ctx, xw, att, bias, graph, edge_index, H, C, slope, want_alpha, train, drop=None):
         # attention dropout (drop = (seed, p)) runs in the training forward, with
         # or without a backward to follow (training mode under no_grad)
-        fused = (train or drop is not None) and _gat_bwd_fused_ok(C)
+        wide = not _gat_bwd_fused_ok(C) and gat_wide_ok(H, C)
+        fused = (train or drop is not None) and (_gat_bwd_fused_ok(C) or wide)
         # the fused backward needs the pre-bias aggregate (rs_i = <g_i, agg_i>):
         # the training forward writes it next to the output; otherwise the
         # bias is added here
         train2 = fused and _gat_train_fwd_ok(graph, xw, H, C)
+        if wide and fused and not train2:
+            fused = False  # the wide backward needs the training forward's extras
         if drop is not None and not train2:
             raise ValueError("mi355_mp: fused attention dropout needs the training forward (gat_dropout_ok)")
         out, alpha, a_src, a_dst, stats, extra = _gat_forward(graph, edge_index, xw, att, H, C, slope,
@@ -809,6 +870,7 @@ class _GatPropagate(torch.autograd.Function):
             agg = out
             out = agg + bias if bias is not None else agg.clone()
         ctx.graph, ctx.H, ctx.C, ctx.slope, ctx.drop = graph, H, C, slope, drop
+        ctx.wide = wide
         ctx.has_bias = bias is not None
         ctx.fused = fused
         ctx.has_extra = extra is not None
@@ -837,6 +899,11 @@ class _GatPropagate(torch.autograd.Function):
         if g.data_ptr() % 16:
             g = g.clone()  # a view at an odd offset: the 4-wide transposed pass (the dropout form has no other) needs 16-B rows
         N = xw.shape[0]
+        if ctx.fused and ctx.wide:
+            gx, gatt, gb = _gat_backward_wide(graph, g, xw, att, a_src, a_dst, stats, agg, extra, H, C, slope,
+                                              ctx.needs_input_grad[1], ctx.has_bias and ctx.needs_input_grad[2],
+                                              ctx.drop)
+            return gx, gatt, gb, None, None, None, None, None, None, None, None
         if ctx.fused:
             gx, gatt, gb = _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope,
                                                ctx.needs_input_grad[1], ctx.has_bias and ctx.needs_input_grad[2],

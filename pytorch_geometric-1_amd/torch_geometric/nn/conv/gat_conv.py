@@ -13,6 +13,13 @@ mask of (edge, head) is a hash of a seed drawn from torch's generator and the
 edge's CSR slot, evaluated again by the backward, never stored
 (mp_gat_aggregate_train_drop_f32; shapes outside mi355_mp.ops.gat_dropout_ok
 take the generic message path).
+
+Heads of any width: out_channels not a multiple of 4 are padded per head to
+the next multiple of 4 (zero columns of W, att and bias; the padded output
+columns are dropped), so the 16-byte row kernels apply; heads whose C/4 is not
+a power of two <= 64 (the reference's own GAT stacks, heads=1 with random
+widths) run the wide forms (mp_gat_node_scores_wide_f32, the training forward
+reading a_src from the node-score array, mp_gat_backward_wide_f32).
 """
 import torch
 import torch.nn.functional as F
@@ -62,12 +69,15 @@ class GATConv(MessagePassing):
         glorot(self.att)
         zeros(self.bias)
 
+    def _padded_channels(self):
+        return (self.out_channels + 3) // 4 * 4
+
     def _can_fuse(self, x, size):
         return (size is None and torch.is_tensor(x) and x.is_cuda and x.dtype == torch.float32
                 and type(self).message is GATConv.message and type(self).update is GATConv.update
                 and type(self).aggregate is MessagePassing.aggregate and self.node_dim == 0
                 and (self.dropout == 0 or not self.training
-                     or _ops.gat_dropout_ok(self.heads, self.out_channels, self.dropout)))
+                     or _ops.gat_dropout_ok(self.heads, self._padded_channels(), self.dropout)))
 
     def forward(self, x, edge_index, size=None, return_attention_weights=False):
         """"""
@@ -75,13 +85,23 @@ class GATConv(MessagePassing):
             edge_index = gat_loops(edge_index, x.size(self.node_dim))
 
         if self._can_fuse(x, size):
-            xw = _ops.feature_transform(x, self.weight)
+            H, C = self.heads, self.out_channels
+            C4 = self._padded_channels()
+            weight, att = self.weight, self.att
+            fused_bias = self.bias if self.concat else None
+            if C4 != C:  # zero columns per head: the 16-byte row kernels apply
+                weight = F.pad(weight.view(-1, H, C), (0, C4 - C)).view(-1, H * C4)
+                att = F.pad(att.view(1, H, 2, C), (0, C4 - C)).view(1, H, 2 * C4)
+                if fused_bias is not None:
+                    fused_bias = F.pad(fused_bias.view(H, C), (0, C4 - C)).view(H * C4)
+            xw = _ops.feature_transform(x, weight)
             N = xw.size(0)
             graph = graph_for(edge_index, N, N, self.flow, target_tasks=GAT_TARGET_TASKS)
-            fused_bias = self.bias if self.concat else None
             drop = self.dropout if self.training else 0.0
-            out, alpha = _ops.gat_propagate(graph, edge_index, xw, self.att, self.heads, self.out_channels,
-                                            self.negative_slope, fused_bias, return_attention_weights, dropout=drop)
+            out, alpha = _ops.gat_propagate(graph, edge_index, xw, att, H, C4, self.negative_slope, fused_bias,
+                                            return_attention_weights, dropout=drop)
+            if C4 != C:
+                out = out.view(-1, H, C4)[:, :, :C].reshape(-1, H * C).contiguous()
             if not self.concat:
                 out = out.view(-1, self.heads, self.out_channels).mean(dim=1)
                 if self.bias is not None:

@@ -1064,8 +1064,9 @@ def test_sage_concat_and_gat_mean_heads():
 
 
 def test_gat_dropout_training_shapes_and_eval_deterministic():
-    """GATConv(dropout=0.5): training mode runs (fused for C = 4, generic for
-    C = 6, which mp_gat_train_ok rejects); eval mode is deterministic."""
+    """GATConv(dropout=0.5): training mode runs (C = 4 fused; C = 6 fused after
+    padding its heads to 8 columns, gat_dropout_ok itself rejects an unpadded 6);
+    eval mode is deterministic."""
     from torch_geometric.nn import GATConv
     from mi355_mp import ops
     _, _, _, _, pl = _mods()
@@ -1186,6 +1187,63 @@ def test_gat_native_backward_pieces(H, C):
     for got, want in ((xd.grad, x64.grad), (conv.weight.grad, W.grad), (conv.att.grad, att.grad),
                       (conv.bias.grad, b.grad)):
         assert torch.allclose(got.cpu().double(), want, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("H,C,p", [(1, 100, 0.0), (1, 200, 0.0), (1, 255, 0.0), (1, 731, 0.0), (3, 100, 0.0),
+                                   (2, 300, 0.0), (1, 1021, 0.4), (4, 52, 0.3)])
+def test_gat_wide_heads_training(H, C, p):
+    """The reference's own GAT stacks (ConvexPruning.py:209-214: heads=1, widths
+    drawn at random): heads padded to a multiple of 4, C/4 not a power of two
+    <= 64 or wider than one tile -> wide node scores, the training forward on the
+    node-score array, mp_gat_backward_wide_f32 + its node-wise epilogue.  Output
+    and all gradients against float64 autograd of the reference formula (hub rows
+    split across tasks), with attention dropout for two shapes."""
+    from torch_geometric.nn import GATConv
+    from torch_geometric.nn.conv._structure import gat_loops
+    from mi355_mp import ops
+    from mi355_mp.graph import graph_for, GAT_TARGET_TASKS
+    _, _, _, _, pl = _mods()
+    N, Fi = 700, 24
+    g = torch.Generator().manual_seed(H * 1000 + C)
+    ei = pl(N, 9000, seed=C)
+    ei = torch.cat([ei, torch.stack([torch.randint(0, N, (2500,), generator=g), torch.zeros(2500, dtype=torch.long)]),
+                    torch.stack([torch.zeros(2500, dtype=torch.long), torch.randint(0, N, (2500,), generator=g)])], 1)
+    x = torch.randn(N, Fi, generator=g)
+    gout = torch.randn(N, H * C, generator=g)
+    C4 = (C + 3) // 4 * 4
+    assert ops.gat_wide_ok(H, C4) and (C4 == 256) == ops._gat_bwd_fused_ok(C4)  # 255 pads to 256: fused
+    conv = GATConv(Fi, C, heads=H, dropout=p).to(DEV)
+    with torch.no_grad():
+        conv.bias.normal_()
+    conv.train()
+    xd = x.to(DEV).requires_grad_(True)
+    eid = ei.to(DEV)
+    torch.manual_seed(99)
+    out = conv(xd, eid)
+    out.backward(gout.to(DEV))
+    keep = None
+    if p > 0:
+        torch.manual_seed(99)
+        seed = int(torch.randint(-2 ** 63, 2 ** 63 - 1, (), dtype=torch.int64)) & 0xFFFFFFFFFFFFFFFF
+        graph = graph_for(gat_loops(eid, N), N, N, conv.flow, target_tasks=GAT_TARGET_TASKS)
+        keep = ops.gat_dropout_keep(graph, seed, p, H).cpu()
+    W = conv.weight.detach().cpu().double().requires_grad_(True)
+    a64 = conv.att.detach().cpu().double().requires_grad_(True)
+    b = conv.bias.detach().cpu().double().requires_grad_(True)
+    x64 = x.double().requires_grad_(True)
+    want = P.gat_conv(x64, ei, W, a64, b, H, C, drop_keep=keep, drop_p=p)
+    assert out.shape == (N, H * C) and out.is_contiguous()
+    assert torch.allclose(out.detach().cpu().double(), want.detach(), rtol=1e-5, atol=1e-5)
+    want.backward(gout.double())
+    for got, ref in ((xd.grad, x64.grad), (conv.weight.grad, W.grad), (conv.att.grad, a64.grad),
+                     (conv.bias.grad, b.grad)):
+        assert torch.allclose(got.cpu().double(), ref, rtol=1e-4, atol=1e-4)
+    # inference on the same layer: the non-own fused forward within the bound
+    conv.eval()
+    with torch.no_grad():
+        inf = conv(x.to(DEV), eid).cpu().double()
+    want_inf = P.gat_conv(x.double(), ei, W.detach(), a64.detach(), b.detach(), H, C)
+    assert torch.allclose(inf, want_inf, rtol=1e-5, atol=1e-5)
 
 
 def test_aggregate_heads_direct():

@@ -417,6 +417,25 @@ def c3train_drop(dev):
                       "on RMAT21, attention dropout fused", "forward_backward_ms": step}), flush=True)
 
 
+def c3train_h1(dev):
+    """The reference's own GAT stacks (ConvexPruning.py:209-214) use heads=1 and
+    arbitrary widths: GATConv(256, C, heads=1) training steps on the config-3
+    graph for C = 256 (C/4 a power of two: fused backward) and C = 200 / 255
+    (C % 4 padded, the wide forms for C/4 not a power of two)."""
+    from mi355_mp.graphgen import rmat_edge_index
+    from torch_geometric.nn import GATConv
+    N = 1 << 21
+    ei = rmat_edge_index(scale=21, n_samples=30_000_000, seed=1, device=dev)
+    x = torch.randn(N, 256, device=dev).requires_grad_(True)
+    for C in (256, 200, 255, 100, 731):
+        conv = GATConv(256, C, heads=1).to(dev)
+        fwd, step = _train_step_ms(conv, x, ei)
+        print(json.dumps({"config": "c3train_h1", "desc": "GATConv(256, %d, heads=1) layer on RMAT21" % C,
+                          "C": C, "forward_ms": fwd, "forward_backward_ms": step}), flush=True)
+        del conv
+        torch.cuda.empty_cache()
+
+
 def c5reorder(dev):
     """ogbn-products-shaped first layer GCNConv(100, 256): reference order
     A (X W) vs aggregate_first (A X) W, forward + backward."""
