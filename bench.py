@@ -14,7 +14,11 @@ are timed separately and reported beside the metric.
 N > 1: the same graph is sharded by destination range (edge balanced), built
 from per-rank slices of the edge list (ShardedGraph.for_gcn_from_slices: no
 rank holds the whole list); a step is the halo all_to_all (RCCL) overlapped
-with the interior edges, then the boundary edges, on every rank; value = E' /
+with the interior edges, then the boundary edges, on every rank.  The
+exchange is the hybrid cover (dist.HaloCover: a remote source row is pulled, or
+its owner pushes a partial row of the destination, whichever covers the cross
+edges with fewer rows; 0.60x the pull rows on this graph); --no-halo-cover
+pulls every remote source.  value = E' /
 max-over-ranks step time (strong scaling).  extra.per_rank carries each rank's
 halo bytes and the interior / exposed-exchange / boundary split of its steps.
 
@@ -58,6 +62,9 @@ def parse():
     ap.add_argument("--cpu-sample-edges", type=int, default=48_000_000)
     ap.add_argument("--chunk", type=int, default=0, help="merge-path task size (0: auto_chunk)")
     ap.add_argument("--no-overlap", action="store_true", help="N>1: exchange, then aggregate (no overlap)")
+    ap.add_argument("--no-halo-cover", action="store_true",
+                    help="N>1: pull exchange (every remote source row) instead of the hybrid pull / push "
+                         "cover (dist.HaloCover)")
     ap.add_argument("--halo-tile", type=int, default=128,
                     help="N>1: exchange and finish the boundary edges per feature tile of this width "
                          "(pipelined); 0 = one exchange of whole rows")
@@ -281,19 +288,23 @@ def main():
         x_local = plan.local_buffer(F_DIM)
         x_local[:plan.n_own].copy_(x_full[plan.lo:plan.hi])
         x = x_local[:plan.n_own]
-        x_tiles = None
+        overlap = mdist.OverlappedAggregation(plan, sg.norm_fwd, chunk=args.chunk or None, local_weights=True,
+                                              cover=not (args.no_halo_cover or args.no_overlap))
+        x_tiles = x_ov = None
         if args.halo_tile > 0 and not args.no_overlap:
-            x_tiles = plan.local_tiles(F_DIM, args.halo_tile)
+            x_tiles = overlap.local_tiles(F_DIM, args.halo_tile)
             c0 = 0
             for xt in x_tiles:
                 xt[:plan.n_own].copy_(x_full[plan.lo:plan.hi, c0:c0 + xt.shape[1]])
                 c0 += xt.shape[1]
+        elif not args.no_overlap:
+            x_ov = overlap.local_buffer(F_DIM)
+            x_ov[:plan.n_own].copy_(x_full[plan.lo:plan.hi])
         del x_full
         lei = plan.local_edge_index
         graph = sg.g_fwd
         csr = graph.dst
         w_csr = sg._w[0]
-        overlap = mdist.OverlappedAggregation(plan, sg.norm_fwd, chunk=args.chunk or None, local_weights=True)
         n_rows = plan.n_own
         E_local = lei.shape[1]
     torch.cuda.synchronize()
@@ -331,7 +342,7 @@ def main():
         elif x_tiles is not None:
             overlap.step_tiled(x_tiles, out_buf, bias, events=None if i is None else step_events[i])
         else:
-            overlap.step(x_local, out_buf, bias)
+            overlap.step(x_ov, out_buf, bias)
 
     step_events = [dict() for _ in range(args.steps)]
     for _ in range(args.warmup):
@@ -451,13 +462,22 @@ def main():
             return sum(lst[j].elapsed_time(lst[j + 1]) for j in range(0, len(lst) - 1, 2))
         torch.cuda.synchronize()
         mine = {"rank": rank, "rows": plan.n_own, "edges": E_local, "interior_edges": overlap.n_interior,
-                "boundary_edges": overlap.n_boundary, "halo_rows": plan.n_local_src - plan.n_own,
-                "halo_bytes_in": (plan.n_local_src - plan.n_own) * F_DIM * 4,
-                "halo_bytes_out": int(plan.send_idx.numel()) * F_DIM * 4,
-                "peers_in": [int(c) for c in plan.recv_counts]}
+                "boundary_edges": overlap.n_boundary,
+                "exchange": "pull" if args.no_overlap or overlap.cover is None else "cover (pull + push partials)",
+                "halo_rows": (plan.n_local_src if args.no_overlap else overlap.n_local_src) - plan.n_own,
+                "halo_bytes_in": ((plan.n_local_src if args.no_overlap else overlap.n_local_src) - plan.n_own)
+                * F_DIM * 4,
+                "halo_bytes_out": (int(plan.send_idx.numel()) if args.no_overlap else overlap.n_send) * F_DIM * 4,
+                "pull_exchange_rows_in": plan.n_local_src - plan.n_own,
+                "peers_in": [int(c) for c in (plan.recv_counts if args.no_overlap else overlap.recv_counts)]}
+        if overlap.cover is not None:
+            mine.update({"cover_pulled_rows": overlap.cover.n_pull_rows,
+                         "cover_partial_rows": overlap.cover.n_push_rows,
+                         "cover_push_edges": overlap.cover.n_push_edges})
         if x_tiles is not None:
             n = max(1, len(step_events))
-            mine.update({"interior_ms": sum(span(e, "interior") for e in step_events) / n,
+            mine.update({"send_pack_ms": sum(span(e, "send") for e in step_events) / n,
+                         "interior_ms": sum(span(e, "interior") for e in step_events) / n,
                          "exchange_exposed_ms": sum(span(e, "wait") for e in step_events) / n,
                          "boundary_ms": sum(span(e, "boundary") for e in step_events) / n})
         ranks = [None] * world
@@ -502,7 +522,9 @@ def main():
             "extra": {"gemm_xW_ms": gemm_ms, "layer_ms_est": gemm_ms + main_avg + fix_avg,
                       "one_time_build_s": t_build, "graph_gen_s": t_gen,
                       "edges_local_rank0": E_local, "n_split_rows": csr.n_split,
-                      "halo_rows_rank0": (plan.n_local_src - plan.n_own) if world > 1 else 0,
+                      "halo_rows_rank0": ((plan.n_local_src if args.no_overlap else overlap.n_local_src)
+                                          - plan.n_own) if world > 1 else 0,
+                      "halo_cover": world > 1 and not args.no_overlap and not args.no_halo_cover,
                       "interior_edges_rank0": overlap.n_interior if world > 1 else E_local,
                       "overlap": world > 1 and not args.no_overlap,
                       "halo_tile": args.halo_tile if world > 1 and not args.no_overlap else None,

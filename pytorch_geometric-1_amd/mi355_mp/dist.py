@@ -14,7 +14,12 @@ examples/data_parallel.py:35-49).  One large graph is sharded here instead:
   * per layer: every rank packs the rows its peers requested (native row
     gather), one all_to_all_single moves them (RCCL over xGMI: each peer pair
     on its own link), then the local fused aggregation runs on
-    [own rows ; halo rows].
+    [own rows ; halo rows];
+  * HaloCover (the bench's exchange): a cross edge is covered either by
+    pulling its source row or by its source's owner pushing a partial row of
+    the destination, whichever covers the pair's cross edges with fewer rows
+    (0.60x the pull rows on RMAT21); the sender fills its send buffer with one
+    aggregation over a send graph.
 
 The plan is built natively on the device (mp_shard_plan: flag + scan, no
 sort); host tensors take its torch-op form (_plan_torch), which the gloo tests
@@ -363,6 +368,158 @@ def _norm_over_plan(plan, deg_own, w_local, group=None):
     return dinv[lei[0]] * w_local * dinv[lei[1]]
 
 
+class HaloCover:
+    """Hybrid halo exchange of a sum aggregation: fewer rows over the links.
+
+    The pull exchange (ShardPlan) ships x_j of every remote source of the
+    rank's in-edges.  A cross edge j -> i (j owned by q, i by p) can equally be
+    covered by q shipping its PARTIAL row of i, sum over its own sources j of
+    w_ji x_j.  Covering every cross edge of the pair (q, p) with the fewest rows
+    is a minimum vertex cover of the bipartite cross-edge graph; on power-law
+    graphs a hub source is best pulled and a hub destination best pushed.
+    Rule (one-time, on the receiver p, from its own in-edges): an edge goes to
+    the endpoint with the larger cross-degree of the pair (ties: pull), then two
+    clean-ups -- an edge whose source is pulled anyway is pulled, an edge whose
+    destination is pushed anyway is pushed.  On RMAT graphs that ships 0.60x the
+    pull rows, within 2-3 % of the exact minimum cover (Konig / Hopcroft-Karp;
+    tools/exp_halo_cover.py, profiles/r03_halo_cover.log).
+
+    Per step the sender fills its whole send buffer with ONE aggregation over a
+    "send graph": a pulled row is a row with one edge of weight 1.0 (an exact
+    copy), a pushed row sums its push edges in global edge order.  The receiver
+    aggregates its boundary edges over [own rows ; received rows]: the pulled
+    edges with their weights plus one weight-1.0 edge per received partial.
+    Rows sum the same terms as the single-GPU kernel, regrouped: within the
+    1e-5 * sum|w x| bound, not bit-identical (exact on integer-valued data).
+
+    Built from a forward ShardPlan (flow source_to_target) and the plan's local
+    edge weights; every rank of `group` builds its cover together (three
+    all_to_alls of the requests)."""
+
+    def __init__(self, plan, w_local, group=None):
+        dev = plan.halo_nodes.device
+        world, rank = plan.world, plan.rank
+        n_own = plan.n_own
+        lei = plan.local_edge_index
+        src_l, dst_l = lei[0], lei[1]
+        if w_local is None:
+            w_local = torch.ones(src_l.numel(), dtype=torch.float32, device=dev)
+        w_local = w_local.to(torch.float32)
+        cuts_t = torch.tensor(plan.cuts[1:], dtype=torch.int64, device=dev)
+        interior = src_l < n_own
+        self.int_src, self.int_dst, self.int_w = src_l[interior], dst_l[interior], w_local[interior]
+        rem = ~interior
+        r_src = plan.halo_nodes[src_l[rem] - n_own]          # global source ids, plan (global edge) order
+        r_dst = dst_l[rem]
+        r_w = w_local[rem]
+        r_own = torch.searchsorted(cuts_t, r_src, right=True)
+        stride = max(n_own, 1)
+        # --- the cover: larger cross-degree endpoint, then the two clean-ups.  Dense
+        # O(N + E) counting (bincount / cumsum / nonzero), no sort or unique
+        N = plan.cuts[-1]
+        key = r_own * stride + r_dst                          # (owner, destination) of a cross edge
+        nkey = world * stride
+        if r_src.numel():
+            cs = torch.bincount(r_src, minlength=N)           # cross out-degree of each remote source
+            cd = torch.bincount(key, minlength=nkey)          # cross in-degree per (owner, destination)
+            pick = cs[r_src] >= cd[key]
+            in_s = torch.bincount(r_src[pick], minlength=N) > 0
+            push = ~in_s[r_src]
+            in_d = torch.bincount(key[push], minlength=nkey) > 0
+            push = in_d[key]
+            pull = ~push
+            in_s = torch.bincount(r_src[pull], minlength=N) > 0
+            del cs, cd, pick
+        else:
+            in_s = torch.zeros(N, dtype=torch.bool, device=dev)
+            in_d = torch.zeros(nkey, dtype=torch.bool, device=dev)
+            push = pull = torch.zeros(0, dtype=torch.bool, device=dev)
+        S = torch.nonzero(in_s).view(-1)                      # ascending node ids: grouped by owner
+        D = torch.nonzero(in_d).view(-1)                      # ascending (owner, destination) keys
+        s_rank = torch.cumsum(in_s, 0) - 1                    # position of a pulled node in S
+        d_rank = torch.cumsum(in_d, 0) - 1                    # position of a pushed key in D
+        del in_s, in_d
+        S_own = torch.searchsorted(cuts_t, S, right=True)
+        D_own = D // stride
+        nS = torch.bincount(S_own, minlength=world)
+        nD = torch.bincount(D_own, minlength=world)
+        p_own = r_own[push]
+        nP = torch.bincount(p_own, minlength=world)
+        self.recv_counts = (nS + nD).tolist()
+        off = [0]
+        for c in self.recv_counts:
+            off.append(off[-1] + c)
+        off_t = torch.tensor(off[:-1], dtype=torch.int64, device=dev)
+        S_start = torch.cumsum(nS, 0) - nS
+        D_start = torch.cumsum(nD, 0) - nD
+        # halo slot of each pulled source / pushed destination row: per owner q,
+        # [its pulled rows ; its partial rows]
+        s_pos = s_rank[r_src[pull]]
+        s_q = S_own[s_pos]
+        pull_halo = n_own + off_t[s_q] + (s_pos - S_start[s_q])
+        d_q = D_own
+        d_halo = n_own + off_t[d_q] + nS[d_q] + (torch.arange(D.numel(), device=dev) - D_start[d_q])
+        self.bnd_src = torch.cat([pull_halo, d_halo])
+        self.bnd_dst = torch.cat([r_dst[pull], D - d_q * stride])
+        self.bnd_w = torch.cat([r_w[pull], torch.ones(D.numel(), dtype=torch.float32, device=dev)])
+        self.n_halo = off[-1]
+        self.n_local_src = n_own + self.n_halo
+        self.n_pull_rows, self.n_push_rows = int(S.numel()), int(D.numel())
+        self.n_pull_edges, self.n_push_edges = int(pull.sum()), int(push.sum())
+        # --- requests to the owners: pulled ids, and the push edges (source, partial row, weight)
+        p_row = d_rank[key[push]] - D_start[p_own]
+        del s_rank, d_rank
+        # push edges grouped by owner, global edge order inside (a stable partition)
+        order = torch.cat([torch.nonzero(p_own == q).view(-1) for q in range(world)])
+        cnt = torch.stack([nS, nD, nP], 1).reshape(-1).contiguous()
+        cnt_in = torch.empty_like(cnt)
+        _a2a(cnt_in, cnt, group=group)
+        cin = cnt_in.view(world, 3).tolist()
+        snS = [c[0] for c in cin]
+        snD = [c[1] for c in cin]
+        snP = [c[2] for c in cin]
+        req = S.new_empty(sum(snS))
+        _a2a(req, S.contiguous(), snS, nS.tolist(), group)
+        lo = plan.lo
+        ps = S.new_empty(sum(snP))
+        _a2a(ps, r_src[push][order].contiguous(), snP, nP.tolist(), group)
+        pr = S.new_empty(sum(snP))
+        _a2a(pr, p_row[order].contiguous(), snP, nP.tolist(), group)
+        pw = r_w.new_empty(sum(snP))
+        _a2a(pw, r_w[push][order].contiguous(), snP, nP.tolist(), group)
+        # --- the send graph: rows = this rank's send buffer (per peer: pulled rows, then partial rows)
+        self.send_counts = [a + b for a, b in zip(snS, snD)]
+        base = [0]
+        for c in self.send_counts:
+            base.append(base[-1] + c)
+        peer_s = torch.repeat_interleave(torch.arange(world, device=dev), torch.tensor(snS, device=dev))
+        peer_p = torch.repeat_interleave(torch.arange(world, device=dev), torch.tensor(snP, device=dev))
+        base_t = torch.tensor(base[:-1], dtype=torch.int64, device=dev)
+        sS_start = torch.tensor([sum(snS[:k]) for k in range(world)], dtype=torch.int64, device=dev)
+        snS_t = torch.tensor(snS, dtype=torch.int64, device=dev)
+        pull_rows = base_t[peer_s] + (torch.arange(req.numel(), device=dev) - sS_start[peer_s])
+        push_rows = base_t[peer_p] + snS_t[peer_p] + pr
+        self.send_src = torch.cat([req - lo, ps - lo])
+        self.send_dst = torch.cat([pull_rows, push_rows])
+        self.send_w = torch.cat([torch.ones(req.numel(), dtype=torch.float32, device=dev), pw])
+        self.n_send = base[-1]
+        if self.send_src.numel() and (int(self.send_src.min()) < 0 or int(self.send_src.max()) >= n_own):
+            raise RuntimeError("HaloCover: a peer requested a row this rank does not own")
+        self.n_own = n_own
+
+    def host_step(self, x_own, aggregate, group=None):
+        """Reference form of one step on host tensors: aggregate(x_src, src_idx,
+        dst_idx, w, n_dst) is the serial edge-order sum (the oracle).  Returns
+        the rank's [n_own, F] sum over all its in-edges."""
+        F = x_own.shape[1]
+        send = aggregate(x_own, self.send_src, self.send_dst, self.send_w, self.n_send)
+        xl = x_own.new_empty((self.n_local_src, F))
+        xl[:self.n_own] = x_own
+        _a2a(xl[self.n_own:], send.contiguous(), self.recv_counts, self.send_counts, group)
+        out = aggregate(x_own, self.int_src, self.int_dst, self.int_w, self.n_own)
+        return out + aggregate(xl, self.bnd_src, self.bnd_dst, self.bnd_w, self.n_own)
+
+
 class OverlappedAggregation:
     """GCN-style sharded aggregation with the halo exchange hidden behind the
     interior edges.
@@ -379,40 +536,81 @@ class OverlappedAggregation:
     1e-5 bound of the single-GPU order, not bit-identical to it.
     """
 
-    def __init__(self, plan, edge_weight=None, chunk=None, local_weights=False):
+    def __init__(self, plan, edge_weight=None, chunk=None, local_weights=False, cover=False, group=None):
         """edge_weight: per-edge weights of the list the plan was built from
         (indexed by plan.edge_pos); local_weights=True: already in the plan's
-        local edge order."""
+        local edge order.  cover=True: the hybrid pull / push exchange of
+        HaloCover (fewer rows over the links; built collectively over `group`),
+        else the plan's pull exchange."""
         from .graph import Graph
         self.plan = plan
+        self.n_own = plan.n_own
         lei = plan.local_edge_index
         src_local = lei[0]
         interior = src_local < plan.n_own
         w = None
         if edge_weight is not None:
             w = edge_weight if local_weights else edge_weight[plan.edge_pos]
-        ei_int = lei[:, interior]
-        ei_bnd = lei[:, ~interior]
+        self.cover = None
+        if cover:
+            hc = HaloCover(plan, w, group)
+            self.cover = hc
+            ei_int = torch.stack([hc.int_src, hc.int_dst])
+            ei_bnd = torch.stack([hc.bnd_src, hc.bnd_dst])
+            w_int, w_bnd = hc.int_w, hc.bnd_w
+            self.recv_counts, self.send_counts = hc.recv_counts, hc.send_counts
+            self.n_local_src = hc.n_local_src
+            self.n_send = hc.n_send
+            self.g_send = Graph(torch.stack([hc.send_src, hc.send_dst]), hc.n_send, plan.n_own, chunk=chunk)
+            self.w_send = self.g_send.dst.to_csr_order(hc.send_w.contiguous())
+        else:
+            ei_int = lei[:, interior]
+            ei_bnd = lei[:, ~interior]
+            w_int = w[interior] if w is not None else None
+            w_bnd = w[~interior] if w is not None else None
+            self.recv_counts, self.send_counts = plan.recv_counts, plan.send_counts
+            self.n_local_src = plan.n_local_src
+            self.n_send = int(plan.send_idx.numel())
         self.g_int = Graph(ei_int, plan.n_own, plan.n_own, chunk=chunk)
-        self.g_bnd = Graph(ei_bnd, plan.n_own, plan.n_local_src, chunk=chunk)
-        self.w_int = self.g_int.dst.to_csr_order(w[interior].contiguous()) if w is not None else None
-        self.w_bnd = self.g_bnd.dst.to_csr_order(w[~interior].contiguous()) if w is not None else None
+        self.g_bnd = Graph(ei_bnd, plan.n_own, self.n_local_src, chunk=chunk)
+        self.w_int = self.g_int.dst.to_csr_order(w_int.contiguous()) if w_int is not None else None
+        self.w_bnd = self.g_bnd.dst.to_csr_order(w_bnd.contiguous()) if w_bnd is not None else None
         self.n_interior = int(ei_int.shape[1])
         self.n_boundary = int(ei_bnd.shape[1])
+
+    def local_buffer(self, F, dtype=torch.float32, device=None):
+        """[n_own + n_halo, F]: the owner writes rows [:n_own], the exchange the rest."""
+        return torch.empty((self.n_local_src, F), dtype=dtype, device=device or self.plan.halo_nodes.device)
+
+    def local_tiles(self, F, tile=128, dtype=torch.float32, device=None):
+        """Tile-major buffers for step_tiled (see ShardPlan.local_tiles)."""
+        dev = device or self.plan.halo_nodes.device
+        return [torch.empty((self.n_local_src, min(tile, F - c0)), dtype=dtype, device=dev)
+                for c0 in range(0, F, tile)]
+
+    def _send(self, own):
+        """This rank's send buffer: the requested rows (pull), or with a cover
+        one aggregation over the send graph (copies + partial rows)."""
+        from . import ops
+        F = own.shape[1]
+        if self.n_send == 0:
+            return own.new_empty((0, F))
+        if self.cover is not None:
+            return ops._aggregate(self.g_send.dst, "other", own, self.w_send, "sum", 0, None)[0]
+        return ops.gather_rows(own, self.plan.send_idx)
 
     def step(self, x_local, out, bias=None, group=None):
         from . import _lib, ops
         plan = self.plan
-        F = x_local.shape[1]
         own = x_local[:plan.n_own]
-        send = ops.gather_rows(own, plan.send_idx) if plan.send_idx.numel() else x_local.new_empty((0, F))
+        send = self._send(own)
         halo = x_local[plan.n_own:]
         work = None
         if x_local.is_cuda and dist.get_backend(group) == "gloo":
-            _a2a(halo, send, plan.recv_counts, plan.send_counts, group)
+            _a2a(halo, send, self.recv_counts, self.send_counts, group)
         else:
-            work = dist.all_to_all_single(halo, send, output_split_sizes=plan.recv_counts,
-                                          input_split_sizes=plan.send_counts, group=group, async_op=True)
+            work = dist.all_to_all_single(halo, send, output_split_sizes=self.recv_counts,
+                                          input_split_sizes=self.send_counts, group=group, async_op=True)
         ops._aggregate(self.g_int.dst, "other", own, self.w_int, "sum", 0, None, out=out)
         if work is not None:
             work.wait()
@@ -431,7 +629,9 @@ class OverlappedAggregation:
         Tile t's boundary pass overlaps tile t+1's exchange.  Per row and
         feature the arithmetic is that of step(): bitwise the same output.
         events (optional dict of lists): HIP events recorded on the compute
-        stream -- 'interior' (start, end) of the interior passes, 'wait'
+        stream -- 'send' (start, end) of packing every tile's send buffer (the
+        cover's send graph: copies + partial rows), 'interior' (start, end) of
+        the interior passes, 'wait'
         (before, after) around each tile's wait (the exchange time the compute
         stream is exposed to), 'boundary' (start, end) of each boundary pass."""
         def rec(name):
@@ -450,18 +650,22 @@ class OverlappedAggregation:
         if offs[-1] != out.shape[1]:
             raise ValueError("step_tiled: tiles cover %d features, out has %d" % (offs[-1], out.shape[1]))
         pending = []
+        rec("send")
         for xt in x_tiles:
+            if xt.shape[0] != self.n_local_src:
+                raise ValueError("step_tiled: tiles have %d rows, this exchange needs %d (use local_tiles())"
+                                 % (xt.shape[0], self.n_local_src))
             own = xt[:plan.n_own]
-            send = (ops.gather_rows(own, plan.send_idx) if plan.send_idx.numel()
-                    else xt.new_empty((0, xt.shape[1])))
+            send = self._send(own)
             halo = xt[plan.n_own:]
             if gloo:
-                _a2a(halo, send, plan.recv_counts, plan.send_counts, group)
+                _a2a(halo, send, self.recv_counts, self.send_counts, group)
                 pending.append((None, send))
             else:
-                work = dist.all_to_all_single(halo, send, output_split_sizes=plan.recv_counts,
-                                              input_split_sizes=plan.send_counts, group=group, async_op=True)
+                work = dist.all_to_all_single(halo, send, output_split_sizes=self.recv_counts,
+                                              input_split_sizes=self.send_counts, group=group, async_op=True)
                 pending.append((work, send))
+        rec("send")
         rec("interior")
         for t, xt in enumerate(x_tiles):
             ops._aggregate(self.g_int.dst, "other", xt[:plan.n_own], self.w_int, "sum", 0, None,

@@ -79,7 +79,15 @@ def main():
                         ds = np.bincount(si)[si]
                         dd = np.bincount(di)[di]
                         pick_s = ds >= dd
-                        r = np.unique(si[pick_s]).size + np.unique(di[~pick_s]).size
+                        # refinement 1: an edge whose source is pulled anyway is pulled
+                        in_s = np.zeros(us.size, bool)
+                        in_s[si[pick_s]] = True
+                        push = ~in_s[si]
+                        # refinement 2: an edge whose destination is pushed anyway is pushed
+                        in_d = np.zeros(ud.size, bool)
+                        in_d[di[push]] = True
+                        pull = ~in_d[di]
+                        r = np.unique(si[pull]).size + int(in_d.sum())
                     else:
                         if not a.exact:
                             continue
