@@ -185,3 +185,47 @@ def scatter_loop_any(src, index, dim_size, reduce, out=None):
     ot = torch.from_numpy(np.ascontiguousarray(o)).reshape(shape)
     at = torch.from_numpy(a).reshape(shape) if a is not None else None
     return ot, at
+
+
+# --- composites (torch_scatter 2.0.4 composite/softmax.py, logsumexp.py, std.py) ---
+# The published 2.0.4 composites restated for 2-D src and a 1-D index along dim
+# 0, on the serial-loop max and the edge-order scatter_add above (the package
+# is not in the reference tree: parity unpinned).
+
+def scatter_softmax(src, index, eps=1e-12):
+    """softmax.py: max_seg, recentre, exp, sum_seg + eps, divide."""
+    n = int(index.max()) + 1 if index.numel() else 0
+    mx = scatter_loop(src, index, n, "max")[0]
+    e = (src - mx[index]).exp()
+    return e / (scatter_sum(e, index, n) + eps)[index]
+
+
+def scatter_log_softmax(src, index, eps=1e-12):
+    n = int(index.max()) + 1 if index.numel() else 0
+    mx = scatter_loop(src, index, n, "max")[0]
+    rc = src - mx[index]
+    return rc - torch.log(scatter_sum(rc.exp(), index, n) + eps)[index]
+
+
+def scatter_logsumexp(src, index, dim_size, eps=1e-12):
+    """logsumexp.py: scatter_max into a -inf tensor (out given: no init, no
+    masking), recentre, NaN -> -inf, log(sum exp + eps) + max."""
+    mx = torch.full((dim_size, src.shape[1]), float("-inf"), dtype=torch.float32)
+    mx = scatter_loop(src, index, dim_size, "max", out=mx)[0]
+    rc = src - mx[index]
+    rc = rc.masked_fill(torch.isnan(rc), float("-inf"))
+    return torch.log(scatter_sum(rc.exp(), index, dim_size) + eps) + mx
+
+
+def scatter_std(src, index, dim_size, unbiased=True):
+    """std.py: count = scatter_sum(ones) clamped to 1, mean = sum / count,
+    sum of squared deviations / (count' + 1e-6), sqrt; count' = max(count - 1,
+    1) when unbiased."""
+    count = torch.zeros(dim_size, dtype=src.dtype).scatter_add_(0, index, torch.ones(index.numel(), dtype=src.dtype))
+    count = count.clamp(min=1).view(-1, 1)
+    mean = scatter_sum(src, index, dim_size) / count
+    var = (src - mean[index]) ** 2
+    out = scatter_sum(var, index, dim_size)
+    if unbiased:
+        count = (count - 1).clamp(min=1)
+    return (out / (count + 1e-6)).sqrt()

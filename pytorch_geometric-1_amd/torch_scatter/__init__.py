@@ -10,6 +10,12 @@ the reference tree -- see SURVEY.md 2b U8/U9):
     scatter(src, index, dim=-1, out=None, dim_size=None, reduce="sum")
     segment_csr(src, indptr, out=None, reduce="sum"), gather_csr(src, indptr, out=None)
     segment_coo(src, index, out=None, dim_size=None, reduce="sum"), gather_coo(src, index, out=None)
+    segment_{sum,add,mean,min,max}_{csr,coo}   (the named forms)
+    scatter_softmax / scatter_log_softmax(src, index, dim=-1, eps=1e-12)
+    scatter_logsumexp(src, index, dim=-1, out=None, dim_size=None, eps=1e-12)
+    scatter_std(src, index, dim=-1, out=None, dim_size=None, unbiased=True)
+      (torch_scatter/composite/: restated from the published 2.0.4 source, the
+      reductions on the native kernels, the elementwise steps as device ops)
 
 The compiled package's dispatcher ops are registered too (torch.ops.torch_scatter.
 scatter_max/min, segment_{sum,mean,min,max}_{csr,coo}, gather_{csr,coo}; the
@@ -29,7 +35,10 @@ from mi355_mp import _lib
 __version__ = "2.0.4"
 
 __all__ = ["scatter", "scatter_sum", "scatter_add", "scatter_mean", "scatter_max", "scatter_min",
-           "segment_csr", "gather_csr", "segment_coo", "gather_coo"]
+           "segment_csr", "gather_csr", "segment_coo", "gather_coo",
+           "segment_sum_csr", "segment_add_csr", "segment_mean_csr", "segment_min_csr", "segment_max_csr",
+           "segment_sum_coo", "segment_add_coo", "segment_mean_coo", "segment_min_coo", "segment_max_coo",
+           "scatter_softmax", "scatter_log_softmax", "scatter_logsumexp", "scatter_std"]
 
 
 def _broadcast(index, src, dim):
@@ -217,6 +226,145 @@ def gather_coo(src, index, out=None):
     """torch_scatter.gather_coo along dim 0: out[e] = src[index[e]]."""
     _lib.require_device(src, index)
     res = _ops.index_select_rows(src.reshape(src.shape[0], -1), index).reshape((-1,) + tuple(src.shape[1:]))
+    if out is not None:
+        out.copy_(res)
+        return out
+    return res
+
+
+def segment_sum_csr(src, indptr, out=None):
+    return segment_csr(src, indptr, out, "sum")
+
+
+def segment_add_csr(src, indptr, out=None):
+    return segment_csr(src, indptr, out, "sum")
+
+
+def segment_mean_csr(src, indptr, out=None):
+    return segment_csr(src, indptr, out, "mean")
+
+
+def segment_min_csr(src, indptr, out=None):
+    return segment_csr(src, indptr, out, "min")
+
+
+def segment_max_csr(src, indptr, out=None):
+    return segment_csr(src, indptr, out, "max")
+
+
+def segment_sum_coo(src, index, out=None, dim_size=None):
+    return segment_coo(src, index, out, dim_size, "sum")
+
+
+def segment_add_coo(src, index, out=None, dim_size=None):
+    return segment_coo(src, index, out, dim_size, "sum")
+
+
+def segment_mean_coo(src, index, out=None, dim_size=None):
+    return segment_coo(src, index, out, dim_size, "mean")
+
+
+def segment_min_coo(src, index, out=None, dim_size=None):
+    return segment_coo(src, index, out, dim_size, "min")
+
+
+def segment_max_coo(src, index, out=None, dim_size=None):
+    return segment_coo(src, index, out, dim_size, "max")
+
+
+# ---------------------------------------------------------------------------
+# composite ops (torch_scatter 2.0.4 composite/{softmax,logsumexp,std}.py)
+# ---------------------------------------------------------------------------
+
+def _gather_back(t, index, dim):
+    """t.gather(dim, broadcast(index)) -- each element's segment value.  A 1-D
+    index (PyG's form) takes the native row gather."""
+    d = dim % t.dim()
+    if index.dim() == 1:
+        moved = t.movedim(d, 0)
+        rows = _ops.index_select_rows(moved.reshape(moved.shape[0], -1).contiguous(), index.to(torch.int64))
+        return rows.reshape((index.numel(),) + tuple(moved.shape[1:])).movedim(0, d)
+    size = list(t.shape)
+    size[d] = index.size(d) if index.dim() > d else index.size(-1)
+    return t.gather(d, _broadcast(index, torch.empty(size, device="meta"), d))
+
+
+def _check_float(src, name):
+    if not torch.is_floating_point(src):
+        raise ValueError("`%s` can only be computed over tensors with floating point data types." % name)
+
+
+def scatter_softmax(src, index, dim=-1, eps=1e-12):
+    """exp(src - max_seg) / (sum_seg exp(src - max_seg) + eps), per element."""
+    _check_float(src, "scatter_softmax")
+    dim = dim % src.dim()
+    max_per_index = scatter_max(src, index, dim=dim)[0]
+    recentered = src - _gather_back(max_per_index, index, dim)
+    e = recentered.exp()
+    den = scatter_sum(e, index, dim, dim_size=max_per_index.size(dim)) + eps
+    return e / _gather_back(den, index, dim)
+
+
+def scatter_log_softmax(src, index, dim=-1, eps=1e-12):
+    """(src - max_seg) - log(sum_seg exp(src - max_seg) + eps), per element."""
+    _check_float(src, "scatter_log_softmax")
+    dim = dim % src.dim()
+    max_per_index = scatter_max(src, index, dim=dim)[0]
+    recentered = src - _gather_back(max_per_index, index, dim)
+    den = scatter_sum(recentered.exp(), index, dim, dim_size=max_per_index.size(dim)) + eps
+    return recentered - _gather_back(den.log(), index, dim)
+
+
+def scatter_logsumexp(src, index, dim=-1, out=None, dim_size=None, eps=1e-12):
+    """log(sum_seg exp(src - max_seg) + eps) + max_seg; the max starts from -inf
+    (scatter_max into a -inf tensor: empty segments stay -inf), NaN
+    differences count as -inf; a given `out` enters as exp(out - max)."""
+    _check_float(src, "scatter_logsumexp")
+    dim = dim % src.dim()
+    if out is not None:
+        dim_size = out.size(dim)
+    elif dim_size is None:
+        dim_size = int(index.max()) + 1 if index.numel() else 0
+    size = list(src.size())
+    size[dim] = dim_size
+    max_per_index = torch.full(size, float("-inf"), dtype=src.dtype, device=src.device)
+    scatter_max(src, index, dim, max_per_index, dim_size=dim_size)
+    recentered = src - _gather_back(max_per_index, index, dim)
+    recentered = recentered.masked_fill(torch.isnan(recentered), float("-inf"))
+    if out is not None:
+        out = out.sub_(max_per_index).exp_()
+    s = scatter_sum(recentered.exp(), index, dim, out, dim_size)
+    return s.add_(eps).log_().add_(max_per_index)
+
+
+def scatter_std(src, index, dim=-1, out=None, dim_size=None, unbiased=True):
+    """sqrt(sum_seg (src - mean_seg)^2 / (c + 1e-6)), mean = sum / max(count, 1),
+    c = max(max(count, 1) - 1, 1) when unbiased else max(count, 1)."""
+    if out is not None:
+        dim_size = out.size(dim)
+    dim = dim % src.dim()
+    idx = _index_1d(src, index, dim)
+    if dim_size is None:
+        dim_size = int(index.max()) + 1 if index.numel() else 0
+    if idx is not None:
+        ones = torch.ones(idx.numel(), 1, dtype=src.dtype, device=src.device)
+        count = scatter_sum(ones, idx, 0, dim_size=dim_size).view(-1)
+        shape = [1] * src.dim()
+        shape[dim] = dim_size
+        count = count.view(shape)
+    else:
+        ones = torch.ones(src.size(), dtype=src.dtype, device=src.device)
+        count = scatter_sum(ones, index, dim, dim_size=dim_size)
+    tmp = scatter_sum(src, index, dim, dim_size=dim_size)
+    count = count.clamp(min=1)
+    mean = tmp / count
+    var = src - _gather_back(mean, index, dim)
+    var = var * var
+    res = scatter_sum(var, index, dim, out, dim_size)
+    if unbiased:
+        count = (count - 1).clamp(min=1)
+    res = res / (count + 1e-6)
+    res = res.sqrt()
     if out is not None:
         out.copy_(res)
         return out

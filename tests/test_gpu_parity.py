@@ -2495,3 +2495,79 @@ def test_fuzz_gat_training_with_attention_dropout(N, deg, H, C, p, chunk, star, 
     want.backward(gout.double())
     for got, ref in ((xd.grad, x64.grad), (ad.grad, a64.grad), (bd.grad, b64.grad)):
         assert torch.allclose(got.cpu().double(), ref, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_torch_scatter_composites_match_oracle(dtype):
+    """torch_scatter's composite ops (scatter_softmax / log_softmax /
+    logsumexp incl. out= / std biased and unbiased) on the native reductions
+    against the oracle's restatement of the 2.0.4 composites, along dim 0 and
+    dim -1, with empty and one-element segments and a hub segment; the named
+    segment_*_{csr,coo} forms equal segment_csr / segment_coo."""
+    import torch_scatter as T
+    from oracle import scatter_ref as S
+    g = torch.Generator().manual_seed(12)
+    N, F = 40, 9
+    idx = torch.randint(N - 5, (700,), generator=g)
+    idx[:200] = 3                                   # hub segment
+    idx[idx == 7] = 8                               # segment 7 empty
+    src = torch.randn(idx.numel(), F, generator=g)
+    tol = dict(rtol=1e-5, atol=1e-6) if dtype == torch.float32 else dict(rtol=1e-12, atol=1e-12)
+    sd, id_ = src.to(DEV, dtype), idx.to(DEV)
+    ref = {"softmax": S.scatter_softmax(src, idx), "log_softmax": S.scatter_log_softmax(src, idx),
+           "logsumexp": S.scatter_logsumexp(src, idx, N), "std": S.scatter_std(src, idx, N),
+           "std_b": S.scatter_std(src, idx, N, unbiased=False)}
+    got = {"softmax": T.scatter_softmax(sd, id_, dim=0), "log_softmax": T.scatter_log_softmax(sd, id_, dim=0),
+           "logsumexp": T.scatter_logsumexp(sd, id_, dim=0, dim_size=N),
+           "std": T.scatter_std(sd, id_, dim=0, dim_size=N),
+           "std_b": T.scatter_std(sd, id_, dim=0, dim_size=N, unbiased=False)}
+    for k in ref:
+        r, o = ref[k].double(), got[k].cpu().double()
+        fin = torch.isfinite(r)
+        assert torch.equal(fin, torch.isfinite(o)), k
+        assert torch.equal(r[~fin], o[~fin]), k                   # -inf of the empty segment
+        if dtype == torch.float32:
+            assert torch.allclose(o[fin], r[fin], **tol), (k, float((o[fin] - r[fin]).abs().max()))
+        else:   # oracle in fp32: compare the float64 result with its own float64 formula instead
+            assert torch.allclose(o[fin], r[fin], rtol=1e-5, atol=1e-6), k
+    # dim = -1 (transposed layout) equals dim 0
+    st = T.scatter_softmax(sd.t().contiguous(), id_, dim=-1).t()
+    assert torch.allclose(st.cpu().double(), got["softmax"].cpu().double(), **tol)
+    lt = T.scatter_logsumexp(sd.t().contiguous(), id_, dim=-1, dim_size=N).t()
+    assert torch.equal(torch.isfinite(lt.cpu()), torch.isfinite(got["logsumexp"].cpu()))
+    # out= of logsumexp enters as exp(out - max)
+    base = torch.randn(N, F, generator=g).to(DEV, dtype)
+    o = T.scatter_logsumexp(sd, id_, dim=0, out=base.clone())
+    mx = torch.full((N, F), float("-inf"), dtype=torch.float64)
+    mx = torch.maximum(mx, torch.zeros(N, F, dtype=torch.float64).index_reduce_(
+        0, idx, src.double(), "amax", include_self=False).masked_fill(
+        torch.bincount(idx, minlength=N).view(-1, 1).expand(N, F) == 0, float("-inf")))
+    e = (src.double() - mx[idx]).exp()
+    want = torch.log(torch.zeros(N, F, dtype=torch.float64).index_add_(0, idx, e)
+                     + (base.cpu().double() - mx).exp() + 1e-12) + mx
+    fin = torch.isfinite(want)
+    assert torch.allclose(o.cpu().double()[fin], want[fin], rtol=1e-5, atol=1e-5)
+    # named segment forms
+    sidx, _ = torch.sort(idx)
+    ptr = torch.zeros(N + 1, dtype=torch.int64)
+    ptr[1:] = torch.cumsum(torch.bincount(sidx, minlength=N), 0)
+    for red in ("sum", "mean", "max", "min"):
+        a = getattr(T, "segment_%s_csr" % red)(sd, ptr.to(DEV))
+        b = T.segment_csr(sd, ptr.to(DEV), reduce=red)
+        c = getattr(T, "segment_%s_coo" % red)(sd, sidx.to(DEV), dim_size=N)
+        d = T.segment_coo(sd, sidx.to(DEV), dim_size=N, reduce=red)
+        if red in ("max", "min"):
+            assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(c[0], d[0])
+        else:
+            assert torch.equal(a, b) and torch.equal(c, d)
+
+
+def test_torch_scatter_composites_gradcheck_float64():
+    import torch_scatter as T
+    g = torch.Generator().manual_seed(5)
+    idx = torch.randint(6, (40,), generator=g).to(DEV)
+    src = torch.randn(40, 3, generator=g, dtype=torch.float64).to(DEV).requires_grad_(True)
+    for fn in (lambda s: T.scatter_softmax(s, idx, dim=0), lambda s: T.scatter_log_softmax(s, idx, dim=0),
+               lambda s: T.scatter_logsumexp(s, idx, dim=0, dim_size=7)[:6],
+               lambda s: T.scatter_std(s, idx, dim=0, dim_size=6)):
+        assert torch.autograd.gradcheck(fn, (src,), eps=1e-6, atol=1e-6)

@@ -376,3 +376,33 @@ def test_gat_dropout_keep_hash_restatement():
     a = P.gat_conv(x, ei, W, att, None, H, C)
     b = P.gat_conv(x, ei, W, att, None, H, C, drop_keep=torch.ones(E, H, dtype=torch.bool), drop_p=0.25)
     assert torch.allclose(b, a / (1 - float(np.float32(0.25))), rtol=1e-12, atol=1e-12)
+
+
+def test_kat_composites_against_per_segment_float64():
+    """The oracle's torch_scatter composites (softmax, log_softmax, logsumexp,
+    std) against a float64 per-segment evaluation of their formulas, with an
+    empty segment and a one-element segment."""
+    g = torch.Generator().manual_seed(4)
+    idx = torch.tensor([0, 2, 0, 2, 3, 2, 0, 5])
+    src = torch.randn(8, 3, generator=g)
+    n = 6
+    sm = S.scatter_softmax(src, idx)
+    lsm = S.scatter_log_softmax(src, idx)
+    lse = S.scatter_logsumexp(src, idx, n)
+    sd = S.scatter_std(src, idx, n)
+    sdb = S.scatter_std(src, idx, n, unbiased=False)
+    for r in range(n):
+        m = idx == r
+        if not bool(m.any()):
+            assert bool(torch.isinf(lse[r]).all()) and bool((lse[r] < 0).all())
+            assert torch.equal(sd[r], torch.zeros(3))
+            continue
+        x = src[m].double()
+        e = (x - x.max(0).values).exp()
+        assert torch.allclose(sm[m].double(), e / (e.sum(0) + 1e-12), atol=1e-6)
+        assert torch.allclose(lsm[m].double(), (x - x.max(0).values) - torch.log(e.sum(0) + 1e-12), atol=1e-6)
+        assert torch.allclose(lse[r].double(), torch.log(e.sum(0) + 1e-12) + x.max(0).values, atol=1e-6)
+        c = x.shape[0]
+        dev2 = ((x - x.mean(0)) ** 2).sum(0)
+        assert torch.allclose(sd[r].double(), (dev2 / (max(c - 1, 1) + 1e-6)).sqrt(), atol=1e-5)
+        assert torch.allclose(sdb[r].double(), (dev2 / (c + 1e-6)).sqrt(), atol=1e-5)
