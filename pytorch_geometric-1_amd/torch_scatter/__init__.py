@@ -298,7 +298,9 @@ def scatter_softmax(src, index, dim=-1, eps=1e-12):
     """exp(src - max_seg) / (sum_seg exp(src - max_seg) + eps), per element."""
     _check_float(src, "scatter_softmax")
     dim = dim % src.dim()
-    max_per_index = scatter_max(src, index, dim=dim)[0]
+    # the shift carries no gradient (softmax is shift-invariant: upstream's
+    # gradient through the max cancels), so the max runs without autograd
+    max_per_index = scatter_max(src.detach(), index, dim=dim)[0]
     recentered = src - _gather_back(max_per_index, index, dim)
     e = recentered.exp()
     den = scatter_sum(e, index, dim, dim_size=max_per_index.size(dim)) + eps
@@ -309,7 +311,7 @@ def scatter_log_softmax(src, index, dim=-1, eps=1e-12):
     """(src - max_seg) - log(sum_seg exp(src - max_seg) + eps), per element."""
     _check_float(src, "scatter_log_softmax")
     dim = dim % src.dim()
-    max_per_index = scatter_max(src, index, dim=dim)[0]
+    max_per_index = scatter_max(src.detach(), index, dim=dim)[0]
     recentered = src - _gather_back(max_per_index, index, dim)
     den = scatter_sum(recentered.exp(), index, dim, dim_size=max_per_index.size(dim)) + eps
     return recentered - _gather_back(den.log(), index, dim)
@@ -328,7 +330,7 @@ def scatter_logsumexp(src, index, dim=-1, out=None, dim_size=None, eps=1e-12):
     size = list(src.size())
     size[dim] = dim_size
     max_per_index = torch.full(size, float("-inf"), dtype=src.dtype, device=src.device)
-    scatter_max(src, index, dim, max_per_index, dim_size=dim_size)
+    scatter_max(src.detach(), index, dim, max_per_index, dim_size=dim_size)   # shift: no gradient (cancels)
     recentered = src - _gather_back(max_per_index, index, dim)
     recentered = recentered.masked_fill(torch.isnan(recentered), float("-inf"))
     if out is not None:
