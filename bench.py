@@ -17,7 +17,7 @@ rank holds the whole list); a step is the halo all_to_all (RCCL) overlapped
 with the interior edges, then the boundary edges, on every rank.  The
 exchange is the hybrid cover (dist.HaloCover: a remote source row is pulled, or
 its owner pushes a partial row of the destination, whichever covers the cross
-edges with fewer rows; 0.60x the pull rows on this graph); --no-halo-cover
+edges with fewer rows; 0.57x the pull rows on this graph); --no-halo-cover
 pulls every remote source.  value = E' /
 max-over-ranks step time (strong scaling).  extra.per_rank carries each rank's
 halo bytes and the interior / exposed-exchange / boundary split of its steps.

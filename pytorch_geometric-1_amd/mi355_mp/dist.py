@@ -18,7 +18,7 @@ examples/data_parallel.py:35-49).  One large graph is sharded here instead:
   * HaloCover (the bench's exchange): a cross edge is covered either by
     pulling its source row or by its source's owner pushing a partial row of
     the destination, whichever covers the pair's cross edges with fewer rows
-    (0.60x the pull rows on RMAT21); the sender fills its send buffer with one
+    (0.57x the pull rows on RMAT21); the sender fills its send buffer with one
     aggregation over a send graph.
 
 The plan is built natively on the device (mp_shard_plan: flag + scan, no
@@ -380,8 +380,8 @@ class HaloCover:
     Rule (one-time, on the receiver p, from its own in-edges): an edge goes to
     the endpoint with the larger cross-degree of the pair (ties: pull), then two
     clean-ups -- an edge whose source is pulled anyway is pulled, an edge whose
-    destination is pushed anyway is pushed.  On RMAT graphs that ships 0.60x the
-    pull rows, within 2-3 % of the exact minimum cover (Konig / Hopcroft-Karp;
+    destination is pushed anyway is pushed.  On RMAT graphs that ships 0.56-0.57x
+    the pull rows, within 2 % of the exact minimum cover (Konig / Hopcroft-Karp;
     tools/exp_halo_cover.py, profiles/r03_halo_cover.log).
 
     Per step the sender fills its whole send buffer with ONE aggregation over a
