@@ -719,6 +719,8 @@ class ShardedGraph:
         self.g_bwd = Graph(self.bwd.local_edge_index, self.n_own, self.bwd.n_local_src,
                            flow="target_to_source", chunk=chunk)
         self._w = None
+        self.cover = None
+        self._chunk = chunk
 
     @classmethod
     def for_gcn(cls, edge_index, num_nodes, rank, world, group=None, improved=False, edge_weight=None, chunk=None):
@@ -753,6 +755,8 @@ class ShardedGraph:
         self.g_bwd = Graph(self.bwd.local_edge_index, self.n_own, self.bwd.n_local_src,
                            flow="target_to_source", chunk=chunk)
         self.deg = d["deg"]
+        self.cover = None
+        self._chunk = chunk
         self.norm_fwd = _norm_over_plan(self.fwd, d["deg"], f_w[self.fwd.edge_pos], group)
         self.norm_bwd = _norm_over_plan(self.bwd, d["deg"], b_w[self.bwd.edge_pos], group)
         self._w = None
@@ -777,6 +781,31 @@ class ShardedGraph:
         w = edge_weight.to(torch.float32)
         return self._set_local_weights(w[self.fwd.edge_pos], w[self.bwd.edge_pos])
 
+    def enable_halo_cover(self):
+        """Run sum / mean propagate (forward AND backward) over the hybrid halo
+        cover (HaloCover, 0.57x the pull rows on the config-2 graph) instead of
+        the pull exchange.  Forward: send graph -> all_to_all -> one aggregation
+        over the rank's interior + boundary edges.  Backward (its transpose): the
+        transposed local graph gives the gradient of every local row, the halo
+        rows' gradients go back over the reverse all_to_all, and the transposed
+        send graph folds them into the owned rows.  Both directions move the
+        cover's rows; deterministic; within 1e-5 of the pull form (regrouped
+        sums).  max / min keep the pull exchange (arg ids).  Collective, once;
+        call after the edge weights are set."""
+        from .graph import Graph
+        w = self._w[2] if self._w is not None else None        # the plan's local edge order
+        hc = HaloCover(self.fwd, w, self.group)
+        self.cover = hc
+        ch = self._chunk
+        self.g_cov = Graph(torch.stack([torch.cat([hc.int_src, hc.bnd_src]), torch.cat([hc.int_dst, hc.bnd_dst])]),
+                           self.n_own, hc.n_local_src, chunk=ch)
+        w_cov = torch.cat([hc.int_w, hc.bnd_w]).contiguous()
+        self.w_cov = (self.g_cov.dst.to_csr_order(w_cov), self.g_cov.src.to_csr_order(w_cov))
+        self.g_send = Graph(torch.stack([hc.send_src, hc.send_dst]), hc.n_send, self.n_own, chunk=ch)
+        ws = hc.send_w.contiguous()
+        self.w_send = (self.g_send.dst.to_csr_order(ws), self.g_send.src.to_csr_order(ws))
+        return self
+
     def propagate(self, x_own, reduce="sum"):
         """Sharded MessagePassing.propagate for message = w * x_j: this rank's
         rows of REDUCE_{e: dst(e) = i} w_e x[src(e)] (autograd included).
@@ -796,6 +825,19 @@ class _ShardedAggregate(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x_own, sg, reduce):
         from . import ops
+        ctx.sg, ctx.reduce = sg, reduce
+        if sg.cover is not None and reduce in ("sum", "mean"):
+            hc = sg.cover
+            F = x_own.shape[1]
+            x_local = x_own.new_empty((hc.n_local_src, F))
+            x_local[:hc.n_own].copy_(x_own)
+            send = (ops._aggregate(sg.g_send.dst, "other", x_own, sg.w_send[0], "sum", 0, None)[0]
+                    if hc.n_send else x_own.new_empty((0, F)))
+            _a2a(x_local[hc.n_own:], send, hc.recv_counts, hc.send_counts, sg.group)
+            out, _ = ops._aggregate(sg.g_cov.dst, "other", x_local, sg.w_cov[0], "sum", 0, None)
+            if reduce == "mean":   # the true in-degree (a partial row stands for several edges)
+                out = out / sg.g_fwd.dst.degree().clamp(min=1).to(torch.float32).view(-1, 1)
+            return out, None
         plan = sg.fwd
         F = x_own.shape[1]
         x_local = plan.local_buffer(F, device=x_own.device)
@@ -803,7 +845,6 @@ class _ShardedAggregate(torch.autograd.Function):
         plan.exchange_into(x_local, ops.gather_rows, sg.group)
         w_fwd = sg._w[0] if sg._w is not None else None
         out, arg = ops._aggregate(sg.g_fwd.dst, "other", x_local, w_fwd, reduce, 0, None)
-        ctx.sg, ctx.reduce = sg, reduce
         arg_g = None
         if arg is not None:
             ctx.save_for_backward(arg)
@@ -837,6 +878,17 @@ class _ShardedAggregate(torch.autograd.Function):
             return gx.contiguous(), None, None
         if reduce == "mean":
             g = g / sg.g_fwd.dst.degree().clamp(min=1).to(torch.float32).view(-1, 1)
+        if sg.cover is not None:
+            # transpose of the cover forward: local rows' gradients over the transposed
+            # local graph, the halo part back to its senders, the transposed send graph
+            hc = sg.cover
+            gl, _ = ops._aggregate(sg.g_cov.src, "other", g.contiguous(), sg.w_cov[1], "sum", 0, None)
+            back = g.new_empty((hc.n_send, F))
+            _a2a(back, gl[hc.n_own:].contiguous(), hc.send_counts, hc.recv_counts, sg.group)
+            gx = gl[:hc.n_own]
+            if hc.n_send:
+                gx = gx + ops._aggregate(sg.g_send.src, "other", back, sg.w_send[1], "sum", 0, None)[0]
+            return gx.contiguous(), None, None
         plan = sg.bwd
         g_local = plan.local_buffer(F, device=g.device)
         g_local[:plan.n_own].copy_(g)

@@ -495,3 +495,88 @@ def test_overlapped_halo_cover_on_one_gpu(world):
     assert all(r[1] and r[2] and r[3] for r in res), res
     assert sum(r[4] for r in res) < sum(r[5] for r in res), res
     assert any(r[6] > 0 for r in res), res
+
+
+def _cover_layer_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "pytorch_geometric-1_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mi355_mp import dist as mdist, ops
+        from mi355_mp.graph import Graph
+        from mi355_mp.graphgen import powerlaw_edge_index
+        from torch_geometric.nn import GCNConv
+        from torch_geometric.nn.conv.gcn_conv import GCNConv as G
+        dev = torch.device("cuda", 0)
+        N, E, Fi, Fo = 3000, 60000, 64, 128
+        ei = powerlaw_edge_index(N, E, seed=43).to(dev)
+        gen = torch.Generator().manual_seed(43)
+        x = torch.randn(N, Fi, generator=gen).to(dev)
+        gout = torch.randn(N, Fo, generator=gen).to(dev)
+        ref = GCNConv(Fi, Fo).to(dev)
+        with torch.no_grad():
+            ref.bias.normal_()
+        mdist.broadcast_parameters(ref)
+        xr = x.clone().requires_grad_(True)
+        out_ref = ref(xr, ei)
+        (out_ref * gout).sum().backward()
+        sg = mdist.ShardedGraph.for_gcn(ei, N, rank, world).enable_halo_cover()
+        conv = mdist.ShardedGCNConv(Fi, Fo).to(dev)
+        conv.load_state_dict(ref.state_dict())
+        lo, hi = sg.lo, sg.hi
+        xo = x[lo:hi].clone().requires_grad_(True)
+        out = conv(xo, sg)
+        (out * gout[lo:hi]).sum().backward()
+        mdist.allreduce_gradients(conv)
+        r = {"out": float((out.detach() - out_ref.detach()[lo:hi]).abs().max()),
+             "gx": float((xo.grad - xr.grad[lo:hi]).abs().max()),
+             "gw": float((conv.weight.grad - ref.weight.grad).abs().max() / ref.weight.grad.abs().max()),
+             "rows_cover": sg.cover.n_halo, "rows_pull": sg.fwd.n_local_src - sg.n_own}
+        # integer-valued data and weights: every regrouping is exact, so forward and
+        # backward equal the single-GPU fused aggregation bit for bit (sum and mean)
+        ei2, _ = G.norm(ei, N)
+        wi = torch.randint(1, 4, (ei2.shape[1],), generator=gen).to(torch.float32).to(dev)
+        sgi = mdist.ShardedGraph(ei2, N, rank, world).set_edge_weight(wi).enable_halo_cover()
+        g1 = Graph(ei2, N, N)
+        xi = torch.randint(-8, 9, (N, Fo), generator=gen).to(torch.float32).to(dev)
+        gi = torch.randint(-4, 5, (N, Fo), generator=gen).to(torch.float32).to(dev)
+        exact = {}
+        for red in ("sum", "mean"):
+            xs = xi[lo:hi].clone().requires_grad_(True)
+            o = sgi.propagate(xs, red)
+            (o * gi[lo:hi]).sum().backward()
+            xf = xi.clone().requires_grad_(True)
+            of = ops.fused_propagate(g1, xf, ei2, wi, red)
+            (of * gi).sum().backward()
+            if red == "sum":
+                exact[red] = bool(torch.equal(o, of[lo:hi])) and bool(torch.equal(xs.grad, xf.grad[lo:hi]))
+            else:
+                # forward: the same exact sum divided once by the same degree; backward: g / deg is
+                # not integer-valued, so the regrouped sums agree to rounding (relative bound)
+                o, of = o.detach(), of.detach()
+                r["mean_fwd_diff"] = float((o - of[lo:hi]).abs().max())
+                gref = xf.grad[lo:hi]
+                r["mean_bwd_excess"] = float(((xs.grad - gref).abs() - 1e-5 * gref.abs().clamp(min=1.0)).max())
+                exact[red] = bool(torch.equal(o, of[lo:hi])) and r["mean_bwd_excess"] <= 0
+        r["exact"] = exact
+        q.put((rank, r))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_gcnconv_over_halo_cover_on_one_gpu(world):
+    """ShardedGraph.enable_halo_cover(): ShardedGCNConv forward + backward over the
+    hybrid cover (ranks sharing the GPU over gloo) within 1e-5 of the single-GPU
+    GCNConv, integer-valued sum / mean forward and backward equal to the
+    single-GPU kernel, fewer rows than the pull exchange."""
+    res = _spawn(_cover_layer_worker, world=world)
+    for rank, r in res:
+        assert r["out"] < 1e-5 and r["gx"] < 1e-5 and r["gw"] < 1e-5, r
+        assert r["exact"]["sum"] and r["exact"]["mean"], r
+    assert sum(r["rows_cover"] for _, r in res) < sum(r["rows_pull"] for _, r in res), res
