@@ -342,6 +342,14 @@ def _rccl_worker(rank, world, port, q):
         ov.step_tiled(tiles, out_t, bias)
         res["step"] = float((out - ref).abs().max())
         res["tiled_eq_step"] = bool(torch.equal(out_t, out))
+        # the halo cover's collective build and step over RCCL (empty exchanges at one rank)
+        ovc = mdist.OverlappedAggregation(plan, norm, chunk=64, cover=True)
+        tc = ovc.local_tiles(F, 128)
+        for t, xt in enumerate(tc):
+            xt[:plan.n_own].copy_(x[:, 128 * t:128 * t + xt.shape[1]])
+        out_c = torch.empty(plan.n_own, F, device=dev)
+        ovc.step_tiled(tc, out_c, bias)
+        res["cover_step"] = float((out_c - ref).abs().max())
         # sharded GCNConv forward + backward, RCCL broadcast / all_reduce of the weights
         gout = torch.randn(N, F, generator=gen).to(dev)
         xi = torch.randn(N, Fi, generator=gen).to(dev)
@@ -366,6 +374,12 @@ def _rccl_worker(rank, world, port, q):
         res["layer_gx"] = float((xo.grad - xr.grad).abs().max())
         res["layer_gw"] = float((conv.weight.grad - conv_ref.weight.grad).abs().max()
                                 / conv_ref.weight.grad.abs().max())
+        sgc = mdist.ShardedGraph.for_gcn(ei, N, rank, world).enable_halo_cover()
+        xc = xi.clone().requires_grad_(True)
+        oc = conv(xc, sgc)
+        (oc * gout).sum().backward()
+        res["cover_layer_out"] = float((oc.detach() - o.detach()).abs().max())
+        res["cover_layer_gx"] = float((xc.grad - xo.grad).abs().max())
         # max / min with global edge ids
         xm = torch.randint(-3, 4, (N, F), generator=gen).to(torch.float32).to(dev)
         sgm = mdist.ShardedGraph(ei2, N, rank, world)
@@ -389,13 +403,15 @@ def test_sharded_path_over_rccl_world_one():
     bench makes -- communicator setup with device_id, async all_to_all_single
     with split sizes on device tensors + work.wait() (OverlappedAggregation
     step / step_tiled), the blocking exchanges of ShardPlan / ShardedGraph,
-    broadcast and all_reduce of the replicated GCNConv weights -- with empty
-    halo splits, against the single-GPU kernel and GCNConv."""
+    broadcast and all_reduce of the replicated GCNConv weights, the halo
+    cover's collective build, step and autograd -- with empty halo splits,
+    against the single-GPU kernel and GCNConv."""
     (rank, r), = _spawn(_rccl_worker, world=1, timeout=300)
     assert r["step"] < 1e-5 and r["tiled_eq_step"], r
     assert r["layer_out"] < 1e-5 and r["layer_gx"] < 1e-5 and r["layer_gw"] < 1e-5, r
     assert r["max_exact"], r
     assert r["slices_equal"], r
+    assert r["cover_step"] < 1e-5 and r["cover_layer_out"] < 1e-6 and r["cover_layer_gx"] < 1e-6, r
 
 
 def test_bench_multi_rank_path_end_to_end():
