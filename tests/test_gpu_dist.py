@@ -233,8 +233,13 @@ def _products_worker(rank, world, port, q):
         ref = ops._aggregate(g1.dst, "other", x, w1, "sum", 0, None)[0][lo:hi]
         terms = ops._aggregate(g1.dst, "other", x.abs(), w1.abs(), "sum", 0, None)[0][lo:hi]
         excess = float(((out - ref).abs() - 1e-5 * terms.clamp(min=1)).max())
+        excess_c, rows_c = None, None
+        if world == 2:   # the hybrid halo cover at full size (8 ranks on one GPU oversubscribe its queues)
+            out_c = sg.enable_halo_cover().propagate(x[lo:hi])
+            excess_c = float(((out_c - ref).abs() - 1e-5 * terms.clamp(min=1)).max())
+            rows_c = sg.cover.n_halo
         q.put((rank, excess, float((out == ref).float().mean()), hi - lo, int(sg.fwd.edge_pos.numel()),
-               int(sg.fwd.halo_nodes.numel())))
+               int(sg.fwd.halo_nodes.numel()), excess_c, rows_c))
     finally:
         dist.destroy_process_group()
 
@@ -245,13 +250,17 @@ def test_full_size_products_sharded_rehearsal(world):
     destination-range sharded over 2 ranks, and over 8 -- config 5's own
     partition count -- sharing the device (gloo staging of the halo rows; the
     RCCL call is covered by test_sharded_path_over_rccl_world_one): every
-    rank's owned rows within 1e-5 * sum|w x| of the single-GPU kernel."""
+    rank's owned rows within 1e-5 * sum|w x| of the single-GPU kernel; at 2
+    ranks also over the hybrid halo cover (ShardedGraph.enable_halo_cover),
+    which must receive fewer rows than the pull halo."""
     res = _spawn(_products_worker, world=world, timeout=900)
     assert sum(r[3] for r in res) == 2_449_029
-    for rank, excess, frac, n_own, n_edges, n_halo in res:
+    for rank, excess, frac, n_own, n_edges, n_halo, excess_c, rows_c in res:
         assert excess <= 0, res
         assert frac > 0.95, res   # rows split across merge-path tasks differ in the last bits
         assert n_halo > 0
+        if world == 2:
+            assert excess_c <= 0 and rows_c < n_halo, res
 
 
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
