@@ -380,9 +380,12 @@ class HaloCover:
     Rule (one-time, on the receiver p, from its own in-edges): an edge goes to
     the endpoint with the larger cross-degree of the pair (ties: pull), then two
     clean-ups -- an edge whose source is pulled anyway is pulled, an edge whose
-    destination is pushed anyway is pushed.  On RMAT graphs that ships 0.56-0.57x
-    the pull rows, within 2 % of the exact minimum cover (Konig / Hopcroft-Karp;
-    tools/exp_halo_cover.py, profiles/r03_halo_cover.log).
+    destination is pushed anyway is pushed; per owner the fewest rows of that
+    cover, pull only and push only is kept (on a dense pair the degree rule can
+    lose to either), so the cover never ships more rows than the pull halo.  On
+    RMAT graphs it ships 0.56-0.57x the pull rows, within 2 % of the exact
+    minimum cover (Konig / Hopcroft-Karp; tools/exp_halo_cover.py,
+    profiles/r03_halo_cover_model.log).
 
     Per step the sender fills its whole send buffer with ONE aggregation over a
     "send graph": a pulled row is a row with one edge of weight 1.0 (an exact
@@ -427,8 +430,21 @@ class HaloCover:
             push = ~in_s[r_src]
             in_d = torch.bincount(key[push], minlength=nkey) > 0
             push = in_d[key]
+            # per owner the fewest rows of three covers: this one, pull only, push only
+            # (the degree rule can lose to either on a dense pair)
+            in_s = torch.bincount(r_src[~push], minlength=N) > 0
+            cover_q = (torch.bincount(torch.searchsorted(cuts_t, torch.nonzero(in_s).view(-1), right=True),
+                                      minlength=world)
+                       + torch.bincount(torch.nonzero(in_d).view(-1) // stride, minlength=world))
+            pull_q = torch.bincount(torch.searchsorted(cuts_t, torch.nonzero(cs).view(-1), right=True),
+                                    minlength=world)
+            push_q = torch.bincount(torch.nonzero(cd).view(-1) // stride, minlength=world)
+            mode = torch.where((pull_q <= cover_q) & (pull_q <= push_q), 0, torch.where(push_q < cover_q, 1, 2))
+            m = mode[r_own]
+            push = torch.where(m == 0, torch.zeros_like(push), torch.where(m == 1, torch.ones_like(push), push))
             pull = ~push
             in_s = torch.bincount(r_src[pull], minlength=N) > 0
+            in_d = torch.bincount(key[push], minlength=nkey) > 0
             del cs, cd, pick
         else:
             in_s = torch.zeros(N, dtype=torch.bool, device=dev)

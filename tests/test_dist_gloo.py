@@ -246,3 +246,73 @@ def test_halo_cover_matches_single_process(world, cuts):
         # fewer rows than the pull exchange (this small graph is dense: ~0.86x; RMAT21 0.57x)
         assert sum(r[3] for r in res) < 0.95 * sum(r[4] for r in res), res
         assert any(r[5] > 0 for r in res), res
+
+
+def _cover_fuzz_worker(rank, world, port, result_q, n_cases):
+    """Random graphs and cuts (empty ranks, isolated nodes, duplicate edges,
+    self loops, star hubs, a fully-connected tail): the cover's step on
+    integer-valued data equals the oracle bit for bit, every in-edge is
+    accounted for exactly once, and the cover never ships more rows than the
+    pull halo.  Every rank draws the same cases from the same seeds."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "pytorch_geometric-1_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mi355_mp import dist as mdist
+        from oracle import scatter_ref as S
+        bad = []
+        for case in range(n_cases):
+            g = torch.Generator().manual_seed(1000 + case)
+            N = int(torch.randint(1, 300, (1,), generator=g))
+            E = int(torch.randint(0, 3000, (1,), generator=g))
+            kind = case % 3
+            if kind == 0:      # uniform
+                ei = torch.randint(N, (2, E), generator=g)
+            elif kind == 1:    # star hubs: a few sources / destinations carry most edges
+                hubs = torch.randint(N, (3,), generator=g)
+                src = torch.where(torch.rand(E, generator=g) < 0.5, hubs[torch.randint(3, (E,), generator=g)],
+                                  torch.randint(N, (E,), generator=g))
+                dst = torch.where(torch.rand(E, generator=g) < 0.5, hubs[torch.randint(3, (E,), generator=g)],
+                                  torch.randint(N, (E,), generator=g))
+                ei = torch.stack([src, dst])
+            else:              # dense tail block + duplicates
+                k = max(1, min(N, 20))
+                a = torch.arange(N - k, N)
+                blk = torch.stack([a.repeat_interleave(k), a.repeat(k)])
+                ei = torch.cat([torch.randint(N, (2, E), generator=g), blk, blk[:, :E % (k * k + 1)]], 1)
+            cuts = sorted(int(c) for c in torch.randint(0, N + 1, (world - 1,), generator=g))
+            cuts = [0] + cuts + [N]
+            w = torch.randint(1, 4, (ei.shape[1],), generator=g).to(torch.float32)
+            x = torch.randint(-8, 9, (N, 3), generator=g).to(torch.float32)
+            plan = mdist.ShardPlan(ei, N, rank, world, cuts=cuts).exchange_requests()
+            hc = mdist.HaloCover(plan, w[plan.edge_pos])
+            out = hc.host_step(x[plan.lo:plan.hi].contiguous(),
+                               lambda xs, s, d, ws, n: S.gather_sum(xs, s, d, ws, n))
+            want = S.gather_sum(x, ei[0], ei[1], w, N)[plan.lo:plan.hi]
+            n_edges = hc.n_pull_edges + hc.n_push_edges + int(hc.int_src.numel())
+            if not (torch.equal(out, want) and n_edges == int(plan.edge_pos.numel())
+                    and hc.n_halo <= plan.n_local_src - plan.n_own):
+                bad.append((case, N, ei.shape[1], cuts))
+        result_q.put((rank, bad))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_halo_cover_fuzz(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cover_fuzz_worker, args=(r, world, port, q, 30)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+        assert p.exitcode == 0
+    res = sorted(q.get(timeout=10) for _ in range(world))
+    assert all(not r[1] for r in res), res
