@@ -832,7 +832,11 @@ struct GatBwdRed {
       aw = alpha * dsc;
       dal = dal * dsc;
     }
-    const float de = alpha * (dal - q.w) * lk;
+    // a one-hot softmax row (1/den == 1 and this edge's alpha == 1: a single edge, or the others
+    // below 2^-24 of it) has d score = alpha (d alpha - rs) = 0 up to those others' weight; the
+    // reference's autograd cancels the identical value there, rs = <g_i, agg_i> would leave the
+    // rounding of two different evaluations -- so the term is 0, as the reference's
+    const float de = (q.z == 1.f && alpha == 1.f) ? 0.f : alpha * (dal - q.w) * lk;
 #pragma unroll
     for (int k = 0; k < VEC; ++k) acc[k] = __builtin_fmaf(aw, v.v[k], acc[k]);
     dacc += de;
@@ -930,10 +934,13 @@ struct GatBwdWideRed {
     const float score = as + q.x;
     const float lk = score > 0.f ? 1.f : p.slope;
     const float alpha = __expf(score * lk - q.y) * q.z;
-    sc = __builtin_fmaf(lk * alpha, q.w, sc);
+    // one-hot softmax row (see GatBwdRed::consume_gatb): its d score is 0, so the edge adds
+    // nothing to d a_src's two node-wise sums (acc2, sc)
+    const bool one_hot = q.z == 1.f && alpha == 1.f;
+    sc = one_hot ? sc : __builtin_fmaf(lk * alpha, q.w, sc);
     float aw = alpha;
     if constexpr (DR) aw = alpha * drop_factor(p, dbits, h);
-    const float law = lk * aw;
+    const float law = one_hot ? 0.f : lk * aw;
 #pragma unroll
     for (int k = 0; k < VEC; ++k) {
       acc[k] = __builtin_fmaf(aw, v.v[k], acc[k]);

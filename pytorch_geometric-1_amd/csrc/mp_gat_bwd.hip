@@ -243,7 +243,8 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep_wave(const float* __restri
         for (int k = 0; k < 4; ++k) t2 = __builtin_fmaf(x.v[k], z.v[k], t2);
         for (int o = 1; o < G; o <<= 1) t2 += __shfl_xor(t2, o);
         const int64_t q = r * H + fs / C;
-        if (act && (lane & (G - 1)) == 0) ga_dst[q] = __builtin_fmaf(-t, s2[q], t2);
+        // a one-hot softmax row (den == 1) has d a_dst = 0 (GatBwdRed::consume_gatb)
+        if (act && (lane & (G - 1)) == 0) ga_dst[q] = stats[2 * q + 1] == 1.f ? 0.f : __builtin_fmaf(-t, s2[q], t2);
       }
       if (gsum_part && act) {
 #pragma unroll

@@ -76,7 +76,7 @@ __global__ __launch_bounds__(64 * kWideWaves) void k_gat_bwd_prep_wide(
         const int64_t q = r * H + h;
         f32x4 v = {a_dst[q], stats[2 * q], 1.f / stats[2 * q + 1], rs};
         *reinterpret_cast<f32x4*>(pack + 4 * q) = v;
-        ga_dst[q] = __builtin_fmaf(-rs, s2[q], t2);
+        ga_dst[q] = stats[2 * q + 1] == 1.f ? 0.f : __builtin_fmaf(-rs, s2[q], t2);  // one-hot row: 0
       }
     }
   }
