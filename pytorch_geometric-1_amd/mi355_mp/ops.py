@@ -323,7 +323,8 @@ def segment_reduce_into(src, index, out, reduce="sum"):
     reduce = "sum" if reduce == "add" else reduce
     _lib.require_device(src, index, out)
     src = _any_2d(src, "src")
-    if out.dtype != src.dtype or out.dim() != 2 or out.stride(1) != 1:
+    # (a one-feature out may carry any stride on its size-1 dim: torch calls it contiguous)
+    if out.dtype != src.dtype or out.dim() != 2 or (out.shape[1] > 1 and out.stride(1) != 1):
         raise ValueError("mi355_mp: out must be a row-major [dim_size, F] tensor of src's dtype")
     if torch.is_grad_enabled() and (src.requires_grad or out.requires_grad):
         raise NotImplementedError("mi355_mp: autograd through torch_scatter `out=` is not supported")

@@ -118,7 +118,7 @@ def _reduce_general(src, index, dim, out, dim_size, reduce):
     keys = (torch.arange(B, device=src.device).view(-1, 1) * dim_size + ix.reshape(B, L)).reshape(-1)
     vals = s.reshape(-1, 1)
     if out is not None:
-        o = out.movedim(dim, -1).reshape(B * dim_size, 1).contiguous()
+        o = out.movedim(dim, -1).reshape(B * dim_size, 1).clone(memory_format=torch.contiguous_format)
         res, arg = _ops.segment_reduce_into(vals, keys, o, reduce)
         out.copy_(res.view(lead + (dim_size,)).movedim(-1, dim))
         res_t = out
@@ -148,10 +148,16 @@ def _reduce(src, index, dim, out, dim_size, reduce):
     if out is not None:
         _lib.require_device(out)
         o2 = out.movedim(dim, 0).reshape(dim_size, -1)
-        contiguous_view = o2.data_ptr() == out.data_ptr() and o2.is_contiguous() and dim == 0
-        buf = o2 if contiguous_view else o2.contiguous()
+        # reduce straight into out when the [dim_size, F] form is a row-major view of
+        # it (the reshape did not copy); otherwise into a fresh row-major copy, then
+        # copied back (never a copy that aliases out: size-1 dims make torch call
+        # odd strides contiguous)
+        F2 = o2.shape[1] if o2.dim() == 2 else 0
+        in_place = (o2.untyped_storage().data_ptr() == out.untyped_storage().data_ptr()
+                    and (F2 <= 1 or o2.stride(1) == 1) and (dim_size <= 1 or o2.stride(0) >= F2))
+        buf = o2 if in_place else o2.clone(memory_format=torch.contiguous_format)
         res, arg = _ops.segment_reduce_into(src2, idx, buf, reduce)
-        if not contiguous_view:
+        if not in_place:
             out.copy_(_finish(res, dim, rest))
         arg_full = _finish(arg, dim, rest) if arg is not None else None
         return out, arg_full

@@ -2615,3 +2615,69 @@ def test_gat_backward_one_hot_rows_exact(H, C, p):
     scale = torch.tensor(1.0 / (1.0 - p), dtype=torch.float32)
     want = (keep.to(torch.float32) * scale).repeat_interleave(C, dim=1) * gout
     assert torch.allclose(xd.grad.cpu(), want, rtol=1e-6, atol=0), float((xd.grad.cpu() - want).abs().max())
+
+
+_FUZZ_TS_N = int(__import__("os").environ.get("MP_FUZZ_TS_EXAMPLES", "80"))
+
+
+@settings(max_examples=_FUZZ_TS_N, deadline=None, derandomize=True, database=None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+@given(shape=st.lists(st.integers(1, 7), min_size=1, max_size=3), dim=st.integers(-3, 2),
+       elementwise=st.booleans(), dtype=st.sampled_from([torch.float32, torch.float64, torch.int64]),
+       reduce=st.sampled_from(["sum", "mean", "max", "min"]), extra=st.integers(-1, 3),
+       use_out=st.booleans(), seed=st.integers(0, 1 << 16))
+def test_fuzz_torch_scatter_api(shape, dim, elementwise, dtype, reduce, extra, use_out, seed):
+    """torch_scatter's scatter_{sum,mean,max,min} over random src shapes, dims
+    (negative included), 1-D and element-wise indices, dim_size and out=,
+    against the serial loop of scatter_cpu.cpp applied line by line along dim:
+    max/min values and args exact, float64 / int64 exact, float32 sum / mean
+    within 1e-5 of the sum of |terms|."""
+    import torch_scatter as T
+    _fuzz_tick("torch_scatter")
+    if dim >= len(shape) or dim < -len(shape):
+        dim = dim % len(shape)
+    d = dim % len(shape)
+    g = torch.Generator().manual_seed(seed)
+    L = shape[d]
+    n_out = 5
+    src = (torch.randint(-4, 5, tuple(shape), generator=g).to(dtype) if reduce in ("max", "min") or dtype == torch.int64
+           else torch.randn(tuple(shape), generator=g).to(dtype))
+    if elementwise:
+        index = torch.randint(n_out, tuple(shape), generator=g)
+    else:
+        index = torch.randint(n_out, (L,), generator=g)
+    dim_size = None if extra < 0 else int(index.max()) + 1 + extra
+    size_d = dim_size if dim_size is not None else int(index.max()) + 1
+    base = None
+    if use_out:
+        oshape = list(shape)
+        oshape[d] = size_d
+        base = torch.randint(-2, 3, tuple(oshape), generator=g).to(dtype)
+    fn = getattr(T, "scatter_" + reduce)
+    kw = {"out": base.clone().to(DEV)} if use_out else {"dim_size": dim_size}
+    res = fn(src.to(DEV), index.to(DEV), dim, **kw)
+    got, garg = (res if reduce in ("max", "min") else (res, None))
+    # reference: the serial loop along dim for every line of the other dims
+    s_m = src.movedim(d, -1).reshape(-1, L)
+    i_m = (index.movedim(d, -1).reshape(-1, L) if elementwise else index.view(1, L).expand(s_m.shape[0], L))
+    o_m = base.movedim(d, -1).reshape(-1, size_d) if use_out else None
+    want_rows, arg_rows = [], []
+    for r in range(s_m.shape[0]):
+        o, a = S.scatter_loop_any(s_m[r].reshape(L, 1), i_m[r], size_d, reduce,
+                                  out=None if o_m is None else o_m[r].reshape(size_d, 1))
+        want_rows.append(o.view(-1))
+        arg_rows.append(a.view(-1) if a is not None else None)
+    lead = list(src.movedim(d, -1).shape[:-1])
+    want = torch.stack(want_rows).reshape(lead + [size_d]).movedim(-1, d)
+    got = got.cpu()
+    if reduce in ("max", "min") or dtype != torch.float32:
+        assert torch.equal(got, want), (got, want)
+        if garg is not None:
+            warg = torch.stack(arg_rows).reshape(lead + [size_d]).movedim(-1, d)
+            assert torch.equal(garg.cpu(), warg)
+    else:
+        terms = torch.stack([S.scatter_loop_any(s_m[r].abs().reshape(L, 1), i_m[r], size_d, "sum")[0].view(-1)
+                             for r in range(s_m.shape[0])]).reshape(lead + [size_d]).movedim(-1, d)
+        if use_out:
+            terms = terms + base.abs()
+        assert bool(((got - want).abs() <= 1e-5 * terms.clamp(min=1.0)).all()), (got, want)
