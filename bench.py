@@ -282,6 +282,8 @@ def main():
         from mi355_mp import dist as mdist
         sg = mdist.ShardedGraph.for_gcn_from_slices(ei_slice, s0, N, rank, world, chunk=args.chunk or None)
         del ei_slice
+        torch.cuda.synchronize()
+        t_shards = time.perf_counter() - t0
         E2 = sg.n_edges
         plan = sg.fwd
         x_full = torch.randn(N, F_DIM, device=dev, generator=g)
@@ -290,6 +292,8 @@ def main():
         x = x_local[:plan.n_own]
         overlap = mdist.OverlappedAggregation(plan, sg.norm_fwd, chunk=args.chunk or None, local_weights=True,
                                               cover=not (args.no_halo_cover or args.no_overlap))
+        torch.cuda.synchronize()
+        t_exchange_plan = time.perf_counter() - t0 - t_shards
         x_tiles = x_ov = None
         if args.halo_tile > 0 and not args.no_overlap:
             x_tiles = overlap.local_tiles(F_DIM, args.halo_tile)
@@ -461,7 +465,8 @@ def main():
             lst = evs.get(k, [])
             return sum(lst[j].elapsed_time(lst[j + 1]) for j in range(0, len(lst) - 1, 2))
         torch.cuda.synchronize()
-        mine = {"rank": rank, "rows": plan.n_own, "edges": E_local, "interior_edges": overlap.n_interior,
+        mine = {"rank": rank, "build_shards_s": t_shards, "build_exchange_s": t_exchange_plan,
+                "rows": plan.n_own, "edges": E_local, "interior_edges": overlap.n_interior,
                 "boundary_edges": overlap.n_boundary,
                 "exchange": "pull" if args.no_overlap or overlap.cover is None else "cover (pull + push partials)",
                 "halo_rows": (plan.n_local_src if args.no_overlap else overlap.n_local_src) - plan.n_own,
