@@ -224,31 +224,65 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep_wave(const float* __restri
   // bias-gradient partial (column sums of g) for rows of one 256-feature tile
   // (HC <= 256 when gsum_part != nullptr)
   float cs[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int64_t r = (int64_t)blockIdx.x * 4 + wid; r < n; r += nw) {
-    for (int64_t base = 0; base < HC; base += 256) {
-      const int64_t f = base + lane * 4;
-      const bool act = f < HC;
-      const int64_t fs = act ? f : 0;
-      Frag<4> x = load_frag<4>(g + r * ldg + fs);
-      Frag<4> y = load_frag<4>(agg + r * lda + fs);
-      float t = 0.f;
+  // per row: rs (and d a_dst from the second accumulator) of the 4 features at fs,
+  // the pack / ga_dst stores, the bias-gradient column sums -- rows are folded
+  // into cs in the wave's row order, whatever the number in flight
+  auto row = [&](int64_t r, int64_t fs, bool act, const Frag<4>& x, const Frag<4>& y, const Frag<4>& z) {
+    float t = 0.f;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) t = __fadd_rn(t, __fmul_rn(x.v[k], y.v[k]));
-      for (int o = 1; o < G; o <<= 1) t = __fadd_rn(t, __shfl_xor(t, o));
-      if (act && (lane & (G - 1)) == 0) write_pack(pack, a_dst, stats, r * H + fs / C, t);
-      if (agg2) {  // d a_dst = <g, agg2>_h - rs s2  (training forward's second accumulator)
-        Frag<4> z = load_frag<4>(agg2 + r * HC + fs);
-        float t2 = 0.f;
+    for (int k = 0; k < 4; ++k) t = __fadd_rn(t, __fmul_rn(x.v[k], y.v[k]));
+    for (int o = 1; o < G; o <<= 1) t = __fadd_rn(t, __shfl_xor(t, o));
+    if (act && (lane & (G - 1)) == 0) write_pack(pack, a_dst, stats, r * H + fs / C, t);
+    if (agg2) {  // d a_dst = <g, agg2>_h - rs s2  (training forward's second accumulator)
+      float t2 = 0.f;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) t2 = __builtin_fmaf(x.v[k], z.v[k], t2);
-        for (int o = 1; o < G; o <<= 1) t2 += __shfl_xor(t2, o);
-        const int64_t q = r * H + fs / C;
-        // a one-hot softmax row (den == 1) has d a_dst = 0 (GatBwdRed::consume_gatb)
-        if (act && (lane & (G - 1)) == 0) ga_dst[q] = stats[2 * q + 1] == 1.f ? 0.f : __builtin_fmaf(-t, s2[q], t2);
+      for (int k = 0; k < 4; ++k) t2 = __builtin_fmaf(x.v[k], z.v[k], t2);
+      for (int o = 1; o < G; o <<= 1) t2 += __shfl_xor(t2, o);
+      const int64_t q = r * H + fs / C;
+      // a one-hot softmax row (den == 1) has d a_dst = 0 (GatBwdRed::consume_gatb)
+      if (act && (lane & (G - 1)) == 0) ga_dst[q] = stats[2 * q + 1] == 1.f ? 0.f : __builtin_fmaf(-t, s2[q], t2);
+    }
+    if (gsum_part && act) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) cs[k] += x.v[k];
+    }
+  };
+  int64_t r = (int64_t)blockIdx.x * 4 + wid;
+  if (HC <= 256) {
+    // one 256-feature pass per row: two rows in flight, every load of both issued
+    // before the first reduction (the prologue streams 3 rows per node)
+    const int64_t f = lane * 4;
+    const bool act = f < HC;
+    const int64_t fs = act ? f : 0;
+    Frag<4> z0 = {}, z1 = {};
+    for (; r + nw < n; r += 2 * nw) {
+      const int64_t r1 = r + nw;
+      Frag<4> x0 = load_frag<4>(g + r * ldg + fs), x1 = load_frag<4>(g + r1 * ldg + fs);
+      Frag<4> y0 = load_frag<4>(agg + r * lda + fs), y1 = load_frag<4>(agg + r1 * lda + fs);
+      if (agg2) {
+        z0 = load_frag<4>(agg2 + r * HC + fs);
+        z1 = load_frag<4>(agg2 + r1 * HC + fs);
       }
-      if (gsum_part && act) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) cs[k] += x.v[k];
+      row(r, fs, act, x0, y0, z0);
+      row(r1, fs, act, x1, y1, z1);
+    }
+    if (r < n) {
+      Frag<4> x0 = load_frag<4>(g + r * ldg + fs);
+      Frag<4> y0 = load_frag<4>(agg + r * lda + fs);
+      if (agg2) z0 = load_frag<4>(agg2 + r * HC + fs);
+      row(r, fs, act, x0, y0, z0);
+    }
+  } else {
+    for (; r < n; r += nw) {
+      for (int64_t base = 0; base < HC; base += 256) {
+        const int64_t f = base + lane * 4;
+        const bool act = f < HC;
+        const int64_t fs = act ? f : 0;
+        Frag<4> x = load_frag<4>(g + r * ldg + fs);
+        Frag<4> y = load_frag<4>(agg + r * lda + fs);
+        Frag<4> z = {};
+        if (agg2) z = load_frag<4>(agg2 + r * HC + fs);
+        row(r, fs, act, x, y, z);
       }
     }
   }

@@ -231,10 +231,27 @@ class _FusedPropagate(torch.autograd.Function):
             w_src = in_csr_order(src, edge_weight) if edge_weight is not None else None
             gx, _ = _aggregate(src, "other", g, w_src, "sum", 0, None)
         if ctx.needs_input_grad[1] and edge_weight is not None:
-            xi = gather_rows(x, edge_index[graph.j])
-            gi = gather_rows(g, edge_index[graph.i])
-            gw = (xi * gi).sum(-1).to(edge_weight.dtype)
+            gw = _edge_dot(graph.dst, g.contiguous(), x).to(edge_weight.dtype)
         return gx, gw, gb, None, None, None, None, None
+
+
+def _edge_dot(csr, g, x):
+    """d w_e = <g[dst_e], x[src_e]> for every edge, in original edge order: one
+    CSR SDDMM over the destination CSR (mp_gat_sddmm_f32 with one head of width
+    F), then a permutation by eid -- no [E, F] gathers of x_j and g_i."""
+    E = csr.n_edges
+    F = g.shape[1]
+    dev = g.device
+    out = torch.zeros(E, dtype=torch.float32, device=dev)
+    if E == 0 or F == 0:
+        return out
+    sr = csr.slot_rows()
+    d = torch.empty(E, dtype=torch.float32, device=dev)
+    _lib.check(_lib.load().mp_gat_sddmm_f32(csr.struct("other"), sr.data_ptr(), g.data_ptr(), g.stride(0),
+                                            x.data_ptr(), x.stride(0), 1, F, d.data_ptr(), _lib.stream_ptr(dev)),
+               "mp_gat_sddmm_f32")
+    out[csr.eid[:E].long()] = d
+    return out
 
 
 def fused_propagate(graph, x, edge_index, edge_weight=None, reduce="sum", bias=None, pyg_mask=False,

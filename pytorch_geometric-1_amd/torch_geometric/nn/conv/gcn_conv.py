@@ -17,6 +17,8 @@ two orders agree to rounding, not bit for bit.
 import torch
 from torch.nn import Parameter
 
+import torch_scatter
+
 from mi355_mp import ops as _ops
 from mi355_mp.graph import graph_for
 
@@ -76,6 +78,15 @@ class GCNConv(MessagePassing):
             norm = cached_value(edge_index, ("gcn_norm", int(num_nodes), fill_value), build)
             return ei, norm
         w = remaining_loops_weight(edge_weight, pos, fill_value)
+        if torch.is_grad_enabled() and w.requires_grad:
+            # learned edge weights: upstream's differentiable form, so the gradient
+            # reaches edge_weight through deg and norm (the degree's scatter_add on
+            # the native segmented sum with its autograd, as get_laplacian does)
+            row, col = ei
+            deg = torch_scatter.scatter_add(w, row, dim=0, dim_size=num_nodes)
+            deg_inv_sqrt = deg.pow(-0.5)
+            deg_inv_sqrt = deg_inv_sqrt.masked_fill(deg_inv_sqrt == float("inf"), 0)
+            return ei, deg_inv_sqrt[row] * w * deg_inv_sqrt[col]
         return ei, _ops.gcn_norm_weights(ei, num_nodes, w)
 
     def forward(self, x, edge_index, edge_weight=None):

@@ -20,6 +20,7 @@ MI355X engine:
     reduction of aggregate still run on native kernels (row gather and
     segmented reduce), the user's message runs as ordinary torch code.
 """
+import math as _math
 import inspect
 from collections import OrderedDict
 
@@ -94,7 +95,7 @@ class MessagePassing(torch.nn.Module):
             out = _ops.index_select_rows(flat, idx_vec)
             return out if data.dim() == 2 else out.view(-1)
         if self.node_dim == 0 and data.dtype == torch.float32 and data.is_cuda:
-            flat = data.reshape(data.shape[0], -1)
+            flat = data.reshape(data.shape[0], _math.prod(data.shape[1:]))
             return _ops.index_select_rows(flat, idx_vec).view((-1,) + tuple(data.shape[1:]))
         return data.index_select(self.node_dim, idx_vec)
 

@@ -7,6 +7,7 @@ Sparse (segment-wise) softmax over the rows grouped by `index`; every
 scatter/gather step runs on the native engine.  (GATConv itself does not
 call this: its softmax is fused into mp_gat_aggregate_f32.)
 """
+import math as _math
 from mi355_mp import ops as _ops
 
 from .num_nodes import maybe_num_nodes
@@ -14,7 +15,7 @@ from .num_nodes import maybe_num_nodes
 
 def softmax(src, index, num_nodes=None):
     num_nodes = maybe_num_nodes(index, num_nodes)
-    flat = src.reshape(src.shape[0], -1)
+    flat = src.reshape(src.shape[0], _math.prod(src.shape[1:]))
     mx, _ = _ops.segment_reduce(flat, index, num_nodes, "max")
     out = (flat - _ops.index_select_rows(mx, index)).exp()
     den, _ = _ops.segment_reduce(out, index, num_nodes, "sum")

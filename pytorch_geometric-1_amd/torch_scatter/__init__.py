@@ -27,6 +27,7 @@ fused hot-path kernels; float64 / float16 / bfloat16 / int64 the
 mp_segment_reduce kernels (every row in edge order: float64 and int64 bit for
 bit, the half types accumulated in fp32).
 """
+import math as _math
 import torch
 
 from mi355_mp import ops as _ops
@@ -91,7 +92,7 @@ def _prepare(src, index, dim, dim_size):
         dim_size = int(idx.max()) + 1 if idx.numel() > 0 else 0
     moved = src.movedim(dim, 0)
     rest = moved.shape[1:]
-    src2 = moved.reshape(moved.shape[0], -1)
+    src2 = moved.reshape(moved.shape[0], _math.prod(moved.shape[1:]))
     return dim, idx, int(dim_size), src2, rest
 
 
@@ -211,7 +212,7 @@ def gather_csr(src, indptr, out=None):
     _lib.require_device(src, indptr)
     counts = indptr[1:] - indptr[:-1]
     index = torch.repeat_interleave(torch.arange(counts.numel(), device=src.device), counts)
-    res = _ops.index_select_rows(src.reshape(src.shape[0], -1), index).reshape((-1,) + tuple(src.shape[1:]))
+    res = _ops.index_select_rows(src.reshape(src.shape[0], _math.prod(src.shape[1:])), index).reshape((-1,) + tuple(src.shape[1:]))
     if out is not None:
         out.copy_(res)
         return out
@@ -231,7 +232,7 @@ def segment_coo(src, index, out=None, dim_size=None, reduce="sum"):
 def gather_coo(src, index, out=None):
     """torch_scatter.gather_coo along dim 0: out[e] = src[index[e]]."""
     _lib.require_device(src, index)
-    res = _ops.index_select_rows(src.reshape(src.shape[0], -1), index).reshape((-1,) + tuple(src.shape[1:]))
+    res = _ops.index_select_rows(src.reshape(src.shape[0], _math.prod(src.shape[1:])), index).reshape((-1,) + tuple(src.shape[1:]))
     if out is not None:
         out.copy_(res)
         return out
@@ -288,7 +289,7 @@ def _gather_back(t, index, dim):
     d = dim % t.dim()
     if index.dim() == 1:
         moved = t.movedim(d, 0)
-        rows = _ops.index_select_rows(moved.reshape(moved.shape[0], -1).contiguous(), index.to(torch.int64))
+        rows = _ops.index_select_rows(moved.reshape(moved.shape[0], _math.prod(moved.shape[1:])).contiguous(), index.to(torch.int64))
         return rows.reshape((index.numel(),) + tuple(moved.shape[1:])).movedim(0, d)
     size = list(t.shape)
     size[d] = index.size(d) if index.dim() > d else index.size(-1)

@@ -1,0 +1,280 @@
+"""Layer-level fuzzing of the PyG 1.4.3 API surface on the engine.
+
+The kernel-level fuzz tests (test_gpu_parity.py) drive mi355_mp.ops directly;
+these drive the public layers -- GCNConv with every constructor / forward
+option, and user MessagePassing subclasses on the fused and the generic path
+(both flows, bipartite inputs, explicit sizes) -- on random graphs with
+duplicate edges, pre-existing self loops (weighted, repeated) and isolated
+nodes, against
+
+  * the CPU oracle (oracle/pyg_ref.py, oracle/scatter_ref.py: the reference's
+    algorithm) for forward values: max bit-exact on tie-heavy integer data,
+    sum / mean within 1e-5 * max(1, sum |terms|);
+  * float64 autograd of the reference formula for every gradient (x, W,
+    bias, learned edge weights), within 1e-4 * max(1, |ref|).
+"""
+import os
+
+import pytest
+import torch
+from hypothesis import HealthCheck, given, settings, strategies as st
+
+from oracle import pyg_ref as P
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+_N_EX = int(os.environ.get("MP_FUZZ_LAYER_EXAMPLES", "60"))
+_SETTINGS = dict(max_examples=_N_EX, deadline=None, derandomize=True, database=None,
+                 suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+
+
+def _graph(N, deg, loops, seed, n_src=None):
+    """Random edge list with duplicates; `loops` of its edges made self loops
+    (some nodes get several).  n_src: bipartite source count (no loops)."""
+    g = torch.Generator().manual_seed(seed)
+    E = int(N * deg)
+    ns = N if n_src is None else n_src
+    ei = torch.stack([torch.randint(ns, (E,), generator=g), torch.randint(N, (E,), generator=g)])
+    if E and N > 1 and n_src is None:
+        hub = torch.randint(N, (1,), generator=g)
+        ei[1, : E // 4] = hub                       # one hub destination
+    if loops and E and n_src is None:
+        k = max(1, int(E * loops))
+        pos = torch.randint(E, (k,), generator=g)
+        ei[0, pos] = ei[1, pos]
+    return ei, g
+
+
+def _bound(got, want, terms, rel):
+    tol = rel * terms.clamp(min=1.0)
+    excess = ((got - want).abs() - tol).max() if got.numel() else torch.tensor(-1.0)
+    assert float(excess) <= 0, "excess %g" % float(excess)
+
+
+def _gcn64(x, ei, W, b, w, improved):
+    """GCNConv 1.4.3 in float64 with autograd: x W, add_remaining_self_loops
+    (a node keeps its last pre-existing loop with that edge's weight -- ones when
+    edge_weight is None, as upstream fills them before the loops), deg over row, deg^-1/2 (inf -> 0),
+    norm * x_j summed at col, + bias."""
+    N = x.shape[0]
+    h = x @ W
+    ww = torch.ones(ei.shape[1], dtype=torch.float64) if w is None else w
+    row, col = ei
+    mask = row != col
+    fill = torch.tensor(2.0 if improved else 1.0, dtype=torch.float64)
+    last = {}
+    for k in torch.nonzero(~mask).view(-1).tolist():   # sequential: the last loop wins (CPU index_put_)
+        last[int(row[k])] = k
+    loop_w = torch.stack([ww[last[v]] if v in last else fill for v in range(N)]) \
+        if N else torch.zeros(0, dtype=torch.float64)
+    r2 = torch.cat([row[mask], torch.arange(N)])
+    c2 = torch.cat([col[mask], torch.arange(N)])
+    w2 = torch.cat([ww[mask], loop_w])
+    deg = torch.zeros(N, dtype=torch.float64).index_add(0, r2, w2)
+    dis = deg.pow(-0.5)
+    dis = dis.masked_fill(dis == float("inf"), 0)
+    norm = dis[r2] * w2 * dis[c2]
+    out = torch.zeros(N, h.shape[1], dtype=torch.float64).index_add(0, c2, norm.view(-1, 1) * h[r2])
+    terms = torch.zeros(N, h.shape[1], dtype=torch.float64).index_add(
+        0, c2, (norm.abs().view(-1, 1) * (x.abs() @ W.abs())[r2]))
+    if b is not None:
+        out = out + b
+        terms = terms + b.abs()
+    return out, terms
+
+
+@settings(**_SETTINGS)
+@given(N=st.integers(1, 300), deg=st.floats(0.0, 12.0), Fi=st.integers(1, 40),
+       Fo=st.sampled_from([1, 3, 16, 64, 100, 256]), improved=st.booleans(),
+       weights=st.sampled_from(["none", "fixed", "learned"]), loops=st.sampled_from([0.0, 0.05, 0.3]),
+       cached=st.booleans(), bias=st.booleans(), seed=st.integers(0, 1 << 16))
+def test_fuzz_gcnconv_layer(N, deg, Fi, Fo, improved, weights, loops, cached, bias, seed):
+    """GCNConv(Fi, Fo, improved, cached, bias)(x, edge_index, edge_weight):
+    output within the float64 bound; d x, d W, d bias and (learned weights) d
+    edge_weight against float64 autograd of the 1.4.3 formula -- the degree,
+    deg^-1/2 and the loop weights carry the edge-weight gradient as upstream."""
+    from torch_geometric.nn import GCNConv
+    ei, g = _graph(N, deg, loops, seed)
+    E = ei.shape[1]
+    x = torch.randn(N, Fi, generator=g)
+    w = None
+    if weights != "none":
+        w = torch.rand(E, generator=g) + 0.25
+    conv = GCNConv(Fi, Fo, improved=improved, cached=cached, bias=bias).to(DEV)
+    if bias:
+        with torch.no_grad():
+            conv.bias.copy_(torch.randn(Fo, generator=g))
+    xd = x.to(DEV).requires_grad_()
+    wd = None
+    if w is not None:
+        wd = w.to(DEV).requires_grad_(weights == "learned")
+    eid = ei.to(DEV)
+    out = conv(xd, eid, wd)
+    if cached:
+        out = conv(xd, eid, wd)          # second call reads the cache
+    R = torch.randn(N, Fo, generator=g)
+    (out * R.to(DEV)).sum().backward()
+
+    x64 = x.double().requires_grad_()
+    W64 = conv.weight.detach().cpu().double().requires_grad_()
+    b64 = conv.bias.detach().cpu().double().requires_grad_() if bias else None
+    w64 = w.double().requires_grad_(weights == "learned") if w is not None else None
+    ref, terms = _gcn64(x64, ei, W64, b64, w64, improved)
+    _bound(out.detach().cpu().double(), ref.detach(), terms.detach(), 1e-5)
+    # the oracle itself (fp32, the reference's algorithm) agrees to the same bound
+    want = P.gcn_conv(x, ei, conv.weight.detach().cpu(), conv.bias.detach().cpu() if bias else None, w, improved)
+    _bound(out.detach().cpu().double(), want.double(), terms.detach(), 1e-5)
+
+    (ref * R.double()).sum().backward()
+
+    def close(a, b, what):
+        tol = 1e-4 * b.abs().clamp(min=1.0)
+        assert bool(((a.double() - b).abs() <= tol).all()), "%s: max err %g" % (what, float((a.double() - b).abs().max()))
+    close(xd.grad.cpu(), x64.grad, "d x")
+    close(conv.weight.grad.cpu(), W64.grad, "d W")
+    if bias:
+        close(conv.bias.grad.cpu(), b64.grad, "d bias")
+    if weights == "learned":
+        assert wd.grad is not None, "edge_weight gradient dropped"
+        close(wd.grad.cpu(), w64.grad, "d edge_weight")
+
+
+def _mp_classes():
+    from torch_geometric.nn import MessagePassing
+
+    class Plain(MessagePassing):            # default message: the fused path
+        def forward(self, x, edge_index, size=None):
+            return self.propagate(edge_index, size=size, x=x)
+
+    class Weighted(MessagePassing):         # a user message w * x_j: the generic path
+        def forward(self, x, edge_index, w, size=None):
+            return self.propagate(edge_index, size=size, x=x, w=w)
+
+        def message(self, x_j, w):
+            return w.view(-1, 1) * x_j
+
+    class Diff(MessagePassing):             # message over x_i and x_j: the generic path
+        def forward(self, x, edge_index, w, size=None):
+            return self.propagate(edge_index, size=size, x=x, w=w)
+
+        def message(self, x_i, x_j, w):
+            return w.view(-1, 1) * (x_j - x_i)
+
+        def update(self, aggr_out, x):
+            xd = x[1] if isinstance(x, (tuple, list)) else x
+            return aggr_out + 0.5 * xd if xd.shape == aggr_out.shape else aggr_out
+
+    return Plain, Weighted, Diff
+
+
+def _mp_reference(kind, x, ei, w, aggr, flow, size):
+    """The message, scatter_ and update of the 1.4.3 MessagePassing on the CPU
+    (float32, materialised messages, the reference's serial reduction)."""
+    i, j = (0, 1) if flow == "target_to_source" else (1, 0)
+    if isinstance(x, tuple):
+        xj_src, xi_src = x[j], x[i]
+        n_out = size[i] if size is not None else x[i].shape[0]
+    else:
+        xj_src = xi_src = x
+        n_out = size[i] if size is not None else x.shape[0]
+    x_j = xj_src[ei[j]]
+    if kind == "plain":
+        msg = x_j
+    elif kind == "weighted":
+        msg = w.view(-1, 1) * x_j
+    else:
+        msg = w.view(-1, 1) * (x_j - xi_src[ei[i]])
+    out = P.scatter_({"add": "add", "mean": "mean", "max": "max"}[aggr], msg, ei[i], n_out)
+    if kind == "diff":
+        xd = x[1] if isinstance(x, tuple) else x
+        if xd.shape == out.shape:
+            out = out + 0.5 * xd
+    return out, msg
+
+
+@settings(**_SETTINGS)
+@given(N=st.integers(1, 200), deg=st.floats(0.0, 10.0), F=st.sampled_from([1, 2, 5, 8, 33, 64, 128, 200]),
+       aggr=st.sampled_from(["add", "mean", "max"]), flow=st.sampled_from(["source_to_target", "target_to_source"]),
+       kind=st.sampled_from(["plain", "weighted", "diff"]), bipartite=st.booleans(), explicit_size=st.booleans(),
+       seed=st.integers(0, 1 << 16))
+def test_fuzz_message_passing_api(N, deg, F, aggr, flow, kind, bipartite, explicit_size, seed):
+    """User MessagePassing subclasses (default message -> fused kernel; a w * x_j
+    message and an x_i / x_j message -> native gathers + native segmented
+    reduce) over both flows, bipartite (x_src, x_dst) pairs and explicit
+    sizes: values against the CPU MessagePassing (max bit-exact on integer data
+    with ties, sum / mean within the bound), and for sum / mean the gradient
+    of x (and w) against float64 autograd of the same messages."""
+    Plain, Weighted, Diff = _mp_classes()
+    g = torch.Generator().manual_seed(seed)
+    n0 = N
+    n1 = max(1, N // 2 + 1) if bipartite else N
+    E = int(max(n0, n1) * deg)
+    ei = torch.stack([torch.randint(n0, (E,), generator=g), torch.randint(n1, (E,), generator=g)])
+    ints = aggr == "max"
+    mk = (lambda n: torch.randint(-3, 4, (n, F), generator=g).float()) if ints else \
+        (lambda n: torch.randn(n, F, generator=g))
+    if bipartite:
+        x = (mk(n0), mk(n1))
+    else:
+        x = mk(N)
+    w = (torch.tensor([0.5, 1.0, 2.0])[torch.randint(3, (E,), generator=g)] if ints
+         else torch.rand(E, generator=g) + 0.1)
+    size = (n0, n1) if explicit_size else None
+    if not bipartite and explicit_size:
+        size = (N, N)
+    layer = {"plain": Plain, "weighted": Weighted, "diff": Diff}[kind](aggr=aggr, flow=flow)
+    want, msg = _mp_reference(kind, x, ei, w, aggr, flow, size)
+
+    def dev(t):
+        return tuple(a.to(DEV).requires_grad_(not ints) for a in t) if isinstance(t, tuple) \
+            else t.to(DEV).requires_grad_(not ints)
+    xd = dev(x)
+    wd = w.to(DEV).requires_grad_(not ints and kind != "plain")
+    eid = ei.to(DEV)
+    if kind == "plain":
+        out = layer(xd, eid, size=size)
+    else:
+        out = layer(xd, eid, wd, size=size)
+    assert out.shape == want.shape
+    if ints:
+        assert torch.equal(out.detach().cpu(), want)
+        return
+    i, _ = (0, 1) if flow == "target_to_source" else (1, 0)
+    n_out = want.shape[0]
+    terms = P.scatter_("add", msg.abs(), ei[i], n_out)
+    if aggr == "mean":
+        terms = terms / torch.bincount(ei[i], minlength=n_out).clamp(min=1).view(-1, 1).float()
+    if kind == "diff":
+        xdst = x[1] if bipartite else x
+        if xdst.shape == terms.shape:
+            terms = terms + 0.5 * xdst.abs()
+    _bound(out.detach().cpu(), want, terms, 1e-5)
+
+    # gradients vs float64 autograd of the same messages and reduction
+    R = torch.randn(out.shape, generator=g)
+    (out * R.to(DEV)).sum().backward()
+    x64 = tuple(a.double().requires_grad_() for a in x) if bipartite else x.double().requires_grad_()
+    w64 = w.double().requires_grad_(kind != "plain")
+    ii, jj = (0, 1) if flow == "target_to_source" else (1, 0)
+    xj_src = x64[jj] if bipartite else x64
+    xi_src = x64[ii] if bipartite else x64
+    xj = xj_src[ei[jj]]
+    m64 = xj if kind == "plain" else (w64.view(-1, 1) * xj if kind == "weighted"
+                                      else w64.view(-1, 1) * (xj - xi_src[ei[ii]]))
+    o64 = torch.zeros(n_out, F, dtype=torch.float64).index_add(0, ei[ii], m64)
+    if aggr == "mean":
+        o64 = o64 / torch.bincount(ei[ii], minlength=n_out).clamp(min=1).view(-1, 1).double()
+    if kind == "diff":
+        xdd = x64[1] if bipartite else x64
+        if xdd.shape == o64.shape:
+            o64 = o64 + 0.5 * xdd
+    (o64 * R.double()).sum().backward()
+    pairs = list(zip(xd, x64)) if bipartite else [(xd, x64)]
+    if kind != "plain":
+        pairs.append((wd, w64))
+    for a, b in pairs:
+        ga = a.grad.cpu().double() if a.grad is not None else torch.zeros_like(b)
+        gb = b.grad if b.grad is not None else torch.zeros_like(b)
+        tol = 1e-4 * gb.abs().clamp(min=1.0)
+        assert bool(((ga - gb).abs() <= tol).all()), float((ga - gb).abs().max())
