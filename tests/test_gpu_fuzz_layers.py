@@ -278,3 +278,214 @@ def test_fuzz_message_passing_api(N, deg, F, aggr, flow, kind, bipartite, explic
         gb = b.grad if b.grad is not None else torch.zeros_like(b)
         tol = 1e-4 * gb.abs().clamp(min=1.0)
         assert bool(((ga - gb).abs() <= tol).all()), float((ga - gb).abs().max())
+
+
+@settings(**_SETTINGS)
+@given(N=st.integers(1, 200), deg=st.floats(0.0, 15.0), Fi=st.integers(1, 40), H=st.sampled_from([1, 2, 3, 4, 8]),
+       C=st.sampled_from([1, 2, 3, 4, 5, 8, 16, 30, 32]), concat=st.booleans(), bias=st.booleans(),
+       loops=st.sampled_from([0.0, 0.1]), ret=st.booleans(), mode=st.sampled_from(["train", "eval_dropout"]),
+       seed=st.integers(0, 1 << 16))
+def test_fuzz_gatconv_layer(N, deg, Fi, H, C, concat, bias, loops, ret, mode, seed):
+    """GATConv(Fi, C, heads=H, concat, bias, dropout)(x, edge_index,
+    return_attention_weights): pre-existing loops removed and one loop per node
+    appended, padded head widths, mean heads, eval-mode dropout (identity):
+    output, the returned (edge_index, alpha) and the gradients of x, W, att and
+    bias against float64 autograd of the oracle's 1.4.3 formula."""
+    from torch_geometric.nn import GATConv
+    ei, g = _graph(N, deg, loops, seed)
+    x = torch.randn(N, Fi, generator=g)
+    conv = GATConv(Fi, C, heads=H, concat=concat, bias=bias, dropout=0.6 if mode == "eval_dropout" else 0.0).to(DEV)
+    with torch.no_grad():
+        conv.att.mul_(3.0)                      # sharper softmax rows than glorot's
+        if bias:
+            conv.bias.copy_(torch.randn(conv.bias.shape, generator=g))
+    conv.train(mode == "train")
+    xd = x.to(DEV).requires_grad_()
+    res = conv(xd, ei.to(DEV), return_attention_weights=ret)
+    out, (ei_out, alpha) = res if ret else (res, (None, None))
+    x64 = x.double().requires_grad_()
+    W64 = conv.weight.detach().cpu().double().requires_grad_()
+    a64 = conv.att.detach().cpu().double().requires_grad_()
+    b64 = conv.bias.detach().cpu().double().requires_grad_() if bias else None
+    want, ei_l, alpha_ref = P.gat_conv(x64, ei, W64, a64, b64, H, C, concat=concat, return_alpha=True)
+    assert out.shape == want.shape
+    assert torch.allclose(out.detach().cpu().double(), want.detach(), rtol=1e-5, atol=1e-5), \
+        float((out.detach().cpu().double() - want.detach()).abs().max())
+    if ret:
+        assert torch.equal(ei_out.cpu(), ei_l)
+        assert alpha.shape == alpha_ref.shape
+        assert bool(((alpha.detach().cpu().double() - alpha_ref.detach()).abs() <= 1e-5).all())
+    R = torch.randn(out.shape, generator=g)
+    (out * R.to(DEV)).sum().backward()
+    (want * R.double()).sum().backward()
+    pairs = [(xd.grad, x64.grad, "x"), (conv.weight.grad, W64.grad, "W"), (conv.att.grad, a64.grad, "att")]
+    if bias:
+        pairs.append((conv.bias.grad, b64.grad, "bias"))
+    for got, ref, what in pairs:
+        err = (got.cpu().double() - ref).abs()
+        assert bool((err <= 1e-4 * ref.abs().clamp(min=1.0)).all()), "%s: %g" % (what, float(err.max()))
+
+
+# --------------------------------------------------------------------------
+# utilities: self loops (a7), scatter_ (a2), softmax (a6), global pooling (8f-3)
+# --------------------------------------------------------------------------
+
+@settings(**_SETTINGS)
+@given(N=st.integers(1, 200), deg=st.floats(0.0, 8.0), loops=st.sampled_from([0.0, 0.1, 0.5]),
+       attr=st.sampled_from(["none", "1d", "2d"]), fill=st.sampled_from([1, 2, 0.5]), extra=st.integers(0, 3),
+       seed=st.integers(0, 1 << 16))
+def test_fuzz_loop_utilities(N, deg, loops, attr, fill, extra, seed):
+    """remove_self_loops / add_self_loops / add_remaining_self_loops on the
+    device (mp_self_loops) bit-equal to the oracle's restatement of the 1.4.3
+    utilities: edge order, loop order, a repeated loop's LAST weight, fill
+    values, num_nodes past the largest index, 2-D edge attributes."""
+    from torch_geometric.utils import remove_self_loops, add_self_loops, add_remaining_self_loops
+    ei, g = _graph(N, deg, loops, seed)
+    E = ei.shape[1]
+    a = None if attr == "none" else (torch.randn(E, generator=g) if attr == "1d" else torch.randn(E, 3, generator=g))
+    eid = ei.to(DEV)
+    ad = a.to(DEV) if a is not None else None
+    got_ei, got_a = remove_self_loops(eid, ad)
+    want_ei, want_a = P.remove_self_loops(ei, a)
+    assert torch.equal(got_ei.cpu(), want_ei)
+    assert (got_a is None) == (want_a is None) and (got_a is None or torch.equal(got_a.cpu(), want_a))
+    n = N + extra
+    w = a if attr == "1d" else None
+    wd = w.to(DEV) if w is not None else None
+    for fn, ref in ((add_self_loops, P.add_self_loops), (add_remaining_self_loops, P.add_remaining_self_loops)):
+        got_ei, got_w = fn(eid, wd, fill, n)
+        want_ei, want_w = ref(ei, w, fill, n)
+        assert torch.equal(got_ei.cpu(), want_ei), fn.__name__
+        assert (got_w is None) == (want_w is None), fn.__name__
+        if got_w is not None:
+            assert torch.equal(got_w.cpu(), want_w.to(got_w.dtype)), fn.__name__
+
+
+@settings(**_SETTINGS)
+@given(N=st.integers(1, 150), E=st.integers(0, 3000), shape=st.sampled_from([(), (1,), (5,), (3, 4), (64,)]),
+       name=st.sampled_from(["add", "mean", "max", "min"]), extra=st.integers(0, 3), hub=st.booleans(),
+       seed=st.integers(0, 1 << 16))
+def test_fuzz_scatter_softmax_pool_utilities(N, E, shape, name, extra, hub, seed):
+    """utils.scatter_ (every name, 1-3-D src, dim_size past the largest index;
+    max / min with the +-10000 masks bit-exact on integer data, sum / mean within
+    the bound), utils.softmax (1-D and multi-head scores, empty segments,
+    +1e-16) and global_{add,mean,max}_pool over a sorted batch vector, against
+    the oracle."""
+    from torch_geometric.utils import scatter_, softmax
+    from torch_geometric.nn import global_add_pool, global_mean_pool, global_max_pool
+    g = torch.Generator().manual_seed(seed)
+    idx = torch.randint(N, (E,), generator=g)
+    if hub and E:
+        idx[: E // 3] = 0
+    ints = name in ("max", "min")
+    src = (torch.randint(-20000, 20000, (E,) + shape, generator=g).float() if ints
+           else torch.randn((E,) + shape, generator=g))
+    n = N + extra
+    got = scatter_(name, src.to(DEV), idx.to(DEV), 0, n)
+    want = P.scatter_(name, src, idx, n)
+    assert got.shape == want.shape
+    if ints:
+        assert torch.equal(got.cpu(), want)
+    else:
+        terms = P.scatter_("add", src.abs(), idx, n)
+        if name == "mean":
+            cnt = torch.bincount(idx, minlength=n).clamp(min=1).float().view((-1,) + (1,) * len(shape))
+            terms = terms / cnt
+        _bound(got.cpu(), want, terms, 1e-5)
+    # softmax over the same segments
+    sc = torch.randn((E,) + shape[:1], generator=g) * 4
+    sm = softmax(sc.to(DEV), idx.to(DEV), n)
+    ref = P.softmax(sc, idx, n)
+    assert sm.shape == ref.shape
+    assert bool(((sm.cpu() - ref).abs() <= 1e-5).all())
+    # global pooling: a sorted batch vector over the rows of src
+    if E and len(shape) == 1:
+        batch = torch.sort(idx).values
+        x = src
+        for fn, nm in ((global_add_pool, "add"), (global_mean_pool, "mean"), (global_max_pool, "max")):
+            out = fn(x.to(DEV), batch.to(DEV))
+            B = int(batch.max()) + 1
+            ref = P.scatter_(nm, x, batch, B)
+            if nm == "max" or ints:
+                assert torch.equal(out.cpu(), ref), nm
+            else:
+                t = P.scatter_("add", x.abs(), batch, B)
+                _bound(out.cpu(), ref, t, 1e-5)
+
+
+@settings(**_SETTINGS)
+@given(N=st.integers(1, 200), deg=st.floats(0.0, 10.0), Fi=st.integers(1, 40), Fo=st.sampled_from([1, 7, 64, 130]),
+       layer=st.sampled_from(["sage", "sage_concat", "graph_add", "graph_mean", "graph_max"]),
+       normalize=st.booleans(), bias=st.booleans(), weighted=st.booleans(), loops=st.sampled_from([0.0, 0.2]),
+       seed=st.integers(0, 1 << 16))
+def test_fuzz_sage_graph_conv_layers(N, deg, Fi, Fo, layer, normalize, bias, weighted, loops, seed):
+    """SAGEConv(normalize, concat, bias) and GraphConv(aggr) with and without edge
+    weights, against float64 autograd of the 1.4.3 formulas: SAGE's
+    add_remaining_self_loops (last loop's weight wins) + mean + x W (+ b,
+    L2-normalised), concat's [x, mean] W; GraphConv's aggr(w h_j) + lin(x).
+    Values within 1e-5 (max: the selected terms), gradients of x, W (and w)
+    within 1e-4 for add / mean."""
+    from torch_geometric.nn import SAGEConv, GraphConv
+    ei, g = _graph(N, deg, loops, seed)
+    E = ei.shape[1]
+    x = torch.randn(N, Fi, generator=g)
+    w = torch.rand(E, generator=g) + 0.25 if weighted else None
+    if layer.startswith("sage"):
+        conv = SAGEConv(Fi, Fo, normalize=normalize, concat=layer == "sage_concat", bias=bias)
+    else:
+        conv = GraphConv(Fi, Fo, aggr=layer.split("_")[1], bias=bias)
+    conv = conv.to(DEV)
+    xd = x.to(DEV).requires_grad_()
+    wd = w.to(DEV).requires_grad_() if weighted else None
+    out = conv(xd, ei.to(DEV), wd)
+
+    x64 = x.double().requires_grad_()
+    w64 = w.double().requires_grad_() if weighted else None
+    params = {k: v.detach().cpu().double().requires_grad_() for k, v in conv.named_parameters()}
+    if layer.startswith("sage"):
+        if layer == "sage_concat":
+            e2, ww = ei, w64
+        else:
+            e2, ww = P.add_remaining_self_loops(ei, w64, 1, N)
+        xj = x64[e2[0]]
+        msg = xj if ww is None else ww.view(-1, 1) * xj
+        agg = torch.zeros(N, Fi, dtype=torch.float64).index_add(0, e2[1], msg)
+        agg = agg / torch.bincount(e2[1], minlength=N).clamp(min=1).view(-1, 1).double()
+        if layer == "sage_concat":
+            agg = torch.cat([x64, agg], dim=-1)
+        ref = agg @ params["weight"]
+        if bias:
+            ref = ref + params["bias"]
+        if normalize:
+            ref = torch.nn.functional.normalize(ref, p=2, dim=-1)
+    else:
+        aggr = layer.split("_")[1]
+        h = x64 @ params["weight"]
+        msg = h[ei[0]] if w64 is None else w64.view(-1, 1) * h[ei[0]]
+        if aggr == "max":
+            agg = torch.full((N, Fo), float("-inf"), dtype=torch.float64).scatter_reduce(
+                0, ei[1].view(-1, 1).expand(-1, Fo), msg, "amax")
+            agg = torch.where(torch.isinf(agg) | (agg < -10000), torch.zeros_like(agg), agg)
+        else:
+            agg = torch.zeros(N, Fo, dtype=torch.float64).index_add(0, ei[1], msg)
+            if aggr == "mean":
+                agg = agg / torch.bincount(ei[1], minlength=N).clamp(min=1).view(-1, 1).double()
+        ref = agg + torch.nn.functional.linear(x64, params["lin.weight"], params.get("lin.bias"))
+    assert out.shape == ref.shape
+    err = (out.detach().cpu().double() - ref.detach()).abs()
+    assert bool((err <= 1e-5 * ref.detach().abs().clamp(min=1.0)).all()), float(err.max())
+    if layer == "graph_max":
+        return
+    if normalize and layer.startswith("sage") and Fo == 1:
+        # v / |v| of one feature is +-1: its exact gradient is 0 and the fp32 one is
+        # roundoff / |v| (ill-conditioned in torch's own F.normalize, not the engine)
+        return
+    R = torch.randn(out.shape, generator=g)
+    (out * R.to(DEV)).sum().backward()
+    (ref * R.double()).sum().backward()
+    pairs = [(xd.grad, x64.grad, "x")] + [(dict(conv.named_parameters())[k].grad, v.grad, k) for k, v in params.items()]
+    if weighted:
+        pairs.append((wd.grad, w64.grad, "w"))
+    for got, want, what in pairs:
+        err = (got.cpu().double() - want).abs()
+        assert bool((err <= 1e-4 * want.abs().clamp(min=1.0)).all()), "%s: %g" % (what, float(err.max()))
