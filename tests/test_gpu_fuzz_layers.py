@@ -95,6 +95,7 @@ def test_fuzz_gcnconv_layer(N, deg, Fi, Fo, improved, weights, loops, cached, bi
     edge_weight against float64 autograd of the 1.4.3 formula -- the degree,
     deg^-1/2 and the loop weights carry the edge-weight gradient as upstream."""
     from torch_geometric.nn import GCNConv
+    torch.manual_seed(seed)               # layer initialisers: a failing example replays
     ei, g = _graph(N, deg, loops, seed)
     E = ei.shape[1]
     x = torch.randn(N, Fi, generator=g)
@@ -206,6 +207,7 @@ def test_fuzz_message_passing_api(N, deg, F, aggr, flow, kind, bipartite, explic
     with ties, sum / mean within the bound), and for sum / mean the gradient
     of x (and w) against float64 autograd of the same messages."""
     Plain, Weighted, Diff = _mp_classes()
+    torch.manual_seed(seed)
     g = torch.Generator().manual_seed(seed)
     n0 = N
     n1 = max(1, N // 2 + 1) if bipartite else N
@@ -292,6 +294,7 @@ def test_fuzz_gatconv_layer(N, deg, Fi, H, C, concat, bias, loops, ret, mode, se
     output, the returned (edge_index, alpha) and the gradients of x, W, att and
     bias against float64 autograd of the oracle's 1.4.3 formula."""
     from torch_geometric.nn import GATConv
+    torch.manual_seed(seed)               # layer initialisers: a failing example replays
     ei, g = _graph(N, deg, loops, seed)
     x = torch.randn(N, Fi, generator=g)
     conv = GATConv(Fi, C, heads=H, concat=concat, bias=bias, dropout=0.6 if mode == "eval_dropout" else 0.0).to(DEV)
@@ -340,6 +343,7 @@ def test_fuzz_loop_utilities(N, deg, loops, attr, fill, extra, seed):
     utilities: edge order, loop order, a repeated loop's LAST weight, fill
     values, num_nodes past the largest index, 2-D edge attributes."""
     from torch_geometric.utils import remove_self_loops, add_self_loops, add_remaining_self_loops
+    torch.manual_seed(seed)               # layer initialisers: a failing example replays
     ei, g = _graph(N, deg, loops, seed)
     E = ei.shape[1]
     a = None if attr == "none" else (torch.randn(E, generator=g) if attr == "1d" else torch.randn(E, 3, generator=g))
@@ -426,6 +430,7 @@ def test_fuzz_sage_graph_conv_layers(N, deg, Fi, Fo, layer, normalize, bias, wei
     Values within 1e-5 (max: the selected terms), gradients of x, W (and w)
     within 1e-4 for add / mean."""
     from torch_geometric.nn import SAGEConv, GraphConv
+    torch.manual_seed(seed)               # layer initialisers: a failing example replays
     ei, g = _graph(N, deg, loops, seed)
     E = ei.shape[1]
     x = torch.randn(N, Fi, generator=g)
@@ -487,5 +492,89 @@ def test_fuzz_sage_graph_conv_layers(N, deg, Fi, Fo, layer, normalize, bias, wei
     if weighted:
         pairs.append((wd.grad, w64.grad, "w"))
     for got, want, what in pairs:
+        err = (got.cpu().double() - want).abs()
+        assert bool((err <= 1e-4 * want.abs().clamp(min=1.0)).all()), "%s: %g" % (what, float(err.max()))
+
+
+@settings(**_SETTINGS)
+@given(N=st.integers(1, 150), deg=st.floats(0.0, 8.0), Fi=st.integers(1, 24), Fo=st.sampled_from([1, 5, 64]),
+       layer=st.sampled_from(["cheb", "agnn", "sg", "gin"]), K=st.integers(1, 3),
+       norm=st.sampled_from(["sym", "rw", None]), weighted=st.booleans(), bias=st.booleans(),
+       loops=st.sampled_from([0.0, 0.2]), seed=st.integers(0, 1 << 16))
+def test_fuzz_cheb_agnn_sg_gin_layers(N, deg, Fi, Fo, layer, K, norm, weighted, bias, loops, seed):
+    """The reference's other propagate callers at the layer API: ChebConv(K,
+    sym / rw / None, lambda_max, edge weights), AGNNConv(beta), SGConv(K,
+    edge weights), GINConv(eps, train_eps) against float64 autograd of the
+    oracle's 1.4.3 formulas: values within 1e-5 * max(1, |ref|), gradients of
+    x and every parameter within 1e-4."""
+    from torch_geometric.nn import ChebConv, AGNNConv, SGConv, GINConv
+    torch.manual_seed(seed)               # layer initialisers: a failing example replays
+    ei, g = _graph(N, deg, loops, seed)
+    E = ei.shape[1]
+    x = torch.randn(N, Fi, generator=g)
+    w = torch.rand(E, generator=g) + 0.25 if weighted else None
+    lam = 2.0 if norm == "sym" else 1.7
+    if layer == "cheb":
+        conv = ChebConv(Fi, Fo, K, normalization=norm, bias=bias)
+    elif layer == "agnn":
+        conv = AGNNConv(requires_grad=True)
+    elif layer == "sg":
+        conv = SGConv(Fi, Fo, K=K, bias=bias)
+    else:
+        conv = GINConv(torch.nn.Sequential(torch.nn.Linear(Fi, Fo), torch.nn.ReLU(), torch.nn.Linear(Fo, Fo)),
+                       eps=0.25, train_eps=True)
+    conv = conv.to(DEV)
+    with torch.no_grad():
+        for p in conv.parameters():
+            p.add_(0.1 * torch.randn(p.shape, generator=g).to(DEV))
+    xd = x.to(DEV).requires_grad_()
+    wd = w.to(DEV) if weighted else None
+    if layer == "cheb":
+        out = conv(xd, ei.to(DEV), wd, lambda_max=None if norm == "sym" else lam)
+    elif layer == "sg":
+        out = conv(xd, ei.to(DEV), wd)
+    else:
+        out = conv(xd, ei.to(DEV))
+    x64 = x.double().requires_grad_()
+    w64 = w.double() if weighted else None
+    params = {k: v.detach().cpu().double().requires_grad_() for k, v in conv.named_parameters()}
+    if layer == "cheb":
+        ref = P.cheb_conv(x64, ei, params["weight"], params.get("bias"), w64, norm, lam)
+    elif layer == "agnn":
+        ref = P.agnn_conv(x64, ei, params["beta"])
+    elif layer == "sg":
+        ref = P.sg_conv(x64, ei, K, params["lin.weight"], params.get("lin.bias"), w64)
+    else:
+        ref = P.gin_conv(x64, ei, lambda t: torch.nn.functional.linear(
+            torch.relu(torch.nn.functional.linear(t, params["nn.0.weight"], params["nn.0.bias"])),
+            params["nn.2.weight"], params["nn.2.bias"]), params["eps"])
+    assert out.shape == ref.shape
+    scale = ref.detach().abs()
+    if layer == "cheb":
+        # the Chebyshev recursion cancels large terms (L = D - A has entries of the
+        # degree's size): bound by the magnitude of the terms, sum_k |T_k| |W_k| + |b|
+        with torch.no_grad():
+            e2, nw = P.cheb_norm(ei, N, w64, norm, lam, torch.float64)
+            A = lambda t: torch.zeros_like(t).index_add(0, e2[1], nw.abs().view(-1, 1) * t[e2[0]])
+            W = params["weight"].abs()
+            t0, t1 = x64.abs(), A(x64.abs())
+            scale = t0 @ W[0] + (t1 @ W[1] if K > 1 else 0)
+            for k in range(2, K):
+                t0, t1 = t1, 2 * A(t1) + t0
+                scale = scale + t1 @ W[k]
+            if bias:
+                scale = scale + params["bias"].abs()
+    err = (out.detach().cpu().double() - ref.detach()).abs()
+    assert bool((err <= 1e-5 * scale.clamp(min=1.0)).all()), float(err.max())
+    R = torch.randn(out.shape, generator=g)
+    (out * R.to(DEV)).sum().backward()
+    (ref * R.double()).sum().backward()
+    if layer == "cheb" and norm is None and K > 1:
+        return   # gradients of the unnormalised recursion carry the same cancellation; values are the check
+    named = dict(conv.named_parameters())
+    pairs = [(xd.grad, x64.grad, "x")] + [(named[k].grad, v.grad, k) for k, v in params.items()]
+    for got, want, what in pairs:
+        got = got if got is not None else torch.zeros_like(want)
+        want = want if want is not None else torch.zeros_like(want)
         err = (got.cpu().double() - want).abs()
         assert bool((err <= 1e-4 * want.abs().clamp(min=1.0)).all()), "%s: %g" % (what, float(err.max()))
