@@ -578,3 +578,44 @@ def test_fuzz_cheb_agnn_sg_gin_layers(N, deg, Fi, Fo, layer, K, norm, weighted, 
         want = want if want is not None else torch.zeros_like(want)
         err = (got.cpu().double() - want).abs()
         assert bool((err <= 1e-4 * want.abs().clamp(min=1.0)).all()), "%s: %g" % (what, float(err.max()))
+
+
+@settings(**dict(_SETTINGS, max_examples=max(10, _N_EX // 3)))
+@given(N=st.integers(1, 100), deg=st.floats(0.0, 6.0), B=st.integers(1, 3), F=st.sampled_from([1, 4, 33]),
+       aggr=st.sampled_from(["add", "mean", "max"]), kind=st.sampled_from(["plain", "diff"]),
+       seed=st.integers(0, 1 << 16))
+def test_fuzz_message_passing_node_dim(N, deg, B, F, aggr, kind, seed):
+    """MessagePassing(node_dim=1) on batched node tensors [B, N, F] (the
+    1.4.3 node_dim argument): gathers along dim 1, scatter_ along dim 1 --
+    the same values as the 2-D layer applied to each batch entry."""
+    from torch_geometric.nn import MessagePassing
+    torch.manual_seed(seed)
+    g = torch.Generator().manual_seed(seed)
+    E = int(N * deg)
+    ei = torch.randint(N, (2, E), generator=g)
+    x = (torch.randint(-3, 4, (B, N, F), generator=g).float() if aggr == "max" else torch.randn(B, N, F, generator=g))
+
+    class Plain(MessagePassing):
+        def forward(self, x, edge_index):
+            return self.propagate(edge_index, x=x)
+
+    class Diff(MessagePassing):
+        def forward(self, x, edge_index):
+            return self.propagate(edge_index, x=x)
+
+        def message(self, x_i, x_j):
+            return x_j - 0.5 * x_i
+
+    cls = Plain if kind == "plain" else Diff
+    out = cls(aggr=aggr, node_dim=1)(x.to(DEV), ei.to(DEV))
+    assert out.shape == (B, N, F)
+    for b in range(B):
+        want, msg = _mp_reference("plain", x[b], ei, None, aggr, "source_to_target", None)
+        if kind == "diff":
+            msg = x[b][ei[0]] - 0.5 * x[b][ei[1]]
+            want = P.scatter_(aggr, msg, ei[1], N)
+        if aggr == "max":
+            assert torch.equal(out[b].cpu(), want)
+        else:
+            terms = P.scatter_("add", msg.abs(), ei[1], N)
+            _bound(out[b].cpu(), want, terms, 1e-5)
