@@ -70,18 +70,21 @@ class GCNConv(MessagePassing):
         fill_value = 1 if not improved else 2
         ei, pos = remaining_loops_structure(edge_index, num_nodes)
         if edge_weight is None:
-            # depends on the structure only: cache it with the structure
-            def build():
-                ones = torch.ones((edge_index.size(1),), dtype=torch.float32, device=edge_index.device)
-                w = remaining_loops_weight(ones, pos, fill_value)
-                return _ops.gcn_norm_weights(ei, num_nodes, w, integer_weights=True)
-            norm = cached_value(edge_index, ("gcn_norm", int(num_nodes), fill_value), build)
-            return ei, norm
+            if dtype in (None, torch.float32):
+                # depends on the structure only: cache it with the structure
+                def build():
+                    ones = torch.ones((edge_index.size(1),), dtype=torch.float32, device=edge_index.device)
+                    w = remaining_loops_weight(ones, pos, fill_value)
+                    return _ops.gcn_norm_weights(ei, num_nodes, w, integer_weights=True)
+                norm = cached_value(edge_index, ("gcn_norm", int(num_nodes), fill_value), build)
+                return ei, norm
+            edge_weight = torch.ones((edge_index.size(1),), dtype=dtype, device=edge_index.device)
         w = remaining_loops_weight(edge_weight, pos, fill_value)
-        if torch.is_grad_enabled() and w.requires_grad:
-            # learned edge weights: upstream's differentiable form, so the gradient
-            # reaches edge_weight through deg and norm (the degree's scatter_add on
-            # the native segmented sum with its autograd, as get_laplacian does)
+        if w.dtype != torch.float32 or (torch.is_grad_enabled() and w.requires_grad):
+            # a float64 / half model, or learned edge weights: upstream's form in the
+            # weights' dtype and differentiable, so the gradient reaches edge_weight
+            # through deg and norm (the degree's scatter_add on the native segmented
+            # sum of that dtype, in edge order, with its autograd)
             row, col = ei
             deg = torch_scatter.scatter_add(w, row, dim=0, dim_size=num_nodes)
             deg_inv_sqrt = deg.pow(-0.5)

@@ -619,3 +619,48 @@ def test_fuzz_message_passing_node_dim(N, deg, B, F, aggr, kind, seed):
         else:
             terms = P.scatter_("add", msg.abs(), ei[1], N)
             _bound(out[b].cpu(), want, terms, 1e-5)
+
+
+# --------------------------------------------------------------------------
+# float64 models (upstream computes every step, the GCN norm included, in the
+# model's dtype): gradcheck of each layer and float64-accurate values
+# --------------------------------------------------------------------------
+
+@pytest.mark.parametrize("layer", ["gcn", "gcn_w", "gcn_improved", "gat", "sage", "graph_add", "graph_mean",
+                                   "cheb", "sg", "gin", "agnn"])
+def test_float64_layers_gradcheck(layer):
+    """A float64 model on the engine: torch.autograd.gradcheck of the layer with
+    respect to x (and the edge weights where the layer takes them) on a graph
+    with duplicate edges and weighted self loops, and for GCNConv the output
+    against the float64 formula to 1e-12 (the norm is built in float64, not
+    rounded through float32)."""
+    from torch_geometric.nn import (GCNConv, GATConv, SAGEConv, GraphConv, ChebConv, SGConv, GINConv,
+                                    AGNNConv)
+    torch.manual_seed(5)
+    ei, g = _graph(12, 3.0, 0.2, 11)
+    E = ei.shape[1]
+    x = torch.randn(12, 5, generator=g, dtype=torch.float64)
+    w = torch.rand(E, generator=g, dtype=torch.float64) + 0.25
+    mk = {"gcn": lambda: GCNConv(5, 4), "gcn_w": lambda: GCNConv(5, 4), "gcn_improved": lambda: GCNConv(5, 4, improved=True),
+          "gat": lambda: GATConv(5, 3, heads=2), "sage": lambda: SAGEConv(5, 4), "graph_add": lambda: GraphConv(5, 4),
+          "graph_mean": lambda: GraphConv(5, 4, aggr="mean"), "cheb": lambda: ChebConv(5, 4, 3),
+          "sg": lambda: SGConv(5, 4, K=2), "agnn": lambda: AGNNConv(),
+          "gin": lambda: GINConv(torch.nn.Sequential(torch.nn.Linear(5, 4), torch.nn.Tanh()), train_eps=True)}
+    conv = mk[layer]().double().to(DEV)
+    eid = ei.to(DEV)
+    xd = x.to(DEV).requires_grad_()
+    wd = w.to(DEV).requires_grad_()
+    takes_w = layer in ("gcn_w", "sage", "graph_add", "graph_mean", "cheb", "sg")
+
+    def f(xx, ww):
+        if takes_w:
+            return conv(xx, eid, ww)
+        return conv(xx, eid)
+    assert torch.autograd.gradcheck(f, (xd, wd if takes_w else wd.detach()), eps=1e-6, atol=1e-6, rtol=1e-5)
+    if layer.startswith("gcn"):
+        out = f(xd, wd)
+        assert out.dtype == torch.float64
+        ref, _ = _gcn64(x, ei, conv.weight.detach().cpu(), conv.bias.detach().cpu(), w if takes_w else None,
+                        layer == "gcn_improved")
+        assert torch.allclose(out.detach().cpu(), ref, rtol=1e-12, atol=1e-12), \
+            float((out.detach().cpu() - ref).abs().max())
