@@ -976,6 +976,11 @@ def gat_propagate(graph, edge_index, xw, att, heads, out_channels, negative_slop
     _lib.require_device(xw, edge_index, att, bias)
     xw = _f32_2d(xw, "x@W").contiguous()
     H, C = int(heads), int(out_channels)
+    if xw.shape[0] == 0:
+        # no nodes (hence no edges): an empty output, still connected to xw / bias
+        # for autograd -- the kernels are not launched
+        out = xw * 0.0 if bias is None else xw * 0.0 + bias
+        return out, (xw.new_zeros((edge_index.shape[1], H)) if return_alpha else None)
     drop = None
     if dropout > 0:
         if not (gat_dropout_ok(H, C, dropout) and _gat_train_fwd_ok(graph, xw, H, C)):

@@ -664,3 +664,42 @@ def test_float64_layers_gradcheck(layer):
                         layer == "gcn_improved")
         assert torch.allclose(out.detach().cpu(), ref, rtol=1e-12, atol=1e-12), \
             float((out.detach().cpu() - ref).abs().max())
+
+
+def test_empty_graphs_through_every_layer():
+    """Zero nodes and zero edges (an empty mini-batch shard, a graph whose edges
+    were all filtered): every layer returns [0, F_out] / [N, F_out] as upstream,
+    and the backward runs."""
+    from torch_geometric.nn import (GCNConv, GATConv, SAGEConv, GraphConv, ChebConv, SGConv, GINConv,
+                                    AGNNConv, MessagePassing, global_add_pool, global_max_pool)
+    from torch_geometric.utils import softmax, scatter_, add_remaining_self_loops
+    import torch_scatter
+
+    class Plain(MessagePassing):
+        def forward(self, x, edge_index):
+            return self.propagate(edge_index, x=x)
+
+    layers = [GCNConv(4, 3), GATConv(4, 3, heads=2), SAGEConv(4, 3), GraphConv(4, 3), ChebConv(4, 3, 2),
+              SGConv(4, 3, K=2), GINConv(torch.nn.Linear(4, 3)), AGNNConv(), Plain(aggr="max"), Plain(aggr="mean")]
+    for N in (0, 5):
+        ei = torch.empty(2, 0, dtype=torch.long, device=DEV)
+        for conv in layers:
+            conv = conv.to(DEV)
+            x = torch.randn(N, 4, device=DEV, requires_grad=True)
+            out = conv(x, ei)
+            assert out.shape[0] == N, type(conv).__name__
+            out.sum().backward()
+            assert x.grad is not None and x.grad.shape == x.shape, type(conv).__name__
+        e_w = torch.empty(0, device=DEV)
+        ei2, w2 = add_remaining_self_loops(ei, e_w, 1, N)
+        assert ei2.shape == (2, N) and w2.shape == (N,)
+    src = torch.empty(0, 3, device=DEV)
+    idx = torch.empty(0, dtype=torch.long, device=DEV)
+    for name in ("add", "mean", "max", "min"):
+        assert scatter_(name, src, idx, 0, 4).shape == (4, 3)
+        assert torch.equal(scatter_(name, src, idx, 0, 4), torch.zeros(4, 3, device=DEV))
+    out, arg = torch_scatter.scatter_max(src, idx, dim=0, dim_size=2)
+    assert torch.equal(out, torch.zeros(2, 3, device=DEV)) and bool((arg == 0).all())
+    assert softmax(torch.empty(0, device=DEV), idx, 3).shape == (0,)
+    assert global_add_pool(torch.empty(0, 3, device=DEV), idx, size=2).shape == (2, 3)
+    assert global_max_pool(torch.empty(0, 3, device=DEV), idx, size=2).shape == (2, 3)
