@@ -703,3 +703,66 @@ def test_empty_graphs_through_every_layer():
     assert softmax(torch.empty(0, device=DEV), idx, 3).shape == (0,)
     assert global_add_pool(torch.empty(0, 3, device=DEV), idx, size=2).shape == (2, 3)
     assert global_max_pool(torch.empty(0, 3, device=DEV), idx, size=2).shape == (2, 3)
+
+
+@settings(**dict(_SETTINGS, max_examples=max(10, _N_EX // 2)))
+@given(N=st.integers(1, 150), deg=st.floats(0.0, 8.0), F=st.sampled_from([1, 3, 8, 64, 100]),
+       layer=st.sampled_from(["plain_add", "plain_max", "gcn", "gat", "sage", "graph"]),
+       xview=st.sampled_from(["contiguous", "offset", "strided", "transposed"]), eiview=st.booleans(),
+       seed=st.integers(0, 1 << 16))
+def test_fuzz_layer_input_views(N, deg, F, layer, xview, eiview, seed):
+    """Layers fed non-contiguous inputs -- x as a column slice at an odd offset
+    (rows not 16-byte aligned), a strided column view, a transposed view, and
+    edge_index as the transposed view of an [E, 2] tensor -- give the same
+    output and gradients as on contiguous copies: bitwise for the aggregation
+    (the kernels see the same values in the same order), to the GEMM's rounding
+    for layers with an x W."""
+    from torch_geometric.nn import GCNConv, GATConv, SAGEConv, GraphConv, MessagePassing
+
+    class Plain(MessagePassing):
+        def forward(self, x, edge_index):
+            return self.propagate(edge_index, x=x)
+
+    torch.manual_seed(seed)
+    g = torch.Generator().manual_seed(seed)
+    E = int(N * deg)
+    ei = torch.randint(N, (2, E), generator=g)
+    base = torch.randn(N, F, generator=g)
+    mk = {"plain_add": lambda: Plain(aggr="add"), "plain_max": lambda: Plain(aggr="max"),
+          "gcn": lambda: GCNConv(F, 8), "gat": lambda: GATConv(F, 4, heads=2), "sage": lambda: SAGEConv(F, 8),
+          "graph": lambda: GraphConv(F, 8)}
+    conv = mk[layer]().to(DEV)
+
+    def x_as(kind):
+        b = base.to(DEV)
+        if kind == "offset":
+            big = torch.zeros(N, F + 3, device=DEV)
+            big[:, 1:F + 1] = b
+            v = big[:, 1:F + 1]
+        elif kind == "strided":
+            big = torch.zeros(N, 2 * F, device=DEV)
+            big[:, ::2] = b
+            v = big[:, ::2]
+        elif kind == "transposed":
+            v = b.t().contiguous().t()
+        else:
+            v = b.clone()
+        return v.requires_grad_() if v.is_leaf else v.detach().requires_grad_()
+    e_ref = ei.to(DEV)
+    e_in = ei.t().contiguous().to(DEV).t() if eiview else e_ref.clone()
+    xa, xb = x_as("contiguous"), x_as(xview)
+    if not xb.is_leaf:
+        xb.retain_grad()
+    oa = conv(xa, e_ref)
+    ob = conv(xb, e_in)
+    R = torch.randn(oa.shape, generator=g).to(DEV)
+    (oa * R).sum().backward()
+    (ob * R).sum().backward()
+    if layer.startswith("plain"):
+        assert torch.equal(oa, ob)
+        assert torch.equal(xa.grad, xb.grad)
+    else:
+        # x W: hipBLASLt picks its kernel by the operand layout (a transposed view
+        # is a TN GEMM), so the layer agrees to the GEMM's rounding, not bitwise
+        for a, b in ((oa, ob), (xa.grad, xb.grad)):
+            assert torch.allclose(a, b, rtol=1e-5, atol=1e-6), float((a - b).abs().max())
