@@ -65,14 +65,18 @@ def parse():
     ap.add_argument("--no-halo-cover", action="store_true",
                     help="N>1: pull exchange (every remote source row) instead of the hybrid pull / push "
                          "cover (dist.HaloCover)")
+    ap.add_argument("--sharded", action="store_true",
+                    help="run the N>1 sharded path (shards, plans, halo exchange, per-rank split) even at "
+                         "one rank -- under torch.distributed.run --nproc-per-node 1 it rehearses the "
+                         "driver's multi-GPU code path on the RCCL backend with empty halos")
     ap.add_argument("--halo-tile", type=int, default=128,
                     help="N>1: exchange and finish the boundary edges per feature tile of this width "
                          "(pipelined); 0 = one exchange of whole rows")
     return ap.parse_args()
 
 
-def setup_dist(n):
-    if n <= 1 or "RANK" not in os.environ:
+def setup_dist(n, sharded=False):
+    if (n <= 1 and not sharded) or "RANK" not in os.environ:
         return 0, 1, 0
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
@@ -240,9 +244,10 @@ def device_reference_paths(ei, norm, x, csr, w_csr, bias, fused_out, terms, reps
 
 def main():
     args = parse()
-    rank, world, local = setup_dist(args.gpus)
+    rank, world, local = setup_dist(args.gpus, args.sharded)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    sharded = world > 1 or (args.sharded and dist.is_initialized())
     import mi355_mp
     from mi355_mp import _lib, ops
     from mi355_mp.graph import Graph
@@ -253,7 +258,7 @@ def main():
     N = 1 << SCALE
     t0 = time.perf_counter()
     ei = rmat_edge_index(scale=SCALE, n_samples=SAMPLES, seed=1, device=dev)
-    if world > 1:
+    if sharded:
         # each rank keeps only its contiguous 1/world slice of the edge list (the
         # generator, deterministic on every rank, stands in for reading the rank's
         # shard of an edge file): loops, norm, cuts and plans are built from the
@@ -269,7 +274,7 @@ def main():
     t0 = time.perf_counter()
     bias = torch.randn(F_DIM, device=dev, generator=torch.Generator(device=dev).manual_seed(7)) * 0.1
     g = torch.Generator(device=dev).manual_seed(1)
-    if world == 1:
+    if not sharded:
         ei2, norm = GCNConv.norm(ei, N)
         E2 = ei2.shape[1]
         graph = Graph(ei2, N, N, chunk=args.chunk or None)
@@ -332,7 +337,7 @@ def main():
     ev = None
 
     def step(i=None):
-        if world == 1:
+        if not sharded:
             if i is None or ev is None:
                 aggregate(x, out=out_buf)
             else:
@@ -351,7 +356,7 @@ def main():
     step_events = [dict() for _ in range(args.steps)]
     for _ in range(args.warmup):
         step()
-    if world == 1:
+    if not sharded:
         ev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.steps)]
     torch.cuda.synchronize()
     barrier(world)
@@ -363,7 +368,7 @@ def main():
     barrier(world)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    if world > 1:
+    if sharded:
         tt = torch.tensor([dt], dtype=torch.float64)
         tt = tt.to(dev) if dist.get_backend() == "nccl" else tt
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -374,7 +379,7 @@ def main():
     # dominant kernel (main aggregation launch) timed with HIP events on the
     # stream it runs on (torch's current stream): `reps` back-to-back launches
     # between two events (host launch latency amortised), averaged
-    x_src = x if world == 1 else plan.exchange_into(x_local, ops.gather_rows)
+    x_src = x if not sharded else plan.exchange_into(x_local, ops.gather_rows)
     reps = max(args.steps, 10)
 
     def timed(stages, rounds=3):
@@ -389,7 +394,7 @@ def main():
             per.append(a.elapsed_time(b) / reps)
         return sorted(per)
 
-    if world == 1:
+    if not sharded:
         main_ms = sorted(a.elapsed_time(b) for a, b, _ in ev)
         fix_ms = sorted(b.elapsed_time(c) for _, b, c in ev)
         timing_src = "HIP events around each main / fix-up launch inside the timed steps"
@@ -430,7 +435,7 @@ def main():
     # summary names the same kernel and the same native source hash
     traffic, traffic_src = None, "no profile for this build"
     src_hash = lib.mp_source_hash().decode()   # the LOADED library's build (load() checks it against the tree)
-    if os.path.exists(PMC_FILE) and world == 1:
+    if os.path.exists(PMC_FILE) and not sharded:
         try:
             with open(PMC_FILE) as f:
                 pmc = json.load(f)
@@ -446,7 +451,7 @@ def main():
     # the reference's own device path and a vendor SpMM on the same GPU, same
     # CSR / weights (outside the timed region; checked against the fused output)
     ref_paths = None
-    if world == 1 and not args.no_ref_paths:
+    if not sharded and not args.no_ref_paths:
         aggregate(x, out=out_buf)
         fused_out = out_buf.clone()
         terms = ops._aggregate(csr, "other", x.abs(), w_csr.abs(), "sum", 0, None)[0]
@@ -460,7 +465,7 @@ def main():
     # tile's work.wait() (exchange time the compute stream is exposed to) and
     # around each boundary pass; gathered to rank 0
     ranks = None
-    if world > 1:
+    if sharded:
         def span(evs, k):
             lst = evs.get(k, [])
             return sum(lst[j].elapsed_time(lst[j + 1]) for j in range(0, len(lst) - 1, 2))
@@ -489,7 +494,7 @@ def main():
         dist.all_gather_object(ranks, mine)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not sharded and not args.no_cpu_baseline:
         cpu = cpu_baseline(ei2, norm, x, args.cpu_sample_edges)
 
     if rank == 0:
@@ -509,7 +514,7 @@ def main():
             "config": {"workload": "rmat21_gcn_f256", "graph": "RMAT scale 21 (.57,.19,.19,.05) "
                        "30M samples symmetrised + add_remaining_self_loops", "num_nodes": N,
                        "num_edges": E2, "features": F_DIM, "seed": 1,
-                       "parallelism": "dst-range shards x%d, RCCL halo all_to_all" % world if world > 1
+                       "parallelism": "dst-range shards x%d, RCCL halo all_to_all" % world if sharded
                        else "single GPU", "chunk": csr.chunk},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -528,11 +533,11 @@ def main():
                       "one_time_build_s": t_build, "graph_gen_s": t_gen,
                       "edges_local_rank0": E_local, "n_split_rows": csr.n_split,
                       "halo_rows_rank0": ((plan.n_local_src if args.no_overlap else overlap.n_local_src)
-                                          - plan.n_own) if world > 1 else 0,
-                      "halo_cover": world > 1 and not args.no_overlap and not args.no_halo_cover,
-                      "interior_edges_rank0": overlap.n_interior if world > 1 else E_local,
-                      "overlap": world > 1 and not args.no_overlap,
-                      "halo_tile": args.halo_tile if world > 1 and not args.no_overlap else None,
+                                          - plan.n_own) if sharded else 0,
+                      "halo_cover": sharded and not args.no_overlap and not args.no_halo_cover,
+                      "interior_edges_rank0": overlap.n_interior if sharded else E_local,
+                      "overlap": sharded and not args.no_overlap,
+                      "halo_tile": args.halo_tile if sharded and not args.no_overlap else None,
                       "n_wave_tasks": csr.n_waves,
                       "per_rank": ranks,
                       "gpu_reference_path_ms": ((ref_paths or {}).get("reference_path") or {}).get("ms"),
@@ -541,7 +546,7 @@ def main():
                       "agg_only_GBps_incl_fixup": alg_bytes / ((main_avg + fix_avg) * 1e-3) / 1e9},
         }
         print(json.dumps(line))
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -455,6 +455,40 @@ def test_bench_multi_rank_path_end_to_end():
         assert p["interior_ms"] > 0 and p["boundary_ms"] > 0 and p["exchange_exposed_ms"] >= 0
 
 
+def test_bench_sharded_path_over_rccl_one_rank():
+    """bench.py's N > 1 code path on the RCCL backend -- the one the driver's
+    8-GPU run takes -- as ONE rank (two ranks cannot share a device under
+    RCCL): `--sharded` routes the one-rank job through the slice-built shards,
+    the collective plan / halo-cover build, the tiled overlapped step with its
+    (empty) all_to_all_single per tile, the max-over-ranks all_reduce and the
+    per-rank all_gather_object; the rate must match the single-GPU kernel's
+    order of magnitude and every edge must be interior."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.pop("MP_BENCH_BACKEND", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "1",
+           "--sharded", "--steps", "3", "--warmup", "1"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["config"]["num_edges"] == 62_094_512 and d["cpu_baseline"] is None
+    assert d["config"]["parallelism"].startswith("dst-range shards x1")
+    ex = d["extra"]
+    assert ex["overlap"] and ex["halo_cover"] and ex["halo_tile"] == 128 and ex["halo_rows_rank0"] == 0
+    assert ex["interior_edges_rank0"] == ex["edges_local_rank0"] == d["config"]["num_edges"]
+    (p,) = ex["per_rank"]
+    assert p["rank"] == 0 and p["halo_bytes_in"] == 0 and p["peers_in"] == [0]
+    assert p["interior_ms"] > 0 and p["exchange_exposed_ms"] >= 0
+    # the same kernels over the whole graph: within 2x of the single-GPU step
+    assert d["value"] > 4e9, d["value"]
+
+
 def _cover_worker(rank, world, port, q):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
