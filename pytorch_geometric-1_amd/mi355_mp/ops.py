@@ -372,11 +372,28 @@ class GatherRows(torch.autograd.Function):
         return gx, None
 
 
+def check_row_index(idx, n, what="index_select"):
+    """IndexError when an index falls outside [0, n), as x.index_select(0, idx)
+    raises on the CPU (the native row gather reads whatever row it is given, so
+    a bad index must never reach it).  One aminmax and one host read; skipped
+    while a HIP graph is being captured (the captured call was checked when it
+    ran eagerly before capture, and a capture cannot read values back)."""
+    if idx.numel() == 0 or (idx.is_cuda and torch.cuda.is_current_stream_capturing()):
+        return
+    mn, mx = torch.aminmax(idx)
+    lo, hi = torch.stack([mn, mx]).tolist()
+    if lo < 0 or hi >= n:
+        raise IndexError("%s: index %d out of range for %d rows" % (what, lo if lo < 0 else hi, n))
+
+
 def index_select_rows(x, idx):
     """Differentiable native replacement of x.index_select(0, idx) for 2-D x
-    (fp32 / fp64 / fp16 / bf16 / int64)."""
+    (fp32 / fp64 / fp16 / bf16 / int64); an index outside [0, x.size(0))
+    raises IndexError (check_row_index)."""
     _lib.require_device(x, idx)
-    return GatherRows.apply(_any_2d(x, "x"), idx)
+    x = _any_2d(x, "x")
+    check_row_index(idx, x.shape[0])
+    return GatherRows.apply(x, idx)
 
 
 # ---------------------------------------------------------------------------

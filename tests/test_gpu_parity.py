@@ -2314,6 +2314,48 @@ def test_self_loop_out_of_range_raises_without_writing():
     torch.cuda.synchronize()
 
 
+def test_row_gather_out_of_range_raises():
+    """The native row gather behind the generic propagate path, utils.softmax and
+    torch_scatter.gather_coo / gather_csr: an index outside [0, N) raises
+    IndexError before any launch (x.index_select does on the CPU; the kernel
+    would read whatever row it is given), for every dtype; in-range calls are
+    still x.index_select bit for bit."""
+    import torch_scatter
+    from mi355_mp import ops
+    from torch_geometric.nn import MessagePassing
+
+    class Diff(MessagePassing):
+        def __init__(self):
+            super().__init__(aggr="add")
+
+        def forward(self, x, edge_index):
+            return self.propagate(edge_index, x=x)
+
+        def message(self, x_i, x_j):
+            return x_i - x_j
+
+    N = 10
+    for dtype in (torch.float32, torch.float64, torch.float16, torch.int64):
+        x = (torch.arange(N * 3, device=DEV).view(N, 3) % 7).to(dtype)
+        ok = torch.tensor([0, 9, 3, 3], device=DEV)
+        assert torch.equal(ops.index_select_rows(x, ok), x.index_select(0, ok))
+        for bad in (N, N + 7, -1):
+            idx = torch.tensor([0, bad, 3], device=DEV)
+            with pytest.raises(IndexError):
+                ops.index_select_rows(x, idx)
+            with pytest.raises(IndexError):
+                torch_scatter.gather_coo(x, idx)
+    for bad in (N, -1):
+        ei = torch.tensor([[0, 1, bad], [1, 2, 3]], device=DEV)
+        with pytest.raises(IndexError):
+            Diff()(torch.randn(N, 4, device=DEV), ei)
+    ei = torch.tensor([[0, 1, 9], [1, 2, 3]], device=DEV)
+    x = torch.randn(N, 4, device=DEV)
+    ref = torch.zeros(N, 4, device=DEV).index_add_(0, ei[1], x[ei[1]] - x[ei[0]])
+    assert torch.equal(Diff()(x, ei), ref)
+    torch.cuda.synchronize()
+
+
 # --------------------------------------------------------------------------
 # round 3: the torch_scatter replacement for float64 / float16 / bfloat16 / int64
 # --------------------------------------------------------------------------
