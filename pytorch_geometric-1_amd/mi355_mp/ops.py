@@ -521,6 +521,9 @@ def gcn_norm_weights(edge_index, num_nodes, edge_weight=None, integer_weights=Fa
     lib = _lib.load()
     E = edge_index.shape[1]
     N = int(num_nodes)
+    # the degree kernel adds at deg[row[e]]: a node id outside [0, N) raises
+    # here, as the reference's scatter_add(edge_weight, row, dim_size=N) does
+    check_row_index(edge_index, N, "gcn_norm")
     dev = edge_index.device
     st = _lib.stream_ptr(dev)
     row = edge_index[0].contiguous()

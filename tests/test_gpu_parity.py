@@ -2353,6 +2353,14 @@ def test_row_gather_out_of_range_raises():
     x = torch.randn(N, 4, device=DEV)
     ref = torch.zeros(N, 4, device=DEV).index_add_(0, ei[1], x[ei[1]] - x[ei[0]])
     assert torch.equal(Diff()(x, ei), ref)
+    # GCNConv's degree (deg[row[e]] += w) with a non-loop edge leaving [0, N):
+    # IndexError, as the reference's scatter_add(.., dim_size=N); no device write
+    from torch_geometric.nn import GCNConv
+    for bad_ei in ([[0, 1, N], [1, 2, 3]], [[0, 1, 2], [1, 2, N + 3]], [[0, -1], [1, 2]]):
+        ei = torch.tensor(bad_ei, device=DEV)
+        for w in (None, torch.rand(ei.shape[1], device=DEV)):
+            with pytest.raises(IndexError):
+                GCNConv(4, 4).to(DEV)(x, ei, w)
     torch.cuda.synchronize()
 
 
