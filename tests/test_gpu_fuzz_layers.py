@@ -17,7 +17,7 @@ import os
 
 import pytest
 import torch
-from hypothesis import HealthCheck, given, settings, strategies as st
+from hypothesis import HealthCheck, example, given, settings, strategies as st
 
 from oracle import pyg_ref as P
 
@@ -369,6 +369,7 @@ def test_fuzz_loop_utilities(N, deg, loops, attr, fill, extra, seed):
 @given(N=st.integers(1, 150), E=st.integers(0, 3000), shape=st.sampled_from([(), (1,), (5,), (3, 4), (64,)]),
        name=st.sampled_from(["add", "mean", "max", "min"]), extra=st.integers(0, 3), hub=st.booleans(),
        seed=st.integers(0, 1 << 16))
+@example(N=1, E=3000, shape=(64,), name="add", extra=0, hub=False, seed=1)
 def test_fuzz_scatter_softmax_pool_utilities(N, E, shape, name, extra, hub, seed):
     """utils.scatter_ (every name, 1-3-D src, dim_size past the largest index;
     max / min with the +-10000 masks bit-exact on integer data, sum / mean within
@@ -400,8 +401,15 @@ def test_fuzz_scatter_softmax_pool_utilities(N, E, shape, name, extra, hub, seed
     sc = torch.randn((E,) + shape[:1], generator=g) * 4
     sm = softmax(sc.to(DEV), idx.to(DEV), n)
     ref = P.softmax(sc, idx, n)
+    ref64 = P.softmax(sc.double(), idx, n)
     assert sm.shape == ref.shape
-    assert bool(((sm.cpu() - ref).abs() <= 1e-5).all())
+    # within 1e-5 of the exact softmax, and of the fp32 reference up to that
+    # reference's own rounding: its edge-order fp32 denominator over a
+    # 3000-slot segment is itself 1.07e-5 off the exact alpha (N=1, E=3000,
+    # 64 heads, seed 1 -- found by a 3000-example soak, pinned by the @example above)
+    own = (ref.double() - ref64).abs()
+    assert bool(((sm.cpu().double() - ref64).abs() <= 1e-5).all())
+    assert bool(((sm.cpu() - ref).abs().double() <= 1e-5 + own).all())
     # global pooling: a sorted batch vector over the rows of src
     if E and len(shape) == 1:
         batch = torch.sort(idx).values
