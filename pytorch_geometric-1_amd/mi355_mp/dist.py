@@ -627,11 +627,15 @@ class OverlappedAggregation:
         else:
             work = dist.all_to_all_single(halo, send, output_split_sizes=self.recv_counts,
                                           input_split_sizes=self.send_counts, group=group, async_op=True)
-        ops._aggregate(self.g_int.dst, "other", own, self.w_int, "sum", 0, None, out=out)
+        # no boundary edge (one rank, or rows fed only by local sources): the
+        # interior pass is the whole row and adds the bias itself
+        last = self.n_boundary == 0
+        ops._aggregate(self.g_int.dst, "other", own, self.w_int, "sum", 0, bias if last else None, out=out)
         if work is not None:
             work.wait()
-        ops._aggregate(self.g_bnd.dst, "other", x_local, self.w_bnd, "sum", _lib.MP_FLAG_INIT_FROM_OUT, bias,
-                       out=out)
+        if not last:
+            ops._aggregate(self.g_bnd.dst, "other", x_local, self.w_bnd, "sum", _lib.MP_FLAG_INIT_FROM_OUT, bias,
+                           out=out)
         return out
 
     def step_tiled(self, x_tiles, out, bias=None, group=None, events=None):
@@ -683,8 +687,10 @@ class OverlappedAggregation:
                 pending.append((work, send))
         rec("send")
         rec("interior")
+        last = self.n_boundary == 0   # the interior pass is the whole row (see step)
         for t, xt in enumerate(x_tiles):
-            ops._aggregate(self.g_int.dst, "other", xt[:plan.n_own], self.w_int, "sum", 0, None,
+            b = bias[offs[t]:offs[t + 1]] if (last and bias is not None) else None
+            ops._aggregate(self.g_int.dst, "other", xt[:plan.n_own], self.w_int, "sum", 0, b,
                            out=out[:, offs[t]:offs[t + 1]])
         rec("interior")
         for t, xt in enumerate(x_tiles):
@@ -694,9 +700,10 @@ class OverlappedAggregation:
                 work.wait()
             rec("wait")
             rec("boundary")
-            b = bias[offs[t]:offs[t + 1]] if bias is not None else None
-            ops._aggregate(self.g_bnd.dst, "other", xt, self.w_bnd, "sum", _lib.MP_FLAG_INIT_FROM_OUT, b,
-                           out=out[:, offs[t]:offs[t + 1]])
+            if not last:
+                b = bias[offs[t]:offs[t + 1]] if bias is not None else None
+                ops._aggregate(self.g_bnd.dst, "other", xt, self.w_bnd, "sum", _lib.MP_FLAG_INIT_FROM_OUT, b,
+                               out=out[:, offs[t]:offs[t + 1]])
             rec("boundary")
         return out
 
