@@ -430,6 +430,7 @@ def test_fuzz_scatter_softmax_pool_utilities(N, E, shape, name, extra, hub, seed
        layer=st.sampled_from(["sage", "sage_concat", "graph_add", "graph_mean", "graph_max"]),
        normalize=st.booleans(), bias=st.booleans(), weighted=st.booleans(), loops=st.sampled_from([0.0, 0.2]),
        seed=st.integers(0, 1 << 16))
+@example(N=32, deg=1.0, Fi=1, Fo=7, layer="sage", normalize=True, bias=False, weighted=False, loops=0.0, seed=238)
 def test_fuzz_sage_graph_conv_layers(N, deg, Fi, Fo, layer, normalize, bias, weighted, loops, seed):
     """SAGEConv(normalize, concat, bias) and GraphConv(aggr) with and without edge
     weights, against float64 autograd of the 1.4.3 formulas: SAGE's
@@ -499,7 +500,14 @@ def test_fuzz_sage_graph_conv_layers(N, deg, Fi, Fo, layer, normalize, bias, wei
     pairs = [(xd.grad, x64.grad, "x")] + [(dict(conv.named_parameters())[k].grad, v.grad, k) for k, v in params.items()]
     if weighted:
         pairs.append((wd.grad, w64.grad, "w"))
+    # SAGE(normalize, mean, one input feature, no bias): the output is
+    # sign(mean x_j) W / |W|, so the exact d x is 0 and the fp32 one is the
+    # roundoff of torch's F.normalize backward / |v| (the same ill-conditioning as
+    # Fo == 1 above; found by a 6000-example soak: N=32, Fi=1, Fo=7, seed 238)
+    degenerate_x = normalize and layer == "sage" and Fi == 1 and not bias
     for got, want, what in pairs:
+        if what == "x" and degenerate_x:
+            continue
         err = (got.cpu().double() - want).abs()
         assert bool((err <= 1e-4 * want.abs().clamp(min=1.0)).all()), "%s: %g" % (what, float(err.max()))
 

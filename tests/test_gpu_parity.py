@@ -2144,7 +2144,7 @@ def test_gin_conv_forward_backward(train_eps):
         assert torch.allclose(conv.eps.grad.cpu().double(), eps64.grad, rtol=1e-4, atol=1e-4)
 
 
-from hypothesis import HealthCheck, given, settings, strategies as st  # noqa: E402
+from hypothesis import HealthCheck, example, given, settings, strategies as st  # noqa: E402
 
 # example counts: the suite's defaults, raised for a long soak by MP_FUZZ_EXAMPLES /
 # MP_FUZZ_GAT_EXAMPLES (a progress line every 100 examples keeps a long run visibly alive)
@@ -2525,6 +2525,7 @@ def test_gat_node_scores_in_kernel_bitwise(H, C, chunk, monkeypatch):
 @given(N=st.integers(1, 300), deg=st.floats(0.0, 30.0), H=st.sampled_from([1, 2, 3, 4, 8]),
        C=st.sampled_from([4, 8, 16, 32, 64]), p=st.sampled_from([0.0, 0.1, 0.5, 0.9]),
        chunk=st.sampled_from([16, 64, 256]), star=st.booleans(), seed=st.integers(0, 1 << 16))
+@example(N=121, deg=23.8203125, H=4, C=64, p=0.9, chunk=16, star=False, seed=121)
 def test_fuzz_gat_training_with_attention_dropout(N, deg, H, C, p, chunk, star, seed):
     """Shape fuzzing of the fused GAT training forward + transposed backward,
     with and without attention dropout: output and the gradients of xw, att and
@@ -2557,8 +2558,23 @@ def test_fuzz_gat_training_with_attention_dropout(N, deg, H, C, p, chunk, star, 
     want = P.gat_conv(x64, ei_l, torch.eye(H * C, dtype=torch.float64), a64, b64, H, C, drop_keep=keep, drop_p=p)
     assert torch.allclose(out.detach().cpu().double(), want.detach(), rtol=1e-5, atol=1e-5)
     want.backward(gout.double())
-    for got, ref in ((xd.grad, x64.grad), (ad.grad, a64.grad), (bd.grad, b64.grad)):
-        assert torch.allclose(got.cpu().double(), ref, rtol=1e-4, atol=1e-4)
+    # the same formula in fp32 (the reference's own precision): d att sums every
+    # edge's term (x 1/(1-p) = 10 at p = 0.9) with cancellation, so one of its
+    # entries can sit ~1e-4 from float64 in the fp32 reference itself (N=121,
+    # H=4, C=64, p=0.9, seed 121: fp32 reference 1.24e-4 off at |d att| = 0.23 of
+    # max 199; found by a 2500-example soak); each gradient is held to
+    # 1e-4 * max(1, |ref|) plus twice that tensor's fp32-reference error
+    x32 = xw.clone().requires_grad_(True)
+    a32 = att.clone().requires_grad_(True)
+    b32 = bias.clone().requires_grad_(True)
+    w32 = P.gat_conv(x32, ei_l, torch.eye(H * C), a32, b32, H, C, drop_keep=keep, drop_p=p)
+    w32.backward(gout)
+    for got, ref, r32, what in ((xd.grad, x64.grad, x32.grad, "d xw"), (ad.grad, a64.grad, a32.grad, "d att"),
+                                (bd.grad, b64.grad, b32.grad, "d bias")):
+        own = float((r32.double() - ref).abs().max())
+        err = (got.cpu().double() - ref).abs()
+        assert bool((err <= 1e-4 * ref.abs().clamp(min=1.0) + 2 * own).all()), \
+            "%s: err %g, fp32 reference err %g" % (what, float(err.max()), own)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
