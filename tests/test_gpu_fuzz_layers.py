@@ -431,6 +431,7 @@ def test_fuzz_scatter_softmax_pool_utilities(N, E, shape, name, extra, hub, seed
        normalize=st.booleans(), bias=st.booleans(), weighted=st.booleans(), loops=st.sampled_from([0.0, 0.2]),
        seed=st.integers(0, 1 << 16))
 @example(N=32, deg=1.0, Fi=1, Fo=7, layer="sage", normalize=True, bias=False, weighted=False, loops=0.0, seed=238)
+@example(N=90, deg=3.953125, Fi=1, Fo=64, layer="sage", normalize=True, bias=False, weighted=True, loops=0.0, seed=25)
 def test_fuzz_sage_graph_conv_layers(N, deg, Fi, Fo, layer, normalize, bias, weighted, loops, seed):
     """SAGEConv(normalize, concat, bias) and GraphConv(aggr) with and without edge
     weights, against float64 autograd of the 1.4.3 formulas: SAGE's
@@ -504,9 +505,10 @@ def test_fuzz_sage_graph_conv_layers(N, deg, Fi, Fo, layer, normalize, bias, wei
     # sign(mean x_j) W / |W|, so the exact d x is 0 and the fp32 one is the
     # roundoff of torch's F.normalize backward / |v| (the same ill-conditioning as
     # Fo == 1 above; found by a 6000-example soak: N=32, Fi=1, Fo=7, seed 238)
+    # (d edge_weight likewise: N=90, Fi=1, Fo=64, weighted, seed 25, 12000-example soak)
     degenerate_x = normalize and layer == "sage" and Fi == 1 and not bias
     for got, want, what in pairs:
-        if what == "x" and degenerate_x:
+        if what in ("x", "w") and degenerate_x:
             continue
         err = (got.cpu().double() - want).abs()
         assert bool((err <= 1e-4 * want.abs().clamp(min=1.0)).all()), "%s: %g" % (what, float(err.max()))
@@ -517,6 +519,7 @@ def test_fuzz_sage_graph_conv_layers(N, deg, Fi, Fo, layer, normalize, bias, wei
        layer=st.sampled_from(["cheb", "agnn", "sg", "gin"]), K=st.integers(1, 3),
        norm=st.sampled_from(["sym", "rw", None]), weighted=st.booleans(), bias=st.booleans(),
        loops=st.sampled_from([0.0, 0.2]), seed=st.integers(0, 1 << 16))
+@example(N=141, deg=4.125, Fi=1, Fo=1, layer="agnn", K=1, norm="sym", weighted=False, bias=False, loops=0.2, seed=141)
 def test_fuzz_cheb_agnn_sg_gin_layers(N, deg, Fi, Fo, layer, K, norm, weighted, bias, loops, seed):
     """The reference's other propagate callers at the layer API: ChebConv(K,
     sym / rw / None, lambda_max, edge weights), AGNNConv(beta), SGConv(K,
@@ -589,6 +592,12 @@ def test_fuzz_cheb_agnn_sg_gin_layers(N, deg, Fi, Fo, layer, K, norm, weighted, 
         return   # gradients of the unnormalised recursion carry the same cancellation; values are the check
     named = dict(conv.named_parameters())
     pairs = [(xd.grad, x64.grad, "x")] + [(named[k].grad, v.grad, k) for k, v in params.items()]
+    # AGNN with one input feature: its attention reads F.normalize(x) = sign(x),
+    # whose exact gradient is 0 and whose fp32 backward is roundoff / |x_j| --
+    # torch's own normalize, ill-conditioned on small |x_j| (12000-example soak:
+    # N=141, Fi=1, seed 141); the values above still hold to 1e-5
+    if layer == "agnn" and Fi == 1:
+        pairs = pairs[1:]
     for got, want, what in pairs:
         got = got if got is not None else torch.zeros_like(want)
         want = want if want is not None else torch.zeros_like(want)
