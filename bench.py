@@ -1,32 +1,49 @@
-"""Benchmark: GCNConv F=256 aggregation on the BASELINE config-2 graph.
+"""Benchmark: GCNConv F=256 aggregation (PyG 1.4.3 propagate, fused on MI355X).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload rmat21|products]
     torchrun --nproc-per-node N bench.py --gpus N ...     (driver, N > 1)
 
-Workload (BASELINE.json configs[1]): RMAT scale 21 (N = 2,097,152),
-(a,b,c,d) = (.57,.19,.19,.05), 30M samples symmetrised (E = 60M), GCN
-add_remaining_self_loops (E' ~ 62M), x ~ N(0,1) [N, 256] fp32, seed 1.
-One step = one GCNConv propagate: the fused gather * norm -> segment-sum
-+ bias HIP kernel (plus its split-row fix-up) over all E' edges.  The CSR /
-schedule / norm build (one-time, cached=True semantics) and the x @ W GEMM
-are timed separately and reported beside the metric.
+--gpus N > 1 without a launcher (RANK unset): bench.py starts the N rank
+processes itself -- a `python -m torch.distributed.run` child, started before
+this process touches the GPU, whose exit code it returns -- the way the
+reference's own multi-GPU entry takes --gpus directly
+(/root/reference/ConvexPruning.py:613).  Every rank checks that the job has
+exactly N ranks and exits non-zero otherwise; the process group has an
+explicit collective timeout, and each rank logs its stages to stderr.
 
-N > 1: the same graph is sharded by destination range (edge balanced), built
-from per-rank slices of the edge list (ShardedGraph.for_gcn_from_slices: no
-rank holds the whole list); a step is the halo all_to_all (RCCL) overlapped
-with the interior edges, then the boundary edges, on every rank.  The
-exchange is the hybrid cover (dist.HaloCover: a remote source row is pulled, or
-its owner pushes a partial row of the destination, whichever covers the cross
-edges with fewer rows; 0.57x the pull rows on this graph); --no-halo-cover
-pulls every remote source.  value = E' /
-max-over-ranks step time (strong scaling).  extra.per_rank carries each rank's
-halo bytes and the interior / exposed-exchange / boundary split of its steps.
+Workloads (one GCNConv propagate per step, F = 256, fp32):
+  rmat21   (default; BASELINE.json configs[1]) RMAT scale 21 (N = 2,097,152),
+           (a,b,c,d) = (.57,.19,.19,.05), 30M samples symmetrised (E = 60M),
+           add_remaining_self_loops (E' = 62,094,512), x ~ N(0,1), seed 1.
+  products (BASELINE.json configs[4], the 8 x MI355X configuration)
+           ogbn-products scale power-law graph, N = 2,449,029,
+           E = 123,718,280 (E' = 126,163,923), x ~ N(0,1), seed 4.
+One step = the fused gather * norm -> segment-sum + bias HIP kernel (plus its
+split-row fix-up) over all E' edges.  The CSR / schedule / norm build
+(one-time, cached=True semantics) and the x @ W GEMM are timed separately and
+reported beside the metric.
+
+N > 1: the graph is sharded by destination range (edge balanced), built from
+per-rank slices of the edge list (ShardedGraph.for_gcn_from_slices: no rank
+holds the whole list); a step is the halo all_to_all (RCCL) overlapped with
+the interior edges, then the boundary edges, on every rank.  The exchange is
+the hybrid cover (dist.HaloCover: a remote source row is pulled, or its owner
+pushes a partial row of the destination, whichever covers the cross edges
+with fewer rows); --no-halo-cover pulls every remote source.  value = E' /
+max-over-ranks step time (strong scaling).  extra.per_rank carries each
+rank's halo bytes, the interior / exposed-exchange / boundary split of its
+timed steps, and the same step taken apart after the timed region: the
+exchange alone, the compute alone and the exchange-then-compute step.
 
 Prints ONE JSON line on rank 0.
 """
 import argparse
+import datetime
+import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -35,12 +52,10 @@ for _p in (ROOT, os.path.join(ROOT, "pytorch_geometric-1_amd")):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
-import torch  # noqa: E402
+import torch  # noqa: E402  (importing torch does not initialise the GPU)
 import torch.distributed as dist  # noqa: E402
 
 F_DIM = 256
-SCALE = 21
-SAMPLES = 30_000_000
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md chip table)
 # SURVEY 8(d) / BASELINE.md section 2 algorithmic bytes: every gathered x_j row
 # counted at full size, no cache-reuse credit.  Reported, but its ratio to the
@@ -48,17 +63,43 @@ HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md chip table)
 # Cache, so it can exceed 1).
 BYTES_PER_EDGE = 4 * F_DIM + 4 + 4   # x_j row + col + norm
 BYTES_PER_NODE = 4 * F_DIM + 4       # out row + rowptr
-PMC_FILE = os.path.join(ROOT, "profiles", "r03_pmc_traffic.json")
+COLLECTIVE_TIMEOUT_S = 300
+T_START = time.perf_counter()
 
 
-def parse():
+def _rmat21(dev):
+    from mi355_mp.graphgen import rmat_edge_index
+    return rmat_edge_index(scale=21, n_samples=30_000_000, seed=1, device=dev)
+
+
+def _products(dev):
+    from mi355_mp.graphgen import powerlaw_edge_index
+    return powerlaw_edge_index(2_449_029, 123_718_280, seed=4, device=dev)
+
+
+WORKLOADS = {
+    "rmat21": {"name": "rmat21_gcn_f256", "num_nodes": 1 << 21, "seed": 1, "gen": _rmat21,
+               "baseline_config": 2,
+               "graph": "RMAT scale 21 (.57,.19,.19,.05) 30M samples symmetrised + add_remaining_self_loops"},
+    "products": {"name": "products_gcn_f256", "num_nodes": 2_449_029, "seed": 4, "gen": _products,
+                 "baseline_config": 5,
+                 "graph": "ogbn-products-scale power-law (RMAT into [0, N)), 123,718,280 directed edges "
+                          "+ add_remaining_self_loops"},
+}
+
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="rmat21")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ref-paths", action="store_true",
                     help="skip timing the reference's ATen device path and the vendor SpMM")
+    ap.add_argument("--verify", action="store_true",
+                    help="after the timed region, hold every output row to |out - ref| <= 1e-5 * max(1, "
+                         "sum|w x_j|) against a float64 reference over the rank's own edges")
     ap.add_argument("--cpu-sample-edges", type=int, default=48_000_000)
     ap.add_argument("--chunk", type=int, default=0, help="merge-path task size (0: auto_chunk)")
     ap.add_argument("--no-overlap", action="store_true", help="N>1: exchange, then aggregate (no overlap)")
@@ -72,30 +113,88 @@ def parse():
     ap.add_argument("--halo-tile", type=int, default=128,
                     help="N>1: exchange and finish the boundary edges per feature tile of this width "
                          "(pipelined); 0 = one exchange of whole rows")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-def setup_dist(n, sharded=False):
-    if (n <= 1 and not sharded) or "RANK" not in os.environ:
+def stage(rank, msg):
+    """One progress line per stage on stderr (the JSON line stays alone on stdout)."""
+    print("[bench rank %s +%.1fs] %s" % (rank, time.perf_counter() - T_START, msg), file=sys.stderr, flush=True)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args, argv):
+    """--gpus N > 1 and no launcher: run N ranks under a torch.distributed.run
+    CHILD process (this process has not touched the GPU, and is not replaced:
+    it waits and returns the child's exit code; a failing rank makes
+    torch.distributed.run stop the others and exit non-zero)."""
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    stage("-", "no launcher for --gpus %d: starting %d ranks (torch.distributed.run, port %d)"
+          % (args.gpus, args.gpus, port))
+    return subprocess.call(cmd, env=env, cwd=ROOT)
+
+
+def setup_dist(args):
+    """(rank, world, local device index).  Single process unless launched as
+    ranks (RANK set) -- then the job must have exactly --gpus ranks."""
+    if "RANK" not in os.environ:
+        if args.sharded:
+            raise SystemExit("bench.py --sharded needs a launcher (torch.distributed.run)")
         return 0, 1, 0
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", rank))
+    if world != args.gpus:
+        stage(rank, "ERROR: the job has %d ranks but --gpus %d" % (world, args.gpus))
+        raise SystemExit(3)
+    timeout = datetime.timedelta(seconds=COLLECTIVE_TIMEOUT_S)
+    if os.environ.get("MP_BENCH_LAUNCH_PROBE"):
+        # CPU test of the launch path (tests/test_host.py): the ranks meet over
+        # gloo without touching a GPU, report themselves and stop
+        dist.init_process_group("gloo", timeout=timeout)
+        ok = dist.get_world_size() == args.gpus
+        got = [None] * dist.get_world_size()
+        dist.all_gather_object(got, {"rank": rank, "local_rank": local, "world": dist.get_world_size()})
+        stage(rank, "launch probe: %s" % got[rank])
+        if rank == 0:
+            print(json.dumps({"launch_probe": got, "gpus": args.gpus}), flush=True)
+        dist.destroy_process_group()
+        raise SystemExit(0 if ok else 3)
+    if world == 1 and not args.sharded:
+        return 0, 1, local
     backend = os.environ.get("MP_BENCH_BACKEND", "nccl")
     if backend == "gloo":
         # rehearsal of the multi-GPU path on a box with fewer GPUs than ranks:
         # ranks share devices, halo rows are staged through the host
         local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("gloo")
+        dist.init_process_group("gloo", timeout=timeout)
     else:
+        n_dev = torch.cuda.device_count()
+        if local >= n_dev:
+            stage(rank, "ERROR: local rank %d but only %d visible GPUs (RCCL ranks cannot share a device)"
+                  % (local, n_dev))
+            raise SystemExit(3)
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=timeout)
+    if dist.get_world_size() != args.gpus:
+        stage(rank, "ERROR: process group has %d ranks, --gpus %d" % (dist.get_world_size(), args.gpus))
+        raise SystemExit(3)
+    stage(rank, "process group up: backend %s, world %d, device cuda:%d" % (dist.get_backend(), world, local))
     return rank, world, local
 
 
 def barrier(world):
-    if world > 1:
+    if world > 1 or dist.is_initialized():
         dist.barrier()
 
 
@@ -128,7 +227,7 @@ def cpu_baseline(ei_loops, norm, x, sample_edges):
     """The reference algorithm on the host (oracle, kind 'port'): index_select
     -> norm * x_j -> scatter_add_ (torch_scatter scatter_sum), timed on a
     bounded sample of the same edges in their original order, in 4M-edge
-    chunks (the materialised x_j of all 62M edges is 64 GB)."""
+    chunks (the materialised x_j of all edges is 64-130 GB)."""
     from oracle import pyg_ref  # noqa: F401  (checker/baseline only)
     model, threads, machine = cpu_info()
     torch.set_num_threads(threads)
@@ -136,7 +235,6 @@ def cpu_baseline(ei_loops, norm, x, sample_edges):
     ei = ei_loops[:, :E].cpu()
     w = norm[:E].cpu()
     xc = x.cpu()
-    N = xc.shape[0]
     out = torch.zeros_like(xc)
     chunk = 4_000_000
     t0 = time.perf_counter()
@@ -151,7 +249,7 @@ def cpu_baseline(ei_loops, norm, x, sample_edges):
             "cpu_model": model, "machine_cpus": machine,
             "sample": "first %d of the %d edges (original order), F=%d, torch CPU index_select+mul+"
                       "scatter_add_ in 4M-edge chunks, %d threads (the CPUs this job may use; the machine "
-                      "has %d), %.1f s" % (E, ei_loops.shape[1], N and F_DIM, threads, machine, dt)}
+                      "has %d), %.1f s" % (E, ei_loops.shape[1], F_DIM, threads, machine, dt)}
 
 
 def _ev_ms(fn, reps):
@@ -177,7 +275,7 @@ def device_reference_paths(ei, norm, x, csr, w_csr, bias, fused_out, terms, reps
         x.index_select(0, edge_index[0]) -> GCNConv.message norm.view(-1, 1) * x_j
         -> torch_scatter 2.0.4 scatter_sum = zeros.scatter_add_(0, broadcast
         index, msg) (ATen atomics) -> update + bias.  The [E', 256] x_j and
-        message tensors are materialised at full size (63.6 GB each).
+        message tensors are materialised at full size (63.6 GB each on rmat21).
       vendor_spmm: torch.sparse_csr_tensor(rowptr, col, norm) @ x on the same
         CSR and weights (rocSPARSE / hipSPARSE SpMM) + bias.
 
@@ -242,22 +340,62 @@ def device_reference_paths(ei, norm, x, csr, w_csr, bias, fused_out, terms, reps
     return res
 
 
-def main():
-    args = parse()
-    rank, world, local = setup_dist(args.gpus, args.sharded)
+def verify_f64(out, x_src, src, dst, w, bias, step=4_000_000):
+    """|out - ref| <= 1e-5 * max(1, sum|w x_j|) per element, ref = a float64
+    index_add of w_e x[src_e] (+ bias) over the given edges in edge chunks (the
+    whole [E, F] message tensor does not fit).  Returns a small report."""
+    n, F = out.shape
+    ref = torch.zeros(n, F, device=out.device, dtype=torch.float64)
+    terms = torch.zeros(n, F, device=out.device, dtype=torch.float64)
+    for s in range(0, src.numel(), step):
+        msg = w[s:s + step].double().view(-1, 1) * x_src[src[s:s + step]].double()
+        ref.index_add_(0, dst[s:s + step], msg)
+        terms.index_add_(0, dst[s:s + step], msg.abs())
+        del msg
+    if bias is not None:
+        ref += bias.double()
+    excess = float(((out.double() - ref).abs() - 1e-5 * terms.clamp(min=1.0)).max()) if n else -1.0
+    res = {"rows": n, "edges": int(src.numel()), "max_abs_diff": float((out.double() - ref).abs().max()) if n else 0.0,
+           "bound_excess": excess, "within_1e-5_bound": excess <= 0,
+           "reference": "float64 index_add of w * x_j over the same edges (+ bias)"}
+    del ref, terms
+    torch.cuda.empty_cache()
+    return res
+
+
+def find_pmc(workload, kernel, src_hash):
+    """The newest committed PMC summary (profiles/r*_pmc_traffic*.json) of THIS
+    build's dispatched kernel on this workload: (hbm bytes per launch, path)."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic*.json")), reverse=True):
+        try:
+            with open(path) as f:
+                pmc = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if pmc.get("workload") == workload and pmc.get("kernel") == kernel and pmc.get("source_hash") == src_hash:
+            return pmc.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+    return None, "no committed profile of this build's kernel on %s" % workload
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(launch_ranks(args, argv))
+    rank, world, local = setup_dist(args)
+    sharded = dist.is_initialized()
+    wl = WORKLOADS[args.workload]
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    sharded = world > 1 or (args.sharded and dist.is_initialized())
     import mi355_mp
     from mi355_mp import _lib, ops
     from mi355_mp.graph import Graph
-    from mi355_mp.graphgen import rmat_edge_index
     from torch_geometric.nn.conv.gcn_conv import GCNConv
     mi355_mp.load_native()
 
-    N = 1 << SCALE
+    N = wl["num_nodes"]
     t0 = time.perf_counter()
-    ei = rmat_edge_index(scale=SCALE, n_samples=SAMPLES, seed=1, device=dev)
+    ei = wl["gen"](dev)
     if sharded:
         # each rank keeps only its contiguous 1/world slice of the edge list (the
         # generator, deterministic on every rank, stands in for reading the rank's
@@ -269,13 +407,16 @@ def main():
         del ei
     torch.cuda.synchronize()
     t_gen = time.perf_counter() - t0
+    stage(rank, "%s graph generated (%.1f s)" % (args.workload, t_gen))
 
     # one-time build: loops + norm (GCNConv.norm), CSR + schedule
     t0 = time.perf_counter()
     bias = torch.randn(F_DIM, device=dev, generator=torch.Generator(device=dev).manual_seed(7)) * 0.1
-    g = torch.Generator(device=dev).manual_seed(1)
+    g = torch.Generator(device=dev).manual_seed(wl["seed"])
+    t_shards = t_exchange_plan = None
     if not sharded:
         ei2, norm = GCNConv.norm(ei, N)
+        del ei
         E2 = ei2.shape[1]
         graph = Graph(ei2, N, N, chunk=args.chunk or None)
         csr = graph.dst
@@ -289,6 +430,8 @@ def main():
         del ei_slice
         torch.cuda.synchronize()
         t_shards = time.perf_counter() - t0
+        stage(rank, "shards built: %d rows, %d in-edges, %d pull-halo rows (%.1f s)"
+              % (sg.n_own, sg.fwd.edge_pos.numel(), sg.fwd.n_local_src - sg.n_own, t_shards))
         E2 = sg.n_edges
         plan = sg.fwd
         x_full = torch.randn(N, F_DIM, device=dev, generator=g)
@@ -310,12 +453,14 @@ def main():
             x_ov = overlap.local_buffer(F_DIM)
             x_ov[:plan.n_own].copy_(x_full[plan.lo:plan.hi])
         del x_full
-        lei = plan.local_edge_index
         graph = sg.g_fwd
         csr = graph.dst
         w_csr = sg._w[0]
         n_rows = plan.n_own
-        E_local = lei.shape[1]
+        E_local = plan.local_edge_index.shape[1]
+        stage(rank, "exchange plan built: %s, %d interior / %d boundary edges (%.1f s)"
+              % ("cover" if overlap.cover is not None else "pull", overlap.n_interior, overlap.n_boundary,
+                 t_exchange_plan))
     torch.cuda.synchronize()
     t_build = time.perf_counter() - t0
 
@@ -360,6 +505,7 @@ def main():
         ev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.steps)]
     torch.cuda.synchronize()
     barrier(world)
+    stage(rank, "warm-up done (%d steps)" % args.warmup)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -367,14 +513,33 @@ def main():
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    dt_local = dt = time.perf_counter() - t0
     if sharded:
         tt = torch.tensor([dt], dtype=torch.float64)
         tt = tt.to(dev) if dist.get_backend() == "nccl" else tt
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
+    stage(rank, "timed steps done: %d steps, %.3f ms/step (max over ranks)" % (args.steps, dt / args.steps * 1e3))
     ms_per_step = dt / args.steps * 1e3
     value = E2 * args.steps / dt    # whole-job edges aggregated per second
+
+    # the step once more, outside the timed region, for --verify
+    verify = None
+    if args.verify:
+        step()
+        torch.cuda.synchronize()
+        if not sharded:
+            verify = verify_f64(out_buf, x, ei2[0], ei2[1], norm, bias)
+        else:
+            # the rank's own edges over [own rows ; pulled halo rows] (plan order =
+            # global edge order), whatever exchange (pull / cover, tiled) the step used
+            xv = plan.local_buffer(F_DIM)
+            xv[:plan.n_own].copy_(x)
+            plan.exchange_into(xv, ops.gather_rows)
+            lei = plan.local_edge_index
+            verify = verify_f64(out_buf, xv, lei[0], lei[1], sg.norm_fwd, bias)
+            del xv
+        stage(rank, "verify: %s" % json.dumps(verify))
 
     # dominant kernel (main aggregation launch) timed with HIP events on the
     # stream it runs on (torch's current stream): `reps` back-to-back launches
@@ -431,22 +596,11 @@ def main():
     gemm_ms = e0.elapsed_time(e1) / 10
 
     # counter traffic (FETCH_SIZE + WRITE_SIZE, corrected) of THIS build's
-    # dispatched kernel, from the committed profile summary -- used only when the
-    # summary names the same kernel and the same native source hash
-    traffic, traffic_src = None, "no profile for this build"
+    # dispatched kernel, from a committed profile summary -- used only when the
+    # summary names the same workload, kernel and native source hash
     src_hash = lib.mp_source_hash().decode()   # the LOADED library's build (load() checks it against the tree)
-    if os.path.exists(PMC_FILE) and not sharded:
-        try:
-            with open(PMC_FILE) as f:
-                pmc = json.load(f)
-            if (pmc.get("workload") == "rmat21_gcn_f256" and pmc.get("kernel") == kernel
-                    and pmc.get("source_hash") == src_hash):
-                traffic = pmc.get("hbm_bytes_per_launch")
-                traffic_src = os.path.relpath(PMC_FILE, ROOT)
-            else:
-                traffic_src = "%s is for another build (kernel/source hash differ)" % os.path.relpath(PMC_FILE, ROOT)
-        except (OSError, ValueError):
-            traffic = None
+    traffic, traffic_src = (None, "N>1: per-rank graphs are not profiled") if sharded else \
+        find_pmc(wl["name"], kernel, src_hash)
 
     # the reference's own device path and a vendor SpMM on the same GPU, same
     # CSR / weights (outside the timed region; checked against the fused output)
@@ -459,11 +613,13 @@ def main():
         ref_paths["fused_ms"] = main_avg + fix_avg
         del fused_out, terms
         torch.cuda.empty_cache()
+        stage(rank, "same-GPU reference paths timed")
 
-    # per-rank exchange / compute split of the timed steps (N > 1, tiled overlap):
-    # HIP events on the compute stream around the interior passes, around each
-    # tile's work.wait() (exchange time the compute stream is exposed to) and
-    # around each boundary pass; gathered to rank 0
+    # per-rank exchange / compute split (N > 1): of the timed steps (tiled
+    # overlap: HIP events on the compute stream around the interior passes,
+    # around each tile's work.wait() -- exchange time the compute stream is
+    # exposed to -- and around each boundary pass), then the step taken apart:
+    # the exchange alone, the compute alone, exchange-then-compute; gathered to rank 0
     ranks = None
     if sharded:
         def span(evs, k):
@@ -479,7 +635,8 @@ def main():
                 * F_DIM * 4,
                 "halo_bytes_out": (int(plan.send_idx.numel()) if args.no_overlap else overlap.n_send) * F_DIM * 4,
                 "pull_exchange_rows_in": plan.n_local_src - plan.n_own,
-                "peers_in": [int(c) for c in (plan.recv_counts if args.no_overlap else overlap.recv_counts)]}
+                "peers_in": [int(c) for c in (plan.recv_counts if args.no_overlap else overlap.recv_counts)],
+                "step_ms_this_rank": dt_local / args.steps * 1e3}
         if overlap.cover is not None:
             mine.update({"cover_pulled_rows": overlap.cover.n_pull_rows,
                          "cover_partial_rows": overlap.cover.n_push_rows,
@@ -490,12 +647,25 @@ def main():
                          "interior_ms": sum(span(e, "interior") for e in step_events) / n,
                          "exchange_exposed_ms": sum(span(e, "wait") for e in step_events) / n,
                          "boundary_ms": sum(span(e, "boundary") for e in step_events) / n})
+        if not args.no_overlap:
+            tiles = x_tiles if x_tiles is not None else [x_ov]
+            reps_d = max(3, min(args.steps, 10))
+            mine["decomposed"] = overlap.decompose(tiles, out_buf, bias, reps_d, barrier=lambda: barrier(world))
+            stage(rank, "step decomposition: %s" % json.dumps(mine["decomposed"]))
+        if verify is not None:
+            mine["verify"] = verify
         ranks = [None] * world
         dist.all_gather_object(ranks, mine)
+        if verify is not None:
+            verify = {"all_ranks_within_1e-5_bound": all(r["verify"]["within_1e-5_bound"] for r in ranks),
+                      "max_bound_excess": max(r["verify"]["bound_excess"] for r in ranks),
+                      "rows": sum(r["verify"]["rows"] for r in ranks),
+                      "reference": ranks[0]["verify"]["reference"] + ", per rank over its own edges"}
 
     cpu = None
     if rank == 0 and not sharded and not args.no_cpu_baseline:
         cpu = cpu_baseline(ei2, norm, x, args.cpu_sample_edges)
+        stage(rank, "cpu baseline done")
 
     if rank == 0:
         line = {
@@ -510,10 +680,9 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic RMAT (seeded, generated on device), random-init features",
-            "config": {"workload": "rmat21_gcn_f256", "graph": "RMAT scale 21 (.57,.19,.19,.05) "
-                       "30M samples symmetrised + add_remaining_self_loops", "num_nodes": N,
-                       "num_edges": E2, "features": F_DIM, "seed": 1,
+            "data": "synthetic %s graph (seeded, generated on device), random-init features" % args.workload,
+            "config": {"workload": wl["name"], "baseline_config": wl["baseline_config"], "graph": wl["graph"],
+                       "num_nodes": N, "num_edges": E2, "features": F_DIM, "seed": wl["seed"],
                        "parallelism": "dst-range shards x%d, RCCL halo all_to_all" % world if sharded
                        else "single GPU", "chunk": csr.chunk},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -538,14 +707,17 @@ def main():
                       "interior_edges_rank0": overlap.n_interior if sharded else E_local,
                       "overlap": sharded and not args.no_overlap,
                       "halo_tile": args.halo_tile if sharded and not args.no_overlap else None,
+                      "collective_timeout_s": COLLECTIVE_TIMEOUT_S if sharded else None,
                       "n_wave_tasks": csr.n_waves,
                       "per_rank": ranks,
+                      "verify": verify,
                       "gpu_reference_path_ms": ((ref_paths or {}).get("reference_path") or {}).get("ms"),
                       "hipsparse_spmm_ms": ((ref_paths or {}).get("vendor_spmm") or {}).get("ms"),
                       "same_gpu_paths": ref_paths,
                       "agg_only_GBps_incl_fixup": alg_bytes / ((main_avg + fix_avg) * 1e-3) / 1e9},
         }
-        print(json.dumps(line))
+        print(json.dumps(line), flush=True)
+    stage(rank, "done")
     if dist.is_initialized():
         dist.destroy_process_group()
 

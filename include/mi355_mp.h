@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MP_ABI_VERSION 4
+#define MP_ABI_VERSION 5
 
 /* status codes */
 #define MP_OK 0
@@ -614,19 +614,15 @@ int mp_scatter_arg_grad_w_f32(const int64_t* src_map, const int64_t* dst_map, in
                               const float* grad_out, int64_t ldg, const float* x, int64_t ldx,
                               float* grad_w, void* stream);
 
-/* ScatterMax/ScatterMin backward [U8]: for every (r,f) with arg[r,f] = e != n_edges
- *   src_map == NULL: grad[e, f]            = grad_out[r,f]          (plain store)
- *   src_map != NULL: grad[src_map[e], f]  += grad_out[r,f] * w[e]   (atomic; w NULL = 1 --
- *                    NOT deterministic; the Python layer uses the CSR form above)
- *   grad_w != NULL:  grad_w[e]            += grad_out[r,f] * x[src_map[e], f]
- * (the message of a weighted max/min aggregation is w[e] * x[src_map[e]];
- * grad_w is d w).  grad / grad_w must be zero-initialised by the caller; either
- * may be NULL. */
+/* ScatterMax/ScatterMin backward [U8] on materialised message rows (torch_scatter
+ * scatter_max / scatter_min of src [n_edges, F]): for every (r,f) with
+ * arg[r,f] = e != n_edges, grad[e, f] = grad_out[r,f] -- a plain store (row e
+ * belongs to one output row), deterministic.  grad must be zero-initialised by
+ * the caller.  The fused message w_e * x[src_e] takes the CSR form above.
+ * (ABI 5: the float-atomic src_map / grad_w form of ABI <= 4 is gone.) */
 int mp_scatter_arg_backward_f32(const float* grad_out, const int64_t* arg,
                                 int64_t n_rows, int32_t F, int64_t n_edges,
-                                const int64_t* src_map, const float* w, const float* x,
-                                int64_t ldx, float* grad, int64_t ldg, float* grad_w,
-                                void* stream);
+                                float* grad, int64_t ldg, void* stream);
 
 /* GCNConv.norm [U5]: deg = scatter_add(w, row); dinv = deg^-1/2 (inf -> 0);
  * norm[e] = dinv[row[e]] * w[e] * dinv[col[e]] (original edge order).

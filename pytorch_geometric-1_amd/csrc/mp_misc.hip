@@ -27,29 +27,20 @@ __global__ void k_permute(const float* __restrict__ src, const int32_t* __restri
   if (k < n) dst[k] = src[perm[k]];
 }
 
-// torch_scatter ScatterMax.backward [U8]:
+// torch_scatter ScatterMax.backward [U8] on materialised message rows:
 //   grad_src = zeros(E+1, F).scatter_(0, arg, grad_out)[:E]
-// (src_map != null: message was w_e * x_j, so the gradient lands on x[src_map[e]]
-// scaled by w_e; grad_w != null: d w_e = sum over the (r, f) whose argmax is e of
-// grad_out[r, f] * x[src_map[e], f]).
+// Message row e belongs to exactly one output row, so each (e, f) is stored by
+// at most one (r, f): plain stores, no atomics, deterministic.  (A fused
+// message w_e * x_j has the CSR form: mp_scatter_arg_backward_csr_f32.)
 __global__ void k_scatter_arg_backward(const float* __restrict__ grad_out, const int64_t* __restrict__ arg,
-                                       int64_t n_rows, int32_t F, int64_t n_edges,
-                                       const int64_t* __restrict__ src_map, const float* __restrict__ w,
-                                       const float* __restrict__ x, int64_t ldx, float* __restrict__ grad,
-                                       int64_t ldg, float* __restrict__ grad_w) {
+                                       int64_t n_rows, int32_t F, int64_t n_edges, float* __restrict__ grad,
+                                       int64_t ldg) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_rows * (int64_t)F) return;
   const int64_t e = arg[i];
   if (e < 0 || e >= n_edges) return;
   const int f = (int)(i % F);
-  const float g = grad_out[i];
-  const int64_t j = src_map ? src_map[e] : e;
-  if (grad) {
-    const float gv = w ? __fmul_rn(g, w[e]) : g;
-    if (src_map) atomicAdd(grad + j * ldg + f, gv);
-    else grad[e * ldg + f] = gv;
-  }
-  if (grad_w) atomicAdd(grad_w + e, __fmul_rn(g, x[j * ldx + f]));
+  grad[e * ldg + f] = grad_out[i];
 }
 
 // GCNConv.norm [U5], step 1: deg = scatter_add(edge_weight, row)
@@ -229,17 +220,14 @@ int mp_permute_f32(const float* src, const int32_t* perm, int64_t n, float* dst,
 }
 
 int mp_scatter_arg_backward_f32(const float* grad_out, const int64_t* arg, int64_t n_rows, int32_t F,
-                                int64_t n_edges, const int64_t* src_map, const float* w, const float* x,
-                                int64_t ldx, float* grad, int64_t ldg, float* grad_w, void* stream) {
+                                int64_t n_edges, float* grad, int64_t ldg, void* stream) {
   MP_DEVICE_GUARD(stream);
   if (n_rows == 0 || F == 0) return MP_OK;
-  MP_CHECK_ARG(grad_out && arg && (grad || grad_w), "mp_scatter_arg_backward_f32: null pointer");
-  MP_CHECK_ARG(!grad || ldg >= F, "mp_scatter_arg_backward_f32: ldg < F");
-  MP_CHECK_ARG(!grad_w || (x && ldx >= F), "mp_scatter_arg_backward_f32: grad_w needs x (ldx >= F)");
-  MP_CHECK_ARG(!w || src_map, "mp_scatter_arg_backward_f32: edge weights need src_map");
+  MP_CHECK_ARG(grad_out && arg && grad, "mp_scatter_arg_backward_f32: null pointer");
+  MP_CHECK_ARG(ldg >= F, "mp_scatter_arg_backward_f32: ldg < F");
   int64_t total = n_rows * (int64_t)F;
-  k_scatter_arg_backward<<<(unsigned)ceil_div(total, 256), 256, 0, as_stream(stream)>>>(
-      grad_out, arg, n_rows, F, n_edges, src_map, w, x, ldx, grad, ldg, grad_w);
+  k_scatter_arg_backward<<<(unsigned)ceil_div(total, 256), 256, 0, as_stream(stream)>>>(grad_out, arg, n_rows, F,
+                                                                                          n_edges, grad, ldg);
   MP_CHECK_LAUNCH();
   return MP_OK;
 }

@@ -121,7 +121,7 @@ SIGNATURES = {
     "mp_heads_outer_add_f32": (ctypes.c_int, [c_p, i64, c_p, i64, i32, i32, c_p, i64, c_p]),
     "mp_gather_rows_f32": (ctypes.c_int, [c_p, i64, c_p, i64, i32, c_p, i64, c_p]),
     "mp_permute_f32": (ctypes.c_int, [c_p, c_p, i64, c_p, c_p]),
-    "mp_scatter_arg_backward_f32": (ctypes.c_int, [c_p, c_p, i64, i32, i64, c_p, c_p, c_p, i64, c_p, i64, c_p, c_p]),
+    "mp_scatter_arg_backward_f32": (ctypes.c_int, [c_p, c_p, i64, i32, i64, c_p, i64, c_p]),
     "mp_self_loop_count": (ctypes.c_int, [c_p, c_p, i64, i64, c_p, c_p]),
     "mp_self_loops_workspace": (sz, [i64, i64]),
     "mp_self_loops": (ctypes.c_int, [c_p, c_p, i64, i64, i32, i64, c_p, c_p, c_p, c_p, sz, c_p]),

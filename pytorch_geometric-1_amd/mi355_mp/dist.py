@@ -202,6 +202,55 @@ class ShardPlan:
         return torch.where(arg_local >= n_local, torch.full_like(ids, n_edges_global), ids)
 
 
+def _sum_returned_rows(plan, back):
+    """Rows returned by the peers (plan.return_halo: aligned with send_idx, peer
+    order, then each peer's request order) summed into this rank's own rows in
+    that fixed order: the native segmented sum keyed on send_idx on the device,
+    torch's serial CPU index_add_ on host tensors.  Deterministic."""
+    if back.is_cuda:
+        from . import ops
+        from .graph import csr_for_index
+        return ops._aggregate(csr_for_index(plan.send_idx, plan.n_own), "eid", back.contiguous(), None, "sum", 0,
+                              None)[0]
+    return torch.zeros((plan.n_own, back.shape[1]), dtype=back.dtype).index_add_(0, plan.send_idx, back)
+
+
+class _HaloRows(torch.autograd.Function):
+    """x_own [n_own, F] -> [own rows ; halo rows] over a pull plan; the backward
+    sends the halo rows' gradients back to their owners (return_halo), which add
+    them to their own rows' gradients (_sum_returned_rows)."""
+
+    @staticmethod
+    def forward(ctx, x_own, plan, group):
+        ctx.plan, ctx.group = plan, group
+        x_local = plan.local_buffer(x_own.shape[1], dtype=x_own.dtype, device=x_own.device)
+        x_local[:plan.n_own].copy_(x_own)
+        if x_own.is_cuda:
+            from . import ops
+            plan.exchange_into(x_local, ops.gather_rows, group)
+        else:
+            plan.exchange_into(x_local, lambda t, idx: t[idx], group)
+        return x_local
+
+    @staticmethod
+    def backward(ctx, g):
+        plan = ctx.plan
+        g = g.contiguous()
+        gx = g[:plan.n_own]
+        back = plan.return_halo(g[plan.n_own:], ctx.group)
+        if back.shape[0]:
+            gx = gx + _sum_returned_rows(plan, back)
+        return gx.contiguous(), None, None
+
+
+def halo_rows(x_own, plan, group=None):
+    """Differentiable [own rows ; halo rows] of x over a pull plan (after
+    plan.exchange_requests()): one all_to_all forward, the reverse one backward."""
+    if x_own.shape[0] != plan.n_own:
+        raise ValueError("mi355_mp.dist: x_own has %d rows, this rank owns %d" % (x_own.shape[0], plan.n_own))
+    return _HaloRows.apply(x_own, plan, group)
+
+
 def sharded_propagate(plan, x_own, local_aggregate, gather_rows, edge_weight=None, group=None, n_edges_global=None):
     """One sharded aggregation: halo exchange then local aggregation.
 
@@ -252,6 +301,15 @@ def scatter_edges_by_owner(key, cuts, payloads, group=None):
     return out
 
 
+def _any_rank(flag, dev, group=None):
+    """True on every rank when `flag` is nonzero on any rank (MAX all_reduce)."""
+    t = torch.tensor([int(flag)], dtype=torch.int64)
+    if dev.type != "cpu" and dist.get_backend(group) != "gloo":
+        t = t.to(dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return bool(t.item())
+
+
 def _all_gather_ints(vals, group=None):
     """[[vals of rank 0], [vals of rank 1], ...] for a few host ints."""
     got = [None] * dist.get_world_size(group)
@@ -271,7 +329,7 @@ def _segment_sum_in_order(index, values, n, device_native):
 
 
 def gcn_shards_from_slices(edge_slice, slice_offset, num_nodes, rank, world, group=None, edge_weight=None,
-                           improved=False):
+                           improved=False, structure_only=False):
     """GCNConv's graph (add_remaining_self_loops + deg over row + norm, PyG 1.4.3
     [U5]) for a graph held as per-rank slices: rank r holds the global edges
     [slice_offset, slice_offset + n_r) (slices contiguous, in rank order).  No
@@ -293,11 +351,22 @@ def gcn_shards_from_slices(edge_slice, slice_offset, num_nodes, rank, world, gro
 
     Returns a dict: cuts, E (total edges after the loops), deg (own rows),
     fwd = (edge_index [2, m] global ids, global edge ids, weights) of the
-    in-edges, bwd = the same for the out-edges."""
+    in-edges, bwd = the same for the out-edges.
+
+    structure_only=True (GATConv: remove_self_loops + add_self_loops gives the
+    same edge list): steps 3 and 4 are skipped; deg and bwd are None and the
+    fwd weights are ones."""
     row, col = edge_slice[0].to(torch.int64), edge_slice[1].to(torch.int64)
     dev = row.device
     N = int(num_nodes)
     n = row.numel()
+    # every rank learns whether ANY rank holds an id outside [0, N) before the
+    # first collective whose size depends on N, and all of them raise together
+    # (a rank with a bad id would otherwise all_reduce a longer degree vector)
+    bad = int(n > 0 and (int(torch.minimum(row.min(), col.min())) < 0
+                         or int(torch.maximum(row.max(), col.max())) >= N))
+    if _any_rank(bad, dev, group):
+        raise IndexError("mi355_mp.dist: an edge of some rank's slice names a node outside [0, %d)" % N)
     w = (edge_weight.to(torch.float32) if edge_weight is not None
          else torch.ones(n, dtype=torch.float32, device=dev))
     fill = 2.0 if improved else 1.0
@@ -323,6 +392,11 @@ def gcn_shards_from_slices(edge_slice, slice_offset, num_nodes, rank, world, gro
     cuts = edge_balanced_cuts(deg_in + 1, world)
     lo, hi = cuts[rank], cuts[rank + 1]
     own = torch.arange(lo, hi, dtype=torch.int64, device=dev)
+    if structure_only:
+        f_row, f_col, f_gid = scatter_edges_by_owner(kc, cuts, [kr, kc, kgid], group)
+        fwd = (torch.stack([torch.cat([f_row, own]), torch.cat([f_col, own])]), torch.cat([f_gid, E_kept + own]),
+               torch.ones(f_row.numel() + hi - lo, dtype=torch.float32, device=dev))
+        return {"cuts": cuts, "E": E_kept + N, "deg": None, "fwd": fwd, "bwd": None}
     # 3. pre-existing loops -> the node's owner; the last one (largest position) wins
     lidx = torch.nonzero(~keep).view(-1)
     lv, lw = row[lidx], w[lidx]
@@ -707,6 +781,94 @@ class OverlappedAggregation:
             rec("boundary")
         return out
 
+    def _exchange_async(self, xt, send, group=None):
+        """Start one tile's all_to_all into its halo rows; returns the work
+        handle (None: gloo with device tensors, done synchronously)."""
+        halo = xt[self.plan.n_own:]
+        if xt.is_cuda and dist.get_backend(group) == "gloo":
+            _a2a(halo, send, self.recv_counts, self.send_counts, group)
+            return None
+        return dist.all_to_all_single(halo, send, output_split_sizes=self.recv_counts,
+                                      input_split_sizes=self.send_counts, group=group, async_op=True)
+
+    def _passes(self, x_tiles, out, bias, interior=True, boundary=True):
+        """The interior and / or boundary aggregations of every tile (as step_tiled)."""
+        from . import _lib, ops
+        n_own = self.plan.n_own
+        last = self.n_boundary == 0
+        offs = [0]
+        for xt in x_tiles:
+            offs.append(offs[-1] + xt.shape[1])
+        if interior:
+            for t, xt in enumerate(x_tiles):
+                b = bias[offs[t]:offs[t + 1]] if (last and bias is not None) else None
+                ops._aggregate(self.g_int.dst, "other", xt[:n_own], self.w_int, "sum", 0, b,
+                               out=out[:, offs[t]:offs[t + 1]])
+        if boundary and not last:
+            for t, xt in enumerate(x_tiles):
+                b = bias[offs[t]:offs[t + 1]] if bias is not None else None
+                ops._aggregate(self.g_bnd.dst, "other", xt, self.w_bnd, "sum", _lib.MP_FLAG_INIT_FROM_OUT, b,
+                               out=out[:, offs[t]:offs[t + 1]])
+
+    def decompose(self, x_tiles, out, bias=None, reps=5, group=None, barrier=None):
+        """The overlapped step taken apart on this rank, each piece timed alone
+        (wall clock over `reps` repetitions, the device synchronised after
+        them, the ranks lined up by `barrier` before each piece):
+          exchange_only_ms   every tile's all_to_all and its wait, the send
+                             buffers packed beforehand: the links alone
+                             (at one rank the splits are empty: ~0);
+          compute_only_ms    packing + interior + boundary passes and no
+                             exchange (the halo rows keep their last values);
+          serial_step_ms     pack, exchange and wait, then the interior and
+                             boundary passes: the step without overlap;
+          overlapped_step_ms step_tiled itself, timed the same way.
+        hidden_frac = (exchange + compute - overlapped) / min(exchange, compute)
+        is the share of the shorter piece the overlap hides (1 = all of it;
+        below 0, the overlapped step is slower than the two pieces in a row,
+        e.g. RCCL's kernels contending with the aggregation for CUs / L2)."""
+        import time
+        n_own = self.plan.n_own
+
+        def timed(fn):
+            if barrier is not None:
+                barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                fn()
+            torch.cuda.synchronize()
+            return (time.perf_counter() - t0) / reps * 1e3
+
+        sends = [self._send(xt[:n_own]) for xt in x_tiles]
+
+        def exchange_only():
+            works = [self._exchange_async(xt, s, group) for xt, s in zip(x_tiles, sends)]
+            for w in works:
+                if w is not None:
+                    w.wait()
+
+        def compute_only():
+            for xt in x_tiles:
+                self._send(xt[:n_own])
+            self._passes(x_tiles, out, bias)
+
+        def serial():
+            works = [self._exchange_async(xt, self._send(xt[:n_own]), group) for xt in x_tiles]
+            for w in works:
+                if w is not None:
+                    w.wait()
+            self._passes(x_tiles, out, bias)
+
+        res = {"reps": reps,
+               "exchange_only_ms": timed(exchange_only),
+               "compute_only_ms": timed(compute_only),
+               "serial_step_ms": timed(serial),
+               "overlapped_step_ms": timed(lambda: self.step_tiled(x_tiles, out, bias, group))}
+        shorter = min(res["exchange_only_ms"], res["compute_only_ms"])
+        res["hidden_frac"] = ((res["exchange_only_ms"] + res["compute_only_ms"] - res["overlapped_step_ms"]) / shorter
+                              if shorter > 1e-3 else None)
+        return res
+
 
 def transposed_plan(edge_index, num_nodes, rank, world, cuts, group=None):
     """The plan of the backward pass: rank p owns the SOURCE rows [lo_p, hi_p)
@@ -786,6 +948,73 @@ class ShardedGraph:
         if self.norm_fwd.is_cuda:
             self._set_local_weights(self.norm_fwd, self.norm_bwd)
         return self
+
+    @classmethod
+    def for_gat(cls, edge_index, num_nodes, rank, world, group=None, cuts=None):
+        """GATConv's graph (remove_self_loops + add_self_loops, PyG 1.4.3 [U6])
+        from the full edge list, sharded: the forward plan only -- the GAT
+        backward runs over the rank's local transposed CSR, and the gradients of
+        its halo rows go back to their owners (halo_rows)."""
+        from torch_geometric.nn.conv._structure import gat_loops
+        ei = gat_loops(edge_index, num_nodes) if edge_index.is_cuda else _host_gat_loops(edge_index, num_nodes)
+        plan = ShardPlan(ei, num_nodes, rank, world, cuts=cuts).exchange_requests(group)
+        return cls._for_gat_plan(plan, ei.shape[1], group)
+
+    @classmethod
+    def for_gat_from_slices(cls, edge_slice, slice_offset, num_nodes, rank, world, group=None):
+        """for_gat() for a graph held as per-rank slices of its edge list (as
+        for_gcn_from_slices; the loops are the same edge list GCN's
+        add_remaining_self_loops gives, so gcn_shards_from_slices builds it,
+        structure only).  Local edge lists and global edge ids equal for_gat()'s."""
+        d = gcn_shards_from_slices(edge_slice, slice_offset, num_nodes, rank, world, group, structure_only=True)
+        f_ei, f_gid, _ = d["fwd"]
+        plan = ShardPlan(f_ei, num_nodes, rank, world, cuts=d["cuts"], edge_ids=f_gid).exchange_requests(group)
+        return cls._for_gat_plan(plan, d["E"], group)
+
+    @classmethod
+    def _for_gat_plan(cls, plan, n_edges, group):
+        from .graph import GAT_TARGET_TASKS, Graph
+        self = cls.__new__(cls)
+        self.group = group
+        self.num_nodes = int(plan.cuts[-1])
+        self.n_edges = int(n_edges)
+        self.fwd, self.bwd = plan, None
+        self.lo, self.hi, self.n_own = plan.lo, plan.hi, plan.n_own
+        # destination rows = own rows, sources = [own rows ; halo rows]: the fused
+        # GAT kernels' sharded form (ops._gat_rows_ok); built lazily on first use
+        self.g_fwd = Graph(plan.local_edge_index, self.n_own, plan.n_local_src, target_tasks=GAT_TARGET_TASKS)
+        self.g_bwd = None
+        self.deg = None
+        self._w = None
+        self.cover = None
+        self._chunk = None
+        return self
+
+    def gat_propagate(self, xw_own, att, heads, out_channels, negative_slope=0.2, bias=None,
+                      return_alpha=False, dropout=0.0, local_gat=None):
+        """Sharded fused GATConv aggregation (GATConv.message + utils.softmax +
+        scatter_add + update, [U3, U6]): this rank's rows [n_own, H*C] (+ bias).
+
+        xw_own: the rank's rows of X W.  Their halo rows arrive over the pull
+        plan (halo_rows: differentiable, the backward returns the halo rows'
+        gradients to their owners).  A destination row's score a_dst comes from
+        its own xw row, a_src is recomputed from each gathered row, and every
+        in-edge of a destination row lives on its owner -- the softmax and the
+        weighted sum of a row run over the same edges in the same (global)
+        order as on one GPU: no extra collective, alpha bit-equal on rows no
+        merge-path task splits.  return_alpha: (global edge ids, alpha [m, H])
+        of this rank's in-edges.  dropout: the fused attention dropout (its keep
+        mask hashes the rank's local CSR slots, so it differs from one GPU's).
+        local_gat(graph, edge_index, xw_local, att, H, C, slope, bias,
+        return_alpha, dropout) -> (out, alpha): default the HIP path
+        (ops.gat_propagate); the gloo CPU tests pass the oracle."""
+        if local_gat is None:
+            from . import ops
+            local_gat = ops.gat_propagate
+        xw_local = halo_rows(xw_own, self.fwd, self.group)
+        out, alpha = local_gat(self.g_fwd, self.fwd.local_edge_index, xw_local, att, heads, out_channels,
+                               negative_slope, bias, return_alpha, dropout)
+        return out, ((self.fwd.edge_gid, alpha) if return_alpha else None)
 
     def _set_local_weights(self, w_fwd, w_bwd):
         """Per-edge weights already in each plan's local edge order."""
@@ -894,10 +1123,7 @@ class _ShardedAggregate(torch.autograd.Function):
             gx = gl[:plan.n_own]
             back = plan.return_halo(gl[plan.n_own:], sg.group)
             if back.shape[0]:
-                from .graph import csr_for_index
-                ret, _ = ops._aggregate(csr_for_index(plan.send_idx, plan.n_own), "eid", back.contiguous(), None,
-                                        "sum", 0, None)
-                gx = gx + ret
+                gx = gx + _sum_returned_rows(plan, back)
             return gx.contiguous(), None, None
         if reduce == "mean":
             g = g / sg.g_fwd.dst.degree().clamp(min=1).to(torch.float32).view(-1, 1)
@@ -919,6 +1145,13 @@ class _ShardedAggregate(torch.autograd.Function):
         w_bwd = sg._w[1] if sg._w is not None else None
         gx, _ = ops._aggregate(sg.g_bwd.dst, "other", g_local, w_bwd, "sum", 0, None)
         return gx, None, None
+
+
+def _host_gat_loops(edge_index, num_nodes):
+    """remove_self_loops + add_self_loops on host tensors (the gloo CPU tests)."""
+    keep = edge_index[0] != edge_index[1]
+    loops = torch.arange(int(num_nodes), dtype=edge_index.dtype).view(1, -1).repeat(2, 1)
+    return torch.cat([edge_index[:, keep], loops], 1)
 
 
 def broadcast_parameters(module, src=0, group=None):
@@ -974,3 +1207,48 @@ class ShardedGCNConv(torch.nn.Module):
 
     def __repr__(self):
         return "{}({}, {})".format(self.__class__.__name__, self.in_channels, self.out_channels)
+
+
+class ShardedGATConv(torch.nn.Module):
+    """GATConv [U6] over a ShardedGraph made by ShardedGraph.for_gat /
+    for_gat_from_slices: this rank's rows of the layer's output.  x_own holds
+    the rank's rows of X; the X W GEMM is local (hipBLASLt), the halo rows of
+    X W come over the plan's exchange (forward) and their gradients go back to
+    their owners (backward); the fused GAT kernels run on the rank's local
+    graph.  Same parameters, names, init and options as GATConv (a GATConv
+    state_dict loads unchanged); replicated like ShardedGCNConv:
+    broadcast_parameters once, allreduce_gradients after backward."""
+
+    def __init__(self, in_channels, out_channels, heads=1, concat=True, negative_slope=0.2, dropout=0, bias=True):
+        super().__init__()
+        from torch.nn import Parameter
+        self.in_channels, self.out_channels, self.heads = in_channels, out_channels, heads
+        self.concat, self.negative_slope, self.dropout = concat, negative_slope, dropout
+        self.weight = Parameter(torch.Tensor(in_channels, heads * out_channels))
+        self.att = Parameter(torch.Tensor(1, heads, 2 * out_channels))
+        if bias:
+            self.bias = Parameter(torch.Tensor(heads * out_channels if concat else out_channels))
+        else:
+            self.register_parameter("bias", None)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        from torch_geometric.nn.inits import glorot, zeros
+        glorot(self.weight)
+        glorot(self.att)
+        zeros(self.bias)
+
+    def forward(self, x_own, sg, return_attention_weights=False, local_gat=None):
+        from torch_geometric.nn.conv.gat_conv import GATConv
+        from . import ops
+        weight, att, fused_bias, C4 = GATConv._fused_operands(self)
+        xw = ops.feature_transform(x_own, weight)
+        drop = self.dropout if self.training else 0.0
+        out, aw = sg.gat_propagate(xw, att, self.heads, C4, self.negative_slope, fused_bias,
+                                   return_attention_weights, drop, local_gat=local_gat)
+        out = GATConv._finish(self, out, C4)
+        return (out, aw) if return_attention_weights else out
+
+    def __repr__(self):
+        return "{}({}, {}, heads={})".format(self.__class__.__name__, self.in_channels, self.out_channels,
+                                            self.heads)

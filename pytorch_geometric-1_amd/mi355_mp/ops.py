@@ -306,9 +306,8 @@ class _SegmentReduce(torch.autograd.Function):
             gs = torch.zeros((ctx.n_src, g.shape[1]), dtype=g.dtype, device=g.device)
             if g.dtype == torch.float32:
                 _lib.check(lib.mp_scatter_arg_backward_f32(g.data_ptr(), arg.data_ptr(), g.shape[0], g.shape[1],
-                                                           ctx.n_src, None, None, None, 0, gs.data_ptr(),
-                                                           gs.stride(0), None, _lib.stream_ptr(g.device)),
-                           "mp_scatter_arg_backward_f32")
+                                                           ctx.n_src, gs.data_ptr(), gs.stride(0),
+                                                           _lib.stream_ptr(g.device)), "mp_scatter_arg_backward_f32")
             else:
                 _lib.check(lib.mp_scatter_arg_any(g.element_size(), g.data_ptr(), arg.data_ptr(), g.shape[0],
                                                   g.shape[1], ctx.n_src, gs.data_ptr(), gs.stride(0),
@@ -590,7 +589,25 @@ def _gat_train_fwd_ok(graph, xw, H, C):
     (a_src from the gathered rows when C/4 is a power of two <= 64, else from
     the node-score array)."""
     return (GAT_TRAIN_FWD and GAT_OWN_A_SRC and gat_wide_ok(H, C)
-            and not gat_two_pass(graph.dst, H, C) and xw.data_ptr() % 16 == 0 and graph.n_dst == xw.shape[0])
+            and not gat_two_pass(graph.dst, H, C) and xw.data_ptr() % 16 == 0 and _gat_rows_ok(graph, xw))
+
+
+def _gat_rows_ok(graph, xw):
+    """The fused GAT kernels take a square graph (n_dst == n_src == xw rows) or a
+    sharded rank's local graph: n_src == xw rows and destination row i's own xw
+    row is row i of xw (the rank's own rows first, then its halo rows:
+    mi355_mp.dist.ShardedGraph.gat_propagate), so n_dst <= n_src."""
+    return graph.n_src == xw.shape[0] and graph.n_dst <= xw.shape[0]
+
+
+def _pad_rows(t, n):
+    """t [m, ...] -> [n, ...] with zero rows appended (node-wise gradients of the
+    destination rows, extended over the halo rows of a sharded local graph)."""
+    if t.shape[0] == n:
+        return t
+    out = t.new_zeros((n,) + tuple(t.shape[1:]))
+    out[:t.shape[0]] = t
+    return out
 
 
 def gat_wide_ok(H, C):
@@ -635,8 +652,9 @@ def _gat_forward(graph, edge_index, xw, att, H, C, slope, bias, want_alpha, trai
     N = xw.shape[0]
     csr = graph.dst
     st = _lib.stream_ptr(dev)
-    if graph.n_dst != N:
-        raise ValueError("mi355_mp: fused GAT needs a square graph (n_dst == x.size(0))")
+    if not _gat_rows_ok(graph, xw):
+        raise ValueError("mi355_mp: fused GAT needs n_src == x.size(0) >= n_dst (a square graph, or a sharded "
+                         "rank's own rows followed by its halo rows)")
     att_c = att.reshape(H, 2 * C).contiguous().to(torch.float32)
     a_src = torch.empty((N, H), dtype=torch.float32, device=dev)
     a_dst = torch.empty((N, H), dtype=torch.float32, device=dev)
@@ -757,12 +775,14 @@ def _gat_backward_wide(graph, g, xw, att, a_src, a_dst, stats, agg, extra, H, C,
         return (torch.zeros_like(xw), torch.zeros_like(att) if want_att else None,
                 g.new_zeros(F) if want_bias else None)
     agg2, s2 = extra
-    pack = torch.empty((N, H, 4), dtype=torch.float32, device=dev)
-    ga_dst = torch.empty((N, H), dtype=torch.float32, device=dev)
-    _lib.check(lib.mp_gat_backward_prep_wide_f32(g.data_ptr(), g.stride(0), agg.data_ptr(), agg.stride(0),
-                                                 agg2.data_ptr(), s2.data_ptr(), a_dst.data_ptr(), stats.data_ptr(),
-                                                 N, H, C, pack.data_ptr(), ga_dst.data_ptr(), st),
-               "mp_gat_backward_prep_wide_f32")
+    n_dst = graph.n_dst            # < N on a sharded rank's local graph (halo rows receive no edges)
+    pack = torch.empty((max(n_dst, 1), H, 4), dtype=torch.float32, device=dev)
+    ga_dst = (torch.empty if n_dst == N else torch.zeros)((N, H), dtype=torch.float32, device=dev)
+    if n_dst:
+        _lib.check(lib.mp_gat_backward_prep_wide_f32(g.data_ptr(), g.stride(0), agg.data_ptr(), agg.stride(0),
+                                                     agg2.data_ptr(), s2.data_ptr(), a_dst.data_ptr(),
+                                                     stats.data_ptr(), n_dst, H, C, pack.data_ptr(), ga_dst.data_ptr(),
+                                                     st), "mp_gat_backward_prep_wide_f32")
     src = graph.src_with_dst_slots()
     gs = src.struct("dst_slot")
     gx = torch.empty((N, F), dtype=torch.float32, device=dev)
@@ -806,21 +826,24 @@ def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope
         return (torch.zeros_like(xw), torch.zeros_like(att) if want_att else None,
                 g.new_zeros(F) if want_bias else None)
     epi = C % 4 == 0 and F <= 256
-    nb = int(lib.mp_gat_bwd_blocks(N))
-    pack = torch.empty((N, H, 4), dtype=torch.float32, device=dev)
-    gpart = torch.empty((nb, F), dtype=torch.float32, device=dev) if (want_bias and epi) else None
+    n_dst = graph.n_dst            # < N on a sharded rank's local graph (halo rows receive no edges)
+    nb = int(lib.mp_gat_bwd_blocks(n_dst))
+    pack = torch.empty((max(n_dst, 1), H, 4), dtype=torch.float32, device=dev)
+    gpart = torch.empty((nb, F), dtype=torch.float32, device=dev) if (want_bias and epi and n_dst) else None
     ga_dst = None
     if extra is not None:
         # d a_dst[n,h] = <g_n, agg2_n>_h - rs_n,h s2_n,h: node-wise, no per-edge d score
         agg2, s2 = extra
-        ga_dst = torch.empty((N, H), dtype=torch.float32, device=dev)
-        _lib.check(lib.mp_gat_backward_prep_train_f32(g.data_ptr(), g.stride(0), agg.data_ptr(), agg.stride(0),
-                                                      agg2.data_ptr(), s2.data_ptr(), a_dst.data_ptr(),
-                                                      stats.data_ptr(), N, H, C, pack.data_ptr(), _lib.ptr(gpart),
-                                                      ga_dst.data_ptr(), st), "mp_gat_backward_prep_train_f32")
-    else:
+        ga_dst = (torch.empty if n_dst == N else torch.zeros)((N, H), dtype=torch.float32, device=dev)
+        if n_dst:
+            _lib.check(lib.mp_gat_backward_prep_train_f32(g.data_ptr(), g.stride(0), agg.data_ptr(), agg.stride(0),
+                                                          agg2.data_ptr(), s2.data_ptr(), a_dst.data_ptr(),
+                                                          stats.data_ptr(), n_dst, H, C, pack.data_ptr(),
+                                                          _lib.ptr(gpart), ga_dst.data_ptr(), st),
+                       "mp_gat_backward_prep_train_f32")
+    elif n_dst:
         _lib.check(lib.mp_gat_backward_prep_f32(g.data_ptr(), g.stride(0), agg.data_ptr(), agg.stride(0),
-                                                a_dst.data_ptr(), stats.data_ptr(), N, H, C, pack.data_ptr(),
+                                                a_dst.data_ptr(), stats.data_ptr(), n_dst, H, C, pack.data_ptr(),
                                                 _lib.ptr(gpart), st), "mp_gat_backward_prep_f32")
     gb = None
     if want_bias:
@@ -857,6 +880,7 @@ def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope
     del slab, pack
     if ga_dst is None:
         ga_dst, _ = _aggregate(graph.dst, "slot", de, None, "sum", 0, None)
+        ga_dst = _pad_rows(ga_dst, N)
         del de
     gatt = None
     if epi:
@@ -971,6 +995,7 @@ class _GatPropagate(torch.autograd.Function):
         ds = alpha[:E] * (dalpha[:E] - rs[sr[:E].long()])
         de = (ds * torch.where(score[:E] > 0, torch.ones_like(ds), torch.full_like(ds, slope))).contiguous()
         ga_dst, _ = _aggregate(dst, "slot", de, None, "sum", 0, None)
+        ga_dst = _pad_rows(ga_dst, N)
         de_orig = torch.empty_like(de)
         de_orig[eid_d] = de
         ga_src, _ = _aggregate(src, "eid", de_orig, None, "sum", 0, None)
@@ -991,8 +1016,8 @@ def gat_propagate(graph, edge_index, xw, att, heads, out_channels, negative_slop
     """Fused GATConv aggregation: returns (out [N, H*C], alpha [E, H] or None).
     dropout > 0: GATConv's training-mode attention dropout on the messages
     (callers check gat_dropout_ok); the keep mask is a hash of (seed, slot, head),
-    seed drawn from torch's default generator unless given (gat_dropout_keep
-    returns the mask).  alpha is the undropped softmax, as upstream's."""
+    seed drawn from the device's default generator unless given
+    (gat_dropout_keep returns the mask).  alpha is the undropped softmax, as upstream's."""
     _lib.require_device(xw, edge_index, att, bias)
     xw = _f32_2d(xw, "x@W").contiguous()
     H, C = int(heads), int(out_channels)
@@ -1007,7 +1032,9 @@ def gat_propagate(graph, edge_index, xw, att, heads, out_channels, negative_slop
             raise ValueError("mi355_mp: fused attention dropout needs 0 < p < 1, H <= 32, C %% 4 == 0 and C/4 a "
                              "power of two <= 64 (got p=%g, H=%d, C=%d)" % (dropout, H, C))
         if seed is None:
-            seed = int(torch.randint(-2 ** 63, 2 ** 63 - 1, (), dtype=torch.int64))
+            # from the generator of xw's device, as F.dropout on a device tensor
+            # draws its mask (torch's CPU generator stays untouched)
+            seed = int(torch.randint(-2 ** 63, 2 ** 63 - 1, (), dtype=torch.int64, device=xw.device))
         drop = (int(seed) & 0xFFFFFFFFFFFFFFFF, float(dropout))
     # autograd.Function.forward always runs with grad disabled: decide here whether
     # a backward can follow (then the forward keeps the pre-bias aggregate)

@@ -85,27 +85,14 @@ class GATConv(MessagePassing):
             edge_index = gat_loops(edge_index, x.size(self.node_dim))
 
         if self._can_fuse(x, size):
-            H, C = self.heads, self.out_channels
-            C4 = self._padded_channels()
-            weight, att = self.weight, self.att
-            fused_bias = self.bias if self.concat else None
-            if C4 != C:  # zero columns per head: the 16-byte row kernels apply
-                weight = F.pad(weight.view(-1, H, C), (0, C4 - C)).view(-1, H * C4)
-                att = F.pad(att.view(1, H, 2, C), (0, C4 - C)).view(1, H, 2 * C4)
-                if fused_bias is not None:
-                    fused_bias = F.pad(fused_bias.view(H, C), (0, C4 - C)).view(H * C4)
+            weight, att, fused_bias, C4 = self._fused_operands()
             xw = _ops.feature_transform(x, weight)
             N = xw.size(0)
             graph = graph_for(edge_index, N, N, self.flow, target_tasks=GAT_TARGET_TASKS)
             drop = self.dropout if self.training else 0.0
-            out, alpha = _ops.gat_propagate(graph, edge_index, xw, att, H, C4, self.negative_slope, fused_bias,
-                                            return_attention_weights, dropout=drop)
-            if C4 != C:
-                out = out.view(-1, H, C4)[:, :, :C].reshape(-1, H * C).contiguous()
-            if not self.concat:
-                out = out.view(-1, self.heads, self.out_channels).mean(dim=1)
-                if self.bias is not None:
-                    out = out + self.bias
+            out, alpha = _ops.gat_propagate(graph, edge_index, xw, att, self.heads, C4, self.negative_slope,
+                                            fused_bias, return_attention_weights, dropout=drop)
+            out = self._finish(out, C4)
             if return_attention_weights:
                 return out, (edge_index, alpha)
             return out
@@ -120,6 +107,33 @@ class GATConv(MessagePassing):
         if return_attention_weights:
             alpha, self.alpha = self.alpha, None
             return out, (edge_index, alpha)
+        return out
+
+    def _fused_operands(self):
+        """(weight, att, bias for the kernel or None, C4): per head, out_channels
+        padded with zero columns to C4 (a multiple of 4) so the 16-byte row
+        kernels apply; the concat bias is added in the kernel."""
+        H, C = self.heads, self.out_channels
+        C4 = (C + 3) // 4 * 4
+        weight, att = self.weight, self.att
+        fused_bias = self.bias if self.concat else None
+        if C4 != C:
+            weight = F.pad(weight.view(-1, H, C), (0, C4 - C)).view(-1, H * C4)
+            att = F.pad(att.view(1, H, 2, C), (0, C4 - C)).view(1, H, 2 * C4)
+            if fused_bias is not None:
+                fused_bias = F.pad(fused_bias.view(H, C), (0, C4 - C)).view(H * C4)
+        return weight, att, fused_bias, C4
+
+    def _finish(self, out, C4):
+        """The fused output [n, H*C4] -> GATConv.update's: padding dropped, heads
+        concatenated (bias already in) or averaged (+ bias)."""
+        H, C = self.heads, self.out_channels
+        if C4 != C:
+            out = out.view(-1, H, C4)[:, :, :C].reshape(-1, H * C).contiguous()
+        if not self.concat:
+            out = out.view(-1, H, C).mean(dim=1)
+            if self.bias is not None:
+                out = out + self.bias
         return out
 
     def message(self, edge_index_i, x_i, x_j, size_i, return_attention_weights):

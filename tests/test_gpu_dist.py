@@ -204,6 +204,100 @@ def test_sharded_gcnconv_forward_backward_on_one_gpu():
         assert r["gmax_exact"] and r["gmax_repeat"], r   # deterministic on both sides (round 3)
 
 
+def _gat_layer_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "pytorch_geometric-1_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mi355_mp import dist as mdist, ops
+        from mi355_mp.graph import GAT_TARGET_TASKS, Graph
+        from mi355_mp.graphgen import powerlaw_edge_index
+        from torch_geometric.nn import GATConv
+        from torch_geometric.nn.conv._structure import gat_loops
+        dev = torch.device("cuda", 0)
+        N, E, Fi = 3000, 60000, 64
+        ei = powerlaw_edge_index(N, E, seed=47).to(dev)
+        gen = torch.Generator().manual_seed(47)
+        x = torch.randn(N, Fi, generator=gen).to(dev)
+        res = {}
+        # (heads, out_channels, concat): config 3's shape, the reference's heads=1 stacks
+        # (ConvexPruning.py:209-214, a wide head), a padded width, and ppi's mean head
+        for H, C, concat in ((8, 32, True), (1, 96, True), (2, 10, True), (3, 8, False)):
+            Fo = H * C if concat else C
+            gout = torch.randn(N, Fo, generator=gen).to(dev)
+            ref = GATConv(Fi, C, heads=H, concat=concat).to(dev)
+            with torch.no_grad():
+                ref.bias.normal_()
+            mdist.broadcast_parameters(ref)
+            xr = x.clone().requires_grad_(True)
+            out_ref = ref(xr, ei)
+            (out_ref * gout).sum().backward()
+            sg = mdist.ShardedGraph.for_gat(ei, N, rank, world)
+            s0, s1 = rank * E // world, (rank + 1) * E // world
+            sgs = mdist.ShardedGraph.for_gat_from_slices(ei[:, s0:s1].clone(), s0, N, rank, world)
+            same = (sgs.fwd.cuts == sg.fwd.cuts and torch.equal(sgs.fwd.local_edge_index, sg.fwd.local_edge_index)
+                    and torch.equal(sgs.fwd.edge_gid, sg.fwd.edge_pos))
+            conv = mdist.ShardedGATConv(Fi, C, heads=H, concat=concat).to(dev)
+            conv.load_state_dict(ref.state_dict())
+            lo, hi = sg.lo, sg.hi
+            xo = x[lo:hi].clone().requires_grad_(True)
+            out = conv(xo, sgs)
+            (out * gout[lo:hi]).sum().backward()
+            mdist.allreduce_gradients(conv)
+            r = {"slices_equal": bool(same),
+                 "out": float((out.detach() - out_ref.detach()[lo:hi]).abs().max()),
+                 "gx": float((xo.grad - xr.grad[lo:hi]).abs().max() / xr.grad.abs().max())}
+            for k in ("weight", "att", "bias"):
+                a, b = getattr(conv, k).grad, getattr(ref, k).grad
+                r["g" + k] = float((a - b).abs().max() / b.abs().max())
+            res[(H, C, concat)] = r
+        # propagate level, the same X W on both sides: alpha by global edge id and the
+        # output rows equal the single-GPU fused kernel except on rows a merge-path
+        # task boundary splits (different on the rank's local CSR)
+        H, C = 8, 32
+        xw = torch.randn(N, H * C, generator=gen).to(dev)
+        att = torch.randn(1, H, 2 * C, generator=gen).to(dev) * 0.2
+        ei2 = gat_loops(ei, N)
+        g1 = Graph(ei2, N, N, target_tasks=GAT_TARGET_TASKS)
+        o1, a1 = ops.gat_propagate(g1, ei2, xw, att, H, C, return_alpha=True)
+        sg = mdist.ShardedGraph.for_gat(ei, N, rank, world)
+        o2, (gid, a2) = sg.gat_propagate(xw[sg.lo:sg.hi].contiguous(), att, H, C, return_alpha=True)
+        res["prop"] = {"out": float((o2 - o1[sg.lo:sg.hi]).abs().max()),
+                       "out_bitwise_frac": float((o2 == o1[sg.lo:sg.hi]).float().mean()),
+                       "alpha": float((a2 - a1[gid]).abs().max()),
+                       "alpha_bitwise_frac": float((a2 == a1[gid]).float().mean())}
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_gatconv_forward_backward_on_one_gpu(world):
+    """ShardedGATConv over ShardedGraph.for_gat / for_gat_from_slices (ranks
+    sharing the device, halo rows of X W staged through gloo): forward rows,
+    d x (the halo rows' gradients returned to their owners) and the all-reduced
+    d W / d att / d b against the single-GPU GATConv -- config 3's 8 x 32 heads,
+    a heads=1 wide head, a padded width and a mean-of-heads layer; at the
+    propagate level, with the same X W, alpha (by global edge id) and the
+    output rows bit-equal to the single-GPU kernel on all but split rows."""
+    res = _spawn(_gat_layer_worker, world=world)
+    for rank, r in res:
+        for key, v in r.items():
+            if key == "prop":
+                assert v["out"] < 1e-5 and v["alpha"] < 1e-6, (key, v)
+                assert v["out_bitwise_frac"] > 0.9 and v["alpha_bitwise_frac"] > 0.9, (key, v)
+                continue
+            assert v["slices_equal"], (key, v)
+            # tolerance: the rank's X W GEMM has M = n_own rows (hipBLASLt picks its kernel by M)
+            assert v["out"] < 1e-5 and v["gx"] < 1e-5, (key, v)
+            assert v["gweight"] < 1e-5 and v["gatt"] < 1e-5 and v["gbias"] < 1e-5, (key, v)
+
+
 def _products_worker(rank, world, port, q):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -399,6 +493,23 @@ def _rccl_worker(rank, world, port, q):
             exact = exact and bool(torch.equal(om, wo)) and bool(torch.equal(am, wa))
         res["max_exact"] = exact
         res["slices_equal"] = bool(slices_equal)
+        # sharded GATConv forward + backward over RCCL (plan exchange, halo rows and
+        # their gradients' return, replicated parameters)
+        from torch_geometric.nn import GATConv
+        gref = GATConv(Fi, 32, heads=8).to(dev)
+        xg = xi.clone().requires_grad_(True)
+        (gref(xg, ei) * gout).sum().backward()
+        sgg = mdist.ShardedGraph.for_gat_from_slices(ei.clone(), 0, N, rank, world)
+        gconv = mdist.ShardedGATConv(Fi, 32, heads=8).to(dev)
+        gconv.load_state_dict(gref.state_dict())
+        mdist.broadcast_parameters(gconv)
+        xs = xi.clone().requires_grad_(True)
+        og = gconv(xs, sgg)
+        (og * gout).sum().backward()
+        mdist.allreduce_gradients(gconv)
+        res["gat_out"] = float((og.detach() - gref(xi, ei).detach()).abs().max())
+        res["gat_gx"] = float((xs.grad - xg.grad).abs().max() / xg.grad.abs().max())
+        res["gat_gatt"] = float((gconv.att.grad - gref.att.grad).abs().max() / gref.att.grad.abs().max())
         torch.cuda.synchronize()
         q.put((rank, res))
     finally:
@@ -413,46 +524,88 @@ def test_sharded_path_over_rccl_world_one():
     with split sizes on device tensors + work.wait() (OverlappedAggregation
     step / step_tiled), the blocking exchanges of ShardPlan / ShardedGraph,
     broadcast and all_reduce of the replicated GCNConv weights, the halo
-    cover's collective build, step and autograd -- with empty halo splits,
-    against the single-GPU kernel and GCNConv."""
+    cover's collective build, step and autograd, the sharded GATConv (halo
+    rows of X W and their gradients' return) -- with empty halo splits,
+    against the single-GPU kernel, GCNConv and GATConv."""
     (rank, r), = _spawn(_rccl_worker, world=1, timeout=300)
     assert r["step"] < 1e-5 and r["tiled_eq_step"], r
     assert r["layer_out"] < 1e-5 and r["layer_gx"] < 1e-5 and r["layer_gw"] < 1e-5, r
     assert r["max_exact"], r
     assert r["slices_equal"], r
     assert r["cover_step"] < 1e-5 and r["cover_layer_out"] < 1e-6 and r["cover_layer_gx"] < 1e-6, r
+    assert r["gat_out"] < 1e-5 and r["gat_gx"] < 1e-5 and r["gat_gatt"] < 1e-5, r
 
 
-def test_bench_multi_rank_path_end_to_end():
-    """bench.py's N > 1 path (dst-range shards, plan exchange, tiled overlapped
-    halo step, max-over-ranks timing, one JSON line from rank 0) launched the
-    way the driver launches it (torch.distributed.run), as 2 gloo ranks sharing
-    the box's GPU (MP_BENCH_BACKEND=gloo stages the halo rows through the host;
-    the timing is meaningless, the line's shape and the shard bookkeeping are
-    what is checked)."""
+def _run_bench(args, env_extra=None, timeout=900):
     import json
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, MP_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
-           "--steps", "2", "--warmup", "1"]
-    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=600)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", **(env_extra or {}))
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MP_BENCH_LAUNCH_PROBE"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable] + args, cwd=root, env=env, capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
-    d = json.loads(lines[0])
+    return json.loads(lines[0]), r.stderr
+
+
+def test_bench_multi_rank_path_end_to_end():
+    """bench.py --gpus 2 with NO launcher (the driver's plain call): bench.py
+    starts its two ranks itself; here they are gloo ranks sharing the box's GPU
+    (MP_BENCH_BACKEND=gloo stages the halo rows through the host; the timing is
+    meaningless, the line's shape, the shard bookkeeping, the per-rank stage
+    markers and the step decomposition are what is checked).  --verify holds
+    every rank's rows to the float64 bound over its own edges."""
+    d, err = _run_bench(["bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
+                         "--no-ref-paths", "--verify"], {"MP_BENCH_BACKEND": "gloo"})
     assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1 and d["value"] > 0
     assert d["config"]["num_edges"] == 62_094_512 and d["cpu_baseline"] is None
+    assert d["config"]["workload"] == "rmat21_gcn_f256"
     ex = d["extra"]
     assert ex["overlap"] and ex["halo_tile"] == 128 and ex["halo_rows_rank0"] > 0
+    assert ex["collective_timeout_s"] == 300
     assert 0 < ex["interior_edges_rank0"] < ex["edges_local_rank0"] < d["config"]["num_edges"]
+    assert ex["verify"]["all_ranks_within_1e-5_bound"], ex["verify"]
     pr = ex["per_rank"]
     assert [p["rank"] for p in pr] == [0, 1] and sum(p["edges"] for p in pr) == d["config"]["num_edges"]
     for p in pr:
         assert p["halo_bytes_in"] == p["halo_rows"] * 256 * 4 and p["halo_bytes_out"] > 0
         assert p["interior_ms"] > 0 and p["boundary_ms"] > 0 and p["exchange_exposed_ms"] >= 0
+        dc = p["decomposed"]
+        assert dc["exchange_only_ms"] > 0 and dc["compute_only_ms"] > 0
+        assert dc["serial_step_ms"] > 0 and dc["overlapped_step_ms"] > 0
+    for r in (0, 1):
+        for marker in ("process group up", "shards built", "warm-up done", "timed steps done", "done"):
+            assert ("[bench rank %d " % r) in err and marker in err, marker
+
+
+def test_bench_products_workload_one_gpu():
+    """--workload products (BASELINE config 5, N = 2,449,029, E' = 126,163,923)
+    on one GPU: the line names the workload, and --verify holds every output
+    row to test_full_size_products_gcn's bound (|out - ref| <= 1e-5 *
+    max(1, sum|w x_j|) against a float64 reference over all edges)."""
+    d, _ = _run_bench(["bench.py", "--workload", "products", "--steps", "3", "--warmup", "1", "--no-cpu-baseline",
+                       "--no-ref-paths", "--verify"])
+    assert d["n_gpus"] == 1 and d["config"]["workload"] == "products_gcn_f256"
+    assert d["config"]["num_nodes"] == 2_449_029 and d["config"]["num_edges"] == 126_163_923
+    assert d["config"]["baseline_config"] == 5
+    v = d["extra"]["verify"]
+    assert v["within_1e-5_bound"] and v["rows"] == 2_449_029 and v["edges"] == 126_163_923, v
+    assert d["value"] > 4e9 and d["roofline"]["frac"] > 0
+
+
+def test_bench_products_workload_two_ranks():
+    """The config-5 workload under bench.py's own N-rank launch: 2 gloo ranks
+    sharing the GPU, slice-built shards, hybrid-cover tiled overlap, every
+    rank's rows within the float64 bound."""
+    d, _ = _run_bench(["bench.py", "--gpus", "2", "--workload", "products", "--steps", "2", "--warmup", "1",
+                       "--no-cpu-baseline", "--no-ref-paths", "--verify"], {"MP_BENCH_BACKEND": "gloo"})
+    assert d["n_gpus"] == 2 and d["config"]["workload"] == "products_gcn_f256"
+    assert d["config"]["num_edges"] == 126_163_923
+    assert d["extra"]["verify"]["all_ranks_within_1e-5_bound"], d["extra"]["verify"]
+    assert sum(p["rows"] for p in d["extra"]["per_rank"]) == 2_449_029
 
 
 def test_bench_sharded_path_over_rccl_one_rank():
@@ -485,6 +638,8 @@ def test_bench_sharded_path_over_rccl_one_rank():
     (p,) = ex["per_rank"]
     assert p["rank"] == 0 and p["halo_bytes_in"] == 0 and p["peers_in"] == [0]
     assert p["interior_ms"] > 0 and p["exchange_exposed_ms"] >= 0
+    dc = p["decomposed"]   # one rank: empty splits, the exchange alone costs ~nothing
+    assert dc["exchange_only_ms"] < 0.2 * dc["compute_only_ms"], dc
     # the same kernels over the whole graph: within 2x of the single-GPU step
     assert d["value"] > 4e9, d["value"]
 

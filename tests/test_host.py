@@ -42,7 +42,7 @@ def test_ctypes_signatures_cover_the_header():
 
 
 def test_abi_version_and_error_string(lib):
-    assert lib.mp_abi_version() == 4
+    assert lib.mp_abi_version() == 5
     assert isinstance(lib.mp_last_error(), bytes)
 
 
@@ -278,3 +278,60 @@ def test_torch_scatter_dispatcher_ops_registered():
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         torch.ops.torch_scatter.segment_sum_csr(torch.ones(3, 2), torch.tensor([0, 2, 3]), None)
 
+
+
+def _bench(args, env_extra, timeout=240):
+    import sys
+    env = dict(os.environ, MP_BENCH_LAUNCH_PROBE="1", MASTER_ADDR="127.0.0.1", **env_extra)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    return subprocess.run([sys.executable] + args, cwd=ROOT, env=env, capture_output=True, text=True,
+                          timeout=timeout)
+
+
+def test_bench_starts_its_own_ranks():
+    """`python bench.py --gpus N` with no launcher (RANK unset) starts N rank
+    processes itself (a torch.distributed.run child) and every rank sees a world
+    of N -- the driver's plain `--gpus 8` call must never silently run one
+    GPU.  MP_BENCH_LAUNCH_PROBE stops the ranks right after the process group
+    is up (gloo, no GPU touched)."""
+    import json
+    r = _bench(["bench.py", "--gpus", "3", "--steps", "1"], {})
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["gpus"] == 3
+    assert sorted(p["rank"] for p in d["launch_probe"]) == [0, 1, 2]
+    assert all(p["world"] == 3 for p in d["launch_probe"])
+    assert "starting 3 ranks" in r.stderr
+
+
+def test_bench_refuses_a_world_that_differs_from_gpus():
+    """Launched by torch.distributed.run with 2 ranks but --gpus 3: every rank
+    exits non-zero before any work (no line claiming n_gpus it did not use)."""
+    port = __import__("socket").socket()
+    port.bind(("127.0.0.1", 0))
+    p = port.getsockname()[1]
+    port.close()
+    r = _bench(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+                "127.0.0.1", "--master-port", str(p), "bench.py", "--gpus", "3"], {})
+    assert r.returncode != 0
+    assert "the job has 2 ranks but --gpus 3" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_arg_backward_has_no_atomic_form(lib):
+    """ABI 5: mp_scatter_arg_backward_f32 is the plain-store form only (message
+    row e belongs to one output row); the float-atomic src_map / grad_w form of
+    ABI <= 4 -- non-deterministic, unused -- is gone from the header, the
+    ctypes signature and the kernel."""
+    from mi355_mp import _lib
+    text = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    decl = re.search(r"int mp_scatter_arg_backward_f32\((.*?)\);", text, flags=re.S).group(1)
+    assert "src_map" not in decl and "grad_w" not in decl and decl.count(",") == 7
+    assert len(_lib.SIGNATURES["mp_scatter_arg_backward_f32"][1]) == 8
+    src = open(os.path.join(ROOT, "pytorch_geometric-1_amd", "csrc", "mp_misc.hip")).read()
+    body = src[src.index("void k_scatter_arg_backward"):]
+    body = body[:body.index("\n}\n")]
+    assert "atomic" not in body
