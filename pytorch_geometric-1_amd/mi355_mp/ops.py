@@ -16,7 +16,7 @@ import os
 import torch
 
 from . import _lib
-from .graph import csr_for_index, in_csr_order
+from .graph import _Cache, csr_for_index, in_csr_order
 
 _REDUCES = ("sum", "add", "mean", "max", "min")
 
@@ -371,16 +371,30 @@ class GatherRows(torch.autograd.Function):
         return gx, None
 
 
+_range_cache = _Cache()
+
+
+def index_range(idx):
+    """(min, max) of an index tensor: one aminmax and one host read the first
+    time, then cached on the tensor (identity + version counter, dropped with
+    it -- graph._Cache), so the per-forward checks of a reused edge_index cost
+    a dictionary lookup, not a device sync."""
+    def compute():
+        mn, mx = torch.aminmax(idx)
+        return tuple(torch.stack([mn, mx]).tolist())
+    return _range_cache.get(idx, "range", compute)
+
+
 def check_row_index(idx, n, what="index_select"):
     """IndexError when an index falls outside [0, n), as x.index_select(0, idx)
     raises on the CPU (the native row gather reads whatever row it is given, so
-    a bad index must never reach it).  One aminmax and one host read; skipped
-    while a HIP graph is being captured (the captured call was checked when it
-    ran eagerly before capture, and a capture cannot read values back)."""
+    a bad index must never reach it).  The range is cached per index tensor
+    (index_range); skipped while a HIP graph is being captured (the captured
+    call was checked when it ran eagerly before capture, and a capture cannot
+    read values back)."""
     if idx.numel() == 0 or (idx.is_cuda and torch.cuda.is_current_stream_capturing()):
         return
-    mn, mx = torch.aminmax(idx)
-    lo, hi = torch.stack([mn, mx]).tolist()
+    lo, hi = index_range(idx)
     if lo < 0 or hi >= n:
         raise IndexError("%s: index %d out of range for %d rows" % (what, lo if lo < 0 else hi, n))
 
@@ -492,8 +506,12 @@ def segment_sum_serial(csr, values, out=None):
 
 def norm_from_degree(row, col, deg, edge_weight):
     """dinv = deg^-1/2 (inf -> 0, torch's CPU pow(-0.5) rounding), then
-    dinv[row] * w * dinv[col] (mp_gcn_norm_from_deg_f32).  deg is consumed."""
+    dinv[row] * w * dinv[col] (mp_gcn_norm_from_deg_f32).  deg is consumed.
+    The kernel reads deg[row[e]] and deg[col[e]]: an id outside [0, deg.numel())
+    raises IndexError first, as the reference's deg_inv_sqrt[row] / [col] does."""
     _lib.require_device(row, col, deg, edge_weight)
+    check_row_index(row, deg.numel(), "gcn_norm (row)")
+    check_row_index(col, deg.numel(), "gcn_norm (col)")
     E = row.numel()
     w = edge_weight.to(torch.float32).contiguous() if edge_weight is not None else None
     norm = torch.empty(E, dtype=torch.float32, device=row.device)

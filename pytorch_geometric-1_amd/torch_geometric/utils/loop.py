@@ -57,8 +57,12 @@ def _loops(edge_index, num_nodes, mode):
 def _weights(edge_weight, pos, fill_value):
     if edge_weight.is_cuda:
         return _ops.gather_fill(edge_weight, pos, fill_value)
-    v = edge_weight[pos.clamp(min=0)]
-    return torch.where(pos >= 0, v, torch.full_like(v, fill_value))
+    # gather only where an input edge exists: with no input edges (E == 0) the
+    # weights are all fill values, as upstream's concatenation gives
+    out = torch.full((pos.numel(),) + tuple(edge_weight.shape[1:]), fill_value, dtype=edge_weight.dtype)
+    has = pos >= 0
+    out[has] = edge_weight[pos[has]]
+    return out
 
 
 def remove_self_loops(edge_index, edge_attr=None):

@@ -384,16 +384,57 @@ def scatter_std(src, index, dim=-1, out=None, dim_size=None, unbiased=True):
 # dispatcher registration (torch.ops.torch_scatter.*)
 # ---------------------------------------------------------------------------
 
+def _out_rows(*cands):
+    """First known row count among cands (None = unknown), else a data-dependent
+    size from the fake-tensor context (like nonzero's)."""
+    for c in cands:
+        if c is not None:
+            return int(c)
+    return torch.library.get_ctx().new_dynamic_size()
+
+
+def _with_rows(t, rows, dim=0):
+    size = list(t.shape)
+    size[dim] = rows
+    return size
+
+
+def _arg_grad(grad, arg, src_shape, dim):
+    """torch_scatter's ScatterMax / SegmentMax backward: grad_src =
+    zeros(size with src.size(dim) + 1).scatter_(dim, arg, grad).narrow(dim, 0,
+    src.size(dim)) -- the extra slice absorbs the empty-segment sentinel; each
+    (position, column) is stored at most once (plain stores, deterministic)."""
+    size = list(src_shape)
+    n = size[dim]
+    size[dim] = n + 1
+    return grad.new_zeros(size).scatter_(dim, arg, grad).narrow(dim, 0, n)
+
+
+def _csr_counts(indptr):
+    return indptr[1:] - indptr[:-1]
+
+
 def _register_ops():
+    """torch_scatter 2.0.4's compiled ops on the dispatcher, split by key like a
+    compiled extension: the HIP engine on CUDA (ROCm) tensors; CPU tensors
+    raise (no CPU path); a fake (meta) kernel per op for shape propagation
+    under FakeTensor / torch.compile tracing (torch.library.register_fake);
+    and each op's backward (torch.library.register_autograd) on the same
+    native ops -- scatter / segment min-max by their arg, sums and means by the
+    matching gather, gathers by the matching segment sum."""
     try:
         lib = torch.library.Library("torch_scatter", "DEF")
     except RuntimeError:  # namespace already defined by another loader
         return None
+
+    def arg_op(reduce):
+        return lambda s, i, d, o, n: _reduce(s, i, d, o, n, reduce)
+
     defs = {
         "scatter_max": ("(Tensor src, Tensor index, int dim, Tensor? optional_out, int? dim_size) -> (Tensor, Tensor)",
-                        lambda s, i, d, o, n: scatter_max(s, i, d, o, n)),
+                        arg_op("max")),
         "scatter_min": ("(Tensor src, Tensor index, int dim, Tensor? optional_out, int? dim_size) -> (Tensor, Tensor)",
-                        lambda s, i, d, o, n: scatter_min(s, i, d, o, n)),
+                        arg_op("min")),
         "segment_sum_csr": ("(Tensor src, Tensor indptr, Tensor? optional_out) -> Tensor",
                             lambda s, p, o: segment_csr(s, p, o, "sum")),
         "segment_mean_csr": ("(Tensor src, Tensor indptr, Tensor? optional_out) -> Tensor",
@@ -415,9 +456,114 @@ def _register_ops():
         "gather_coo": ("(Tensor src, Tensor index, Tensor? optional_out) -> Tensor",
                        lambda s, i, o: gather_coo(s, i, o)),
     }
+
+    # --- fake kernels: output shapes only (no data_ptr, no launch)
+    def fake_scatter(src, index, dim, out, dim_size):
+        d = dim % src.dim()
+        rows = _out_rows(out.size(d) if out is not None else None, dim_size)
+        size = _with_rows(src, rows, d)
+        return src.new_empty(size), src.new_empty(size, dtype=torch.int64)
+
+    def fake_seg_csr(src, indptr, out):
+        size = _with_rows(src, indptr.numel() - 1)
+        return src.new_empty(size)
+
+    def fake_seg_csr_arg(src, indptr, out):
+        size = _with_rows(src, indptr.numel() - 1)
+        return src.new_empty(size), src.new_empty(size, dtype=torch.int64)
+
+    def fake_gather_csr(src, indptr, out):
+        return src.new_empty(_with_rows(src, _out_rows(out.size(0) if out is not None else None)))
+
+    def fake_seg_coo(src, index, out, dim_size):
+        return src.new_empty(_with_rows(src, _out_rows(out.size(0) if out is not None else None, dim_size)))
+
+    def fake_seg_coo_arg(src, index, out, dim_size):
+        size = _with_rows(src, _out_rows(out.size(0) if out is not None else None, dim_size))
+        return src.new_empty(size), src.new_empty(size, dtype=torch.int64)
+
+    def fake_gather_coo(src, index, out):
+        return src.new_empty(_with_rows(src, index.numel()))
+
+    fakes = {"scatter_max": fake_scatter, "scatter_min": fake_scatter, "segment_sum_csr": fake_seg_csr,
+             "segment_mean_csr": fake_seg_csr, "segment_min_csr": fake_seg_csr_arg,
+             "segment_max_csr": fake_seg_csr_arg, "gather_csr": fake_gather_csr, "segment_sum_coo": fake_seg_coo,
+             "segment_mean_coo": fake_seg_coo, "segment_min_coo": fake_seg_coo_arg,
+             "segment_max_coo": fake_seg_coo_arg, "gather_coo": fake_gather_coo}
+
+    # --- autograd: d src only (index / indptr carry none); through optional_out unsupported
+    def make_setup(name):
+        scatter = name.startswith("scatter")
+
+        def setup(ctx, inputs, output):
+            ctx.src_shape = tuple(inputs[0].shape)
+            ctx.index = inputs[1]
+            ctx.dim = inputs[2] % max(1, inputs[0].dim()) if scatter else 0
+            ctx.has_out = (inputs[3] if scatter else inputs[2]) is not None
+            pair = isinstance(output, (tuple, list))
+            ctx.arg = output[1] if pair else None
+            ctx.out_rows = (output[0] if pair else output).shape[0]
+        return setup
+
+    def no_out(ctx, name):
+        if ctx.has_out:
+            raise NotImplementedError("torch_scatter::%s: autograd through optional_out is not supported" % name)
+
+    def bwd_arg(name):
+        def f(ctx, grad, _grad_arg=None):
+            no_out(ctx, name)
+            g = _arg_grad(grad.contiguous(), ctx.arg, ctx.src_shape, ctx.dim)
+            return (g,) + (None,) * (4 if name.startswith("scatter") else (3 if name.endswith("coo") else 2))
+        return f
+
+    def bwd_sum_csr(ctx, grad):
+        no_out(ctx, "segment_sum_csr")
+        return gather_csr(grad.contiguous(), ctx.index), None, None
+
+    def bwd_mean_csr(ctx, grad):
+        no_out(ctx, "segment_mean_csr")
+        cnt = _csr_counts(ctx.index).clamp(min=1).to(grad.dtype).view((-1,) + (1,) * (grad.dim() - 1))
+        return gather_csr((grad / cnt).contiguous(), ctx.index), None, None
+
+    def bwd_gather_csr(ctx, grad):
+        no_out(ctx, "gather_csr")
+        return segment_csr(grad.contiguous(), ctx.index, None, "sum"), None, None
+
+    def bwd_sum_coo(ctx, grad):
+        no_out(ctx, "segment_sum_coo")
+        return gather_coo(grad.contiguous(), ctx.index), None, None, None
+
+    def bwd_mean_coo(ctx, grad):
+        no_out(ctx, "segment_mean_coo")
+        cnt = torch.bincount(ctx.index, minlength=ctx.out_rows)[:ctx.out_rows].clamp(min=1).to(grad.dtype)
+        cnt = cnt.view((-1,) + (1,) * (grad.dim() - 1))
+        return gather_coo((grad / cnt).contiguous(), ctx.index), None, None, None
+
+    def bwd_gather_coo(ctx, grad):
+        no_out(ctx, "gather_coo")
+        return scatter_sum(grad.contiguous(), ctx.index, 0, dim_size=ctx.src_shape[0]), None, None
+
+    bwds = {"scatter_max": bwd_arg("scatter_max"), "scatter_min": bwd_arg("scatter_min"),
+            "segment_sum_csr": bwd_sum_csr, "segment_mean_csr": bwd_mean_csr,
+            "segment_min_csr": bwd_arg("segment_min_csr"), "segment_max_csr": bwd_arg("segment_max_csr"),
+            "gather_csr": bwd_gather_csr, "segment_sum_coo": bwd_sum_coo, "segment_mean_coo": bwd_mean_coo,
+            "segment_min_coo": bwd_arg("segment_min_coo"), "segment_max_coo": bwd_arg("segment_max_coo"),
+            "gather_coo": bwd_gather_coo}
+
+    def below_autograd(fn):
+        # the kernel runs below autograd (the op's backward is registered below):
+        # the engine's own autograd Functions only run their forward here
+        def k(*args):
+            with torch.no_grad():
+                return fn(*args)
+        return k
+
     for name, (schema, fn) in defs.items():
         lib.define(name + schema)
-        lib.impl(name, fn, "CompositeImplicitAutograd")
+        lib.impl(name, below_autograd(fn), "CUDA")
+        lib.impl(name, below_autograd(fn), "CPU")   # raises: mi355_mp has no CPU fallback (_lib.require_device)
+        torch.library.register_fake("torch_scatter::" + name, fakes[name], lib=lib)
+        torch.library.register_autograd("torch_scatter::" + name, bwds[name], setup_context=make_setup(name), lib=lib)
     return lib
 
 

@@ -413,3 +413,48 @@ def test_sharded_gat_matches_single_process(world):
     for rank, r in res:
         assert r["slices_equal"] and r["out_equal"] and r["alpha_equal"], r
         assert r["gx"] <= 0 and r["gw"] <= 0 and r["gatt"] <= 0 and r["gb"] <= 0, r
+
+
+def _bad_slice_worker(rank, world, port, result_q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "pytorch_geometric-1_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mi355_mp import dist as mdist
+        N = 50
+        ei = torch.randint(N, (2, 400), generator=torch.Generator().manual_seed(3))
+        ei[1, 390] = N + 4                          # only the LAST rank's slice holds the bad id
+        s0, s1 = rank * 400 // world, (rank + 1) * 400 // world
+        raised = []
+        for fn in (mdist.ShardedGraph.for_gcn_from_slices, mdist.ShardedGraph.for_gat_from_slices):
+            try:
+                fn(ei[:, s0:s1].clone(), s0, N, rank, world)
+                raised.append(False)
+            except IndexError:
+                raised.append(True)
+        result_q.put((rank, raised))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_slice_build_rejects_out_of_range_ids_on_every_rank(world):
+    """An edge id outside [0, N) in one rank's slice: every rank raises
+    IndexError before the first collective whose size depends on N (no hang, no
+    all_reduce of vectors of different lengths)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bad_slice_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    res = sorted(q.get(timeout=10) for _ in range(world))
+    assert all(r[1] == [True, True] for r in res), res

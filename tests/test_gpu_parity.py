@@ -1569,6 +1569,67 @@ def test_torch_scatter_coo_csr_and_dispatcher_ops():
     assert torch.equal(scripted(sd, indptr.to(DEV)).cpu(), S.scatter_sum(src, index, N))
 
 
+def test_torch_scatter_dispatcher_ops_autograd():
+    """The dispatcher ops' registered backward (torch.library.register_autograd)
+    equals the autograd of the Python-level torch_scatter functions bit for bit
+    (both run the native kernels): every op, 1-D index along dim 0 and an
+    element-wise index along dim -1; through optional_out it raises."""
+    import torch_scatter as TS
+    ops = torch.ops.torch_scatter
+    g = torch.Generator().manual_seed(73)
+    E, N, F = 3000, 200, 12
+    index = torch.sort(torch.randint(0, N, (E,), generator=g)).values.to(DEV)
+    counts = torch.bincount(index, minlength=N)
+    indptr = torch.cat([torch.zeros(1, dtype=torch.long, device=DEV), counts.cumsum(0)])
+    src = (torch.randint(-3, 4, (E, F), generator=g).to(torch.float32)).to(DEV)
+    gsrc = torch.randn(E, F, generator=g).to(DEV)
+    gnode = torch.randn(N, F, generator=g).to(DEV)
+    rows = torch.randn(N, F, generator=g).to(DEV)
+
+    def grad_of(fn, x, gout):
+        x = x.clone().requires_grad_(True)
+        y = fn(x)
+        y = y[0] if isinstance(y, tuple) else y
+        (y * gout).sum().backward()
+        return x.grad
+    cases = [
+        (lambda x: ops.scatter_max(x, index, 0, None, N), lambda x: TS.scatter_max(x, index, 0, dim_size=N), src, gnode),
+        (lambda x: ops.scatter_min(x, index, 0, None, N), lambda x: TS.scatter_min(x, index, 0, dim_size=N), src, gnode),
+        (lambda x: ops.segment_sum_csr(x, indptr, None), lambda x: TS.segment_csr(x, indptr, reduce="sum"), src, gnode),
+        (lambda x: ops.segment_mean_csr(x, indptr, None), lambda x: TS.segment_csr(x, indptr, reduce="mean"), src,
+         gnode),
+        (lambda x: ops.segment_max_csr(x, indptr, None), lambda x: TS.segment_csr(x, indptr, reduce="max"), src, gnode),
+        (lambda x: ops.segment_min_csr(x, indptr, None), lambda x: TS.segment_csr(x, indptr, reduce="min"), src, gnode),
+        (lambda x: ops.gather_csr(x, indptr, None), lambda x: TS.gather_csr(x, indptr), rows, gsrc),
+        (lambda x: ops.segment_sum_coo(x, index, None, N), lambda x: TS.segment_coo(x, index, dim_size=N), src, gnode),
+        (lambda x: ops.segment_mean_coo(x, index, None, N),
+         lambda x: TS.segment_coo(x, index, dim_size=N, reduce="mean"), src, gnode),
+        (lambda x: ops.segment_max_coo(x, index, None, N),
+         lambda x: TS.segment_coo(x, index, dim_size=N, reduce="max"), src, gnode),
+        (lambda x: ops.segment_min_coo(x, index, None, N),
+         lambda x: TS.segment_coo(x, index, dim_size=N, reduce="min"), src, gnode),
+        (lambda x: ops.gather_coo(x, index, None), lambda x: TS.gather_coo(x, index), rows, gsrc),
+    ]
+    for k, (op, py, x, gout) in enumerate(cases):
+        a, b = grad_of(op, x, gout), grad_of(py, x, gout)
+        # the mean's backward divides by the count in either order: equal to rounding
+        if k in (3, 8):
+            assert torch.allclose(a, b, rtol=1e-6, atol=0), k
+        else:
+            assert torch.equal(a, b), k
+    # element-wise index along the last dim (torch_scatter README shape)
+    s2 = torch.tensor(_README_SRC, dtype=torch.float32, device=DEV)
+    i2 = torch.tensor(_README_INDEX, device=DEV)
+    g2 = torch.randn(2, 6, generator=g).to(DEV)
+    a = grad_of(lambda x: ops.scatter_max(x, i2, -1, None, 6), s2, g2)
+    b = grad_of(lambda x: TS.scatter_max(x, i2, -1, dim_size=6), s2, g2)
+    assert torch.equal(a, b)
+    with pytest.raises(NotImplementedError):
+        x = src.clone().requires_grad_(True)
+        out = torch.zeros(N, F, device=DEV)
+        ops.segment_sum_coo(x, index, out, None).sum().backward()
+
+
 # torch_scatter's README scatter_max example (element-wise 2-D index, dim=-1),
 # with the output and argmax printed there
 _README_SRC = [[2, 0, 1, 4, 3], [0, 2, 1, 3, 4]]
@@ -2361,6 +2422,22 @@ def test_row_gather_out_of_range_raises():
         for w in (None, torch.rand(ei.shape[1], device=DEV)):
             with pytest.raises(IndexError):
                 GCNConv(4, 4).to(DEV)(x, ei, w)
+    # get_laplacian's exact 'sym' branch reads deg[row] and deg[col] on the device:
+    # a column (or row) outside [0, num_nodes) raises, as deg_inv_sqrt[col] does upstream
+    from torch_geometric.utils import get_laplacian
+    for bad_ei in ([[0, 1, 2], [1, 2, N + 3]], [[0, 1, 2], [1, 2, -1]], [[0, N + 1], [1, 2]]):
+        ei = torch.tensor(bad_ei, device=DEV)
+        for w in (None, torch.rand(ei.shape[1], device=DEV)):
+            with pytest.raises(IndexError):
+                get_laplacian(ei, w, "sym", num_nodes=N)
+    # the range check is cached on the index tensor: a second check reads no device value
+    from mi355_mp import ops as _o
+    idx = torch.tensor([0, 3, 9], device=DEV)
+    _o.check_row_index(idx, N)
+    assert _o.index_range(idx) == (0, 9)
+    idx[1] = N            # an in-place write bumps the version: checked again
+    with pytest.raises(IndexError):
+        _o.check_row_index(idx, N)
     torch.cuda.synchronize()
 
 

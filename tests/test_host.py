@@ -335,3 +335,68 @@ def test_arg_backward_has_no_atomic_form(lib):
     body = src[src.index("void k_scatter_arg_backward"):]
     body = body[:body.index("\n}\n")]
     assert "atomic" not in body
+
+
+def test_loop_utilities_host_no_edges_with_weights():
+    """add_self_loops / add_remaining_self_loops on host tensors with E == 0
+    edges and an empty weight vector: the N loops with the fill value, as
+    upstream's concatenation gives (no gather from the empty weights)."""
+    from torch_geometric.utils import add_remaining_self_loops, add_self_loops, remove_self_loops
+    from oracle import pyg_ref as P
+    ei = torch.zeros((2, 0), dtype=torch.long)
+    w = torch.zeros(0)
+    for fn, ref in ((add_self_loops, P.add_self_loops), (add_remaining_self_loops, P.add_remaining_self_loops)):
+        a = fn(ei, w, 2.0, 4)
+        b = ref(ei, w, 2.0, 4)
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+        assert a[0].tolist() == [[0, 1, 2, 3], [0, 1, 2, 3]] and a[1].tolist() == [2.0] * 4
+    a = remove_self_loops(ei, w)
+    assert a[0].shape == (2, 0) and a[1].numel() == 0
+    # the weight gradient still flows through the host rewrite
+    wr = torch.rand(3, requires_grad=True)
+    _, ww = add_remaining_self_loops(torch.tensor([[0, 1, 1], [1, 1, 0]]), wr, 1.0, 3)
+    ww.sum().backward()
+    assert wr.grad.tolist() == [1.0, 1.0, 1.0]
+
+
+def test_torch_scatter_dispatcher_ops_under_fake_tensors():
+    """Every torch.ops.torch_scatter.* op propagates shapes under FakeTensorMode
+    (register_fake kernels: no data_ptr, no launch) -- static sizes where
+    dim_size / out / the index length fix them, data-dependent ones (like
+    nonzero's) under a ShapeEnv; each op also has a registered backward."""
+    import torch_scatter  # noqa: F401
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    from torch.fx.experimental.symbolic_shapes import ShapeEnv
+    ops = torch.ops.torch_scatter
+    with FakeTensorMode(shape_env=ShapeEnv()) as m:
+        src = m.from_tensor(torch.randn(6, 3, 2))
+        idx = m.from_tensor(torch.tensor([0, 0, 1, 2, 2, 2]))
+        ptr = m.from_tensor(torch.tensor([0, 2, 3, 6]))
+        o, a = ops.scatter_max(src, idx, 0, None, 5)
+        assert o.shape == (5, 3, 2) and a.shape == (5, 3, 2) and a.dtype == torch.int64
+        o, a = ops.scatter_min(src, m.from_tensor(torch.zeros(2, dtype=torch.long)), 2, None, 4)
+        assert o.shape == (6, 3, 4) and a.dtype == torch.int64
+        o, _ = ops.scatter_max(src, idx, 0, m.from_tensor(torch.zeros(7, 3, 2)), None)
+        assert o.shape == (7, 3, 2)
+        for n in ("segment_sum_csr", "segment_mean_csr"):
+            assert getattr(ops, n)(src, ptr, None).shape == (3, 3, 2)
+        for n in ("segment_min_csr", "segment_max_csr"):
+            o, a = getattr(ops, n)(src, ptr, None)
+            assert o.shape == (3, 3, 2) and a.dtype == torch.int64
+        for n in ("segment_sum_coo", "segment_mean_coo"):
+            assert getattr(ops, n)(src, idx, None, 4).shape == (4, 3, 2)
+        for n in ("segment_min_coo", "segment_max_coo"):
+            o, a = getattr(ops, n)(src, idx, None, 4)
+            assert o.shape == (4, 3, 2) and a.dtype == torch.int64
+        assert ops.gather_coo(m.from_tensor(torch.randn(3, 5)), idx, None).shape == (6, 5)
+        # data-dependent row counts become unbacked symbolic sizes
+        g = ops.gather_csr(m.from_tensor(torch.randn(3, 5)), ptr, None)
+        assert isinstance(g.shape[0], torch.SymInt) and g.shape[1] == 5
+        s = ops.segment_sum_coo(src, idx, None, None)
+        assert isinstance(s.shape[0], torch.SymInt)
+    for n in ("scatter_max", "scatter_min", "segment_sum_csr", "segment_mean_csr", "segment_min_csr",
+              "segment_max_csr", "gather_csr", "segment_sum_coo", "segment_mean_coo", "segment_min_coo",
+              "segment_max_coo", "gather_coo"):
+        op = getattr(ops, n).default
+        assert torch._C._dispatch_has_kernel_for_dispatch_key(op.name(), "CUDA"), n
+        assert torch._C._dispatch_has_kernel_for_dispatch_key(op.name(), "Autograd"), n
