@@ -357,6 +357,59 @@ def test_full_size_products_sharded_rehearsal(world):
             assert excess_c <= 0 and rows_c < n_halo, res
 
 
+def _gat_full_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "pytorch_geometric-1_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mi355_mp import dist as mdist, ops
+        from mi355_mp.graph import GAT_TARGET_TASKS, Graph
+        from mi355_mp.graphgen import rmat_edge_index
+        from torch_geometric.nn.conv._structure import gat_loops
+        dev = torch.device("cuda", 0)
+        N, H, C = 1 << 21, 8, 32
+        ei = rmat_edge_index(scale=21, n_samples=30_000_000, seed=1, device=dev)
+        g = torch.Generator(device=dev).manual_seed(2)
+        xw = torch.randn(N, H * C, device=dev, generator=g) * 0.5
+        att = torch.randn(1, H, 2 * C, device=dev, generator=g) * 0.2
+        E_raw = ei.shape[1]
+        s0, s1 = rank * E_raw // world, (rank + 1) * E_raw // world
+        sg = mdist.ShardedGraph.for_gat_from_slices(ei[:, s0:s1].clone(), s0, N, rank, world)
+        lo, hi = sg.lo, sg.hi
+        out, (gid, alpha) = sg.gat_propagate(xw[lo:hi].contiguous(), att, H, C, return_alpha=True)
+        # the single-GPU fused kernel on the whole graph, and the bound's sum |alpha x_j|
+        ei2 = gat_loops(ei, N)
+        del ei
+        g1 = Graph(ei2, N, N, target_tasks=GAT_TARGET_TASKS)
+        out1, alpha1 = ops.gat_propagate(g1, ei2, xw, att, H, C, return_alpha=True)
+        eid = g1.dst.eid[:g1.dst.n_edges].long()
+        terms = ops._heads_aggregate(g1.dst, "other", alpha1[eid].contiguous(), H, xw.abs())[lo:hi]
+        excess = float(((out - out1[lo:hi]).abs() - 1e-5 * terms.clamp(min=1.0)).max())
+        da = (alpha - alpha1[gid]).abs()
+        q.put((rank, excess, float(da.max()), float((da == 0).float().mean()),
+               float((out == out1[lo:hi]).float().mean()), sg.n_edges == ei2.shape[1], hi - lo))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_full_size_gat_sharded_rehearsal():
+    """Config 3 at full size (RMAT21 + self loops, 8 heads x 32) sharded over 2
+    ranks sharing the device, built from per-rank edge slices: every rank's
+    rows within 1e-5 * max(1, sum|alpha x_j|) of the single-GPU fused kernel and
+    every (edge, head) alpha within 1e-5 of it (bit-equal on all but the rows a
+    task boundary splits)."""
+    res = _spawn(_gat_full_worker, world=2, timeout=900)
+    assert sum(r[6] for r in res) == 1 << 21
+    for rank, excess, dalpha, a_eq, o_eq, edges_ok, _ in res:
+        assert excess <= 0 and dalpha <= 1e-5 and edges_ok, res
+        assert a_eq > 0.95 and o_eq > 0.9, res
+
+
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
 @pytest.mark.parametrize("flow", ["source_to_target", "target_to_source"])
 def test_native_shard_plan_matches_torch_plan(world, flow):
