@@ -1,6 +1,6 @@
 """Summarise rocprofv3 output of tools/profile.sh into profiles/<round>_*.
 
-  python tools/pmc_summary.py gpurun_out/prof r01
+  python tools/pmc_summary.py gpurun_out/prof r01 [workload] [calib_dir]
 
 Writes profiles/<round>_kernel_stats.csv (copy of the --stats summary),
 profiles/<round>_pmc_traffic.json: per-launch FETCH_SIZE / WRITE_SIZE of the
@@ -36,8 +36,11 @@ def per_launch(path, counter):
 
 def main():
     src, rnd = sys.argv[1], sys.argv[2]
+    workload = sys.argv[3] if len(sys.argv) > 3 else "rmat21_gcn_f256"
+    calib_dir = sys.argv[4] if len(sys.argv) > 4 else src
+    suffix = "" if workload == "rmat21_gcn_f256" else "_" + workload.split("_")[0]
     os.makedirs("profiles", exist_ok=True)
-    shutil.copy(os.path.join(src, "kt", "kt_kernel_stats.csv"), "profiles/%s_kernel_stats.csv" % rnd)
+    shutil.copy(os.path.join(src, "kt", "kt_kernel_stats.csv"), "profiles/%s_kernel_stats%s.csv" % (rnd, suffix))
     global KERNEL
     avg_ns, best = None, -1.0
     for r in csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_stats.csv"))):
@@ -52,7 +55,7 @@ def main():
     # this kernel's own FETCH_SIZE ratio, measured on a known byte count by
     # tools/pmc_calibrate.py in the same profile run (pass pmc_calib)
     ratio = None
-    calib = os.path.join(src, "pmc_calib", "pmc_counter_collection.csv")
+    calib = os.path.join(calib_dir, "pmc_calib", "pmc_counter_collection.csv")
     if os.path.exists(calib):
         cv, _ = per_launch(calib, "FETCH_SIZE")
         if cv:
@@ -92,7 +95,7 @@ def main():
         # summed over the 16 L2 channels of each of the 8 XCDs
         mem["dram_credit_stall_frac_per_channel"] = mem["TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum"] / (128 * cyc)
     out = {
-        "workload": "rmat21_gcn_f256",
+        "workload": workload,
         "kernel": KERNEL,
         "source_hash": source_hash(),
         "launches": {"fetch": nf, "write": nw},
@@ -111,7 +114,7 @@ def main():
                 "on HBM reads; doubled per the gfx950 correction (calibrated for this kernel's own "
                 "load width in profiles/r01_pmc_calibration.json)",
     }
-    with open("profiles/%s_pmc_traffic.json" % rnd, "w") as f:
+    with open("profiles/%s_pmc_traffic%s.json" % (rnd, suffix), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
 
