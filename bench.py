@@ -18,6 +18,11 @@ Workloads (one GCNConv propagate per step, F = 256, fp32):
   products (BASELINE.json configs[4], the 8 x MI355X configuration)
            ogbn-products scale power-law graph, N = 2,449,029,
            E = 123,718,280 (E' = 126,163,923), x ~ N(0,1), seed 4.
+  gat      (BASELINE.json configs[2]) the rmat21 graph, GATConv 8 heads x 32:
+           one step = the fused node scores + leaky_relu + softmax + aggregate +
+           bias (mp_gat_forward_f32); N > 1: the X W halo rows over the pull
+           plan, then the fused kernels on the rank's local graph
+           (ShardedGraph.gat_propagate) -- metric: GAT edges/s.
 One step = the fused gather * norm -> segment-sum + bias HIP kernel (plus its
 split-row fix-up) over all E' edges.  The CSR / schedule / norm build
 (one-time, cached=True semantics) and the x @ W GEMM are timed separately and
@@ -78,6 +83,9 @@ def _products(dev):
 
 
 WORKLOADS = {
+    "gat": {"name": "rmat21_gat_h8c32", "num_nodes": 1 << 21, "seed": 2, "gen": _rmat21,
+            "baseline_config": 3,
+            "graph": "RMAT scale 21 (.57,.19,.19,.05) 30M samples symmetrised + remove/add self loops (GATConv)"},
     "rmat21": {"name": "rmat21_gcn_f256", "num_nodes": 1 << 21, "seed": 1, "gen": _rmat21,
                "baseline_config": 2,
                "graph": "RMAT scale 21 (.57,.19,.19,.05) 30M samples symmetrised + add_remaining_self_loops"},
@@ -377,6 +385,207 @@ def find_pmc(workload, kernel, src_hash):
     return None, "no committed profile of this build's kernel on %s" % workload
 
 
+def cpu_gat_baseline(ei, xw, att, H, C, sample):
+    """GATConv's reference pipeline after x @ W on the host (oracle, kind
+    'port'): x_i / x_j index_select, (cat[x_i, x_j] * att).sum(-1), leaky_relu,
+    utils.softmax (serial scatter_max loop + scatter_add_), x_j * alpha,
+    scatter_add_ -- on the first `sample` edges."""
+    import torch.nn.functional as Fn
+    from oracle import pyg_ref as P, scatter_ref as S  # checker/baseline only
+    model, threads, machine = cpu_info()
+    torch.set_num_threads(threads)
+    E = min(sample, ei.shape[1])
+    eic, h, a = ei[:, :E].cpu(), xw.cpu(), att.cpu()
+    N = h.shape[0]
+    t0 = time.perf_counter()
+    x_i = h.index_select(0, eic[1]).view(-1, H, C)
+    x_j = h.index_select(0, eic[0]).view(-1, H, C)
+    alpha = Fn.leaky_relu((torch.cat([x_i, x_j], dim=-1) * a).sum(dim=-1), 0.2)
+    alpha = P.softmax(alpha, eic[1], N)
+    out = S.scatter_sum(x_j * alpha.view(-1, H, 1), eic[1], N)
+    dt = time.perf_counter() - t0
+    del out, x_i, x_j
+    return {"value": E / dt, "unit": "edges/s", "cores": threads, "kind": "port", "cpu_model": model,
+            "machine_cpus": machine, "sample": "first %d of %d edges, oracle GATConv pipeline (torch CPU ops + "
+            "serial scatter_max loop in the softmax), %d threads, %.1f s" % (E, ei.shape[1], threads, dt)}
+
+
+def main_gat(args, rank, world, local):
+    """--workload gat: BASELINE config 3 (GATConv 8 heads x 32 on the rmat21
+    graph), one step = one fused GAT propagate over all E' edges (N = 1), or
+    per rank the pull exchange of the X W halo rows then the fused kernels on
+    the rank's local graph (N > 1)."""
+    from mi355_mp import ops
+    from mi355_mp.graph import GAT_TARGET_TASKS, Graph
+    from torch_geometric.nn.conv._structure import gat_loops
+    import mi355_mp
+    mi355_mp.load_native()
+    wl = WORKLOADS["gat"]
+    sharded = dist.is_initialized()
+    dev = torch.device("cuda", local)
+    N, H, C = wl["num_nodes"], 8, 32
+    F = H * C
+    t0 = time.perf_counter()
+    ei = wl["gen"](dev)
+    g = torch.Generator(device=dev).manual_seed(wl["seed"])
+    xw_full = torch.randn(N, F, device=dev, generator=g)
+    att = torch.randn(1, H, 2 * C, device=dev, generator=g) * 0.1
+    bias = torch.randn(F, device=dev, generator=g) * 0.1
+    torch.cuda.synchronize()
+    t_gen = time.perf_counter() - t0
+    stage(rank, "gat graph generated (%.1f s)" % t_gen)
+    t0 = time.perf_counter()
+    if not sharded:
+        ei2 = gat_loops(ei, N)
+        del ei
+        graph = Graph(ei2, N, N, target_tasks=GAT_TARGET_TASKS)     # as GATConv builds it
+        graph.dst                                                     # the one-time build
+        E2 = E_local = ei2.shape[1]
+        xw = xw_full
+        n_rows, n_src = N, N
+
+        def step():
+            return ops.gat_propagate(graph, ei2, xw, att, H, C, 0.2, bias)[0]
+    else:
+        from mi355_mp import dist as mdist
+        E_raw = ei.shape[1]
+        s0, s1 = rank * E_raw // world, (rank + 1) * E_raw // world
+        sg = mdist.ShardedGraph.for_gat_from_slices(ei[:, s0:s1].clone(), s0, N, rank, world)
+        del ei
+        sg.g_fwd.dst                                                  # the one-time build
+        E2, E_local = sg.n_edges, int(sg.fwd.edge_pos.numel())
+        xw = xw_full[sg.lo:sg.hi].contiguous()
+        n_rows, n_src = sg.n_own, sg.fwd.n_local_src
+        stage(rank, "gat shards built: %d rows, %d in-edges, %d halo rows" % (n_rows, E_local, n_src - n_rows))
+
+        def step():
+            return sg.gat_propagate(xw, att, H, C, 0.2, bias)[0]
+    del xw_full
+    torch.cuda.synchronize()
+    t_build = time.perf_counter() - t0
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        barrier(world)
+        stage(rank, "warm-up done (%d steps)" % args.warmup)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = step()
+        torch.cuda.synchronize()
+        barrier(world)
+        torch.cuda.synchronize()
+        dt_local = dt = time.perf_counter() - t0
+        if sharded:
+            tt = torch.tensor([dt], dtype=torch.float64)
+            tt = tt.to(dev) if dist.get_backend() == "nccl" else tt
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            dt = float(tt.item())
+        stage(rank, "timed steps done: %.3f ms/step (max over ranks)" % (dt / args.steps * 1e3))
+        # the step's kernel time on this rank (HIP events over back-to-back steps; N > 1:
+        # the exchange alone and the local fused kernels alone, in the same process)
+        reps = max(args.steps, 10)
+        split = {}
+        if sharded:
+            xl = mdist.halo_rows(xw, sg.fwd, sg.group)
+
+            def exchange():
+                mdist.halo_rows(xw, sg.fwd, sg.group)
+
+            def local():
+                ops.gat_propagate(sg.g_fwd, sg.fwd.local_edge_index, xl, att, H, C, 0.2, bias)
+            for name, fn in (("exchange_only_ms", exchange), ("compute_only_ms", local)):
+                barrier(world)
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                for _ in range(reps):
+                    fn()
+                torch.cuda.synchronize()
+                split[name] = (time.perf_counter() - t1) / reps * 1e3
+            kern_ms = split["compute_only_ms"]
+        else:
+            kern_ms = _ev_ms(step, reps)
+        verify = None
+        if args.verify:
+            # alpha (by global edge id) and the rows against the single-GPU fused kernel's
+            # formula in float64 over this rank's edges (edge chunks)
+            ei_l = sg.fwd.local_edge_index if sharded else ei2
+            xs = xl if sharded else xw
+            src, dst = ei_l[0], ei_l[1]
+            x3 = xs.view(-1, H, C).double()
+            a_dst = (x3 * att[:, :, :C].double()).sum(-1)
+            a_src = (x3 * att[:, :, C:].double()).sum(-1)
+            del x3
+            m = torch.full((n_rows, H), float("-inf"), device=dev, dtype=torch.float64)
+            den = torch.zeros(n_rows, H, device=dev, dtype=torch.float64)
+            ref = torch.zeros(n_rows, H, C, device=dev, dtype=torch.float64)
+            terms = torch.zeros_like(ref)
+            step_e = 4_000_000
+            for pss in range(3):
+                for s in range(0, src.numel(), step_e):
+                    sl = slice(s, s + step_e)
+                    sc = torch.nn.functional.leaky_relu(a_dst[dst[sl]] + a_src[src[sl]], 0.2)
+                    if pss == 0:
+                        m.scatter_reduce_(0, dst[sl].view(-1, 1).expand(-1, H), sc, "amax")
+                    elif pss == 1:
+                        den.index_add_(0, dst[sl], torch.exp(sc - m[dst[sl]]))
+                    else:
+                        a = torch.exp(sc - m[dst[sl]]) / (den[dst[sl]] + 1e-16)
+                        msg = a.unsqueeze(-1) * xs.view(-1, H, C)[src[sl]].double()
+                        ref.index_add_(0, dst[sl], msg)
+                        terms.index_add_(0, dst[sl], msg.abs())
+                        del msg
+            ref = ref.view(n_rows, F) + bias.double()
+            excess = float(((out.double() - ref).abs() - 1e-5 * terms.view(n_rows, F).clamp(min=1.0)).max())
+            verify = {"rows": n_rows, "edges": int(src.numel()), "bound_excess": excess,
+                      "within_1e-5_bound": excess <= 0,
+                      "reference": "float64 GATConv formula over the rank's edges (edge chunks)"}
+            del ref, terms
+            stage(rank, "verify: %s" % json.dumps(verify))
+    comp = n_src * F * 4 + n_rows * F * 4 + E_local * 4 + (n_rows + 1) * 4
+    ranks = None
+    if sharded:
+        mine = {"rank": rank, "rows": n_rows, "edges": E_local, "halo_rows": n_src - n_rows,
+                "halo_bytes_in": (n_src - n_rows) * F * 4, "halo_bytes_out": int(sg.fwd.send_idx.numel()) * F * 4,
+                "step_ms_this_rank": dt_local / args.steps * 1e3, **split, "verify": verify}
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
+        if verify is not None:
+            verify = {"all_ranks_within_1e-5_bound": all(r["verify"]["within_1e-5_bound"] for r in ranks),
+                      "max_bound_excess": max(r["verify"]["bound_excess"] for r in ranks)}
+    cpu = None
+    if rank == 0 and not sharded and not args.no_cpu_baseline:
+        cpu = cpu_gat_baseline(ei2, xw, att, H, C, 3_000_000)
+    if rank == 0:
+        line = {
+            "metric": "edges aggregated/sec (GATConv 8x32 propagate: fused node scores + leaky_relu + "
+                      "softmax(+1e-16) + aggregate + bias)",
+            "value": E2 * args.steps / dt, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic rmat21 graph (seeded, generated on device), random X W / att / bias",
+            "config": {"workload": wl["name"], "baseline_config": wl["baseline_config"], "graph": wl["graph"],
+                       "num_nodes": N, "num_edges": E2, "heads": H, "out_channels": C, "seed": wl["seed"],
+                       "parallelism": "dst-range shards x%d, RCCL halo all_to_all (pull)" % world if sharded
+                       else "single GPU"},
+            "roofline": {"bound": "hbm", "achieved": comp / (kern_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": comp / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                         "traffic_source": "not profiled for this workload (profiles/r03_pmc_gat_bwd.json: "
+                                           "the same kernels' counters)",
+                         "bytes": "compulsory: xw rows read once, out written once, col + rowptr",
+                         "compulsory_bytes_per_step": comp, "kernel_ms": kern_ms,
+                         "algorithmic_bytes_per_step": E_local * (4 * F + 4 + 4 * H) + n_rows * (4 * F + 4 * H + 4)},
+            "cpu_baseline": cpu,
+            "extra": {"one_time_build_s": t_build, "graph_gen_s": t_gen, "per_rank": ranks, "verify": verify,
+                      "collective_timeout_s": COLLECTIVE_TIMEOUT_S if sharded else None},
+        }
+        print(json.dumps(line), flush=True)
+    stage(rank, "done")
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
@@ -384,6 +593,8 @@ def main(argv=None):
         sys.exit(launch_ranks(args, argv))
     rank, world, local = setup_dist(args)
     sharded = dist.is_initialized()
+    if args.workload == "gat":
+        return main_gat(args, rank, world, local)
     wl = WORKLOADS[args.workload]
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)

@@ -661,6 +661,27 @@ def test_bench_products_workload_two_ranks():
     assert sum(p["rows"] for p in d["extra"]["per_rank"]) == 2_449_029
 
 
+@pytest.mark.parametrize("gpus", [1, 2])
+def test_bench_gat_workload(gpus):
+    """--workload gat (BASELINE config 3: the rmat21 graph, GATConv 8 heads x 32)
+    at one GPU and as 2 gloo ranks sharing the device (bench.py's own launch):
+    every rank's rows within 1e-5 * max(1, sum|alpha x_j|) of a float64 GATConv
+    formula over its own edges; per-rank exchange-only / compute-only times."""
+    args = ["bench.py", "--workload", "gat", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--verify"]
+    if gpus > 1:
+        d, _ = _run_bench(args[:1] + ["--gpus", str(gpus)] + args[1:], {"MP_BENCH_BACKEND": "gloo"})
+        assert d["extra"]["verify"]["all_ranks_within_1e-5_bound"], d["extra"]["verify"]
+        pr = d["extra"]["per_rank"]
+        assert len(pr) == gpus and sum(p["rows"] for p in pr) == 1 << 21
+        assert all(p["exchange_only_ms"] > 0 and p["compute_only_ms"] > 0 for p in pr)
+    else:
+        d, _ = _run_bench(args)
+        assert d["extra"]["verify"]["within_1e-5_bound"], d["extra"]["verify"]
+    assert d["n_gpus"] == gpus and d["config"]["workload"] == "rmat21_gat_h8c32"
+    assert d["config"]["num_edges"] == 62_094_512      # remove + add self loops: GCN's E'
+    assert d["value"] > 0 and d["roofline"]["frac"] > 0
+
+
 def test_bench_sharded_path_over_rccl_one_rank():
     """bench.py's N > 1 code path on the RCCL backend -- the one the driver's
     8-GPU run takes -- as ONE rank (two ranks cannot share a device under
