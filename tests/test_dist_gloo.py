@@ -398,7 +398,7 @@ def _gat_worker(rank, world, port, result_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [1, 2, 3])
+@pytest.mark.parametrize("world", [1, 2, 3, 4])
 def test_sharded_gat_matches_single_process(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -1085,6 +1085,30 @@ def test_gat_dropout_training_shapes_and_eval_deterministic():
         assert torch.equal(a, b)
 
 
+def test_gat_dropout_seed_leaves_cpu_rng_untouched():
+    """The fused attention dropout draws its seed from the device generator of
+    xw's device, as F.dropout on a device tensor does: training forwards leave
+    torch's CPU generator where it was (later CPU sampling, e.g. a DataLoader
+    shuffle, matches the generic path), and the device generator drives the
+    mask (same torch.cuda seed -> same output)."""
+    from torch_geometric.nn import GATConv
+    from mi355_mp.graphgen import powerlaw_edge_index
+    ei = powerlaw_edge_index(500, 6000, seed=5).to(DEV)
+    x = torch.randn(500, 16, generator=torch.Generator().manual_seed(5)).to(DEV)
+    conv = GATConv(16, 8, heads=4, dropout=0.5).to(DEV).train()
+    torch.manual_seed(11)
+    cpu_state = torch.get_rng_state()
+    outs = []
+    for _ in range(2):
+        torch.cuda.manual_seed(3)
+        outs.append(conv(x, ei))
+        conv(x, ei).sum().backward()
+    assert torch.equal(torch.get_rng_state(), cpu_state)
+    assert torch.equal(outs[0], outs[1])
+    torch.cuda.manual_seed(4)
+    assert not torch.equal(conv(x, ei), outs[0])
+
+
 @pytest.mark.parametrize("H,C", [(8, 32), (4, 16), (2, 64), (3, 4)])
 def test_gat_attention_dropout_fused_vs_masked_reference(H, C):
     """Training-mode attention dropout in the fused kernels (SURVEY 8a GATConv,
