@@ -903,8 +903,10 @@ def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope
     gatt = None
     if epi:
         if want_att or not fused_dst:
-            # att_dst term of d xw (unless the transposed pass added it) + d att partials
-            apart = torch.empty((nb, 2, F), dtype=torch.float32, device=dev)
+            # att_dst term of d xw (unless the transposed pass added it) + d att partials:
+            # the finish pass runs over all N rows (own + halo on a sharded rank's
+            # local graph), one partial per block of mp_gat_bwd_blocks(N)
+            apart = torch.empty((int(lib.mp_gat_bwd_blocks(N)), 2, F), dtype=torch.float32, device=dev)
             _lib.check(lib.mp_gat_backward_finish_f32(None if fused_dst else gx.data_ptr(), xw.data_ptr(),
                                                       ga_dst.data_ptr(), ga_src.data_ptr(), att_c.data_ptr(), N, H, C,
                                                       apart.data_ptr(), st), "mp_gat_backward_finish_f32")

@@ -204,6 +204,24 @@ def test_sharded_gcnconv_forward_backward_on_one_gpu():
         assert r["gmax_exact"] and r["gmax_repeat"], r   # deterministic on both sides (round 3)
 
 
+def _unsplit_equal(sg, g1, alpha, alpha_ref, out, out_ref):
+    """Bit-equality of the sharded GAT and the single-GPU kernel where both
+    schedules keep a row whole: a row of <= snap in-edges is never split across
+    merge-path tasks (graph.default_snap), so its softmax and weighted sum run
+    in one task in global edge order on both sides.  Hub rows above either
+    schedule's snap may be cut at different slots (partials merged by the
+    fix-up), and are held to the tolerance only.  Returns (every alpha of the
+    rank's edges into such rows equal, every such output row equal)."""
+    loc = sg.g_fwd.dst
+    deg = (loc.rowptr[1:] - loc.rowptr[:-1]).long()
+    whole = deg <= min(loc.snap, g1.dst.snap)
+    dst = sg.fwd.local_edge_index[1].long()
+    ok_e = whole[dst]
+    a_eq = bool(torch.equal(alpha[ok_e], alpha_ref[ok_e])) and int(ok_e.sum()) > 0
+    o_eq = bool(torch.equal(out[whole], out_ref[whole])) and int(whole.sum()) > 0
+    return a_eq, o_eq
+
+
 def _gat_layer_worker(rank, world, port, q):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -267,10 +285,10 @@ def _gat_layer_worker(rank, world, port, q):
         o1, a1 = ops.gat_propagate(g1, ei2, xw, att, H, C, return_alpha=True)
         sg = mdist.ShardedGraph.for_gat(ei, N, rank, world)
         o2, (gid, a2) = sg.gat_propagate(xw[sg.lo:sg.hi].contiguous(), att, H, C, return_alpha=True)
+        a_eq, o_eq = _unsplit_equal(sg, g1, a2, a1[gid], o2, o1[sg.lo:sg.hi])
         res["prop"] = {"out": float((o2 - o1[sg.lo:sg.hi]).abs().max()),
-                       "out_bitwise_frac": float((o2 == o1[sg.lo:sg.hi]).float().mean()),
                        "alpha": float((a2 - a1[gid]).abs().max()),
-                       "alpha_bitwise_frac": float((a2 == a1[gid]).float().mean())}
+                       "alpha_unsplit_bitwise": a_eq, "out_unsplit_bitwise": o_eq}
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -290,7 +308,7 @@ def test_sharded_gatconv_forward_backward_on_one_gpu(world):
         for key, v in r.items():
             if key == "prop":
                 assert v["out"] < 1e-5 and v["alpha"] < 1e-6, (key, v)
-                assert v["out_bitwise_frac"] > 0.9 and v["alpha_bitwise_frac"] > 0.9, (key, v)
+                assert v["out_unsplit_bitwise"] and v["alpha_unsplit_bitwise"], (key, v)
                 continue
             assert v["slices_equal"], (key, v)
             # tolerance: the rank's X W GEMM has M = n_own rows (hipBLASLt picks its kernel by M)
@@ -391,8 +409,8 @@ def _gat_full_worker(rank, world, port, q):
         terms = ops._heads_aggregate(g1.dst, "other", alpha1[eid].contiguous(), H, xw.abs())[lo:hi]
         excess = float(((out - out1[lo:hi]).abs() - 1e-5 * terms.clamp(min=1.0)).max())
         da = (alpha - alpha1[gid]).abs()
-        q.put((rank, excess, float(da.max()), float((da == 0).float().mean()),
-               float((out == out1[lo:hi]).float().mean()), sg.n_edges == ei2.shape[1], hi - lo))
+        a_eq, o_eq = _unsplit_equal(sg, g1, alpha, alpha1[gid], out, out1[lo:hi])
+        q.put((rank, excess, float(da.max()), a_eq, o_eq, sg.n_edges == ei2.shape[1], hi - lo))
     finally:
         dist.destroy_process_group()
 
@@ -407,7 +425,7 @@ def test_full_size_gat_sharded_rehearsal():
     assert sum(r[6] for r in res) == 1 << 21
     for rank, excess, dalpha, a_eq, o_eq, edges_ok, _ in res:
         assert excess <= 0 and dalpha <= 1e-5 and edges_ok, res
-        assert a_eq > 0.95 and o_eq > 0.9, res
+        assert a_eq and o_eq, res
 
 
 @pytest.mark.parametrize("world", [1, 2, 3, 8])

@@ -1139,8 +1139,8 @@ def test_gat_attention_dropout_fused_vs_masked_reference(H, C):
     torch.manual_seed(1234)
     out = conv(xd, eid)
     out.backward(gout.to(DEV))
-    torch.manual_seed(1234)  # the seed gat_propagate drew
-    seed = int(torch.randint(-2 ** 63, 2 ** 63 - 1, (), dtype=torch.int64)) & 0xFFFFFFFFFFFFFFFF
+    torch.manual_seed(1234)  # the seed gat_propagate drew (device generator: manual_seed seeds it too)
+    seed = int(torch.randint(-2 ** 63, 2 ** 63 - 1, (), dtype=torch.int64, device=DEV)) & 0xFFFFFFFFFFFFFFFF
     ei_l = gat_loops(eid, N)
     graph = graph_for(ei_l, N, N, conv.flow, target_tasks=GAT_TARGET_TASKS)
     keep = ops.gat_dropout_keep(graph, seed, p, H).cpu()
@@ -1248,7 +1248,7 @@ def test_gat_wide_heads_training(H, C, p):
     keep = None
     if p > 0:
         torch.manual_seed(99)
-        seed = int(torch.randint(-2 ** 63, 2 ** 63 - 1, (), dtype=torch.int64)) & 0xFFFFFFFFFFFFFFFF
+        seed = int(torch.randint(-2 ** 63, 2 ** 63 - 1, (), dtype=torch.int64, device=DEV)) & 0xFFFFFFFFFFFFFFFF
         graph = graph_for(gat_loops(eid, N), N, N, conv.flow, target_tasks=GAT_TARGET_TASKS)
         keep = ops.gat_dropout_keep(graph, seed, p, H).cpu()
     W = conv.weight.detach().cpu().double().requires_grad_(True)
