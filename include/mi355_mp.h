@@ -128,7 +128,13 @@ const char* mp_source_hash(void);
  *     another on all eight XCDs; 0 (default) = XCD-affine tiles.
  *   MP_TUNE_FLAT_FAR_MIN_BYTES: the scalar-batch sum/mean kernel keeps 8
  *     instead of 16 row loads in flight per wave over a gathered x larger than
- *     this (default 256 MiB, the Infinity Cache). */
+ *     this (default 256 MiB, the Infinity Cache).
+ *   MP_TUNE_GAT_BWD_VEC: features per lane of the GAT backward's transposed
+ *     pass (mp_gat_backward_*_f32 with C/4 a power of two): 4 (default,
+ *     256-feature tiles), 2 or 1 (128- / 64-feature XCD-affine tiles, taken
+ *     when a head fits inside one tile).  The exception to the rule above:
+ *     the per-slot <g_i, xw_j> sums its features in another order, so the
+ *     gradients agree to rounding, not bit for bit. */
 #define MP_TUNE_FLAT_VEC1_MIN_BYTES 1
 #define MP_TUNE_FLAT_SMEM 2
 #define MP_TUNE_FLAT_MIN_F 3
@@ -138,6 +144,7 @@ const char* mp_source_hash(void);
 #define MP_TUNE_FLAT_VEC_ARG 7
 #define MP_TUNE_FLAT_SEQ_TILES 8
 #define MP_TUNE_FLAT_FAR_MIN_BYTES 9
+#define MP_TUNE_GAT_BWD_VEC 10
 int64_t mp_tune(int32_t key, int64_t value);
 
 /* ---- CSR build (replaces the sort/bucketing torch_scatter never did: upstream

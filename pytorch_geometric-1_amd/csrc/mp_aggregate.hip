@@ -1795,8 +1795,10 @@ static int launch_main(void (*k)(AggArgs), dim3 grid, hipStream_t s, const AggAr
 
 template <class Red, int VEC, int L>
 static int launch_l(const AggArgs& a, int stages, hipStream_t s) {
-  constexpr int U = VEC == 4 ? (L == 64 ? (kGatTrain<Red> ? kU_GatTrain : kU_Vec4) : kU_Narrow)
-                             : (VEC == 2 ? kU_Vec2 : (L < kU_Vec1 ? L : kU_Vec1));  // VEC=1 groups < 16 lanes: GAT stats
+  // the GAT backward holds a 16-B destination pack per slot in flight: U = 8 at every width
+  constexpr int U = (Red::kGatB && L == 64) ? kU_Vec4
+                    : VEC == 4 ? (L == 64 ? (kGatTrain<Red> ? kU_GatTrain : kU_Vec4) : kU_Narrow)
+                               : (VEC == 2 ? kU_Vec2 : (L < kU_Vec1 ? L : kU_Vec1));  // VEC=1 groups < 16 lanes: GAT stats
   const int ftiles = (int)ceil_div(a.F, L * VEC);
   if (stages & MP_STAGE_MAIN) {
     int64_t nb = ceil_div(a.n_waves, kWavesPerBlock * (64 / L));
@@ -1931,6 +1933,7 @@ struct Tune {
   std::atomic<int64_t> flat_vec_arg{2};
   std::atomic<int64_t> flat_seq_tiles{0};
   std::atomic<int64_t> flat_far_min_bytes{256ll << 20};  // the Infinity Cache
+  std::atomic<int64_t> gat_bwd_vec{4};  // features per lane of the GAT backward's transposed pass
 };
 static Tune g_tune;
 
@@ -1945,6 +1948,7 @@ static std::atomic<int64_t>* tune_slot(int32_t key) {
     case MP_TUNE_FLAT_VEC_ARG: return &g_tune.flat_vec_arg;
     case MP_TUNE_FLAT_SEQ_TILES: return &g_tune.flat_seq_tiles;
     case MP_TUNE_FLAT_FAR_MIN_BYTES: return &g_tune.flat_far_min_bytes;
+    case MP_TUNE_GAT_BWD_VEC: return &g_tune.gat_bwd_vec;
   }
   return nullptr;
 }
@@ -2050,7 +2054,9 @@ int64_t mp_tune(int32_t key, int64_t value) {
   if (!v) return -1;
   if (value < 0) return v->load();
   if (key == MP_TUNE_FLAT_SMEM || key == MP_TUNE_FLAT_SEQ_TILES) value = value ? 1 : 0;
-  if ((key == MP_TUNE_FLAT_VEC || key == MP_TUNE_FLAT_VEC_ARG) && value != 1 && value != 2 && value != 4) return -1;
+  if ((key == MP_TUNE_FLAT_VEC || key == MP_TUNE_FLAT_VEC_ARG || key == MP_TUNE_GAT_BWD_VEC) && value != 1 &&
+      value != 2 && value != 4)
+    return -1;
   return v->exchange(value);
 }
 
@@ -2497,6 +2503,23 @@ static int gat_backward(const mp_csr* gt, const float* grad_out, int64_t ldg, co
   auto pow2 = [](int q) { return q >= 1 && q <= 64 && (q & (q - 1)) == 0; };
   const bool v4 = C % 4 == 0 && pow2(C / 4) && (uintptr_t)grad_out % 16 == 0 && ldg % 4 == 0 &&
                   (uintptr_t)xw % 16 == 0 && (uintptr_t)grad_xw % 16 == 0;
+  // narrower feature tiles for the transposed pass (MP_TUNE_GAT_BWD_VEC 2 / 1: 128- / 64-feature
+  // tiles, XCD-affine like the flat kernel's; a head stays inside one tile)
+  const int bv = (int)tuned(g_tune.gat_bwd_vec);
+  if (v4 && bv < 4 && F >= 64 * bv * 2 && pow2(C / bv) && (64 * bv) % C == 0) {
+    if (bv == 2) {
+      if (p_drop > 0.f) {
+        set_drop(a, drop_seed, p_drop);
+        return launch<GatBwdRed<2, true>, 2>(a, stages, s);
+      }
+      return launch<GatBwdRed<2>, 2>(a, stages, s);
+    }
+    if (p_drop > 0.f) {
+      set_drop(a, drop_seed, p_drop);
+      return launch<GatBwdRed<1, true>, 1>(a, stages, s);
+    }
+    return launch<GatBwdRed<1>, 1>(a, stages, s);
+  }
   if (v4) {
     int lanes = F >= 256 ? kGatLanes : pick_shape(F, ldg, grad_out, F, grad_xw).lanes;
     if (lanes < C / 4) lanes = C / 4;

@@ -31,6 +31,7 @@ MP_TUNE_FLAT_VEC = 6
 MP_TUNE_FLAT_VEC_ARG = 7
 MP_TUNE_FLAT_SEQ_TILES = 8
 MP_TUNE_FLAT_FAR_MIN_BYTES = 9
+MP_TUNE_GAT_BWD_VEC = 10
 MP_DTYPE = {torch.float32: 0, torch.float64: 1, torch.float16: 2, torch.bfloat16: 3, torch.int64: 4}
 MP_LOOPS_REMOVE = 0
 MP_LOOPS_ADD = 1
