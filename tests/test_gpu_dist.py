@@ -2,6 +2,7 @@
 halo rows staged through the host -- the RCCL call is the only part not
 exercised).  Checks the overlapped interior/boundary path and the plain
 exchange-then-aggregate path against the single-GPU result."""
+import datetime
 import os
 import socket
 
@@ -9,6 +10,10 @@ import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+
+# gloo process groups of the spawned ranks: rendezvous and collectives give up
+# after this (a lost peer fails the test instead of stalling the suite)
+_PG_TIMEOUT = datetime.timedelta(seconds=240)
 
 pytestmark = pytest.mark.gpu
 
@@ -29,7 +34,7 @@ def _worker(rank, world, port, q):
             sys.path.insert(0, p)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=_PG_TIMEOUT)
     try:
         from mi355_mp import dist as mdist, ops
         from mi355_mp.graph import Graph
@@ -93,7 +98,7 @@ def _layer_worker(rank, world, port, q):
             sys.path.insert(0, p)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=_PG_TIMEOUT)
     try:
         from mi355_mp import dist as mdist, ops
         from mi355_mp.graph import Graph
@@ -173,16 +178,32 @@ def _layer_worker(rank, world, port, q):
 
 
 def _spawn(target, world=2, timeout=600):
+    """Run target(rank, world, port, q) in `world` spawned processes and return
+    their sorted queue items.  Fails fast: the first rank to exit non-zero, or
+    the deadline, terminates the others (a rank stuck in a collective whose peer
+    died would otherwise sit until the process-group timeout)."""
+    import time
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    for p in procs:
-        p.join(timeout)
-        assert p.exitcode == 0
-    return sorted(q.get(timeout=10) for _ in range(world))
+    deadline = time.monotonic() + timeout
+    try:
+        while any(p.is_alive() for p in procs):
+            bad = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not bad, "a rank exited with %s" % bad
+            assert time.monotonic() < deadline, "ranks still running after %d s" % timeout
+            time.sleep(0.2)
+        assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+        return sorted(q.get(timeout=10) for _ in range(world))
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.terminate()
+        for p in procs:
+            p.join(10)
 
 
 def test_sharded_gcnconv_forward_backward_on_one_gpu():
@@ -230,7 +251,7 @@ def _gat_layer_worker(rank, world, port, q):
             sys.path.insert(0, p)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=_PG_TIMEOUT)
     try:
         from mi355_mp import dist as mdist, ops
         from mi355_mp.graph import GAT_TARGET_TASKS, Graph
@@ -324,7 +345,7 @@ def _products_worker(rank, world, port, q):
             sys.path.insert(0, p)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=_PG_TIMEOUT)
     try:
         from mi355_mp import dist as mdist, ops
         from mi355_mp.graph import Graph
@@ -383,7 +404,7 @@ def _gat_full_worker(rank, world, port, q):
             sys.path.insert(0, p)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=_PG_TIMEOUT)
     try:
         from mi355_mp import dist as mdist, ops
         from mi355_mp.graph import GAT_TARGET_TASKS, Graph
@@ -744,7 +765,7 @@ def _cover_worker(rank, world, port, q):
             sys.path.insert(0, p)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=_PG_TIMEOUT)
     try:
         from mi355_mp import dist as mdist, ops
         from mi355_mp.graph import Graph
@@ -811,7 +832,7 @@ def _cover_layer_worker(rank, world, port, q):
             sys.path.insert(0, p)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=_PG_TIMEOUT)
     try:
         from mi355_mp import dist as mdist, ops
         from mi355_mp.graph import Graph

@@ -1316,6 +1316,54 @@ def test_gat_fused_backward_hub_rows_split_across_tasks():
         assert torch.allclose(got.cpu().double(), want, rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("vec", [2, 1])
+@pytest.mark.parametrize("H,C,p", [(8, 32, 0.0), (4, 64, 0.0), (8, 32, 0.3), (16, 16, 0.0)])
+def test_gat_backward_narrow_tiles(vec, H, C, p):
+    """MP_TUNE_GAT_BWD_VEC 2 / 1 (the 128- / 64-feature tiles of the transposed
+    pass, A/B only: profiles/r04_ab_gat_bwd_vec.log) on a star whose centre's
+    rows span many tasks: every gradient within the float64 bound, and within
+    rounding of the default 256-feature pass (the per-slot <g_i, xw_j> sums
+    its features in another order)."""
+    from torch_geometric.nn import GATConv
+    from torch_geometric.nn.conv._structure import gat_loops
+    from mi355_mp import ops
+    from mi355_mp.graph import graph_for, GAT_TARGET_TASKS
+    N, Fi = 2500, 16
+    leaves = torch.arange(1, N)
+    g = torch.Generator().manual_seed(61 + H + vec)
+    extra = torch.randint(0, N, (2, 6000), generator=g)
+    ei = torch.cat([torch.stack([torch.zeros(N - 1, dtype=torch.long), leaves]),
+                    torch.stack([leaves, torch.zeros(N - 1, dtype=torch.long)]), extra], 1)
+    x = torch.randn(N, Fi, generator=g)
+    gout = torch.randn(N, H * C, generator=g)
+    conv = GATConv(Fi, C, heads=H, dropout=p).to(DEV).train()
+    with torch.no_grad():
+        conv.bias.normal_()
+    grads = {}
+    for v in (4, vec):
+        conv.zero_grad()
+        xd = x.to(DEV).requires_grad_(True)
+        with _tuned(gat_bwd_vec=v):
+            torch.manual_seed(77)
+            conv(xd, ei.to(DEV)).backward(gout.to(DEV))
+        grads[v] = [xd.grad.cpu().double()] + [t.grad.cpu().double() for t in (conv.weight, conv.att, conv.bias)]
+    keep = None
+    if p > 0:
+        torch.manual_seed(77)
+        seed = int(torch.randint(-2 ** 63, 2 ** 63 - 1, (), dtype=torch.int64, device=DEV)) & 0xFFFFFFFFFFFFFFFF
+        ei_l = gat_loops(ei.to(DEV), N)   # held: the graph's CSR is built lazily from it
+        graph = graph_for(ei_l, N, N, conv.flow, target_tasks=GAT_TARGET_TASKS)
+        keep = ops.gat_dropout_keep(graph, seed, p, H).cpu()
+    W = conv.weight.detach().cpu().double().requires_grad_(True)
+    att = conv.att.detach().cpu().double().requires_grad_(True)
+    b = conv.bias.detach().cpu().double().requires_grad_(True)
+    x64 = x.double().requires_grad_(True)
+    P.gat_conv(x64, ei, W, att, b, H, C, drop_keep=keep, drop_p=p).backward(gout.double())
+    for got, base, want in zip(grads[vec], grads[4], (x64.grad, W.grad, att.grad, b.grad)):
+        assert torch.allclose(got, want, rtol=1e-4, atol=1e-4)
+        assert float((got - base).abs().max()) <= 1e-5 * max(1.0, float(base.abs().max()))
+
+
 @pytest.mark.parametrize("H,C,chunk", [(8, 32, 64), (4, 16, 16), (2, 64, 256), (1, 256, 64), (3, 4, 16)])
 def test_gat_training_forward_node_wise_d_a_dst(H, C, chunk, monkeypatch):
     """mp_gat_aggregate_train_f32 leaves agg2 = sum alpha leaky' xw_j and
