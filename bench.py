@@ -371,18 +371,23 @@ def verify_f64(out, x_src, src, dst, w, bias, step=4_000_000):
     return res
 
 
-def find_pmc(workload, kernel, src_hash):
+def find_pmc(workload, kernel, src_hash, full=False):
     """The newest committed PMC summary (profiles/r*_pmc_traffic*.json) of THIS
-    build's dispatched kernel on this workload: (hbm bytes per launch, path)."""
+    build's dispatched kernel on this workload: (hbm bytes per launch, path)
+    (+ the summary itself with full=True).  kernel=None: the summary's own
+    dominant kernel (the GAT workload, whose dispatch has no name query)."""
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic*.json")), reverse=True):
         try:
             with open(path) as f:
                 pmc = json.load(f)
         except (OSError, ValueError):
             continue
-        if pmc.get("workload") == workload and pmc.get("kernel") == kernel and pmc.get("source_hash") == src_hash:
-            return pmc.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
-    return None, "no committed profile of this build's kernel on %s" % workload
+        if (pmc.get("workload") == workload and kernel in (None, pmc.get("kernel"))
+                and pmc.get("source_hash") == src_hash):
+            res = (pmc.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT))
+            return res + (pmc,) if full else res
+    res = (None, "no committed profile of this build's kernel on %s" % workload)
+    return res + (None,) if full else res
 
 
 def cpu_gat_baseline(ei, xw, att, H, C, sample):
@@ -544,6 +549,11 @@ def main_gat(args, rank, world, local):
             del ref, terms
             stage(rank, "verify: %s" % json.dumps(verify))
     comp = n_src * F * 4 + n_rows * F * 4 + E_local * 4 + (n_rows + 1) * 4
+    # counter traffic of the fused GAT kernel from a committed profile of this build
+    # (tools/profile.sh with BENCH_ARGS="--workload gat"), per launch of its main kernel
+    src_hash = mi355_mp.load_native().mp_source_hash().decode()
+    traffic, traffic_src, pmc = (None, "N>1: per-rank graphs are not profiled", None) if sharded else \
+        find_pmc(wl["name"], None, src_hash, full=True)
     ranks = None
     if sharded:
         mine = {"rank": rank, "rows": n_rows, "edges": E_local, "halo_rows": n_src - n_rows,
@@ -570,9 +580,12 @@ def main_gat(args, rank, world, local):
                        "parallelism": "dst-range shards x%d, RCCL halo all_to_all (pull)" % world if sharded
                        else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": comp / (kern_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": comp / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
-                         "traffic_source": "not profiled for this workload (profiles/r03_pmc_gat_bwd.json: "
-                                           "the same kernels' counters)",
+                         "unit": "GB/s", "frac": comp / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_frac": (traffic / (pmc["kernel_trace_avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS)
+                         if traffic else None,
+                         "traffic_source": traffic_src, "kernel": pmc["kernel"] if pmc else None,
+                         "kernel_trace_avg_ms": pmc["kernel_trace_avg_ms"] if pmc else None,
+                         "source_hash": src_hash,
                          "bytes": "compulsory: xw rows read once, out written once, col + rowptr",
                          "compulsory_bytes_per_step": comp, "kernel_ms": kern_ms,
                          "algorithmic_bytes_per_step": E_local * (4 * F + 4 + 4 * H) + n_rows * (4 * F + 4 * H + 4)},

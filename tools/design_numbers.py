@@ -1,0 +1,55 @@
+"""Print the current-state numbers DESIGN.md section 2 quotes, read from the
+committed round files (profiles/<round>_bench_*.json, _bench_configs.jsonl,
+_pmc_traffic*.json), so every number in those tables can be traced to a file.
+    python tools/design_numbers.py [r04]
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def load(name):
+    path = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        if name.endswith(".jsonl"):
+            return {d["config"]: d for d in map(json.loads, f)}
+        return json.load(f)
+
+
+def main():
+    rnd = sys.argv[1] if len(sys.argv) > 1 else "r04"
+    out = {}
+    for wl, f in (("c2", "bench_rmat21"), ("c5", "bench_products_n1"), ("c3", "bench_gat_n1"),
+                  ("c5_gloo2", "bench_products_gloo2")):
+        d = load("%s_%s.json" % (rnd, f))
+        if not d:
+            continue
+        r, ex = d["roofline"], d.get("extra", {})
+        out[wl] = {"edges_per_s": d["value"], "ms_per_step": d["ms_per_step"], "frac_compulsory": r["frac"],
+                   "kernel_ms": r.get("avg_launch_ms", r.get("kernel_ms")), "fixup_ms": r.get("fixup_avg_ms"),
+                   "traffic": r.get("traffic"), "cpu": (d.get("cpu_baseline") or {}).get("value"),
+                   "gemm_ms": ex.get("gemm_xW_ms"), "ref_path_ms": ex.get("gpu_reference_path_ms"),
+                   "spmm_ms": ex.get("hipsparse_spmm_ms"), "verify": ex.get("verify")}
+    for wl, suffix in (("c2", ""), ("c5", "_products"), ("c3", "_gat")):
+        p = load("%s_pmc_traffic%s.json" % (rnd, suffix))
+        if p:
+            out.setdefault(wl, {})["pmc"] = {"bytes_per_launch": p["hbm_bytes_per_launch"],
+                                             "l2_hit": p["l2_hit_rate"], "kernel_trace_ms": p["kernel_trace_avg_ms"],
+                                             "TBps": p["hbm_bytes_per_launch"] / p["kernel_trace_avg_ms"] / 1e9,
+                                             "source_hash": p["source_hash"],
+                                             "ta_busy": (p.get("stall") or {}).get("ta_busy_frac"),
+                                             "l1_queue_stall": (p.get("stall") or {}).get("tcp_pending_stall_frac")}
+    cfg = load("%s_bench_configs.jsonl" % rnd) or {}
+    for k, d in cfg.items():
+        out["cfg_" + k] = {kk: v for kk, v in d.items() if not isinstance(v, (dict, list)) and kk != "desc"}
+        if "repeated_layer_first_occurrences" in d:
+            out["cfg_" + k]["first_occurrences"] = d["repeated_layer_first_occurrences"]
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

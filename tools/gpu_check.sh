@@ -14,7 +14,7 @@ step() {  # name timeout cmd...
 }
 { nproc; python3 -c "import os; print('cpu_count', os.cpu_count(), 'affinity', len(os.sched_getaffinity(0)))";
   cat /sys/fs/cgroup/cpu.max 2>/dev/null; grep -m1 "model name" /proc/cpuinfo; } > gpurun_out/host_probe.log 2>&1
-PT="python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread"
+PT="python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread --durations=25"
 if [ -n "${PYTEST_K:-}" ]; then
   step pytest_gpu 1100 $PT -k "$PYTEST_K"
 else

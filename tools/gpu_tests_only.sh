@@ -2,7 +2,7 @@
 # GPU-box run: the GPU test suite only (optionally -k filtered by PYTEST_K)
 set -u
 mkdir -p gpurun_out
-PT="python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread"
+PT="python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread --durations=25"
 if [ -n "${PYTEST_K:-}" ]; then
   timeout -k 10 1000 $PT -k "$PYTEST_K" > gpurun_out/pytest_gpu.log 2>&1
 else

@@ -38,7 +38,7 @@ def main():
     src, rnd = sys.argv[1], sys.argv[2]
     workload = sys.argv[3] if len(sys.argv) > 3 else "rmat21_gcn_f256"
     calib_dir = sys.argv[4] if len(sys.argv) > 4 else src
-    suffix = "" if workload == "rmat21_gcn_f256" else "_" + workload.split("_")[0]
+    suffix = "" if workload == "rmat21_gcn_f256" else "_" + ("gat" if "_gat" in workload else workload.split("_")[0])
     os.makedirs("profiles", exist_ok=True)
     shutil.copy(os.path.join(src, "kt", "kt_kernel_stats.csv"), "profiles/%s_kernel_stats%s.csv" % (rnd, suffix))
     global KERNEL
