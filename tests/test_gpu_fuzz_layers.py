@@ -438,7 +438,7 @@ def test_fuzz_sage_graph_conv_layers(N, deg, Fi, Fo, layer, normalize, bias, wei
     add_remaining_self_loops (last loop's weight wins) + mean + x W (+ b,
     L2-normalised), concat's [x, mean] W; GraphConv's aggr(w h_j) + lin(x).
     Values within 1e-5 (max: the selected terms), gradients of x, W (and w)
-    within 1e-4 for add / mean."""
+    within 1e-4 (max: with the engine's own winning edges)."""
     from torch_geometric.nn import SAGEConv, GraphConv
     torch.manual_seed(seed)               # layer initialisers: a failing example replays
     ei, g = _graph(N, deg, loops, seed)
@@ -454,8 +454,10 @@ def test_fuzz_sage_graph_conv_layers(N, deg, Fi, Fo, layer, normalize, bias, wei
     wd = w.to(DEV).requires_grad_() if weighted else None
     out = conv(xd, ei.to(DEV), wd)
 
-    def formula(dtype):
-        """The 1.4.3 layer in `dtype` on the CPU with autograd: (ref, leaves)."""
+    def formula(dtype, winners=None):
+        """The 1.4.3 layer in `dtype` on the CPU with autograd: (ref, leaves).
+        winners ([N, Fo] edge ids, E = empty row): max takes these edges'
+        messages instead of its own arg max (the gradient check below)."""
         xx = x.to(dtype).requires_grad_()
         ww = w.to(dtype).requires_grad_() if weighted else None
         prm = {k: v.detach().cpu().to(dtype).requires_grad_() for k, v in conv.named_parameters()}
@@ -479,7 +481,11 @@ def test_fuzz_sage_graph_conv_layers(N, deg, Fi, Fo, layer, normalize, bias, wei
             aggr = layer.split("_")[1]
             h = xx @ prm["weight"]
             msg = h[ei[0]] if ww is None else ww.view(-1, 1) * h[ei[0]]
-            if aggr == "max":
+            if aggr == "max" and winners is not None:
+                pad = torch.cat([msg, torch.zeros(1, Fo, dtype=dtype)])      # row E: an empty row's 0
+                agg = pad.gather(0, winners)
+                agg = torch.where(agg < -10000, torch.zeros_like(agg), agg)
+            elif aggr == "max":
                 agg = torch.full((N, Fo), float("-inf"), dtype=dtype).scatter_reduce(
                     0, ei[1].view(-1, 1).expand(-1, Fo), msg, "amax")
                 agg = torch.where(torch.isinf(agg) | (agg < -10000), torch.zeros_like(agg), agg)
@@ -495,6 +501,27 @@ def test_fuzz_sage_graph_conv_layers(N, deg, Fi, Fo, layer, normalize, bias, wei
     err = (out.detach().cpu().double() - ref.detach()).abs()
     assert bool((err <= 1e-5 * ref.detach().abs().clamp(min=1.0)).all()), float(err.max())
     if layer == "graph_max":
+        # the max gradient follows each (row, feature)'s winning edge, and fp32 and
+        # float64 may pick different winners on a near-tie: the float64 formula takes
+        # the engine's own winners -- torch_scatter.scatter_max (first edge on ties) of
+        # the same fp32 messages w_e * h_j, h from the layer's own x W on the device --
+        # and the gradients of x, W, lin and w must then agree within 1e-4
+        import torch_scatter
+        with torch.no_grad():
+            h32 = torch.matmul(xd, conv.weight)
+            m32 = h32[ei[0].to(DEV)] if wd is None else wd.view(-1, 1) * h32[ei[0].to(DEV)]
+            _, win = torch_scatter.scatter_max(m32, ei[1].to(DEV), dim=0, dim_size=N)
+        ref_w, x64, w64, params = formula(torch.float64, win.cpu())
+        R = torch.randn(out.shape, generator=g)
+        (out * R.to(DEV)).sum().backward()
+        (ref_w * R.double()).sum().backward()
+        named = dict(conv.named_parameters())
+        pairs = [(xd.grad, x64.grad, "x")] + [(named[k].grad, v.grad, k) for k, v in params.items()]
+        if weighted:
+            pairs.append((wd.grad, w64.grad, "w"))
+        for got, want, what in pairs:
+            err = (got.cpu().double() - want).abs()
+            assert bool((err <= 1e-4 * want.abs().clamp(min=1.0)).all()), "%s: err %g" % (what, float(err.max()))
         return
     # gradients: float64 autograd of the formula is the target; the same formula in
     # fp32 on the CPU (the reference's own precision) measures how far that precision
