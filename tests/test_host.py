@@ -116,7 +116,8 @@ def test_tune_table_keys(lib):
     from mi355_mp import _lib
     for key in (_lib.MP_TUNE_FLAT_VEC1_MIN_BYTES, _lib.MP_TUNE_FLAT_SMEM, _lib.MP_TUNE_FLAT_MIN_F,
                 _lib.MP_TUNE_FLAT_MIN_F_ARG, _lib.MP_TUNE_FLAT_NARROW_VEC1, _lib.MP_TUNE_FLAT_VEC,
-                _lib.MP_TUNE_FLAT_VEC_ARG, _lib.MP_TUNE_FLAT_SEQ_TILES, _lib.MP_TUNE_FLAT_FAR_MIN_BYTES):
+                _lib.MP_TUNE_FLAT_VEC_ARG, _lib.MP_TUNE_FLAT_SEQ_TILES, _lib.MP_TUNE_FLAT_FAR_MIN_BYTES,
+                _lib.MP_TUNE_GAT_BWD_VEC):
         v = lib.mp_tune(key, -1)
         assert v >= 0
         assert lib.mp_tune(key, v) == v
@@ -124,6 +125,8 @@ def test_tune_table_keys(lib):
     assert lib.mp_tune(_lib.MP_TUNE_FLAT_MIN_F_ARG, -1) == 64
     assert lib.mp_tune(_lib.MP_TUNE_FLAT_NARROW_VEC1, -1) == 64
     assert lib.mp_tune(_lib.MP_TUNE_FLAT_SEQ_TILES, -1) == 0
+    assert lib.mp_tune(_lib.MP_TUNE_GAT_BWD_VEC, -1) == 4           # 256-feature tiles (A/B default)
+    assert lib.mp_tune(_lib.MP_TUNE_GAT_BWD_VEC, 3) == -1           # 1, 2 or 4 only
     assert lib.mp_tune(99, 1) == -1
 
 
