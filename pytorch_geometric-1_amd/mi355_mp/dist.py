@@ -908,12 +908,14 @@ class ShardedGraph:
         self._chunk = chunk
 
     @classmethod
-    def for_gcn(cls, edge_index, num_nodes, rank, world, group=None, improved=False, edge_weight=None, chunk=None):
+    def for_gcn(cls, edge_index, num_nodes, rank, world, group=None, improved=False, edge_weight=None, chunk=None,
+                cuts=None):
         """GCNConv's graph (add_remaining_self_loops + symmetric norm, [U5]),
-        built from the full edge list, sharded, with the norm as edge weight."""
+        built from the full edge list, sharded, with the norm as edge weight
+        (cuts: explicit row ranges, else edge-balanced)."""
         from torch_geometric.nn.conv.gcn_conv import GCNConv
         ei2, norm = GCNConv.norm(edge_index, num_nodes, edge_weight, improved)
-        return cls(ei2, num_nodes, rank, world, group=group, chunk=chunk).set_edge_weight(norm)
+        return cls(ei2, num_nodes, rank, world, group=group, chunk=chunk, cuts=cuts).set_edge_weight(norm)
 
     @classmethod
     def for_gcn_from_slices(cls, edge_slice, slice_offset, num_nodes, rank, world, group=None, improved=False,
@@ -1169,15 +1171,22 @@ def broadcast_parameters(module, src=0, group=None):
 
 def allreduce_gradients(module, group=None):
     """Sum the gradients of replicated parameters over the ranks (each rank's
-    weight gradient covers its own rows only), as DDP would."""
+    weight gradient covers its own rows only), as DDP would.  Every trainable
+    parameter takes part on every rank, in the same order: a rank whose rows
+    never reached a parameter (e.g. a rank that owns no rows, whose empty
+    output does not involve GATConv's att) contributes zeros -- skipping it
+    there would pair different tensors in the collectives of different ranks."""
     for p in module.parameters():
-        if p.grad is not None:
-            if p.grad.is_cuda and dist.get_backend(group) == "gloo":
-                t = p.grad.cpu()
-                dist.all_reduce(t, group=group)
-                p.grad.copy_(t)
-            else:
-                dist.all_reduce(p.grad, group=group)
+        if not p.requires_grad:
+            continue
+        if p.grad is None:
+            p.grad = torch.zeros_like(p)
+        if p.grad.is_cuda and dist.get_backend(group) == "gloo":
+            t = p.grad.cpu()
+            dist.all_reduce(t, group=group)
+            p.grad.copy_(t)
+        else:
+            dist.all_reduce(p.grad, group=group)
 
 
 class ShardedGCNConv(torch.nn.Module):

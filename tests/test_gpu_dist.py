@@ -337,6 +337,104 @@ def test_sharded_gatconv_forward_backward_on_one_gpu(world):
             assert v["gweight"] < 1e-5 and v["gatt"] < 1e-5 and v["gbias"] < 1e-5, (key, v)
 
 
+def _gat_uneven_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "pytorch_geometric-1_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=_PG_TIMEOUT)
+    try:
+        from mi355_mp import dist as mdist
+        from mi355_mp.graphgen import powerlaw_edge_index
+        from torch_geometric.nn import GATConv
+        dev = torch.device("cuda", 0)
+        N, Fi, H, C = 1500, 24, 4, 16
+        ei = powerlaw_edge_index(N, 20000, seed=71).to(dev)
+        gen = torch.Generator().manual_seed(71)
+        x = torch.randn(N, Fi, generator=gen).to(dev)
+        gout = torch.randn(N, H * C, generator=gen).to(dev)
+        res = {}
+        # an empty rank (cuts [0, N, N]) and a rank holding a single row
+        for name, cuts in (("empty_rank", [0, N, N]), ("one_row", [0, 1, N])):
+            ref = GATConv(Fi, C, heads=H).to(dev)
+            with torch.no_grad():
+                ref.bias.normal_()
+            mdist.broadcast_parameters(ref)
+            xr = x.clone().requires_grad_(True)
+            out_ref = ref(xr, ei)
+            (out_ref * gout).sum().backward()
+            sg = mdist.ShardedGraph.for_gat(ei, N, rank, world, cuts=cuts)
+            conv = mdist.ShardedGATConv(Fi, C, heads=H).to(dev)
+            conv.load_state_dict(ref.state_dict())
+            lo, hi = sg.lo, sg.hi
+            xo = x[lo:hi].clone().requires_grad_(True)
+            out = conv(xo, sg)
+            (out * gout[lo:hi]).sum().backward()
+            mdist.allreduce_gradients(conv)
+            r = {"rows": hi - lo, "out": float((out.detach() - out_ref.detach()[lo:hi]).abs().max()) if hi > lo else 0.0,
+                 "gx": float((xo.grad - xr.grad[lo:hi]).abs().max()) if hi > lo else 0.0}
+            for k in ("weight", "att", "bias"):
+                a, b = getattr(conv, k).grad, getattr(ref, k).grad
+                r["g" + k] = float((a - b).abs().max() / b.abs().max())
+            res[name] = r
+            # GCN on the same cuts: the layer (pull plan), then the hybrid halo cover, then
+            # max with global argmax ids, against the single-GPU layer / kernel
+            from torch_geometric.nn import GCNConv
+            from mi355_mp import ops
+            gref = GCNConv(Fi, 32).to(dev)
+            with torch.no_grad():
+                gref.bias.normal_()
+            mdist.broadcast_parameters(gref)
+            xr = x.clone().requires_grad_(True)
+            gref(xr, ei).square().sum().backward()
+            sgc = mdist.ShardedGraph.for_gcn(ei, N, rank, world, cuts=cuts)
+            gconv = mdist.ShardedGCNConv(Fi, 32).to(dev)
+            gconv.load_state_dict(gref.state_dict())
+            xo = x[lo:hi].clone().requires_grad_(True)
+            go = gconv(xo, sgc)
+            go.square().sum().backward()
+            mdist.allreduce_gradients(gconv)
+            want = gref(x, ei).detach()[lo:hi]
+            r2 = {"rows": hi - lo, "out": float((go.detach() - want).abs().max()) if hi > lo else 0.0,
+                  "gx": float((xo.grad - xr.grad[lo:hi]).abs().max()) if hi > lo else 0.0,
+                  "gweight": float((gconv.weight.grad - gref.weight.grad).abs().max() / gref.weight.grad.abs().max()),
+                  "gatt": 0.0,
+                  "gbias": float((gconv.bias.grad - gref.bias.grad).abs().max() / gref.bias.grad.abs().max())}
+            h = x @ gref.weight.detach()
+            oc = sgc.enable_halo_cover().propagate(h[lo:hi].contiguous())
+            r2["cover"] = float((oc - (want - gref.bias.detach())).abs().max()) if hi > lo else 0.0
+            sgm = mdist.ShardedGraph(ei, N, rank, world, cuts=cuts)
+            om, am = sgm.propagate(h[lo:hi].contiguous(), "max")
+            from mi355_mp.graph import Graph
+            o1, a1 = ops._aggregate(Graph(ei, N, N).dst, "other", h, None, "max", 0, None)
+            r2["max_exact"] = bool(torch.equal(om, o1[lo:hi]) and torch.equal(am, a1[lo:hi]))
+            res[name + "_gcn"] = r2
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_gatconv_uneven_cuts_on_one_gpu():
+    """Sharded layers when a rank owns no rows (its local graph has no
+    destinations but still sends halo rows and joins every collective) and
+    when a rank owns one row: ShardedGATConv and ShardedGCNConv outputs, d x
+    and the all-reduced parameter gradients against the single-GPU layers;
+    the GCN propagate over the hybrid halo cover; max with global argmax ids
+    bit-equal to the single-GPU kernel."""
+    res = _spawn(_gat_uneven_worker, world=2)
+    for rank, r in res:
+        for name, v in r.items():
+            assert v["out"] < 1e-5 and v["gx"] < 1e-5, (rank, name, v)
+            assert v["gweight"] < 1e-5 and v["gatt"] < 1e-5 and v["gbias"] < 1e-5, (rank, name, v)
+            if name.endswith("_gcn"):
+                assert v["cover"] < 1e-4 and v["max_exact"], (rank, name, v)
+        assert sorted(v["rows"] for k, v in r.items() if not k.endswith("_gcn")) == sorted(
+            ({0: 1500, 1: 0}[rank], {0: 1, 1: 1499}[rank]))
+
+
 def _products_worker(rank, world, port, q):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
