@@ -458,3 +458,55 @@ def test_slice_build_rejects_out_of_range_ids_on_every_rank(world):
         assert p.exitcode == 0
     res = sorted(q.get(timeout=10) for _ in range(world))
     assert all(r[1] == [True, True] for r in res), res
+
+
+def _tiny_worker(rank, world, port, result_q, N, edges):
+    """Degenerate shards built from per-rank slices: fewer edges than ranks
+    (empty slices), ranks that own no rows, a graph with no edges at all."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "pytorch_geometric-1_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mi355_mp import dist as mdist
+        from oracle import pyg_ref as P, scatter_ref as S
+        ei = torch.tensor(edges, dtype=torch.long).view(2, -1)
+        E = ei.shape[1]
+        s0, s1 = rank * E // world, (rank + 1) * E // world
+        sg = mdist.ShardedGraph.for_gcn_from_slices(ei[:, s0:s1].clone(), s0, N, rank, world)
+        ei2, norm = P.gcn_norm(ei, N, None, False)
+        x = torch.randn(N, 3, generator=torch.Generator().manual_seed(7))
+
+        def local_aggregate(xl, lei, n_dst, n_src, wl):
+            return S.gather_sum(xl, lei[0], lei[1], wl, n_dst)
+        out = mdist.sharded_propagate(sg.fwd, x[sg.lo:sg.hi].contiguous(), local_aggregate,
+                                      lambda t, idx: t[idx], edge_weight=sg.norm_fwd)
+        want = S.gather_sum(x, ei2[0], ei2[1], norm, N)[sg.lo:sg.hi]
+        result_q.put((rank, bool(torch.equal(out, want)) and sg.n_edges == ei2.shape[1], sg.lo, sg.hi))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,N,edges", [
+    (4, 5, [[0, 3], [1, 4]]),          # 2 edges over 4 ranks: empty slices
+    (3, 4, [[], []]),                  # no edges at all: loops only
+    (3, 1, [[0], [0]]),                # one node: two ranks own nothing
+    (2, 6, [[5, 5, 5, 4], [0, 1, 2, 5]]),
+])
+def test_slice_built_shards_degenerate_graphs(world, N, edges):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tiny_worker, args=(r, world, port, q, N, edges)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    res = sorted(q.get(timeout=10) for _ in range(world))
+    assert all(r[1] for r in res), res
+    assert sum(r[3] - r[2] for r in res) == N

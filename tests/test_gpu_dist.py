@@ -177,7 +177,7 @@ def _layer_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def _spawn(target, world=2, timeout=600):
+def _spawn(target, world=2, timeout=600, args=()):
     """Run target(rank, world, port, q) in `world` spawned processes and return
     their sorted queue items.  Fails fast: the first rank to exit non-zero, or
     the deadline, terminates the others (a rank stuck in a collective whose peer
@@ -186,7 +186,7 @@ def _spawn(target, world=2, timeout=600):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + tuple(args)) for r in range(world)]
     for p in procs:
         p.start()
     deadline = time.monotonic() + timeout
@@ -1024,3 +1024,55 @@ def test_sharded_gcnconv_over_halo_cover_on_one_gpu(world):
         assert r["out"] < 1e-5 and r["gx"] < 1e-5 and r["gw"] < 1e-5, r
         assert r["exact"]["sum"] and r["exact"]["mean"], r
     assert sum(r["rows_cover"] for _, r in res) < sum(r["rows_pull"] for _, r in res), res
+
+
+def _tiny_gpu_worker(rank, world, port, q, N, edges):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "pytorch_geometric-1_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=_PG_TIMEOUT)
+    try:
+        from mi355_mp import dist as mdist, ops
+        from mi355_mp.graph import Graph
+        from torch_geometric.nn.conv.gcn_conv import GCNConv
+        dev = torch.device("cuda", 0)
+        ei = torch.tensor(edges, dtype=torch.long).view(2, -1).to(dev)
+        E = ei.shape[1]
+        s0, s1 = rank * E // world, (rank + 1) * E // world
+        sg = mdist.ShardedGraph.for_gcn_from_slices(ei[:, s0:s1].clone(), s0, N, rank, world)
+        x = torch.randn(N, 64, generator=torch.Generator().manual_seed(7)).to(dev)
+        ei2, norm = GCNConv.norm(ei, N)
+        g1 = Graph(ei2, N, N)
+        want = ops._aggregate(g1.dst, "other", x, g1.dst.to_csr_order(norm), "sum", 0, None)[0][sg.lo:sg.hi]
+        res = {"rows": sg.hi - sg.lo}
+        res["pull"] = float((sg.propagate(x[sg.lo:sg.hi].contiguous()) - want).abs().max()) if sg.n_own else 0.0
+        # the bench's overlapped tiled step (hybrid cover) on the same shards
+        ov = mdist.OverlappedAggregation(sg.fwd, sg.norm_fwd, local_weights=True, cover=True)
+        tiles = ov.local_tiles(64, 32)
+        for t, xt in enumerate(tiles):
+            xt[:sg.n_own].copy_(x[sg.lo:sg.hi, 32 * t:32 * (t + 1)])
+        out = torch.empty((sg.n_own, 64), device=dev)
+        ov.step_tiled(tiles, out)
+        res["cover"] = float((out - want).abs().max()) if sg.n_own else 0.0
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,N,edges", [
+    (4, 5, [[0, 3], [1, 4]]),          # 2 edges over 4 ranks: empty slices
+    (3, 4, [[], []]),                  # no edges at all: loops only
+    (3, 1, [[0], [0]]),                # one node: two ranks own nothing
+])
+def test_slice_built_shards_degenerate_graphs_on_one_gpu(world, N, edges):
+    """The native slice build, the sharded propagate and the bench's overlapped
+    tiled step over the hybrid cover on degenerate graphs (empty slices, ranks
+    owning no rows, no edges at all), against the single-GPU kernel."""
+    res = _spawn(_tiny_gpu_worker, world=world, timeout=300, args=(N, edges))
+    assert sum(r["rows"] for _, r in res) == N
+    for rank, r in res:
+        assert r["pull"] < 1e-6 and r["cover"] < 1e-6, (rank, r)
