@@ -1049,7 +1049,8 @@ def _tiny_gpu_worker(rank, world, port, q, N, edges):
         g1 = Graph(ei2, N, N)
         want = ops._aggregate(g1.dst, "other", x, g1.dst.to_csr_order(norm), "sum", 0, None)[0][sg.lo:sg.hi]
         res = {"rows": sg.hi - sg.lo}
-        res["pull"] = float((sg.propagate(x[sg.lo:sg.hi].contiguous()) - want).abs().max()) if sg.n_own else 0.0
+        po = sg.propagate(x[sg.lo:sg.hi].contiguous())     # every rank: the exchange is collective
+        res["pull"] = float((po - want).abs().max()) if sg.n_own else 0.0
         # the bench's overlapped tiled step (hybrid cover) on the same shards
         ov = mdist.OverlappedAggregation(sg.fwd, sg.norm_fwd, local_weights=True, cover=True)
         tiles = ov.local_tiles(64, 32)
