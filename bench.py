@@ -18,6 +18,10 @@ Workloads (one GCNConv propagate per step, F = 256, fp32):
   products (BASELINE.json configs[4], the 8 x MI355X configuration)
            ogbn-products scale power-law graph, N = 2,449,029,
            E = 123,718,280 (E' = 126,163,923), x ~ N(0,1), seed 4.
+  reddit   (BASELINE.json configs[3], one GPU) Reddit-scale power-law graph,
+           N = 232,965, E = 114,615,892, seed 3, F = 256: one step = the fused
+           segmented max + int64 first-index argmax (+ PyG's -10000 mask) over
+           every edge -- metric: edges aggregated/s with argmax.
   gat      (BASELINE.json configs[2]) the rmat21 graph, GATConv 8 heads x 32:
            one step = the fused node scores + leaky_relu + softmax + aggregate +
            bias (mp_gat_forward_f32); N > 1: the X W halo rows over the pull
@@ -82,6 +86,11 @@ def _products(dev):
     return powerlaw_edge_index(2_449_029, 123_718_280, seed=4, device=dev)
 
 
+def _reddit(dev):
+    from mi355_mp.graphgen import powerlaw_edge_index
+    return powerlaw_edge_index(232_965, 114_615_892, seed=3, device=dev)
+
+
 WORKLOADS = {
     "gat": {"name": "rmat21_gat_h8c32", "num_nodes": 1 << 21, "seed": 2, "gen": _rmat21,
             "baseline_config": 3,
@@ -89,6 +98,10 @@ WORKLOADS = {
     "rmat21": {"name": "rmat21_gcn_f256", "num_nodes": 1 << 21, "seed": 1, "gen": _rmat21,
                "baseline_config": 2,
                "graph": "RMAT scale 21 (.57,.19,.19,.05) 30M samples symmetrised + add_remaining_self_loops"},
+    "reddit": {"name": "reddit_max_f256", "num_nodes": 232_965, "seed": 3, "gen": _reddit,
+               "baseline_config": 4,
+               "graph": "Reddit-scale power-law (RMAT into [0, N)), 114,615,892 directed edges, aggr='max' + "
+                        "int64 first-index argmax + utils.scatter_'s -10000 mask"},
     "products": {"name": "products_gcn_f256", "num_nodes": 2_449_029, "seed": 4, "gen": _products,
                  "baseline_config": 5,
                  "graph": "ogbn-products-scale power-law (RMAT into [0, N)), 123,718,280 directed edges "
@@ -599,15 +612,160 @@ def main_gat(args, rank, world, local):
         dist.destroy_process_group()
 
 
+def cpu_max_baseline(ei, x, sample):
+    """max + argmax on the host (oracle, kind 'port'): torch index_select, then
+    torch_scatter 2.0.4's serial CPU scatter_max loop (scatter_cpu.cpp, restated
+    in oracle/scatter_loop.c), on the first `sample` edges in 4M-edge chunks
+    accumulated through `out` (the loop's has_out path)."""
+    from oracle import scatter_ref as S  # checker/baseline only
+    model, threads, machine = cpu_info()
+    torch.set_num_threads(threads)
+    E = min(sample, ei.shape[1])
+    eic, xc = ei[:, :E].cpu(), x.cpu()
+    N, F = xc.shape
+    out = torch.full((N, F), -3.4028234663852886e38)
+    t0 = time.perf_counter()
+    for s0 in range(0, E, 4_000_000):
+        e1 = min(E, s0 + 4_000_000)
+        msg = xc.index_select(0, eic[0, s0:e1])
+        out, _ = S.scatter_loop(msg, eic[1, s0:e1], N, "max", out=out)
+    dt = time.perf_counter() - t0
+    return {"value": E / dt, "unit": "edges/s", "cores": threads, "kind": "port", "cpu_model": model,
+            "machine_cpus": machine,
+            "sample": "first %d of %d edges: torch index_select (%d threads) + the serial scatter_max loop "
+                      "(1 thread, oracle/scatter_loop.c), %.1f s" % (E, ei.shape[1], threads, dt)}
+
+
+def verify_max(out, arg, x, src, dst, step=2_000_000):
+    """Exact check of a max + first-index argmax aggregation: the max by
+    torch's scatter_reduce('amax') and the arg as the smallest edge id whose
+    message equals it (scatter_reduce('amin') over edge ids), in edge chunks;
+    empty rows (0, E); the PyG -10000 mask.  Bitwise, values and args."""
+    n, F = out.shape
+    E = src.numel()
+    ref = torch.full((n, F), float("-inf"), device=out.device)
+    for s in range(0, E, step):
+        ref.scatter_reduce_(0, dst[s:s + step].view(-1, 1).expand(-1, F), x[src[s:s + step]], "amax")
+    ids = torch.full((n, F), E, dtype=torch.int64, device=out.device)
+    for s in range(0, E, step):
+        d = dst[s:s + step]
+        hit = x[src[s:s + step]] == ref[d]
+        cand = torch.where(hit, torch.arange(s, s + d.numel(), device=out.device).view(-1, 1), E)
+        ids.scatter_reduce_(0, d.view(-1, 1).expand(-1, F), cand, "amin")
+    ref = torch.where(torch.isinf(ref) | (ref < -10000), torch.zeros_like(ref), ref)
+    return {"rows": n, "edges": E, "values_bitwise_equal": bool(torch.equal(out, ref)),
+            "args_bitwise_equal": bool(torch.equal(arg, ids)),
+            "reference": "torch scatter_reduce amax + smallest edge id attaining it (amin), edge chunks"}
+
+
+def main_reddit(args, rank, world, local):
+    """--workload reddit: BASELINE config 4 (one GPU), aggr='max' with int64
+    first-index argmax and PyG's -10000 mask over every edge of the
+    Reddit-scale graph; one step = the fused main launch + its fix-up."""
+    import mi355_mp
+    from mi355_mp import _lib, ops
+    from mi355_mp.graph import Graph
+    wl = WORKLOADS["reddit"]
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    lib = mi355_mp.load_native()
+    N, F = wl["num_nodes"], F_DIM
+    t0 = time.perf_counter()
+    ei = wl["gen"](dev)
+    x = torch.randn(N, F, device=dev, generator=torch.Generator(device=dev).manual_seed(wl["seed"]))
+    torch.cuda.synchronize()
+    t_gen = time.perf_counter() - t0
+    stage(rank, "reddit graph generated (%.1f s)" % t_gen)
+    t0 = time.perf_counter()
+    graph = Graph(ei, N, N)
+    csr = graph.dst
+    torch.cuda.synchronize()
+    t_build = time.perf_counter() - t0
+    E = csr.n_edges
+    out = torch.empty(N, F, device=dev)
+    arg = torch.empty(N, F, dtype=torch.int64, device=dev)
+    st_main = csr.struct("other")
+    slab = torch.empty(lib.mp_aggregate_slab_bytes(st_main, F, _lib.MP_REDUCE["max"]), dtype=torch.uint8, device=dev)
+
+    def aggregate(stages):
+        # stage by stage: every edge is gathered (the one-off form of a layer's
+        # first two calls; ops' first-occurrence CSR engages from the third)
+        ops._aggregate(csr, "other", x, None, "max", _lib.MP_FLAG_PYG_MASK, None, out=out, stages=stages,
+                       slab=slab, arg=arg)
+
+    ev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.steps)]
+    for _ in range(args.warmup):
+        aggregate(_lib.MP_STAGE_MAIN)
+        aggregate(_lib.MP_STAGE_FIXUP)
+    torch.cuda.synchronize()
+    stage(rank, "warm-up done (%d steps)" % args.warmup)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record()
+        aggregate(_lib.MP_STAGE_MAIN)
+        ev[i][1].record()
+        aggregate(_lib.MP_STAGE_FIXUP)
+        ev[i][2].record()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    stage(rank, "timed steps done: %.3f ms/step" % (dt / args.steps * 1e3))
+    main_ms = sorted(a.elapsed_time(b) for a, b, _ in ev)
+    fix_ms = sorted(b.elapsed_time(c) for _, b, c in ev)
+    main_avg, fix_avg = sum(main_ms) / len(main_ms), sum(fix_ms) / len(fix_ms)
+    verify = verify_max(out, arg, x, ei[0], ei[1]) if args.verify else None
+    if verify is not None:
+        stage(rank, "verify: %s" % json.dumps(verify))
+    kernel = _lib.kernel_name(st_main, None, x.data_ptr(), F, F, "max", None, out.data_ptr(), F, dev)
+    src_hash = lib.mp_source_hash().decode()
+    traffic, traffic_src = find_pmc(wl["name"], kernel, src_hash)
+    # compulsory: x once, col + eid per slot, rowptr, out and the int64 arg once
+    comp = N * F * 4 + E * 8 + (N + 1) * 4 + N * F * 12
+    alg = E * (4 * F + 4) + N * (4 * F + 8 * F + 4)       # SURVEY 8(d): 1028 B/edge + 3076 B/node
+    cpu = cpu_max_baseline(ei, x, 12_000_000) if not args.no_cpu_baseline else None
+    line = {
+        "metric": "edges aggregated/sec (aggr='max' + int64 first-index argmax, PyG -10000 mask, F=256)",
+        "value": E * args.steps / dt, "unit": "edges/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "dtype": "f32", "data": "synthetic Reddit-scale power-law graph (seeded, generated on device), random features",
+        "config": {"workload": wl["name"], "baseline_config": wl["baseline_config"], "graph": wl["graph"],
+                   "num_nodes": N, "num_edges": E, "features": F, "seed": wl["seed"], "parallelism": "single GPU",
+                   "chunk": csr.chunk},
+        "roofline": {"bound": "hbm", "achieved": comp / (main_avg * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": comp / (main_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_frac": (traffic / (main_avg * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
+                     "traffic_source": traffic_src,
+                     "bytes": "achieved = compulsory bytes (x read once, col + eid, rowptr, out and int64 arg "
+                              "written once) / avg launch time",
+                     "compulsory_bytes_per_launch": comp, "algorithmic_bytes_per_launch": alg,
+                     "algorithmic_GBps_no_cache_credit": alg / (main_avg * 1e-3) / 1e9,
+                     "kernel": kernel, "source_hash": src_hash, "avg_launch_ms": main_avg,
+                     "median_launch_ms": main_ms[len(main_ms) // 2], "fixup_avg_ms": fix_avg,
+                     "timing": "HIP events around each main / fix-up launch inside the timed steps"},
+        "cpu_baseline": cpu,
+        "extra": {"one_time_build_s": t_build, "graph_gen_s": t_gen, "n_split_rows": csr.n_split,
+                  "n_wave_tasks": csr.n_waves, "verify": verify,
+                  "note": "x is 238 MB: it fits the 256 MB Infinity Cache"},
+    }
+    print(json.dumps(line), flush=True)
+    stage(rank, "done")
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
+    if args.workload == "reddit" and (args.gpus > 1 or args.sharded):
+        # BASELINE config 4 is a one-GPU configuration (x is 238 MB: it fits one
+        # GPU's Infinity Cache); the sharded max path is ShardedGraph.propagate
+        stage("-", "ERROR: --workload reddit is BASELINE config 4, a one-GPU configuration")
+        sys.exit(2)
     if args.gpus > 1 and "RANK" not in os.environ:
         sys.exit(launch_ranks(args, argv))
     rank, world, local = setup_dist(args)
     sharded = dist.is_initialized()
     if args.workload == "gat":
         return main_gat(args, rank, world, local)
+    if args.workload == "reddit":
+        return main_reddit(args, rank, world, local)
     wl = WORKLOADS[args.workload]
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)

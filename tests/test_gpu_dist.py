@@ -817,6 +817,20 @@ def test_bench_products_workload_two_ranks():
     assert sum(p["rows"] for p in d["extra"]["per_rank"]) == 2_449_029
 
 
+def test_bench_reddit_workload_one_gpu():
+    """--workload reddit (BASELINE config 4: N = 232,965, E = 114,615,892,
+    aggr='max' + int64 first-index argmax + the -10000 mask) on one GPU:
+    --verify holds every value and every argmax bit-equal to torch's
+    scatter_reduce amax and the smallest edge id attaining it."""
+    d, _ = _run_bench(["bench.py", "--workload", "reddit", "--steps", "3", "--warmup", "1", "--no-cpu-baseline",
+                       "--verify"])
+    assert d["n_gpus"] == 1 and d["config"]["workload"] == "reddit_max_f256"
+    assert d["config"]["num_edges"] == 114_615_892 and d["config"]["baseline_config"] == 4
+    v = d["extra"]["verify"]
+    assert v["values_bitwise_equal"] and v["args_bitwise_equal"], v
+    assert d["value"] > 5e9 and "ArgRed" in d["roofline"]["kernel"]
+
+
 @pytest.mark.parametrize("gpus", [1, 2])
 def test_bench_gat_workload(gpus):
     """--workload gat (BASELINE config 3: the rmat21 graph, GATConv 8 heads x 32)

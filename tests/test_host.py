@@ -310,6 +310,15 @@ def test_bench_starts_its_own_ranks():
     assert "starting 3 ranks" in r.stderr
 
 
+def test_bench_config4_workload_is_one_gpu():
+    """--workload reddit (BASELINE config 4, a one-GPU configuration) with
+    --gpus 2 exits non-zero before launching ranks or touching a GPU."""
+    r = _bench(["bench.py", "--gpus", "2", "--workload", "reddit"], {})
+    assert r.returncode == 2, r.stderr[-2000:]
+    assert "one-GPU configuration" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
 def test_bench_refuses_a_world_that_differs_from_gpus():
     """Launched by torch.distributed.run with 2 ranks but --gpus 3: every rank
     exits non-zero before any work (no line claiming n_gpus it did not use)."""
