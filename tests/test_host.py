@@ -412,3 +412,24 @@ def test_torch_scatter_dispatcher_ops_under_fake_tensors():
         op = getattr(ops, n).default
         assert torch._C._dispatch_has_kernel_for_dispatch_key(op.name(), "CUDA"), n
         assert torch._C._dispatch_has_kernel_for_dispatch_key(op.name(), "Autograd"), n
+
+
+def test_bench_verify_max_matches_the_serial_loop():
+    """bench.py's chunked max + first-index argmax verifier (the config-4
+    workload's --verify) agrees with the oracle's serial scatter_max loop on a
+    tie-heavy graph with empty rows, and rejects a moved argmax."""
+    import bench
+    from oracle import scatter_ref as S
+    g = torch.Generator().manual_seed(13)
+    N, E, F = 300, 5000, 9
+    src = torch.randint(0, N, (E,), generator=g)
+    dst = torch.randint(0, N - 20, (E,), generator=g)         # the last 20 rows stay empty
+    x = torch.randint(-3, 4, (N, F), generator=g).float()
+    out, arg = S.scatter_loop(x[src], dst, N, "max")
+    out = torch.where(out < -10000, torch.zeros_like(out), out)
+    v = bench.verify_max(out, arg, x, src, dst, step=777)
+    assert v["values_bitwise_equal"] and v["args_bitwise_equal"], v
+    bad = arg.clone()
+    r = int(dst[0])
+    bad[r, 0] = E - 1 if bad[r, 0] != E - 1 else 0
+    assert not bench.verify_max(out, bad, x, src, dst)["args_bitwise_equal"]
