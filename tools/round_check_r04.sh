@@ -1,6 +1,6 @@
 #!/bin/bash
 # One GPU call, round 4: the GPU suite + smoke + default bench (tools/gpu_check.sh),
-# then the other bench workloads at N = 1 (config 5 products, config 3 GAT), the
+# then the other bench workloads at N = 1 (config 5 products, config 3 GAT, config 4 max), the
 # config-5 workload as bench.py's own 2-rank launch (gloo ranks sharing the GPU,
 # --verify), and every other config / layer (tools/bench_configs.py) -- the
 # inputs of DESIGN.md section 2.  Each step under its own time limit; a
@@ -19,6 +19,7 @@ step() {  # name timeout cmd...
 }
 step bench_products_n1 300 python -u bench.py --workload products --steps 20 --warmup 5 --verify
 step bench_gat_n1 300 python -u bench.py --workload gat --steps 20 --warmup 5 --verify
+step bench_reddit_n1 300 python -u bench.py --workload reddit --steps 20 --warmup 5 --verify
 MP_BENCH_BACKEND=gloo step bench_products_gloo2 400 python -u bench.py --gpus 2 --workload products --steps 5 \
   --warmup 2 --no-cpu-baseline --no-ref-paths --verify
 echo "== bench_configs"; date +%T
