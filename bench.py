@@ -65,6 +65,11 @@ import torch  # noqa: E402  (importing torch does not initialise the GPU)
 import torch.distributed as dist  # noqa: E402
 
 F_DIM = 256
+# feature tilings the N>1 warm-up times (--halo-tile -1): two 128-feature tiles, or a
+# 64-feature tile first (the exchange starts after a quarter of the send pack) and last
+# (the step ends a quarter-boundary pass after the last exchange) -- the link-bound
+# P = 2 step's chain pack_0 + exchange + boundary_last
+HALO_TILINGS = ([128, 128], [64, 128, 64])
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md chip table)
 # SURVEY 8(d) / BASELINE.md section 2 algorithmic bytes: every gathered x_j row
 # counted at full size, no cache-reuse credit.  Reported, but its ratio to the
@@ -131,9 +136,10 @@ def parse(argv=None):
                     help="run the N>1 sharded path (shards, plans, halo exchange, per-rank split) even at "
                          "one rank -- under torch.distributed.run --nproc-per-node 1 it rehearses the "
                          "driver's multi-GPU code path on the RCCL backend with empty halos")
-    ap.add_argument("--halo-tile", type=int, default=128,
+    ap.add_argument("--halo-tile", type=int, default=-1,
                     help="N>1: exchange and finish the boundary edges per feature tile of this width "
-                         "(pipelined); 0 = one exchange of whole rows")
+                         "(pipelined); 0 = one exchange of whole rows; -1 (default) = chosen in the warm-up "
+                         "among HALO_TILINGS by timing each on this job's links (max over ranks)")
     return ap.parse_args(argv)
 
 
@@ -825,12 +831,42 @@ def main(argv=None):
         torch.cuda.synchronize()
         t_exchange_plan = time.perf_counter() - t0 - t_shards
         x_tiles = x_ov = None
-        if args.halo_tile > 0 and not args.no_overlap:
-            x_tiles = overlap.local_tiles(F_DIM, args.halo_tile)
+        tile_tune = None
+
+        def make_tiles(tiling):
+            tiles = overlap.local_tiles(F_DIM, tiling)
             c0 = 0
-            for xt in x_tiles:
+            for xt in tiles:
                 xt[:plan.n_own].copy_(x_full[plan.lo:plan.hi, c0:c0 + xt.shape[1]])
                 c0 += xt.shape[1]
+            return tiles
+        if args.halo_tile != 0 and not args.no_overlap:
+            if args.halo_tile > 0:
+                tiling = mdist.tile_widths(F_DIM, args.halo_tile)
+            else:
+                # warm-up autotune: every rank times each tiling (one untimed step, then 3),
+                # the max over ranks decides -- the same choice on every rank
+                tune_out = torch.empty((plan.n_own, F_DIM), device=dev)
+                tile_tune = {}
+                for cand in HALO_TILINGS:
+                    tiles = make_tiles(cand)
+                    overlap.step_tiled(tiles, tune_out, bias)
+                    torch.cuda.synchronize()
+                    barrier(world)
+                    t1 = time.perf_counter()
+                    for _ in range(3):
+                        overlap.step_tiled(tiles, tune_out, bias)
+                    torch.cuda.synchronize()
+                    tt = torch.tensor([(time.perf_counter() - t1) / 3 * 1e3], dtype=torch.float64)
+                    tt = tt.to(dev) if dist.get_backend() == "nccl" else tt
+                    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+                    tile_tune[str(cand)] = float(tt.item())
+                    del tiles
+                del tune_out
+                tiling = min(HALO_TILINGS, key=lambda c: tile_tune[str(c)])
+                stage(rank, "halo tiling chosen in the warm-up: %s (max over ranks, ms/step: %s)"
+                      % (tiling, json.dumps(tile_tune)))
+            x_tiles = make_tiles(tiling)
         elif not args.no_overlap:
             x_ov = overlap.local_buffer(F_DIM)
             x_ov[:plan.n_own].copy_(x_full[plan.lo:plan.hi])
@@ -1089,6 +1125,8 @@ def main(argv=None):
                       "interior_edges_rank0": overlap.n_interior if sharded else E_local,
                       "overlap": sharded and not args.no_overlap,
                       "halo_tile": args.halo_tile if sharded and not args.no_overlap else None,
+                      "halo_tiles": [int(t.shape[1]) for t in x_tiles] if sharded and x_tiles is not None else None,
+                      "halo_tile_autotune_ms": tile_tune if sharded else None,
                       "collective_timeout_s": COLLECTIVE_TIMEOUT_S if sharded else None,
                       "n_wave_tasks": csr.n_waves,
                       "per_rank": ranks,

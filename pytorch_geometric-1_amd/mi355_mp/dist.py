@@ -44,6 +44,17 @@ def _a2a(out, inp, out_splits=None, in_splits=None, group=None):
     return out
 
 
+def tile_widths(F, tile):
+    """Feature-tile widths covering F: `tile` wide each (the last takes the
+    rest), or an explicit list of widths summing to F."""
+    if isinstance(tile, (list, tuple)):
+        widths = [int(w) for w in tile]
+        if sum(widths) != F or min(widths) <= 0:
+            raise ValueError("tile widths %s do not cover %d features" % (widths, F))
+        return widths
+    return [min(int(tile), F - c0) for c0 in range(0, F, int(tile))]
+
+
 def edge_balanced_cuts(in_degree, parts):
     """Row cut points [0=c_0 <= ... <= c_P = N] with ~equal edges per part."""
     N = in_degree.numel()
@@ -164,12 +175,12 @@ class ShardPlan:
         return x_local
 
     def local_tiles(self, F, tile=128, dtype=torch.float32, device=None):
-        """Tile-major [n_own + n_halo, tile] buffers covering F features, for
+        """Tile-major [n_own + n_halo, width] buffers covering F features, for
         OverlappedAggregation.step_tiled: each tile's halo rows are contiguous,
-        so every tile is exchanged (and received in place) on its own."""
+        so every tile is exchanged (and received in place) on its own.  tile:
+        one width (the last tile takes the rest) or the list of widths."""
         dev = device or self.halo_nodes.device
-        widths = [min(tile, F - c0) for c0 in range(0, F, tile)]
-        return [torch.empty((self.n_local_src, w), dtype=dtype, device=dev) for w in widths]
+        return [torch.empty((self.n_local_src, w), dtype=dtype, device=dev) for w in tile_widths(F, tile)]
 
     def halo_exchange(self, x_own, gather_rows, group=None):
         """[own rows ; halo rows] for this rank (allocating form)."""
@@ -675,8 +686,7 @@ class OverlappedAggregation:
     def local_tiles(self, F, tile=128, dtype=torch.float32, device=None):
         """Tile-major buffers for step_tiled (see ShardPlan.local_tiles)."""
         dev = device or self.plan.halo_nodes.device
-        return [torch.empty((self.n_local_src, min(tile, F - c0)), dtype=dtype, device=dev)
-                for c0 in range(0, F, tile)]
+        return [torch.empty((self.n_local_src, w), dtype=dtype, device=dev) for w in tile_widths(F, tile)]
 
     def _send(self, own):
         """This rank's send buffer: the requested rows (pull), or with a cover
