@@ -433,3 +433,15 @@ def test_bench_verify_max_matches_the_serial_loop():
     r = int(dst[0])
     bad[r, 0] = E - 1 if bad[r, 0] != E - 1 else 0
     assert not bench.verify_max(out, bad, x, src, dst)["args_bitwise_equal"]
+
+
+def test_halo_tile_widths():
+    """Feature tilings of the sharded step: uniform widths (the last tile takes
+    the rest) or an explicit list that must cover F exactly."""
+    from mi355_mp import dist as mdist
+    assert mdist.tile_widths(256, 128) == [128, 128]
+    assert mdist.tile_widths(200, 128) == [128, 72]
+    assert mdist.tile_widths(256, [64, 128, 64]) == [64, 128, 64]
+    for bad in ([64, 64], [0, 256], [128, 129]):
+        with pytest.raises(ValueError):
+            mdist.tile_widths(256, bad)
