@@ -20,6 +20,11 @@
  *     all outputs and workspaces (sizes from the *_bytes queries).
  *   - Return value: MP_OK or an MP_ERR_* code; mp_last_error() gives the text
  *     (thread-local).
+ *   - Extents (ABI 6): every caller-allocated workspace, partial or per-edge
+ *     array whose size is not fixed by the call's own row / edge counts alone
+ *     is passed with its size in bytes (`*_bytes`).  A buffer shorter than the
+ *     call needs is rejected with MP_ERR_ARG before anything is launched, so a
+ *     mis-sized array is an error, never an out-of-bounds device write.
  *   - Graph structure is a destination-sorted CSR (stable: inside a row the
  *     edges keep their original order), described by `mp_csr`.  All kernels
  *     are deterministic: no float atomics on any forward output.
@@ -34,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MP_ABI_VERSION 5
+#define MP_ABI_VERSION 6
 
 /* status codes */
 #define MP_OK 0
@@ -323,7 +328,8 @@ int mp_gat_sddmm_f32(const mp_csr* g, const int32_t* slot_row, const float* grow
  *   de[k, h]        = alpha_ij (<g_i, xw_j>_h - rs[i,h]) leaky'(a_src[j,h]+a_dst[i,h])
  *   grad_a_src[j,h] = sum over the row of de
  * alpha_ij = exp(leaky(score) - m_i) / den_i from the forward's row_stats.
- * pack [n_dst, H, 4] = mp_gat_backward_prep_f32 output.  de[gt.eid[k], h]
+ * pack [n_dst, H, 4] = mp_gat_backward_prep_f32 output.  de [gt.n_edges, H]
+ * (de_bytes >= gt.n_edges * H * 4; ABI 6): de[gt.eid[k], h]
  * receives slot k's value: pass the destination-CSR slot of each edge in
  * gt.eid to get de in destination-CSR order (then d a_dst is a contiguous
  * segmented sum: mp_aggregate_f32 with col = NULL).  de = NULL skips it (the
@@ -333,7 +339,8 @@ int mp_gat_sddmm_f32(const mp_csr* g, const int32_t* slot_row, const float* grow
 int mp_gat_backward_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, const float* xw,
                         const float* a_src, const float* pack, const float* att, int32_t H,
                         int32_t C, float slope, float* grad_xw, float* grad_a_src, float* de,
-                        void* slab, size_t slab_bytes, int32_t stages, void* stream);
+                        size_t de_bytes, void* slab, size_t slab_bytes, int32_t stages,
+                        void* stream);
 
 /* The same pass after the training forward: no per-edge d score; grad_a_dst
  * [n_rows, H] (mp_gat_backward_prep_train_f32) is an input, and each row's
@@ -350,10 +357,13 @@ int mp_gat_backward_train_f32(const mp_csr* gt, const float* grad_out, int64_t l
  * rs[n,h] = sum_c grad_out[n, h*C+c] * agg[n, h*C+c]  (agg = pre-bias GAT output;
  * rs = sum_j alpha_nj <g_n, xw_j>_h, the softmax-backward row term).
  * gsum_part (optional, [mp_gat_bwd_blocks(n), H*C], needs C%4==0, H*C<=256):
- * per-block column sums of grad_out (the bias gradient is their sum over blocks). */
+ * per-block column sums of grad_out (the bias gradient is their sum over blocks).
+ * Extents (ABI 6): pack_bytes >= n*H*16, gsum_part_bytes >= mp_gat_bwd_blocks(n)*H*C*4
+ * (ignored when gsum_part is NULL). */
 int mp_gat_backward_prep_f32(const float* grad_out, int64_t ldg, const float* agg, int64_t lda,
                              const float* a_dst, const float* row_stats, int64_t n, int32_t H,
-                             int32_t C, float* pack, float* gsum_part, void* stream);
+                             int32_t C, float* pack, size_t pack_bytes, float* gsum_part,
+                             size_t gsum_part_bytes, void* stream);
 
 /* The same prologue after mp_gat_aggregate_train_f32 (C % 4 == 0, C/4 a power
  * of two <= 64, 16-byte aligned rows), which also writes
@@ -362,7 +372,8 @@ int mp_gat_backward_prep_f32(const float* grad_out, int64_t ldg, const float* ag
 int mp_gat_backward_prep_train_f32(const float* grad_out, int64_t ldg, const float* agg, int64_t lda,
                                    const float* agg2, const float* row_s2, const float* a_dst,
                                    const float* row_stats, int64_t n, int32_t H, int32_t C,
-                                   float* pack, float* gsum_part, float* grad_a_dst, void* stream);
+                                   float* pack, size_t pack_bytes, float* gsum_part,
+                                   size_t gsum_part_bytes, float* grad_a_dst, void* stream);
 
 /* ---- GATConv with heads of any width (C % 4 == 0) --------------------------
  * The reference's own GAT stacks (ConvexPruning.py:209-214) use heads = 1 and
@@ -382,18 +393,20 @@ int mp_gat_backward_prep_train_f32(const float* grad_out, int64_t ldg, const flo
  *     slot), slab mp_gat_train_slab_bytes(gt, H, C)), then
  *     mp_gat_backward_epilogue_wide_f32: grad_a_src = <acc2, xw>_h - sc (written
  *     over sc) and grad_xw += grad_a_src att[h, C:] + grad_a_dst att[h, :C].
- * Rows contiguous [n, H*C] unless an ld is given; 16-byte aligned. */
+ * Rows contiguous [n, H*C] unless an ld is given; 16-byte aligned.
+ * Extents (ABI 6): pack_bytes >= n*H*16; acc2_bytes >= gt->n_rows*H*C*4,
+ * sc_bytes >= gt->n_rows*H*4. */
 int mp_gat_wide_ok(int32_t H, int32_t C);
 int mp_gat_node_scores_wide_f32(const float* xw, int64_t n_nodes, int32_t H, int32_t C, const float* att,
                                 float* a_src, float* a_dst, void* stream);
 int mp_gat_backward_prep_wide_f32(const float* grad_out, int64_t ldg, const float* agg, int64_t lda,
                                   const float* agg2, const float* row_s2, const float* a_dst,
                                   const float* row_stats, int64_t n, int32_t H, int32_t C, float* pack,
-                                  float* grad_a_dst, void* stream);
+                                  size_t pack_bytes, float* grad_a_dst, void* stream);
 int mp_gat_backward_wide_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, const float* a_src,
                              const float* pack, int32_t H, int32_t C, float slope, uint64_t seed, float p_drop,
-                             float* grad_xw, float* acc2, float* sc, void* slab, size_t slab_bytes,
-                             int32_t stages, void* stream);
+                             float* grad_xw, float* acc2, size_t acc2_bytes, float* sc, size_t sc_bytes,
+                             void* slab, size_t slab_bytes, int32_t stages, void* stream);
 int mp_gat_backward_epilogue_wide_f32(float* grad_xw, const float* acc2, const float* xw, const float* att,
                                       const float* grad_a_dst, float* sc_grad_a_src, int64_t n, int32_t H,
                                       int32_t C, void* stream);
@@ -446,9 +459,11 @@ int mp_gat_dropout_keep(uint64_t seed, float p_drop, int32_t H, int64_t n_slots,
                         void* stream);
 
 /* Per-block column sums of x [n, F] (0 < F <= 256, F % 4 == 0, 16-byte aligned
- * rows): part [mp_gat_bwd_blocks(n), F]; sum_i x[i, :] is their sum over the
- * blocks (a layer's bias gradient, sum over rows of grad_out). */
-int mp_col_sums_f32(const float* x, int64_t ldx, int64_t n, int32_t F, float* part, void* stream);
+ * rows): part [mp_gat_bwd_blocks(n), F] (part_bytes >= that * 4; ABI 6);
+ * sum_i x[i, :] is their sum over the blocks (a layer's bias gradient, sum over
+ * rows of grad_out). */
+int mp_col_sums_f32(const float* x, int64_t ldx, int64_t n, int32_t F, float* part, size_t part_bytes,
+                    void* stream);
 
 /* Rows of the per-block partial arrays of the prep/finish kernels for n nodes. */
 int mp_gat_bwd_blocks(int64_t n);
@@ -458,10 +473,13 @@ int mp_gat_bwd_blocks(int64_t n);
  *   att_part[b, 0, :]  = sum over block b's nodes of ga_dst[n,h] * xw[n, h*C+c]
  *   att_part[b, 1, :]  = ... ga_src[n,h] * xw[n, h*C+c]
  * att_part is [mp_gat_bwd_blocks(n), 2, H*C]; d att = its sum over blocks.
+ * att_part_bytes >= mp_gat_bwd_blocks(n) * 2*H*C * 4 (ABI 6: a partial array
+ * sized for fewer rows than n -- e.g. a sharded rank's own rows when the pass
+ * runs over own + halo rows -- is MP_ERR_ARG, not a device write past its end).
  * grad_xw = NULL: the att-gradient partials only. */
 int mp_gat_backward_finish_f32(float* grad_xw, const float* xw, const float* ga_dst,
                                const float* ga_src, const float* att, int64_t n, int32_t H,
-                               int32_t C, float* att_part, void* stream);
+                               int32_t C, float* att_part, size_t att_part_bytes, void* stream);
 
 /* y[n, h*C+c] += s[n,h] * att[h*att_ld + c]  (per-head outer-product update) */
 int mp_heads_outer_add_f32(float* y, int64_t ldy, const float* s, int64_t n, int32_t H,
@@ -609,15 +627,16 @@ int mp_csr_inverse_eid(const mp_csr* g, int32_t* inv, void* stream);
  *   3. (optional) mp_scatter_arg_grad_w_f32: grad_w[e] = sum over the features
  *      e won of grad_out[dst_map[e], f] * x[src_map[e], f] (fixed reduction tree),
  *      0 for edges that won nothing; every entry written.
- * The mask must be 8-byte aligned. */
+ * The mask must be 8-byte aligned; mask_bytes >= n_edges * mp_arg_mask_words(F) * 4
+ * in all three calls (ABI 6). */
 int32_t mp_arg_mask_words(int32_t F);
 int mp_arg_winner_mask(const int64_t* arg, int64_t n_rows, int32_t F, int64_t n_edges,
-                       const int32_t* inv, uint32_t* mask, void* stream);
-int mp_scatter_arg_backward_csr_f32(const mp_csr* gt, const uint32_t* mask,
+                       const int32_t* inv, uint32_t* mask, size_t mask_bytes, void* stream);
+int mp_scatter_arg_backward_csr_f32(const mp_csr* gt, const uint32_t* mask, size_t mask_bytes,
                                     const float* grad_out, int64_t ldg, int32_t F,
                                     const float* w, float* grad, int64_t ldgx, void* stream);
 int mp_scatter_arg_grad_w_f32(const int64_t* src_map, const int64_t* dst_map, int64_t n_edges,
-                              const int32_t* inv, const uint32_t* mask, int32_t F,
+                              const int32_t* inv, const uint32_t* mask, size_t mask_bytes, int32_t F,
                               const float* grad_out, int64_t ldg, const float* x, int64_t ldx,
                               float* grad_w, void* stream);
 

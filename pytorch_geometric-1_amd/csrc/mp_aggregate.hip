@@ -2536,11 +2536,13 @@ static int gat_backward(const mp_csr* gt, const float* grad_out, int64_t ldg, co
 
 int mp_gat_backward_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, const float* xw, const float* a_src,
                         const float* pack, const float* att, int32_t H, int32_t C, float slope, float* grad_xw,
-                        float* grad_a_src, float* de, void* slab, size_t slab_bytes, int32_t stages, void* stream) {
+                        float* grad_a_src, float* de, size_t de_bytes, void* slab, size_t slab_bytes, int32_t stages,
+                        void* stream) {
   // without the training forward's node-wise d a_dst the per-edge d score is the
   // only way d a_dst comes out: it is required (mp_gat_backward_train_f32 otherwise)
   MP_CHECK_ARG(de != nullptr || !gt || gt->n_edges == 0,
                "mp_gat_backward_f32: de is required (use mp_gat_backward_train_f32 after the training forward)");
+  if (gt && H > 0) MP_CHECK_EXTENT("mp_gat_backward_f32", "de", de_bytes, (size_t)gt->n_edges * H * 4);
   return gat_backward(gt, grad_out, ldg, xw, a_src, pack, att, H, C, slope, grad_xw, grad_a_src, de, nullptr, slab,
                       slab_bytes, stages, stream);
 }
@@ -2580,8 +2582,8 @@ int mp_gat_backward_train_drop_f32(const mp_csr* gt, const float* grad_out, int6
 
 int mp_gat_backward_wide_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, const float* a_src,
                              const float* pack, int32_t H, int32_t C, float slope, uint64_t seed, float p_drop,
-                             float* grad_xw, float* acc2, float* sc, void* slab, size_t slab_bytes, int32_t stages,
-                             void* stream) {
+                             float* grad_xw, float* acc2, size_t acc2_bytes, float* sc, size_t sc_bytes, void* slab,
+                             size_t slab_bytes, int32_t stages, void* stream) {
   MP_DEVICE_GUARD(stream);
   int rc = check_graph(gt, "mp_gat_backward_wide_f32");
   if (rc) return rc;
@@ -2598,6 +2600,8 @@ int mp_gat_backward_wide_f32(const mp_csr* gt, const float* grad_out, int64_t ld
                "mp_gat_backward_wide_f32: grad_out, grad_xw, acc2, pack must be 16-byte aligned");
   MP_CHECK_ARG(slab && slab_bytes >= mp_gat_train_slab_bytes(gt, H, C),
                "mp_gat_backward_wide_f32: slab workspace too small (mp_gat_train_slab_bytes)");
+  MP_CHECK_EXTENT("mp_gat_backward_wide_f32", "acc2", acc2_bytes, (size_t)gt->n_rows * F * 4);
+  MP_CHECK_EXTENT("mp_gat_backward_wide_f32", "sc", sc_bytes, (size_t)gt->n_rows * H * 4);
   AggArgs a{};
   fill_graph(a, gt);
   a.F = F;

@@ -19,6 +19,12 @@ void set_error(const char* fmt, ...);
     }                                  \
   } while (0)
 
+// ABI 6: a caller-allocated array passed with its extent in bytes must hold
+// what the call writes (or reads); checked before any launch.
+#define MP_CHECK_EXTENT(fn, name, have, need)                                                  \
+  MP_CHECK_ARG((size_t)(have) >= (size_t)(need), "%s: %s holds %zu bytes, the call needs %zu", \
+               fn, name, (size_t)(have), (size_t)(need))
+
 #define MP_CHECK_HIP(expr)                                                   \
   do {                                                                       \
     hipError_t _e = (expr);                                                  \

@@ -383,13 +383,18 @@ int mp_gat_sddmm_f32(const mp_csr* g, const int32_t* slot_row, const float* grow
 int mp_gat_backward_prep_train_f32(const float* grad_out, int64_t ldg, const float* agg, int64_t lda,
                                    const float* agg2, const float* row_s2, const float* a_dst,
                                    const float* row_stats, int64_t n, int32_t H, int32_t C, float* pack,
-                                   float* gsum_part, float* grad_a_dst, void* stream) {
+                                   size_t pack_bytes, float* gsum_part, size_t gsum_part_bytes, float* grad_a_dst,
+                                   void* stream) {
   MP_DEVICE_GUARD(stream);
   MP_CHECK_ARG(H > 0 && C > 0 && n >= 0, "mp_gat_backward_prep_train_f32: bad sizes");
   if (n == 0) return MP_OK;
   MP_CHECK_ARG(grad_out && agg && agg2 && row_s2 && a_dst && row_stats && pack && grad_a_dst,
                "mp_gat_backward_prep_train_f32: null pointer");
   const int64_t F = (int64_t)H * C;
+  MP_CHECK_EXTENT("mp_gat_backward_prep_train_f32", "pack", pack_bytes, (size_t)n * H * 16);
+  if (gsum_part)
+    MP_CHECK_EXTENT("mp_gat_backward_prep_train_f32", "gsum_part", gsum_part_bytes,
+                    (size_t)mp_gat_bwd_blocks(n) * F * 4);
   const int G = C / 4;
   MP_CHECK_ARG(C % 4 == 0 && G <= 64 && (G & (G - 1)) == 0, "mp_gat_backward_prep_train_f32: needs C/4 a power of two");
   MP_CHECK_ARG((uintptr_t)pack % 16 == 0 && (uintptr_t)grad_out % 16 == 0 && (uintptr_t)agg % 16 == 0 &&
@@ -403,12 +408,14 @@ int mp_gat_backward_prep_train_f32(const float* grad_out, int64_t ldg, const flo
   return MP_OK;
 }
 
-int mp_col_sums_f32(const float* x, int64_t ldx, int64_t n, int32_t F, float* part, void* stream) {
+int mp_col_sums_f32(const float* x, int64_t ldx, int64_t n, int32_t F, float* part, size_t part_bytes,
+                    void* stream) {
   MP_DEVICE_GUARD(stream);
   MP_CHECK_ARG(n >= 0 && F > 0 && F <= 256 && F % 4 == 0, "mp_col_sums_f32: needs 0 < F <= 256, F %% 4 == 0");
   MP_CHECK_ARG(part && (n == 0 || (x && ldx >= F && ldx % 4 == 0 && (uintptr_t)x % 16 == 0)),
                "mp_col_sums_f32: bad argument (16-byte aligned rows required)");
   const int nb = mp_gat_bwd_blocks(n);
+  MP_CHECK_EXTENT("mp_col_sums_f32", "part", part_bytes, (size_t)nb * F * 4);
   if (n == 0) {
     MP_CHECK_HIP(hipMemsetAsync(part, 0, (size_t)nb * F * sizeof(float), as_stream(stream)));
     return MP_OK;
@@ -426,13 +433,16 @@ int mp_gat_bwd_blocks(int64_t n) {
 
 int mp_gat_backward_prep_f32(const float* grad_out, int64_t ldg, const float* agg, int64_t lda, const float* a_dst,
                              const float* row_stats, int64_t n, int32_t H, int32_t C, float* pack,
-                             float* gsum_part, void* stream) {
+                             size_t pack_bytes, float* gsum_part, size_t gsum_part_bytes, void* stream) {
   MP_DEVICE_GUARD(stream);
   MP_CHECK_ARG(H > 0 && C > 0 && n >= 0, "mp_gat_backward_prep_f32: bad sizes");
   if (n == 0) return MP_OK;
   MP_CHECK_ARG(grad_out && agg && a_dst && row_stats && pack, "mp_gat_backward_prep_f32: null pointer");
   MP_CHECK_ARG((uintptr_t)pack % 16 == 0, "mp_gat_backward_prep_f32: pack must be 16-byte aligned");
   const int64_t F = (int64_t)H * C;
+  MP_CHECK_EXTENT("mp_gat_backward_prep_f32", "pack", pack_bytes, (size_t)n * H * 16);
+  if (gsum_part)
+    MP_CHECK_EXTENT("mp_gat_backward_prep_f32", "gsum_part", gsum_part_bytes, (size_t)mp_gat_bwd_blocks(n) * F * 4);
   MP_CHECK_ARG(ldg >= F && lda >= F, "mp_gat_backward_prep_f32: leading dimension < H*C");
   hipStream_t s = as_stream(stream);
   const int G = C / 4;
@@ -451,11 +461,14 @@ int mp_gat_backward_prep_f32(const float* grad_out, int64_t ldg, const float* ag
 }
 
 int mp_gat_backward_finish_f32(float* grad_xw, const float* xw, const float* ga_dst, const float* ga_src,
-                                const float* att, int64_t n, int32_t H, int32_t C, float* att_part, void* stream) {
+                                const float* att, int64_t n, int32_t H, int32_t C, float* att_part,
+                                size_t att_part_bytes, void* stream) {
   MP_DEVICE_GUARD(stream);
   MP_CHECK_ARG(H > 0 && C > 0 && n >= 0, "mp_gat_backward_finish_f32: bad sizes");
   MP_CHECK_ARG(C % 4 == 0 && H * C <= 256, "mp_gat_backward_finish_f32: needs C %% 4 == 0 and H*C <= 256");
   MP_CHECK_ARG(xw && ga_dst && ga_src && att && att_part, "mp_gat_backward_finish_f32: null pointer");
+  MP_CHECK_EXTENT("mp_gat_backward_finish_f32", "att_part", att_part_bytes,
+                  (size_t)mp_gat_bwd_blocks(n) * 2 * H * C * 4);
   MP_CHECK_ARG((uintptr_t)grad_xw % 16 == 0 && (uintptr_t)xw % 16 == 0 && (uintptr_t)att % 16 == 0,
                "mp_gat_backward_finish_f32: 16-byte alignment required");
   k_gat_bwd_finish<<<(unsigned)mp_gat_bwd_blocks(n), 256, 0, as_stream(stream)>>>(grad_xw, xw, ga_dst, ga_src, att, n,

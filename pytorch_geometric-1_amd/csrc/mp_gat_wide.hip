@@ -146,12 +146,14 @@ int mp_gat_node_scores_wide_f32(const float* xw, int64_t n_nodes, int32_t H, int
 
 int mp_gat_backward_prep_wide_f32(const float* grad_out, int64_t ldg, const float* agg, int64_t lda,
                                   const float* agg2, const float* row_s2, const float* a_dst, const float* row_stats,
-                                  int64_t n, int32_t H, int32_t C, float* pack, float* grad_a_dst, void* stream) {
+                                  int64_t n, int32_t H, int32_t C, float* pack, size_t pack_bytes,
+                                  float* grad_a_dst, void* stream) {
   MP_DEVICE_GUARD(stream);
   MP_CHECK_ARG(mp_gat_wide_ok(H, C) && n >= 0, "mp_gat_backward_prep_wide_f32: needs C %% 4 == 0");
   if (n == 0) return MP_OK;
   MP_CHECK_ARG(grad_out && agg && agg2 && row_s2 && a_dst && row_stats && pack && grad_a_dst,
                "mp_gat_backward_prep_wide_f32: null pointer");
+  MP_CHECK_EXTENT("mp_gat_backward_prep_wide_f32", "pack", pack_bytes, (size_t)n * H * 16);
   const int64_t F = (int64_t)H * C;
   MP_CHECK_ARG(ldg >= F && lda >= F && ldg % 4 == 0 && lda % 4 == 0, "mp_gat_backward_prep_wide_f32: bad ld");
   MP_CHECK_ARG(al16(grad_out) && al16(agg) && al16(agg2) && al16(pack),

@@ -200,13 +200,14 @@ int mp_csr_inverse_eid(const mp_csr* g, int32_t* inv, void* stream) {
 int32_t mp_arg_mask_words(int32_t F) { return F > 0 ? 2 * (int32_t)ceil_div(F, 64) : 0; }
 
 int mp_arg_winner_mask(const int64_t* arg, int64_t n_rows, int32_t F, int64_t n_edges, const int32_t* inv,
-                       uint32_t* mask, void* stream) {
+                       uint32_t* mask, size_t mask_bytes, void* stream) {
   MP_DEVICE_GUARD(stream);
   MP_CHECK_ARG(n_rows >= 0 && F >= 0 && n_edges >= 0, "mp_arg_winner_mask: negative size");
   const int32_t W = mp_arg_mask_words(F);
   hipStream_t s = as_stream(stream);
   if (n_edges == 0 || F == 0) return MP_OK;
   MP_CHECK_ARG(mask && inv && (n_rows == 0 || arg), "mp_arg_winner_mask: null pointer");
+  MP_CHECK_EXTENT("mp_arg_winner_mask", "mask", mask_bytes, (size_t)n_edges * W * 4);
   MP_CHECK_HIP(hipMemsetAsync(mask, 0, (size_t)n_edges * W * sizeof(uint32_t), s));
   const int64_t total = n_rows * (int64_t)F;
   if (total == 0) return MP_OK;
@@ -215,8 +216,9 @@ int mp_arg_winner_mask(const int64_t* arg, int64_t n_rows, int32_t F, int64_t n_
   return MP_OK;
 }
 
-int mp_scatter_arg_backward_csr_f32(const mp_csr* gt, const uint32_t* mask, const float* grad_out, int64_t ldg,
-                                    int32_t F, const float* w, float* grad, int64_t ldgx, void* stream) {
+int mp_scatter_arg_backward_csr_f32(const mp_csr* gt, const uint32_t* mask, size_t mask_bytes,
+                                    const float* grad_out, int64_t ldg, int32_t F, const float* w, float* grad,
+                                    int64_t ldgx, void* stream) {
   MP_DEVICE_GUARD(stream);
   MP_CHECK_ARG(gt && F >= 0, "mp_scatter_arg_backward_csr_f32: bad arguments");
   if (gt->n_rows == 0 || F == 0) return MP_OK;
@@ -225,6 +227,7 @@ int mp_scatter_arg_backward_csr_f32(const mp_csr* gt, const uint32_t* mask, cons
   MP_CHECK_ARG(ldg >= F && ldgx >= F, "mp_scatter_arg_backward_csr_f32: leading dimension < F");
   MP_CHECK_ARG((uintptr_t)mask % 8 == 0, "mp_scatter_arg_backward_csr_f32: mask must be 8-byte aligned");
   const int32_t W = mp_arg_mask_words(F);
+  MP_CHECK_EXTENT("mp_scatter_arg_backward_csr_f32", "mask", mask_bytes, (size_t)gt->n_edges * W * 4);
   int64_t bx = ceil_div(gt->n_rows, 4);
   if (bx > 65536) bx = 65536;
   dim3 grid((unsigned)bx, (unsigned)(W / 2));
@@ -235,8 +238,8 @@ int mp_scatter_arg_backward_csr_f32(const mp_csr* gt, const uint32_t* mask, cons
 }
 
 int mp_scatter_arg_grad_w_f32(const int64_t* src_map, const int64_t* dst_map, int64_t n_edges, const int32_t* inv,
-                              const uint32_t* mask, int32_t F, const float* grad_out, int64_t ldg, const float* x,
-                              int64_t ldx, float* grad_w, void* stream) {
+                              const uint32_t* mask, size_t mask_bytes, int32_t F, const float* grad_out, int64_t ldg,
+                              const float* x, int64_t ldx, float* grad_w, void* stream) {
   MP_DEVICE_GUARD(stream);
   MP_CHECK_ARG(n_edges >= 0 && F >= 0, "mp_scatter_arg_grad_w_f32: negative size");
   if (n_edges == 0) return MP_OK;
@@ -244,6 +247,7 @@ int mp_scatter_arg_grad_w_f32(const int64_t* src_map, const int64_t* dst_map, in
                "mp_scatter_arg_grad_w_f32: null pointer");
   MP_CHECK_ARG(ldg >= F && ldx >= F, "mp_scatter_arg_grad_w_f32: leading dimension < F");
   const int32_t W = mp_arg_mask_words(F);
+  MP_CHECK_EXTENT("mp_scatter_arg_grad_w_f32", "mask", mask_bytes, (size_t)n_edges * W * 4);
   if (F == 0) {
     MP_CHECK_HIP(hipMemsetAsync(grad_w, 0, (size_t)n_edges * sizeof(float), as_stream(stream)));
     return MP_OK;

@@ -95,7 +95,7 @@ SIGNATURES = {
                                               sz, i32, c_p]),
     "mp_gat_sddmm_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, i64, c_p, i64, i32, i32, c_p, c_p]),
     "mp_gat_backward_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, i64, c_p, c_p, c_p, c_p, i32, i32,
-                                           ctypes.c_float, c_p, c_p, c_p, c_p, sz, i32, c_p]),
+                                           ctypes.c_float, c_p, c_p, c_p, sz, c_p, sz, i32, c_p]),
     "mp_gat_backward_train_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, i64, c_p, c_p, c_p, c_p, i32, i32,
                                                  ctypes.c_float, c_p, c_p, c_p, c_p, sz, i32, c_p]),
     "mp_gat_aggregate_train_drop_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, c_p, c_p, i32, i32, f32,
@@ -106,19 +106,20 @@ SIGNATURES = {
     "mp_gat_dropout_keep": (ctypes.c_int, [u64, f32, i32, i64, c_p, c_p]),
     "mp_gat_wide_ok": (ctypes.c_int, [i32, i32]),
     "mp_gat_node_scores_wide_f32": (ctypes.c_int, [c_p, i64, i32, i32, c_p, c_p, c_p, c_p]),
-    "mp_gat_backward_prep_wide_f32": (ctypes.c_int, [c_p, i64, c_p, i64, c_p, c_p, c_p, c_p, i64, i32, i32, c_p, c_p,
-                                                     c_p]),
+    "mp_gat_backward_prep_wide_f32": (ctypes.c_int, [c_p, i64, c_p, i64, c_p, c_p, c_p, c_p, i64, i32, i32, c_p, sz,
+                                                     c_p, c_p]),
     "mp_gat_backward_wide_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, i64, c_p, c_p, i32, i32, f32, u64, f32,
-                                                c_p, c_p, c_p, c_p, sz, i32, c_p]),
+                                                c_p, c_p, sz, c_p, sz, c_p, sz, i32, c_p]),
     "mp_gat_backward_epilogue_wide_f32": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, c_p, i64, i32, i32, c_p]),
     "mp_segment_offset_i64": (ctypes.c_int, [c_p, i64, i32, i64, c_p, c_p, i64, c_p]),
     "mp_segment_ids_i64": (ctypes.c_int, [c_p, i64, c_p, i64, c_p]),
-    "mp_gat_backward_prep_f32": (ctypes.c_int, [c_p, i64, c_p, i64, c_p, c_p, i64, i32, i32, c_p, c_p, c_p]),
+    "mp_gat_backward_prep_f32": (ctypes.c_int, [c_p, i64, c_p, i64, c_p, c_p, i64, i32, i32, c_p, sz, c_p, sz,
+                                                c_p]),
     "mp_gat_backward_prep_train_f32": (ctypes.c_int, [c_p, i64, c_p, i64, c_p, c_p, c_p, c_p, i64, i32, i32, c_p,
-                                                      c_p, c_p, c_p]),
+                                                      sz, c_p, sz, c_p, c_p]),
     "mp_gat_bwd_blocks": (ctypes.c_int, [i64]),
-    "mp_col_sums_f32": (ctypes.c_int, [c_p, i64, i64, i32, c_p, c_p]),
-    "mp_gat_backward_finish_f32": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, i64, i32, i32, c_p, c_p]),
+    "mp_col_sums_f32": (ctypes.c_int, [c_p, i64, i64, i32, c_p, sz, c_p]),
+    "mp_gat_backward_finish_f32": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, i64, i32, i32, c_p, sz, c_p]),
     "mp_heads_outer_add_f32": (ctypes.c_int, [c_p, i64, c_p, i64, i32, i32, c_p, i64, c_p]),
     "mp_gather_rows_f32": (ctypes.c_int, [c_p, i64, c_p, i64, i32, c_p, i64, c_p]),
     "mp_permute_f32": (ctypes.c_int, [c_p, c_p, i64, c_p, c_p]),
@@ -135,9 +136,10 @@ SIGNATURES = {
     "mp_segment_sum_serial_f32": (ctypes.c_int, [c_p, c_p, c_p, i64, c_p, c_p]),
     "mp_csr_inverse_eid": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p]),
     "mp_arg_mask_words": (i32, [i32]),
-    "mp_arg_winner_mask": (ctypes.c_int, [c_p, i64, i32, i64, c_p, c_p, c_p]),
-    "mp_scatter_arg_backward_csr_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, i64, i32, c_p, c_p, i64, c_p]),
-    "mp_scatter_arg_grad_w_f32": (ctypes.c_int, [c_p, c_p, i64, c_p, c_p, i32, c_p, i64, c_p, i64, c_p, c_p]),
+    "mp_arg_winner_mask": (ctypes.c_int, [c_p, i64, i32, i64, c_p, c_p, sz, c_p]),
+    "mp_scatter_arg_backward_csr_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, sz, c_p, i64, i32, c_p, c_p, i64,
+                                                       c_p]),
+    "mp_scatter_arg_grad_w_f32": (ctypes.c_int, [c_p, c_p, i64, c_p, c_p, sz, i32, c_p, i64, c_p, i64, c_p, c_p]),
     "mp_segment_reduce": (ctypes.c_int, [ctypes.POINTER(MpCsr), i32, c_p, i64, i32, i32, i32, c_p, i64, c_p, c_p]),
     "mp_gather_rows_any": (ctypes.c_int, [i32, c_p, i64, c_p, i64, i32, c_p, i64, c_p]),
     "mp_scatter_arg_any": (ctypes.c_int, [i32, c_p, c_p, i64, i32, i64, c_p, i64, c_p]),
@@ -241,6 +243,12 @@ def stream_ptr(device=None):
 
 def ptr(t):
     return None if t is None else t.data_ptr()
+
+
+def nbytes(t):
+    """Extent in bytes of a caller-allocated array passed to the C-ABI (ABI 6:
+    workspaces and partial arrays travel with their size; 0 for None)."""
+    return 0 if t is None else t.numel() * t.element_size()
 
 
 def require_device(*tensors):

@@ -383,10 +383,14 @@ def gcn_shards_from_slices(edge_slice, slice_offset, num_nodes, rank, world, gro
     fill = 2.0 if improved else 1.0
     keep = row != col
     kept = torch.nonzero(keep).view(-1)
-    sizes = _all_gather_ints([n, kept.numel()], group)
-    if slice_offset != sum(sz[0] for sz in sizes[:rank]):
-        raise ValueError("gcn_shards_from_slices: rank %d's slice offset %d does not follow the earlier slices"
-                         % (rank, slice_offset))
+    # every rank's offset travels with its sizes, so every rank checks every
+    # offset and all of them raise together (a lone raising rank would leave its
+    # peers waiting in the next collective until the group's timeout)
+    sizes = _all_gather_ints([n, kept.numel(), int(slice_offset)], group)
+    for r, sz in enumerate(sizes):
+        if sz[2] != sum(t[0] for t in sizes[:r]):
+            raise ValueError("gcn_shards_from_slices: rank %d's slice offset %d does not follow the earlier slices"
+                             % (r, sz[2]))
     k_off = sum(sz[1] for sz in sizes[:rank])
     E_kept = sum(sz[1] for sz in sizes)
     kr, kc, kw = row[kept], col[kept], w[kept]
@@ -1181,17 +1185,32 @@ def broadcast_parameters(module, src=0, group=None):
 
 def allreduce_gradients(module, group=None):
     """Sum the gradients of replicated parameters over the ranks (each rank's
-    weight gradient covers its own rows only), as DDP would.  Every trainable
-    parameter takes part on every rank, in the same order: a rank whose rows
-    never reached a parameter (e.g. a rank that owns no rows, whose empty
-    output does not involve GATConv's att) contributes zeros -- skipping it
-    there would pair different tensors in the collectives of different ranks."""
-    for p in module.parameters():
-        if not p.requires_grad:
+    weight gradient covers its own rows only), as DDP would.  The ranks first
+    sum one has-grad flag per parameter (one collective); every parameter some
+    rank has a gradient for then takes part on every rank, in the same order: a
+    rank whose rows never reached it (e.g. a rank that owns no rows, whose
+    empty output does not involve GATConv's att) contributes zeros -- skipping
+    it there would pair different tensors in the collectives of different
+    ranks.  A parameter no rank has a gradient for keeps grad None on every
+    rank (an optimizer with momentum or weight decay leaves it alone, as it
+    does on one GPU)."""
+    params = [p for p in module.parameters() if p.requires_grad]
+    if not params:
+        return
+    # one has-grad flag per parameter, summed over the ranks in one collective:
+    # a parameter no rank formed a gradient for keeps grad None everywhere (an
+    # optimizer with momentum / weight decay then leaves it alone, as on one GPU)
+    gloo = dist.get_backend(group) == "gloo"
+    dev = params[0].device
+    flags = torch.tensor([p.grad is not None for p in params], dtype=torch.int32,
+                         device="cpu" if gloo else dev)
+    dist.all_reduce(flags, group=group)
+    for p, f in zip(params, flags.tolist()):
+        if f == 0:
             continue
         if p.grad is None:
             p.grad = torch.zeros_like(p)
-        if p.grad.is_cuda and dist.get_backend(group) == "gloo":
+        if p.grad.is_cuda and gloo:
             t = p.grad.cpu()
             dist.all_reduce(t, group=group)
             p.grad.copy_(t)

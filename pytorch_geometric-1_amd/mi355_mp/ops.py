@@ -131,8 +131,8 @@ def col_sums(g):
             and g.data_ptr() % 16 == 0 and g.dtype == torch.float32:
         lib = _lib.load()
         part = torch.empty((int(lib.mp_gat_bwd_blocks(n)), F), dtype=torch.float32, device=g.device)
-        _lib.check(lib.mp_col_sums_f32(g.data_ptr(), g.stride(0), n, F, part.data_ptr(), _lib.stream_ptr(g.device)),
-                   "mp_col_sums_f32")
+        _lib.check(lib.mp_col_sums_f32(g.data_ptr(), g.stride(0), n, F, part.data_ptr(), _lib.nbytes(part),
+                                       _lib.stream_ptr(g.device)), "mp_col_sums_f32")
         return part.sum(0)
     return g.sum(0)
 
@@ -155,14 +155,15 @@ def arg_backward(graph, arg, g, n_src, edge_weight=None, x=None, want_gx=True, w
     inv = src.inverse_eid()
     W = int(lib.mp_arg_mask_words(F))
     mask = torch.empty(max(E * W, 2), dtype=torch.int32, device=dev)
-    _lib.check(lib.mp_arg_winner_mask(arg.data_ptr(), g.shape[0], F, E, inv.data_ptr(), mask.data_ptr(), st),
-               "mp_arg_winner_mask")
+    _lib.check(lib.mp_arg_winner_mask(arg.data_ptr(), g.shape[0], F, E, inv.data_ptr(), mask.data_ptr(),
+                                      _lib.nbytes(mask), st), "mp_arg_winner_mask")
     w = edge_weight.to(torch.float32).contiguous() if edge_weight is not None else None
     gx = gw = None
     if want_gx:
         gx = torch.empty((int(n_src), F), dtype=torch.float32, device=dev)
-        _lib.check(lib.mp_scatter_arg_backward_csr_f32(src.struct("other"), mask.data_ptr(), g.data_ptr(), g.stride(0),
-                                                       F, _lib.ptr(w), gx.data_ptr(), gx.stride(0), st),
+        _lib.check(lib.mp_scatter_arg_backward_csr_f32(src.struct("other"), mask.data_ptr(), _lib.nbytes(mask),
+                                                       g.data_ptr(), g.stride(0), F, _lib.ptr(w), gx.data_ptr(),
+                                                       gx.stride(0), st),
                    "mp_scatter_arg_backward_csr_f32")
     if want_gw:
         ei = graph._edge_index()
@@ -170,7 +171,8 @@ def arg_backward(graph, arg, g, n_src, edge_weight=None, x=None, want_gx=True, w
         dsts = ei[graph.i].contiguous()
         gw = torch.empty(max(E, 1), dtype=torch.float32, device=dev)[:E]
         _lib.check(lib.mp_scatter_arg_grad_w_f32(srcs.data_ptr(), dsts.data_ptr(), E, inv.data_ptr(), mask.data_ptr(),
-                                                 F, g.data_ptr(), g.stride(0), x.data_ptr(), x.stride(0),
+                                                 _lib.nbytes(mask), F, g.data_ptr(), g.stride(0), x.data_ptr(),
+                                                 x.stride(0),
                                                  gw.data_ptr(), st), "mp_scatter_arg_grad_w_f32")
     return gx, gw
 
@@ -376,13 +378,27 @@ _range_cache = _Cache()
 
 def index_range(idx):
     """(min, max) of an index tensor: one aminmax and one host read the first
-    time, then cached on the tensor (identity + version counter, dropped with
-    it -- graph._Cache), so the per-forward checks of a reused edge_index cost
-    a dictionary lookup, not a device sync."""
+    time, then cached on the tensor (identity + version counter + data pointer,
+    dropped with it -- graph._Cache), so the per-forward checks of a reused
+    edge_index cost a dictionary lookup, not a device sync.
+
+    Limitation (the same contract as the per-edge_index CSR cache, graph_for):
+    a write that does not bump the version counter -- through ``.data``, a
+    DLPack / from_blob alias, or a raw-pointer kernel -- is not seen.  After such
+    a write call forget_index(idx) (or mutate through ordinary in-place ops)."""
     def compute():
         mn, mx = torch.aminmax(idx)
         return tuple(torch.stack([mn, mx]).tolist())
-    return _range_cache.get(idx, "range", compute)
+    return _range_cache.get(idx, ("range", idx.data_ptr()), compute)
+
+
+def forget_index(idx):
+    """Drop every cached fact about idx (its range and CSR graphs): for index
+    tensors written behind autograd's back (see index_range)."""
+    from .graph import _graph_cache, _index_cache
+    base = idx._base if idx._base is not None else idx
+    for c in (_range_cache, _graph_cache, _index_cache):
+        c._drop(id(base))
 
 
 def check_row_index(idx, n, what="index_select"):
@@ -799,8 +815,8 @@ def _gat_backward_wide(graph, g, xw, att, a_src, a_dst, stats, agg, extra, H, C,
     if n_dst:
         _lib.check(lib.mp_gat_backward_prep_wide_f32(g.data_ptr(), g.stride(0), agg.data_ptr(), agg.stride(0),
                                                      agg2.data_ptr(), s2.data_ptr(), a_dst.data_ptr(),
-                                                     stats.data_ptr(), n_dst, H, C, pack.data_ptr(), ga_dst.data_ptr(),
-                                                     st), "mp_gat_backward_prep_wide_f32")
+                                                     stats.data_ptr(), n_dst, H, C, pack.data_ptr(), _lib.nbytes(pack),
+                                                     ga_dst.data_ptr(), st), "mp_gat_backward_prep_wide_f32")
     src = graph.src_with_dst_slots()
     gs = src.struct("dst_slot")
     gx = torch.empty((N, F), dtype=torch.float32, device=dev)
@@ -810,8 +826,9 @@ def _gat_backward_wide(graph, g, xw, att, a_src, a_dst, stats, agg, extra, H, C,
     slab = torch.empty(sb, dtype=torch.uint8, device=dev)
     seed, p = (0, 0.0) if drop is None else (int(drop[0]), float(drop[1]))
     _lib.check(lib.mp_gat_backward_wide_f32(gs, g.data_ptr(), g.stride(0), a_src.data_ptr(), pack.data_ptr(), H, C,
-                                            float(slope), seed, p, gx.data_ptr(), acc2.data_ptr(), sc.data_ptr(),
-                                            slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st), "mp_gat_backward_wide_f32")
+                                            float(slope), seed, p, gx.data_ptr(), acc2.data_ptr(), _lib.nbytes(acc2),
+                                            sc.data_ptr(), _lib.nbytes(sc), slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
+               "mp_gat_backward_wide_f32")
     del slab, pack
     _lib.check(lib.mp_gat_backward_epilogue_wide_f32(gx.data_ptr(), acc2.data_ptr(), xw.data_ptr(), att_c.data_ptr(),
                                                      ga_dst.data_ptr(), sc.data_ptr(), N, H, C, st),
@@ -825,6 +842,15 @@ def _gat_backward_wide(graph, g, xw, att, a_src, a_dst, stats, agg, extra, H, C,
                          dim=-1).view_as(att)
     gb = col_sums(g) if want_bias else None
     return gx, gatt, gb
+
+
+def _att_part_blocks(n_rows, n_dst):
+    """Blocks of the d att partials of mp_gat_backward_finish_f32: the pass runs
+    over all n_rows rows of xw (own + halo rows on a sharded rank's local graph,
+    n_dst of them own), one partial per block of mp_gat_bwd_blocks(n_rows).
+    (Round 4 sized this for n_dst: the library now rejects such a buffer --
+    ABI 6 extents -- instead of writing past it; tests/test_gpu_dist.py.)"""
+    return int(_lib.load().mp_gat_bwd_blocks(n_rows))
 
 
 def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope, want_att, want_bias,
@@ -857,12 +883,14 @@ def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope
             _lib.check(lib.mp_gat_backward_prep_train_f32(g.data_ptr(), g.stride(0), agg.data_ptr(), agg.stride(0),
                                                           agg2.data_ptr(), s2.data_ptr(), a_dst.data_ptr(),
                                                           stats.data_ptr(), n_dst, H, C, pack.data_ptr(),
-                                                          _lib.ptr(gpart), ga_dst.data_ptr(), st),
+                                                          _lib.nbytes(pack), _lib.ptr(gpart), _lib.nbytes(gpart),
+                                                          ga_dst.data_ptr(), st),
                        "mp_gat_backward_prep_train_f32")
     elif n_dst:
         _lib.check(lib.mp_gat_backward_prep_f32(g.data_ptr(), g.stride(0), agg.data_ptr(), agg.stride(0),
                                                 a_dst.data_ptr(), stats.data_ptr(), n_dst, H, C, pack.data_ptr(),
-                                                _lib.ptr(gpart), st), "mp_gat_backward_prep_f32")
+                                                _lib.nbytes(pack), _lib.ptr(gpart), _lib.nbytes(gpart), st),
+                   "mp_gat_backward_prep_f32")
     gb = None
     if want_bias:
         gb = gpart.sum(0) if gpart is not None else g.sum(0)
@@ -893,8 +921,8 @@ def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope
     else:
         _lib.check(lib.mp_gat_backward_f32(gs, g.data_ptr(), g.stride(0), xw.data_ptr(), a_src.data_ptr(),
                                            pack.data_ptr(), att_c.data_ptr(), H, C, float(slope), gx.data_ptr(),
-                                           ga_src.data_ptr(), _lib.ptr(de), slab.data_ptr(), sb, _lib.MP_STAGE_ALL,
-                                           st), "mp_gat_backward_f32")
+                                           ga_src.data_ptr(), _lib.ptr(de), _lib.nbytes(de), slab.data_ptr(), sb,
+                                           _lib.MP_STAGE_ALL, st), "mp_gat_backward_f32")
     del slab, pack
     if ga_dst is None:
         ga_dst, _ = _aggregate(graph.dst, "slot", de, None, "sum", 0, None)
@@ -906,10 +934,11 @@ def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope
             # att_dst term of d xw (unless the transposed pass added it) + d att partials:
             # the finish pass runs over all N rows (own + halo on a sharded rank's
             # local graph), one partial per block of mp_gat_bwd_blocks(N)
-            apart = torch.empty((int(lib.mp_gat_bwd_blocks(N)), 2, F), dtype=torch.float32, device=dev)
+            apart = torch.empty((_att_part_blocks(N, n_dst), 2, F), dtype=torch.float32, device=dev)
             _lib.check(lib.mp_gat_backward_finish_f32(None if fused_dst else gx.data_ptr(), xw.data_ptr(),
                                                       ga_dst.data_ptr(), ga_src.data_ptr(), att_c.data_ptr(), N, H, C,
-                                                      apart.data_ptr(), st), "mp_gat_backward_finish_f32")
+                                                      apart.data_ptr(), _lib.nbytes(apart), st),
+                       "mp_gat_backward_finish_f32")
         if want_att:
             p = apart.sum(0).view(2, H, C)
             gatt = torch.cat([p[0], p[1]], dim=-1).view_as(att)
@@ -1031,6 +1060,44 @@ class _GatPropagate(torch.autograd.Function):
         return gx.reshape(N, H * C), gatt, gb, None, None, None, None, None, None, None, None
 
 
+_MASK64 = 0xFFFFFFFFFFFFFFFF
+_seed_calls = {}
+
+
+def _mix64(z):
+    """splitmix64 finaliser: spreads (seed, offset) pairs over the 64-bit keys."""
+    z = (z + 0x9E3779B97F4A7C15) & _MASK64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _MASK64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _MASK64
+    return z ^ (z >> 31)
+
+
+def dropout_seed(device):
+    """A fresh attention-dropout key from the device's default generator, with
+    no device read: (its seed, its Philox offset) mixed on the host, and the
+    offset advanced, as a device dropout mask draw advances it -- so
+    torch.cuda.manual_seed(s) makes the key sequence repeat, the CPU generator
+    stays untouched, and nothing blocks on the device (a training step of every
+    sharded rank issues no sync for it).  During HIP-graph capture, or on a
+    generator without offsets, a host counter per (device, seed) replaces the
+    offset (the captured replay reuses the captured key, as any captured
+    constant)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    gen = torch.cuda.default_generators[idx]
+    base = gen.initial_seed()
+    if not torch.cuda.is_current_stream_capturing() and hasattr(gen, "get_offset"):
+        try:
+            off = gen.get_offset()
+            gen.set_offset(off + 4)
+            return _mix64(_mix64(base) ^ off)
+        except RuntimeError:
+            pass
+    k = (idx, base)
+    n = _seed_calls.get(k, 0)
+    _seed_calls[k] = n + 1
+    return _mix64(_mix64(base ^ 0x5EED) ^ n)
+
+
 def gat_propagate(graph, edge_index, xw, att, heads, out_channels, negative_slope=0.2, bias=None,
                   return_alpha=False, dropout=0.0, seed=None):
     """Fused GATConv aggregation: returns (out [N, H*C], alpha [E, H] or None).
@@ -1052,9 +1119,7 @@ def gat_propagate(graph, edge_index, xw, att, heads, out_channels, negative_slop
             raise ValueError("mi355_mp: fused attention dropout needs 0 < p < 1, H <= 32, C %% 4 == 0 and C/4 a "
                              "power of two <= 64 (got p=%g, H=%d, C=%d)" % (dropout, H, C))
         if seed is None:
-            # from the generator of xw's device, as F.dropout on a device tensor
-            # draws its mask (torch's CPU generator stays untouched)
-            seed = int(torch.randint(-2 ** 63, 2 ** 63 - 1, (), dtype=torch.int64, device=xw.device))
+            seed = dropout_seed(xw.device)
         drop = (int(seed) & 0xFFFFFFFFFFFFFFFF, float(dropout))
     # autograd.Function.forward always runs with grad disabled: decide here whether
     # a backward can follow (then the forward keeps the pre-bias aggregate)

@@ -6,20 +6,12 @@ edges in global order and so sums every row in the same order: sum, max/min
 with global argmax ids, and the backward of the sum (a forward over the
 transposed plan)."""
 import os
-import socket
 
 import pytest
 import torch
 import torch.distributed as dist
-import torch.multiprocessing as mp
 
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+from tests._ranks import run_ranks
 
 
 def _worker(rank, world, port, result_q):
@@ -81,16 +73,7 @@ def _worker(rank, world, port, result_q):
 
 @pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
 def test_sharded_gcn_aggregation_matches_single_process(world):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    for p in procs:
-        p.join(120)
-        assert p.exitcode == 0
-    res = sorted(q.get(timeout=10) for _ in range(world))
+    res = run_ranks(_worker, world, timeout=120)
     assert all(r[1] for r in res), res
     # contiguous cover of [0, N)
     assert res[0][2] == 0 and all(res[k][3] == res[k + 1][2] for k in range(world - 1))
@@ -172,16 +155,7 @@ def _slices_worker(rank, world, port, result_q):
 
 @pytest.mark.parametrize("world", [1, 2, 3, 4])
 def test_gcn_shards_from_edge_slices_match_full_list(world):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_slices_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    for p in procs:
-        p.join(180)
-        assert p.exitcode == 0
-    res = sorted(q.get(timeout=10) for _ in range(world))
+    res = run_ranks(_slices_worker, world, timeout=180)
     assert all(r[1] for r in res), res
 
 
@@ -231,16 +205,7 @@ def _cover_worker(rank, world, port, result_q, cuts):
 
 @pytest.mark.parametrize("world,cuts", [(1, None), (2, None), (3, None), (4, None), (3, [0, 600, 600, 1200])])
 def test_halo_cover_matches_single_process(world, cuts):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_cover_worker, args=(r, world, port, q, cuts)) for r in range(world)]
-    for p in procs:
-        p.start()
-    for p in procs:
-        p.join(180)
-        assert p.exitcode == 0
-    res = sorted(q.get(timeout=10) for _ in range(world))
+    res = run_ranks(_cover_worker, world, timeout=180, args=(cuts,))
     assert all(r[1] for r in res), res
     if world > 1:
         # fewer rows than the pull exchange (this small graph is dense: ~0.86x; RMAT21 0.57x)
@@ -305,16 +270,7 @@ def _cover_fuzz_worker(rank, world, port, result_q, n_cases):
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_halo_cover_fuzz(world):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_cover_fuzz_worker, args=(r, world, port, q, 30)) for r in range(world)]
-    for p in procs:
-        p.start()
-    for p in procs:
-        p.join(300)
-        assert p.exitcode == 0
-    res = sorted(q.get(timeout=10) for _ in range(world))
+    res = run_ranks(_cover_fuzz_worker, world, timeout=300, args=(30,))
     assert all(not r[1] for r in res), res
 
 
@@ -400,16 +356,7 @@ def _gat_worker(rank, world, port, result_q):
 
 @pytest.mark.parametrize("world", [1, 2, 3, 4])
 def test_sharded_gat_matches_single_process(world):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_gat_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    for p in procs:
-        p.join(180)
-        assert p.exitcode == 0
-    res = sorted(q.get(timeout=10) for _ in range(world))
+    res = run_ranks(_gat_worker, world, timeout=180)
     for rank, r in res:
         assert r["slices_equal"] and r["out_equal"] and r["alpha_equal"], r
         assert r["gx"] <= 0 and r["gw"] <= 0 and r["gatt"] <= 0 and r["gb"] <= 0, r
@@ -437,6 +384,16 @@ def _bad_slice_worker(rank, world, port, result_q):
                 raised.append(False)
             except IndexError:
                 raised.append(True)
+        # a slice offset that does not follow the earlier slices (only the last
+        # rank's is off by one): every rank raises, none waits in a collective
+        ei[1, 390] = 1
+        off = s0 + (1 if rank == world - 1 else 0)
+        for fn in (mdist.ShardedGraph.for_gcn_from_slices, mdist.ShardedGraph.for_gat_from_slices):
+            try:
+                fn(ei[:, s0:s1].clone(), off, N, rank, world)
+                raised.append(False)
+            except ValueError as e:
+                raised.append("rank %d's slice offset" % (world - 1) in str(e))
         result_q.put((rank, raised))
     finally:
         dist.destroy_process_group()
@@ -446,18 +403,11 @@ def _bad_slice_worker(rank, world, port, result_q):
 def test_slice_build_rejects_out_of_range_ids_on_every_rank(world):
     """An edge id outside [0, N) in one rank's slice: every rank raises
     IndexError before the first collective whose size depends on N (no hang, no
-    all_reduce of vectors of different lengths)."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_bad_slice_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    for p in procs:
-        p.join(120)
-        assert p.exitcode == 0
-    res = sorted(q.get(timeout=10) for _ in range(world))
-    assert all(r[1] == [True, True] for r in res), res
+    all_reduce of vectors of different lengths).  A slice offset out of step
+    with the earlier slices on one rank: every rank raises ValueError naming
+    that rank (the offsets travel with the slice sizes)."""
+    res = run_ranks(_bad_slice_worker, world, timeout=120)
+    assert all(r[1] == [True, True, True, True] for r in res), res
 
 
 def _tiny_worker(rank, world, port, result_q, N, edges):
@@ -498,15 +448,47 @@ def _tiny_worker(rank, world, port, result_q, N, edges):
     (2, 6, [[5, 5, 5, 4], [0, 1, 2, 5]]),
 ])
 def test_slice_built_shards_degenerate_graphs(world, N, edges):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_tiny_worker, args=(r, world, port, q, N, edges)) for r in range(world)]
-    for p in procs:
-        p.start()
-    for p in procs:
-        p.join(120)
-        assert p.exitcode == 0
-    res = sorted(q.get(timeout=10) for _ in range(world))
+    res = run_ranks(_tiny_worker, world, timeout=120, args=(N, edges,))
     assert all(r[1] for r in res), res
     assert sum(r[3] - r[2] for r in res) == N
+
+
+def _grad_flags_worker(rank, world, port, result_q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "pytorch_geometric-1_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mi355_mp import dist as mdist
+        m = torch.nn.Linear(3, 2)
+        m.extra = torch.nn.Parameter(torch.ones(4))      # no rank forms a gradient for it
+        m.only0 = torch.nn.Parameter(torch.ones(2))      # only rank 0 does
+        x = torch.full((5, 3), float(rank + 1))
+        loss = m(x).sum()
+        if rank == 0:
+            loss = loss + (m.only0 * 3).sum()
+        loss.backward()
+        mdist.allreduce_gradients(m)
+        result_q.put((rank, m.extra.grad is None, m.only0.grad.tolist(), m.bias.grad.tolist(),
+                      m.weight.grad.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_allreduce_gradients_keeps_unused_parameters_gradless(world):
+    """allreduce_gradients: a parameter no rank has a gradient for
+    keeps grad None on every rank (an optimizer with weight decay / momentum
+    leaves it alone, as on one GPU); one some ranks lack is summed with zeros
+    from those ranks; the rest are plain sums."""
+    res = run_ranks(_grad_flags_worker, world, timeout=120)
+    s = sum(range(1, world + 1))
+    for rank, extra_none, only0, b, w in res:
+        assert extra_none
+        assert only0 == [3.0, 3.0]
+        assert b == [5.0 * world] * 2
+        assert w == [[5.0 * s] * 3] * 2

@@ -9,7 +9,8 @@ import socket
 import pytest
 import torch
 import torch.distributed as dist
-import torch.multiprocessing as mp
+
+from tests._ranks import DEFAULT_TIMEOUT, run_ranks
 
 # gloo process groups of the spawned ranks: rendezvous and collectives give up
 # after this (a lost peer fails the test instead of stalling the suite)
@@ -73,16 +74,7 @@ def _worker(rank, world, port, q):
 
 
 def test_overlapped_sharded_gcn_on_one_gpu():
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    for p in procs:
-        p.join(300)
-        assert p.exitcode == 0
-    res = sorted(q.get(timeout=10) for _ in range(2))
+    res = _spawn(_worker, world=2, timeout=300)
     for rank, err, exact, n_int, n_bnd in res:
         assert err < 1e-5, res
         assert n_int > 0 and n_bnd > 0
@@ -177,33 +169,10 @@ def _layer_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def _spawn(target, world=2, timeout=600, args=()):
-    """Run target(rank, world, port, q) in `world` spawned processes and return
-    their sorted queue items.  Fails fast: the first rank to exit non-zero, or
-    the deadline, terminates the others (a rank stuck in a collective whose peer
-    died would otherwise sit until the process-group timeout)."""
-    import time
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=target, args=(r, world, port, q) + tuple(args)) for r in range(world)]
-    for p in procs:
-        p.start()
-    deadline = time.monotonic() + timeout
-    try:
-        while any(p.is_alive() for p in procs):
-            bad = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
-            assert not bad, "a rank exited with %s" % bad
-            assert time.monotonic() < deadline, "ranks still running after %d s" % timeout
-            time.sleep(0.2)
-        assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-        return sorted(q.get(timeout=10) for _ in range(world))
-    finally:
-        for p in procs:
-            if p.is_alive():
-                p.terminate()
-        for p in procs:
-            p.join(10)
+def _spawn(target, world=2, timeout=None, args=()):
+    """tests._ranks.run_ranks: the ranks' own deadline (below pytest.ini's
+    session-aborting backstop), every rank terminated when one fails."""
+    return run_ranks(target, world, timeout=timeout or DEFAULT_TIMEOUT, args=args)
 
 
 def test_sharded_gcnconv_forward_backward_on_one_gpu():
@@ -310,6 +279,28 @@ def _gat_layer_worker(rank, world, port, q):
         res["prop"] = {"out": float((o2 - o1[sg.lo:sg.hi]).abs().max()),
                        "alpha": float((a2 - a1[gid]).abs().max()),
                        "alpha_unsplit_bitwise": a_eq, "out_unsplit_bitwise": o_eq}
+        # ABI 6: the round-4 fault's sizing -- d att partials for the rank's own rows
+        # while the finish pass covers own + halo rows -- is now MP_ERR_ARG from the
+        # library, raised before any launch, instead of a device write past the end.
+        # (The rank's local GAT backward only: no collective, so every rank checks alone.)
+        xl = torch.randn(sg.fwd.n_local_src, H * C, generator=gen).to(dev).requires_grad_(True)
+        at = att.clone().requires_grad_(True)
+        gl = torch.randn(sg.n_own, H * C, generator=gen).to(dev)
+        good = ops._att_part_blocks
+        ops._att_part_blocks = lambda n_rows, n_dst: good(n_dst, n_dst)   # the r04 sizing
+        rejected = ""
+        try:
+            o, _ = ops.gat_propagate(sg.g_fwd, sg.fwd.local_edge_index, xl, at, H, C)
+            (o * gl).sum().backward()
+        except RuntimeError as e:
+            rejected = str(e)
+        finally:
+            ops._att_part_blocks = good
+        o, _ = ops.gat_propagate(sg.g_fwd, sg.fwd.local_edge_index, xl, at, H, C)
+        (o * gl).sum().backward()
+        torch.cuda.synchronize()
+        res["short_att_part"] = {"rejected": rejected, "n_local": int(sg.fwd.n_local_src), "n_own": int(sg.n_own),
+                                 "finite_after": bool(torch.isfinite(at.grad).all())}
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -327,6 +318,13 @@ def test_sharded_gatconv_forward_backward_on_one_gpu(world):
     res = _spawn(_gat_layer_worker, world=world)
     for rank, r in res:
         for key, v in r.items():
+            if key == "short_att_part":
+                # an att_part sized for the own rows is refused whenever the halo adds blocks
+                assert v["n_local"] > v["n_own"], v
+                assert "mp_gat_backward_finish_f32" in v["rejected"] and "code 1" in v["rejected"], v
+                assert "att_part holds" in v["rejected"], v
+                assert v["finite_after"], v
+                continue
             if key == "prop":
                 assert v["out"] < 1e-5 and v["alpha"] < 1e-6, (key, v)
                 assert v["out_unsplit_bitwise"] and v["alpha_unsplit_bitwise"], (key, v)
@@ -503,7 +501,7 @@ def test_full_size_products_sharded_rehearsal(world):
     rank's owned rows within 1e-5 * sum|w x| of the single-GPU kernel; at 2
     ranks also over the hybrid halo cover (ShardedGraph.enable_halo_cover),
     which must receive fewer rows than the pull halo."""
-    res = _spawn(_products_worker, world=world, timeout=900)
+    res = _spawn(_products_worker, world=world, timeout=540)
     assert sum(r[3] for r in res) == 2_449_029
     for rank, excess, frac, n_own, n_edges, n_halo, excess_c, rows_c in res:
         assert excess <= 0, res
@@ -559,7 +557,7 @@ def test_full_size_gat_sharded_rehearsal():
     rows within 1e-5 * max(1, sum|alpha x_j|) of the single-GPU fused kernel and
     every (edge, head) alpha within 1e-5 of it (bit-equal on all but the rows a
     task boundary splits)."""
-    res = _spawn(_gat_full_worker, world=2, timeout=900)
+    res = _spawn(_gat_full_worker, world=2, timeout=540)
     assert sum(r[6] for r in res) == 1 << 21
     for rank, excess, dalpha, a_eq, o_eq, edges_ok, _ in res:
         assert excess <= 0 and dalpha <= 1e-5 and edges_ok, res
@@ -745,7 +743,7 @@ def test_sharded_path_over_rccl_world_one():
     assert r["gat_out"] < 1e-5 and r["gat_gx"] < 1e-5 and r["gat_gatt"] < 1e-5, r
 
 
-def _run_bench(args, env_extra=None, timeout=900):
+def _run_bench(args, env_extra=None, timeout=540):
     import json
     import subprocess
     import sys

@@ -1107,6 +1107,19 @@ def test_gat_dropout_seed_leaves_cpu_rng_untouched():
     assert torch.equal(outs[0], outs[1])
     torch.cuda.manual_seed(4)
     assert not torch.equal(conv(x, ei), outs[0])
+    # the key comes from (seed, Philox offset) on the host: no device read, so a
+    # training forward issues no sync for it -- sync debug mode
+    # "error" raises on any synchronising call
+    from mi355_mp import ops
+    torch.cuda.manual_seed(5)
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        k1, k2 = ops.dropout_seed(DEV), ops.dropout_seed(DEV)
+    finally:
+        torch.cuda.set_sync_debug_mode("default")
+    torch.cuda.manual_seed(5)
+    assert [ops.dropout_seed(DEV), ops.dropout_seed(DEV)] == [k1, k2] and k1 != k2
 
 
 @pytest.mark.parametrize("H,C", [(8, 32), (4, 16), (2, 64), (3, 4)])
@@ -1140,7 +1153,7 @@ def test_gat_attention_dropout_fused_vs_masked_reference(H, C):
     out = conv(xd, eid)
     out.backward(gout.to(DEV))
     torch.manual_seed(1234)  # the seed gat_propagate drew (device generator: manual_seed seeds it too)
-    seed = int(torch.randint(-2 ** 63, 2 ** 63 - 1, (), dtype=torch.int64, device=DEV)) & 0xFFFFFFFFFFFFFFFF
+    seed = ops.dropout_seed(DEV)
     ei_l = gat_loops(eid, N)
     graph = graph_for(ei_l, N, N, conv.flow, target_tasks=GAT_TARGET_TASKS)
     keep = ops.gat_dropout_keep(graph, seed, p, H).cpu()
@@ -1248,7 +1261,7 @@ def test_gat_wide_heads_training(H, C, p):
     keep = None
     if p > 0:
         torch.manual_seed(99)
-        seed = int(torch.randint(-2 ** 63, 2 ** 63 - 1, (), dtype=torch.int64, device=DEV)) & 0xFFFFFFFFFFFFFFFF
+        seed = ops.dropout_seed(DEV)
         graph = graph_for(gat_loops(eid, N), N, N, conv.flow, target_tasks=GAT_TARGET_TASKS)
         keep = ops.gat_dropout_keep(graph, seed, p, H).cpu()
     W = conv.weight.detach().cpu().double().requires_grad_(True)
@@ -1350,7 +1363,7 @@ def test_gat_backward_narrow_tiles(vec, H, C, p):
     keep = None
     if p > 0:
         torch.manual_seed(77)
-        seed = int(torch.randint(-2 ** 63, 2 ** 63 - 1, (), dtype=torch.int64, device=DEV)) & 0xFFFFFFFFFFFFFFFF
+        seed = ops.dropout_seed(DEV)
         ei_l = gat_loops(ei.to(DEV), N)   # held: the graph's CSR is built lazily from it
         graph = graph_for(ei_l, N, N, conv.flow, target_tasks=GAT_TARGET_TASKS)
         keep = ops.gat_dropout_keep(graph, seed, p, H).cpu()
@@ -2510,6 +2523,14 @@ def test_row_gather_out_of_range_raises():
     idx[1] = N            # an in-place write bumps the version: checked again
     with pytest.raises(IndexError):
         _o.check_row_index(idx, N)
+    # a write through .data bumps no version counter (the documented limitation):
+    # forget_index drops the stale range, and the check sees the new value
+    idx2 = torch.tensor([0, 3, 9], device=DEV)
+    _o.check_row_index(idx2, N)
+    idx2.data[1] = N + 5
+    _o.forget_index(idx2)
+    with pytest.raises(IndexError):
+        _o.check_row_index(idx2, N)
     torch.cuda.synchronize()
 
 

@@ -42,7 +42,7 @@ def test_ctypes_signatures_cover_the_header():
 
 
 def test_abi_version_and_error_string(lib):
-    assert lib.mp_abi_version() == 5
+    assert lib.mp_abi_version() == 6
     assert isinstance(lib.mp_last_error(), bytes)
 
 
@@ -92,6 +92,121 @@ def test_argument_errors_are_reported(lib):
     rc = lib.mp_schedule_build(None, 0, 0, 100, 10, None, None, None, None, None, 0, None)
     assert rc == 1 and b"chunk" in lib.mp_last_error()
 
+
+
+# ABI 6: every entry point that writes (or reads) a caller-allocated partial,
+# workspace or per-edge array whose size the call's own row / edge counts do not
+# fix takes the array's extent in bytes and rejects a short one before any
+# launch.  (Round 4's sharded GAT backward sized att_part for the rank's own rows
+# while the finish pass covers own + halo rows: a device write past the end.)
+# Each case: (entry point, argument builder(extent) -> args, the exact extent
+# the call needs, the buffer name the error names).
+def _extent_cases():
+    from mi355_mp import _lib
+    lib = _lib.load()
+    D = 0x7F0000000000            # fake device pointer: never dereferenced, the check fails first
+    n_own, n, H, C = 1000, 1700, 8, 32
+    F = H * C
+    blocks = int(lib.mp_gat_bwd_blocks(n))
+    gt = _lib.MpCsr(D, D, D, D, D, D, n, 9000, 256, int(lib.mp_schedule_n_waves(n, 9000, 256)), 0, n_own, 0)
+    slab = lib.mp_gat_slab_bytes(gt, H, C)
+    Cw = 36
+    Fw = H * Cw
+    wslab = lib.mp_gat_train_slab_bytes(gt, H, Cw)
+    E, R, Fa = 5000, 300, 200
+    W = int(lib.mp_arg_mask_words(Fa))
+    ga = _lib.MpCsr(D, D, D, D, D, D, 400, E, 256, int(lib.mp_schedule_n_waves(400, E, 256)), 0, R, 0)
+    return [
+        ("mp_gat_backward_finish_f32", lambda b: (None, D, D, D, D, n, H, C, D, b, None),
+         blocks * 2 * F * 4, "att_part"),
+        ("mp_gat_backward_prep_f32", lambda b: (D, F, D, F, D, D, n, H, C, D, b, None, 0, None), n * H * 16, "pack"),
+        ("mp_gat_backward_prep_f32", lambda b: (D, F, D, F, D, D, n, H, C, D, n * H * 16, D, b, None),
+         blocks * F * 4, "gsum_part"),
+        ("mp_gat_backward_prep_train_f32", lambda b: (D, F, D, F, D, D, D, D, n, H, C, D, b, None, 0, D, None),
+         n * H * 16, "pack"),
+        ("mp_gat_backward_prep_train_f32", lambda b: (D, F, D, F, D, D, D, D, n, H, C, D, n * H * 16, D, b, D, None),
+         blocks * F * 4, "gsum_part"),
+        ("mp_gat_backward_prep_wide_f32", lambda b: (D, Fw, D, Fw, D, D, D, D, n, H, Cw, D, b, D, None),
+         n * H * 16, "pack"),
+        ("mp_col_sums_f32", lambda b: (D, F, n, F, D, b, None), blocks * F * 4, "part"),
+        ("mp_gat_backward_f32", lambda b: (gt, D, F, D, D, D, D, H, C, 0.2, D, D, D, b, D, slab, 7, None),
+         9000 * H * 4, "de"),
+        ("mp_gat_backward_wide_f32", lambda b: (gt, D, Fw, D, D, H, Cw, 0.2, 0, 0.0, D, D, b, D, n * H * 4, D, wslab,
+                                                7, None), n * Fw * 4, "acc2"),
+        ("mp_gat_backward_wide_f32", lambda b: (gt, D, Fw, D, D, H, Cw, 0.2, 0, 0.0, D, D, n * Fw * 4, D, b, D, wslab,
+                                                7, None), n * H * 4, "sc"),
+        ("mp_arg_winner_mask", lambda b: (D, R, Fa, E, D, D, b, None), E * W * 4, "mask"),
+        ("mp_scatter_arg_backward_csr_f32", lambda b: (ga, D, b, D, Fa, Fa, None, D, Fa, None), E * W * 4, "mask"),
+        ("mp_scatter_arg_grad_w_f32", lambda b: (D, D, E, D, D, b, Fa, D, Fa, D, Fa, D, None), E * W * 4, "mask"),
+    ]
+
+
+def test_every_partial_array_carries_its_extent(lib):
+    """One rejection test per ABI-6 extent: a buffer one byte (or, for
+    att_part, the round-4 rank's own rows) short is MP_ERR_ARG with the
+    buffer's name in the error text; checked on the host before any HIP call
+    (this container has no GPU, so an accepted call would fail later with
+    MP_ERR_HIP -- the harness under ASAN checks that side,
+    test_abi_rejections_under_asan)."""
+    cases = _extent_cases()
+    assert {c[0] for c in cases} >= {"mp_gat_backward_finish_f32", "mp_gat_backward_prep_f32",
+                                     "mp_gat_backward_prep_train_f32", "mp_gat_backward_prep_wide_f32",
+                                     "mp_col_sums_f32", "mp_gat_backward_f32", "mp_gat_backward_wide_f32",
+                                     "mp_arg_winner_mask", "mp_scatter_arg_backward_csr_f32",
+                                     "mp_scatter_arg_grad_w_f32"}
+    for name, args, need, what in cases:
+        for short in (need - 1, 0):
+            rc = getattr(lib, name)(*args(short))
+            err = lib.mp_last_error().decode()
+            assert rc == 1 and what in err and str(need) in err, (name, short, rc, err)
+    # the round-4 sizing: att_part for the rank's own rows, the pass over own + halo rows
+    blocks_own = int(lib.mp_gat_bwd_blocks(1000))
+    rc = lib.mp_gat_backward_finish_f32(None, 1 << 40, 1 << 40, 1 << 40, 1 << 40, 1700, 8, 32, 1 << 40,
+                                        blocks_own * 2 * 256 * 4, None)
+    assert rc == 1 and b"att_part" in lib.mp_last_error()
+
+
+def test_extent_arguments_in_the_header():
+    """Every ABI-6 extent is declared next to its array in include/mi355_mp.h and
+    in the ctypes signatures (size_t after the pointer)."""
+    from mi355_mp import _lib
+    text = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    want = {"mp_gat_backward_finish_f32": ["att_part"], "mp_gat_backward_prep_f32": ["pack", "gsum_part"],
+            "mp_gat_backward_prep_train_f32": ["pack", "gsum_part"], "mp_gat_backward_prep_wide_f32": ["pack"],
+            "mp_col_sums_f32": ["part"], "mp_gat_backward_f32": ["de"], "mp_gat_backward_wide_f32": ["acc2", "sc"],
+            "mp_arg_winner_mask": ["mask"], "mp_scatter_arg_backward_csr_f32": ["mask"],
+            "mp_scatter_arg_grad_w_f32": ["mask"]}
+    for fn, arrays in want.items():
+        decl = re.search(r"\b%s\((.*?)\);" % fn, text, flags=re.S).group(1)
+        params = [p.strip() for p in decl.split(",")]
+        for a in arrays:
+            i = next(k for k, p in enumerate(params) if re.search(r"\*\s*%s$" % a, p))
+            assert params[i + 1] == "size_t %s_bytes" % a, (fn, a, params[i + 1])
+            assert _lib.SIGNATURES[fn][1][i + 1] is _lib.sz, (fn, a)
+
+
+def test_abi_rejections_under_asan():
+    """The host-side AddressSanitizer build of the library (make asan: device
+    code as usual, host code under -fsanitize=address) and the C harness
+    tests/abi/abi_reject.c: every entry point's argument checks -- null
+    pointers, bad sizes and shapes, short workspaces and ABI-6 extents (each
+    also at its exact extent, which must pass the checks) -- run without a
+    host memory error, each rejection naming its argument."""
+    csrc = os.path.join(ROOT, "pytorch_geometric-1_amd", "csrc")
+    subprocess.check_call(["make", "-s", "-j8", "-C", csrc, "asan"])
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0:halt_on_error=1",
+               HIP_VISIBLE_DEVICES="", ROCR_VISIBLE_DEVICES="")
+    env.pop("LD_PRELOAD", None) if "asan" in env.get("LD_PRELOAD", "") else None
+    r = subprocess.run([os.path.join(csrc, "build", "asan", "abi_reject")], capture_output=True, text=True,
+                       env=env, timeout=300)
+    assert "AddressSanitizer" not in r.stderr, r.stderr[-4000:]
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
+    last = r.stdout.strip().splitlines()[-1]
+    m = re.match(r"abi_reject: (\d+) cases, 0 failures", last)
+    assert m and int(m.group(1)) >= 100, last
+    # every extent rejection and the matching exact-extent acceptance ran
+    assert r.stdout.count("holds") >= 17
+    assert "att_part holds 512000 bytes" in r.stdout       # the round-4 own-rows sizing, rejected
 
 
 def test_column_array_requires_n_cols(lib):
