@@ -136,6 +136,13 @@ def parse(argv=None):
                     help="run the N>1 sharded path (shards, plans, halo exchange, per-rank split) even at "
                          "one rank -- under torch.distributed.run --nproc-per-node 1 it rehearses the "
                          "driver's multi-GPU code path on the RCCL backend with empty halos")
+    ap.add_argument("--emulate-peers", type=str, default="", metavar="P[,P..]",
+                    help="with --sharded at one rank (RCCL): also measure RCCL beside the aggregation -- rank 0 "
+                         "of a P-way partition of the graph aggregates its in-edges while a world-1 "
+                         "all_to_all_single moves that rank's halo volume as a self split (extra.per_rank[0]"
+                         ".rccl_contention: exchange alone, compute alone, overlapped, hidden_frac)")
+    ap.add_argument("--no-build-split", action="store_true",
+                    help="N>1: do not take the one-time build apart into device-busy and host time")
     ap.add_argument("--halo-tile", type=int, default=-1,
                     help="N>1: exchange and finish the boundary edges per feature tile of this width "
                          "(pipelined); 0 = one exchange of whole rows; -1 (default) = chosen in the warm-up "
@@ -174,9 +181,16 @@ def setup_dist(args):
     """(rank, world, local device index).  Single process unless launched as
     ranks (RANK set) -- then the job must have exactly --gpus ranks."""
     if "RANK" not in os.environ:
-        if args.sharded:
-            raise SystemExit("bench.py --sharded needs a launcher (torch.distributed.run)")
-        return 0, 1, 0
+        if args.sharded and args.gpus == 1:
+            # one rank of the sharded path with no launcher: this process is the
+            # whole job (a world-1 process group over 127.0.0.1), so it can run
+            # directly under rocprofv3
+            os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                              MASTER_PORT=str(_free_port()))
+        elif args.sharded:
+            raise SystemExit("bench.py --sharded with --gpus > 1 needs a launcher (torch.distributed.run)")
+        else:
+            return 0, 1, 0
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", rank))
@@ -476,11 +490,23 @@ def main_gat(args, rank, world, local):
         s0, s1 = rank * E_raw // world, (rank + 1) * E_raw // world
         sg = mdist.ShardedGraph.for_gat_from_slices(ei[:, s0:s1].clone(), s0, N, rank, world)
         del ei
-        sg.g_fwd.dst                                                  # the one-time build
         E2, E_local = sg.n_edges, int(sg.fwd.edge_pos.numel())
         xw = xw_full[sg.lo:sg.hi].contiguous()
         n_rows, n_src = sg.n_own, sg.fwd.n_local_src
-        stage(rank, "gat shards built: %d rows, %d in-edges, %d halo rows" % (n_rows, E_local, n_src - n_rows))
+        cover_stats = None
+        if not args.no_halo_cover:
+            # the hybrid cover: a remote source row is pulled, or its owner pushes its
+            # online-softmax piece of the destination row (mi355_mp.gat_cover)
+            sg.enable_gat_halo_cover()
+            sg.gat_cover.graphs()                                     # the one-time build
+            cover_stats = sg.gat_cover.stats()
+        else:
+            sg.g_fwd.dst                                              # the one-time build
+        stage(rank, "gat shards built: %d rows, %d in-edges, %d pull-halo rows%s"
+              % (n_rows, E_local, n_src - n_rows, "" if cover_stats is None else
+                 ", cover: %d rows in (%d pulled + %d pieces)" % (cover_stats["halo_rows"],
+                                                                  cover_stats["cover_pulled_rows"],
+                                                                  cover_stats["cover_partial_rows"])))
 
         def step():
             return sg.gat_propagate(xw, att, H, C, 0.2, bias)[0]
@@ -512,21 +538,23 @@ def main_gat(args, rank, world, local):
         reps = max(args.steps, 10)
         split = {}
         if sharded:
-            xl = mdist.halo_rows(xw, sg.fwd, sg.group)
+            xl = mdist.halo_rows(xw, sg.fwd, sg.group)      # pull halo: the verify reference's inputs
+            if cover_stats is not None:
+                split = sg.gat_cover.decompose(xw, att, H, C, 0.2, bias, reps, barrier=lambda: barrier(world))
+            else:
+                def exchange():
+                    mdist.halo_rows(xw, sg.fwd, sg.group)
 
-            def exchange():
-                mdist.halo_rows(xw, sg.fwd, sg.group)
-
-            def local():
-                ops.gat_propagate(sg.g_fwd, sg.fwd.local_edge_index, xl, att, H, C, 0.2, bias)
-            for name, fn in (("exchange_only_ms", exchange), ("compute_only_ms", local)):
-                barrier(world)
-                torch.cuda.synchronize()
-                t1 = time.perf_counter()
-                for _ in range(reps):
-                    fn()
-                torch.cuda.synchronize()
-                split[name] = (time.perf_counter() - t1) / reps * 1e3
+                def local():
+                    ops.gat_propagate(sg.g_fwd, sg.fwd.local_edge_index, xl, att, H, C, 0.2, bias)
+                for name, fn in (("exchange_only_ms", exchange), ("compute_only_ms", local)):
+                    barrier(world)
+                    torch.cuda.synchronize()
+                    t1 = time.perf_counter()
+                    for _ in range(reps):
+                        fn()
+                    torch.cuda.synchronize()
+                    split[name] = (time.perf_counter() - t1) / reps * 1e3
             kern_ms = split["compute_only_ms"]
         else:
             kern_ms = _ev_ms(step, reps)
@@ -575,9 +603,20 @@ def main_gat(args, rank, world, local):
         find_pmc(wl["name"], None, src_hash, full=True)
     ranks = None
     if sharded:
-        mine = {"rank": rank, "rows": n_rows, "edges": E_local, "halo_rows": n_src - n_rows,
-                "halo_bytes_in": (n_src - n_rows) * F * 4, "halo_bytes_out": int(sg.fwd.send_idx.numel()) * F * 4,
-                "step_ms_this_rank": dt_local / args.steps * 1e3, **split, "verify": verify}
+        if cover_stats is None:
+            mine = {"rank": rank, "rows": n_rows, "edges": E_local, "exchange": "pull", "halo_rows": n_src - n_rows,
+                    "halo_bytes_in": (n_src - n_rows) * F * 4,
+                    "halo_bytes_out": int(sg.fwd.send_idx.numel()) * F * 4}
+        else:
+            gc = sg.gat_cover
+            mine = {"rank": rank, "rows": n_rows, "edges": E_local,
+                    "exchange": "cover (pulled rows + pushed online-softmax pieces)",
+                    "halo_rows": gc.n_halo, "pull_halo_rows": n_src - n_rows,
+                    "cover_over_pull_rows": gc.n_halo / max(1, n_src - n_rows),
+                    "halo_bytes_in": gc.n_halo * (F + 2 * H) * 4 + sum(gc.adst_send_counts) * H * 4,
+                    "halo_bytes_out": gc.n_send * (F + 2 * H) * 4 + sum(gc.adst_recv_counts) * H * 4,
+                    "peers_in": list(gc.recv_counts), "peers_out": list(gc.send_counts), **cover_stats}
+        mine.update({"step_ms_this_rank": dt_local / args.steps * 1e3, **split, "verify": verify})
         ranks = [None] * world
         dist.all_gather_object(ranks, mine)
         if verify is not None:
@@ -596,7 +635,8 @@ def main_gat(args, rank, world, local):
             "data": "synthetic rmat21 graph (seeded, generated on device), random X W / att / bias",
             "config": {"workload": wl["name"], "baseline_config": wl["baseline_config"], "graph": wl["graph"],
                        "num_nodes": N, "num_edges": E2, "heads": H, "out_channels": C, "seed": wl["seed"],
-                       "parallelism": "dst-range shards x%d, RCCL halo all_to_all (pull)" % world if sharded
+                       "parallelism": ("dst-range shards x%d, RCCL halo all_to_all (%s)"
+                                       % (world, "pull" if args.no_halo_cover else "hybrid cover")) if sharded
                        else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": comp / (kern_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": comp / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": traffic,
@@ -756,6 +796,186 @@ def main_reddit(args, rank, world, local):
     stage(rank, "done")
 
 
+LINK_GBS = (60.0, 77.0, 100.0)   # xGMI per link direction: low / nominal / high
+
+
+class BuildMeter:
+    """Takes a one-time build phase apart on this rank (N > 1 lines, the
+    driver's first 8-GPU run): wall time, the time the device was busy (union
+    of the kernel / copy intervals the torch profiler records, device activity
+    only), the rest = host work and host-device round trips, and the number of
+    synchronising calls (torch's sync debug mode, counted as warnings).
+    enabled=False: wall time only."""
+
+    def __init__(self, enabled):
+        self.enabled = enabled
+        self.res = {}
+
+    def run(self, name, fn):
+        import warnings
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        if not self.enabled:
+            out = fn()
+            torch.cuda.synchronize()
+            self.res[name] = {"wall_s": time.perf_counter() - t0}
+            return out
+        from torch.profiler import ProfilerActivity, profile
+        with warnings.catch_warnings(record=True) as caught:
+            warnings.simplefilter("always")
+            torch.cuda.set_sync_debug_mode("warn")
+            try:
+                with profile(activities=[ProfilerActivity.CUDA]) as prof:
+                    out = fn()
+                    torch.cuda.synchronize()
+            finally:
+                torch.cuda.set_sync_debug_mode("default")
+        wall = time.perf_counter() - t0
+        syncs = sum(1 for w in caught if "synchroniz" in str(w.message).lower())
+        spans = []
+        try:
+            for e in prof.events():
+                if getattr(e, "device_type", None) == torch.autograd.DeviceType.CUDA:
+                    spans.append((e.time_range.start, e.time_range.end))
+        except Exception as ex:  # pragma: no cover - profiler without device events
+            self.res[name] = {"wall_s": wall, "host_syncs": syncs, "device_busy_s": None,
+                              "note": "profiler gave no device events: %s" % ex}
+            return out
+        spans.sort()
+        busy, cur_s, cur_e = 0.0, None, None
+        for a, b in spans:
+            if cur_e is None or a > cur_e:
+                if cur_e is not None:
+                    busy += cur_e - cur_s
+                cur_s, cur_e = a, b
+            else:
+                cur_e = max(cur_e, b)
+        if cur_e is not None:
+            busy += cur_e - cur_s
+        busy_s = busy * 1e-6
+        self.res[name] = {"wall_s": wall, "device_busy_s": busy_s if spans else None,
+                          "host_and_sync_s": (wall - busy_s) if spans else None,
+                          "device_ops": len(spans), "host_syncs": syncs}
+        return out
+
+
+def link_model(mine, rank, n_tiles):
+    """The link-bandwidth model of this rank's step, from its own
+    per-peer halo bytes and the compute it measured: each peer pair has its own
+    xGMI link, so the exchange takes max over peers of max(bytes in, bytes out)
+    / link rate; the step is the longer of the compute (pack + interior +
+    boundary, measured alone) and the chain pack(first tile) + exchange +
+    boundary(last tile).  Predicted at 60 / 77 / 100 GB/s per link direction,
+    next to the measured overlapped step, with the verdict which piece sets it."""
+    row = F_DIM * 4
+    peers = [q for q in range(len(mine["peers_in"])) if q != rank]
+    per_peer = max([max(mine["peers_in"][q], mine["peers_out"][q]) * row for q in peers] or [0])
+    dec = mine.get("decomposed") or {}
+    comp = dec.get("compute_only_ms")
+    if comp is None:
+        return None
+    T = max(1, n_tiles)
+    pack_first = mine.get("send_pack_ms", 0.0) / T
+    bnd_last = mine.get("boundary_ms", 0.0) / T
+    pred = {}
+    for gbs in LINK_GBS:
+        ex = per_peer / (gbs * 1e9) * 1e3
+        pred["%g" % gbs] = {"exchange_ms": ex, "step_ms": max(comp, pack_first + ex + bnd_last)}
+    meas = dec.get("overlapped_step_ms")
+    ex_meas = dec.get("exchange_only_ms")
+    nominal = pred["77"]["step_ms"]
+    res = {"max_peer_bytes": per_peer, "compute_only_ms": comp, "pack_first_tile_ms": pack_first,
+           "boundary_last_tile_ms": bnd_last, "predicted": pred, "measured_step_ms": meas,
+           "measured_exchange_ms": ex_meas,
+           "measured_link_GBps": (per_peer / (ex_meas * 1e-3) / 1e9) if ex_meas and per_peer else None,
+           "measured_over_predicted_77": (meas / nominal) if meas and nominal else None}
+    if meas is not None and ex_meas is not None:
+        longer = max(comp, ex_meas)
+        res["contention_ms"] = meas - longer     # beyond a perfect overlap of the two measured pieces
+        res["sets_the_step"] = ("exchange" if ex_meas > comp else "compute") + \
+            (" + contention" if meas > 1.1 * longer else "")
+    return res
+
+
+# rank 0's halo rows in under the hybrid cover, RMAT21 config 2 (DESIGN 5.4,
+# profiles/r03_halo_cover_p{2,4,8}.jsonl): the exchange volume --emulate-peers moves
+EMULATED_COVER_ROWS = {2: 288_668, 4: 346_920, 8: 313_427}
+
+
+def rccl_contention(sg, P, bias, reps=10, rounds=3):
+    """RCCL beside the aggregation on one GPU (world 1, RCCL): rank 0 of a P-way
+    destination-range partition (edge-balanced cuts of this graph) aggregates
+    its in-edges over [own rows ; halo rows] while all_to_all_single moves that
+    rank's halo volume (EMULATED_COVER_ROWS, 1 KB rows) as the world's one self
+    split -- RCCL's copy kernels then share the CUs, L2 and HBM with k_agg_flat,
+    as on the 8-GPU node (the xGMI transfer itself is not modelled: a self
+    split is a device-local copy).  Times (ms, median of `rounds` x `reps`):
+    exchange alone, compute alone, the two in a row, and overlapped (the
+    collective started async, the aggregation on the compute stream, then its
+    wait); hidden_frac as OverlappedAggregation.decompose."""
+    from mi355_mp import dist as mdist, ops
+    from mi355_mp.graph import Graph
+    dev = bias.device
+    ei = sg.fwd.local_edge_index          # world 1: the global edge list, global ids
+    w = sg.norm_fwd
+    N = sg.num_nodes
+    deg = torch.bincount(ei[1], minlength=N)
+    cuts = mdist.edge_balanced_cuts(deg, P)
+    lo, hi = int(cuts[0]), int(cuts[1])
+    sel = (ei[1] >= lo) & (ei[1] < hi)
+    src, dst, wl = ei[0][sel], ei[1][sel] - lo, w[sel].contiguous()
+    remote = (src < lo) | (src >= hi)
+    halo = torch.unique(src[remote])
+    n_own = hi - lo
+    local_src = torch.where(remote, n_own + torch.searchsorted(halo, src), src - lo)
+    g = Graph(torch.stack([local_src, dst]), n_own, n_own + halo.numel())
+    w_csr = g.dst.to_csr_order(wl)
+    gen = torch.Generator(device=dev).manual_seed(11)
+    x_loc = torch.randn(n_own + halo.numel(), F_DIM, device=dev, generator=gen)
+    out = torch.empty(n_own, F_DIM, device=dev)
+    rows = EMULATED_COVER_ROWS.get(P, int(halo.numel()))
+    send = torch.randn(rows, F_DIM, device=dev, generator=gen)
+    recv = torch.empty_like(send)
+
+    def compute():
+        ops._aggregate(g.dst, "other", x_loc, w_csr, "sum", 0, bias, out=out)
+
+    def exchange():
+        dist.all_to_all_single(recv, send)
+
+    def serial():
+        exchange()
+        compute()
+
+    def overlapped():
+        work = dist.all_to_all_single(recv, send, async_op=True)
+        compute()
+        work.wait()
+
+    def timed(fn):
+        per = []
+        fn()
+        for _ in range(rounds):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                fn()
+            torch.cuda.synchronize()
+            per.append((time.perf_counter() - t0) / reps * 1e3)
+        return sorted(per)[len(per) // 2]
+
+    res = {"P": P, "rank_rows": n_own, "rank_edges": int(src.numel()), "pull_halo_rows": int(halo.numel()),
+           "exchange_rows": rows, "exchange_bytes": rows * F_DIM * 4, "reps": reps, "rounds": rounds,
+           "exchange_only_ms": timed(exchange), "compute_only_ms": timed(compute),
+           "serial_step_ms": timed(serial), "overlapped_step_ms": timed(overlapped)}
+    shorter = min(res["exchange_only_ms"], res["compute_only_ms"])
+    res["hidden_frac"] = (res["exchange_only_ms"] + res["compute_only_ms"] - res["overlapped_step_ms"]) / shorter
+    res["overlap_loss_vs_compute"] = res["overlapped_step_ms"] / res["compute_only_ms"] - 1.0
+    res["note"] = ("self split on one GPU: RCCL's kernels contend with the aggregation for CUs / L2 / HBM; "
+                   "the xGMI transfer time is not part of it")
+    return res
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
@@ -814,7 +1034,9 @@ def main(argv=None):
         E_local = E2
     else:
         from mi355_mp import dist as mdist
-        sg = mdist.ShardedGraph.for_gcn_from_slices(ei_slice, s0, N, rank, world, chunk=args.chunk or None)
+        meter = BuildMeter(not args.no_build_split)
+        sg = meter.run("shards", lambda: mdist.ShardedGraph.for_gcn_from_slices(ei_slice, s0, N, rank, world,
+                                                                               chunk=args.chunk or None))
         del ei_slice
         torch.cuda.synchronize()
         t_shards = time.perf_counter() - t0
@@ -826,8 +1048,9 @@ def main(argv=None):
         x_local = plan.local_buffer(F_DIM)
         x_local[:plan.n_own].copy_(x_full[plan.lo:plan.hi])
         x = x_local[:plan.n_own]
-        overlap = mdist.OverlappedAggregation(plan, sg.norm_fwd, chunk=args.chunk or None, local_weights=True,
-                                              cover=not (args.no_halo_cover or args.no_overlap))
+        overlap = meter.run("exchange_plan", lambda: mdist.OverlappedAggregation(
+            plan, sg.norm_fwd, chunk=args.chunk or None, local_weights=True,
+            cover=not (args.no_halo_cover or args.no_overlap)))
         torch.cuda.synchronize()
         t_exchange_plan = time.perf_counter() - t0 - t_shards
         x_tiles = x_ov = None
@@ -1054,6 +1277,8 @@ def main(argv=None):
                 "halo_bytes_out": (int(plan.send_idx.numel()) if args.no_overlap else overlap.n_send) * F_DIM * 4,
                 "pull_exchange_rows_in": plan.n_local_src - plan.n_own,
                 "peers_in": [int(c) for c in (plan.recv_counts if args.no_overlap else overlap.recv_counts)],
+                "peers_out": [int(c) for c in (plan.send_counts if args.no_overlap else overlap.send_counts)],
+                "build_split": meter.res,
                 "step_ms_this_rank": dt_local / args.steps * 1e3}
         if overlap.cover is not None:
             mine.update({"cover_pulled_rows": overlap.cover.n_pull_rows,
@@ -1070,6 +1295,16 @@ def main(argv=None):
             reps_d = max(3, min(args.steps, 10))
             mine["decomposed"] = overlap.decompose(tiles, out_buf, bias, reps_d, barrier=lambda: barrier(world))
             stage(rank, "step decomposition: %s" % json.dumps(mine["decomposed"]))
+            mine["link_model"] = link_model(mine, rank, len(tiles))
+            stage(rank, "link model: %s" % json.dumps(mine["link_model"]))
+        if args.emulate_peers:
+            if world != 1 or dist.get_backend() != "nccl":
+                raise SystemExit("--emulate-peers needs --sharded at one RCCL rank")
+            mine["rccl_contention"] = []
+            for P in [int(p) for p in args.emulate_peers.split(",") if p]:
+                r = rccl_contention(sg, P, bias)
+                mine["rccl_contention"].append(r)
+                stage(rank, "RCCL beside the aggregation (P = %d): %s" % (P, json.dumps(r)))
         if verify is not None:
             mine["verify"] = verify
         ranks = [None] * world

@@ -255,8 +255,9 @@ int mp_gat_forward_f32(const mp_csr* g, const float* xw, const float* att, int32
 /* Training forward of the same layer (C % 4 == 0; with att given and C/4 a power
  * of two <= 64 -- mp_gat_train_ok -- a_src comes from each gathered row, else
  * from the a_src array).  out = aggregate + bias (bias may be NULL); agg
- * (NULL allowed without a bias) receives the pre-bias aggregate [n_rows, H*C]
- * (contiguous) that the backward's rs needs.  Besides these and row_stats it
+ * (optional, NULL allowed) also receives the pre-bias aggregate [n_rows, H*C]
+ * (contiguous).  The backward's rs needs no such copy: the prologues take the
+ * output and the bias (ABI 6: rs over out - bias).  Besides these and row_stats it
  * leaves, with the same online rescaling,
  *   out2[i,h,:]  = sum_j alpha_ij leaky'_ij xw[j,h,:]    ([n_rows, H*C], contiguous)
  *   row_s2[i,h]  = sum_j alpha_ij leaky'_ij             ([n_rows, H])
@@ -356,12 +357,15 @@ int mp_gat_backward_train_f32(const mp_csr* gt, const float* grad_out, int64_t l
 /* pack[n,h,:] = (a_dst[n,h], m[n,h], 1/den[n,h], rs[n,h]) with
  * rs[n,h] = sum_c grad_out[n, h*C+c] * agg[n, h*C+c]  (agg = pre-bias GAT output;
  * rs = sum_j alpha_nj <g_n, xw_j>_h, the softmax-backward row term).
+ * bias (ABI 6; NULL = none): agg is then the layer OUTPUT agg + bias [H*C] and
+ * rs is taken over out - bias (one rounding per feature), so the forward need
+ * not keep a pre-bias copy; 16-byte aligned.
  * gsum_part (optional, [mp_gat_bwd_blocks(n), H*C], needs C%4==0, H*C<=256):
  * per-block column sums of grad_out (the bias gradient is their sum over blocks).
  * Extents (ABI 6): pack_bytes >= n*H*16, gsum_part_bytes >= mp_gat_bwd_blocks(n)*H*C*4
  * (ignored when gsum_part is NULL). */
 int mp_gat_backward_prep_f32(const float* grad_out, int64_t ldg, const float* agg, int64_t lda,
-                             const float* a_dst, const float* row_stats, int64_t n, int32_t H,
+                             const float* bias, const float* a_dst, const float* row_stats, int64_t n, int32_t H,
                              int32_t C, float* pack, size_t pack_bytes, float* gsum_part,
                              size_t gsum_part_bytes, void* stream);
 
@@ -370,7 +374,7 @@ int mp_gat_backward_prep_f32(const float* grad_out, int64_t ldg, const float* ag
  *   grad_a_dst[n,h] = sum_j de_nj = <grad_out[n,h,:], agg2[n,h,:]> - rs[n,h] * row_s2[n,h]
  * (agg2 / row_s2 = the training forward's out2 / row_s2). */
 int mp_gat_backward_prep_train_f32(const float* grad_out, int64_t ldg, const float* agg, int64_t lda,
-                                   const float* agg2, const float* row_s2, const float* a_dst,
+                                   const float* bias, const float* agg2, const float* row_s2, const float* a_dst,
                                    const float* row_stats, int64_t n, int32_t H, int32_t C,
                                    float* pack, size_t pack_bytes, float* gsum_part,
                                    size_t gsum_part_bytes, float* grad_a_dst, void* stream);
@@ -400,7 +404,7 @@ int mp_gat_wide_ok(int32_t H, int32_t C);
 int mp_gat_node_scores_wide_f32(const float* xw, int64_t n_nodes, int32_t H, int32_t C, const float* att,
                                 float* a_src, float* a_dst, void* stream);
 int mp_gat_backward_prep_wide_f32(const float* grad_out, int64_t ldg, const float* agg, int64_t lda,
-                                  const float* agg2, const float* row_s2, const float* a_dst,
+                                  const float* bias, const float* agg2, const float* row_s2, const float* a_dst,
                                   const float* row_stats, int64_t n, int32_t H, int32_t C, float* pack,
                                   size_t pack_bytes, float* grad_a_dst, void* stream);
 int mp_gat_backward_wide_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, const float* a_src,
@@ -490,6 +494,28 @@ int mp_gat_alpha_f32(const int64_t* src_idx, const int64_t* dst_idx,
                      int64_t n_edges, int32_t H, const float* a_src,
                      const float* a_dst, float slope, const float* row_stats,
                      float* alpha, void* stream);
+
+/* ---- sharded GATConv over the hybrid halo cover ---------------
+ * Merge of online-softmax partials into a destination row's local piece.
+ * Row i (i < n_rows) holds the local piece: out[i] = acc/den (normalised, no
+ * bias) and row_stats[i, h] = (m, den) from mp_gat_aggregate_att_f32 /
+ * mp_gat_aggregate_train_f32 over the rank's own + pulled sources; partial
+ * rows k in [pptr[i], pptr[i+1]) of pidx name rows of part_out [n_parts, ldp] /
+ * part_stats [n_parts, H, 2] (peers' pieces of the same row, the same kernels
+ * on their send graphs).  Per head, local piece first, then the partials in
+ * list order:  M = max m, w_k = den_k e^(m_k - M), tot = sum w_k,
+ *   out[i] = sum_k (w_k / tot) out_k + bias,   row_stats[i, h] = (M, tot),
+ * and (training, optional) agg2[i] / row_s2[i] (the local piece's out2 / row_s2
+ * [n_rows, H*C] / [n_rows, H]) scaled by w_loc / tot, the merged rows'.  A row
+ * with no partial keeps its local piece + bias bit for bit.  pptr [n_rows + 1]
+ * (int32, non-decreasing, pptr[n_rows] <= n_parts) and every pidx entry in
+ * [0, n_parts) are the caller's contract (device arrays, not read on the host).
+ * C % 4 == 0; out, part_out, bias, agg2 16-byte aligned, leading dimensions
+ * multiples of 4.  (ABI 6) */
+int mp_gat_merge_partials_f32(int64_t n_rows, int32_t H, int32_t C, const int32_t* pptr, const int32_t* pidx,
+                              int64_t n_parts, const float* part_out, int64_t ldp, const float* part_stats,
+                              const float* bias, float* out, int64_t ldo, float* row_stats, float* agg2,
+                              float* row_s2, void* stream);
 
 /* ---- self-loop rewrites (PyG 1.4.3 utils.loop [U4]) -----
  * Output edge order is upstream's: the kept edges in original order, then the

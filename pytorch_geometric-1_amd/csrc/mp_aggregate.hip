@@ -2315,7 +2315,6 @@ static int gat_train(const mp_csr* g, const float* xw, const float* a_src, const
   MP_CHECK_ARG((uintptr_t)xw % 16 == 0 && (uintptr_t)att % 16 == 0 && (uintptr_t)out % 16 == 0 && ldo % 4 == 0 &&
                    (uintptr_t)out2 % 16 == 0 && (uintptr_t)agg % 16 == 0 && (uintptr_t)bias % 16 == 0,
                "mp_gat_aggregate_train_f32: xw, att, bias, out, agg, out2 must be 16-byte aligned (ldo %% 4 == 0)");
-  MP_CHECK_ARG(!bias || agg, "mp_gat_aggregate_train_f32: a bias needs agg (the pre-bias output)");
   MP_CHECK_ARG(slab != nullptr && slab_bytes >= mp_gat_train_slab_bytes(g, H, C),
                "mp_gat_aggregate_train_f32: slab workspace too small");
   AggArgs a{};

@@ -201,7 +201,10 @@ __global__ __launch_bounds__(256) void k_gat_bwd_finish(float* __restrict__ gx, 
 
 // Backward prologue of the fused GAT pass, per (node n, head h):
 //   pack[n,h] = (a_dst[n,h], m[n,h], 1/den[n,h], rs[n,h]),  rs = <g[n,h,:], agg[n,h,:]>
-// (rs = sum_j alpha_nj <g_n, xw_j>_h since agg_n = sum_j alpha_nj xw_j).
+// (rs = sum_j alpha_nj <g_n, xw_j>_h since agg_n = sum_j alpha_nj xw_j).  With
+// bias != nullptr, `agg` is the layer output agg + bias and the prologue takes
+// agg = out - bias (one rounding per feature): the training forward then writes
+// no separate pre-bias copy.
 // One wave per node, lane l owns 4 features, a head spans G = C/4 lanes.
 __device__ __forceinline__ void write_pack(float* pack, const float* a_dst, const float* stats, int64_t q, float rs) {
   f32x4 v = {a_dst[q], stats[2 * q], 1.f / stats[2 * q + 1], rs};
@@ -214,6 +217,7 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep_wave(const float* __restri
                                                            const float* __restrict__ stats, int64_t n, int32_t H,
                                                            int32_t C, int32_t G, float* __restrict__ pack,
                                                            float* __restrict__ gsum_part,
+                                                           const float* __restrict__ bias,
                                                            const float* __restrict__ agg2 = nullptr,
                                                            const float* __restrict__ s2 = nullptr,
                                                            float* __restrict__ ga_dst = nullptr) {
@@ -227,6 +231,13 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep_wave(const float* __restri
   // per row: rs (and d a_dst from the second accumulator) of the 4 features at fs,
   // the pack / ga_dst stores, the bias-gradient column sums -- rows are folded
   // into cs in the wave's row order, whatever the number in flight
+  auto debias = [&](Frag<4>& y, int64_t fs) {
+    if (bias) {
+      const Frag<4> b = load_frag<4>(bias + fs);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) y.v[k] = __fsub_rn(y.v[k], b.v[k]);
+    }
+  };
   auto row = [&](int64_t r, int64_t fs, bool act, const Frag<4>& x, const Frag<4>& y, const Frag<4>& z) {
     float t = 0.f;
 #pragma unroll
@@ -263,6 +274,8 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep_wave(const float* __restri
         z0 = load_frag<4>(agg2 + r * HC + fs);
         z1 = load_frag<4>(agg2 + r1 * HC + fs);
       }
+      debias(y0, fs);
+      debias(y1, fs);
       row(r, fs, act, x0, y0, z0);
       row(r1, fs, act, x1, y1, z1);
     }
@@ -270,6 +283,7 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep_wave(const float* __restri
       Frag<4> x0 = load_frag<4>(g + r * ldg + fs);
       Frag<4> y0 = load_frag<4>(agg + r * lda + fs);
       if (agg2) z0 = load_frag<4>(agg2 + r * HC + fs);
+      debias(y0, fs);
       row(r, fs, act, x0, y0, z0);
     }
   } else {
@@ -282,6 +296,7 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep_wave(const float* __restri
         Frag<4> y = load_frag<4>(agg + r * lda + fs);
         Frag<4> z = {};
         if (agg2) z = load_frag<4>(agg2 + r * HC + fs);
+        debias(y, fs);
         row(r, fs, act, x, y, z);
       }
     }
@@ -290,16 +305,18 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep_wave(const float* __restri
 }
 
 __global__ void k_gat_bwd_prep_scalar(const float* __restrict__ g, int64_t ldg, const float* __restrict__ agg,
-                                      int64_t lda, const float* __restrict__ a_dst, const float* __restrict__ stats,
-                                      int64_t n, int32_t H, int32_t C, float* __restrict__ pack) {
+                                      int64_t lda, const float* __restrict__ bias, const float* __restrict__ a_dst,
+                                      const float* __restrict__ stats, int64_t n, int32_t H, int32_t C,
+                                      float* __restrict__ pack) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n * (int64_t)H) return;
   const int64_t r = i / H;
   const int h = (int)(i % H);
   const float* x = g + r * ldg + (int64_t)h * C;
   const float* y = agg + r * lda + (int64_t)h * C;
+  const float* b = bias ? bias + (int64_t)h * C : nullptr;
   float t = 0.f;
-  for (int c = 0; c < C; ++c) t = __fadd_rn(t, __fmul_rn(x[c], y[c]));
+  for (int c = 0; c < C; ++c) t = __fadd_rn(t, __fmul_rn(x[c], b ? __fsub_rn(y[c], b[c]) : y[c]));
   write_pack(pack, a_dst, stats, i, t);
 }
 
@@ -381,7 +398,7 @@ int mp_gat_sddmm_f32(const mp_csr* g, const int32_t* slot_row, const float* grow
 }
 
 int mp_gat_backward_prep_train_f32(const float* grad_out, int64_t ldg, const float* agg, int64_t lda,
-                                   const float* agg2, const float* row_s2, const float* a_dst,
+                                   const float* bias, const float* agg2, const float* row_s2, const float* a_dst,
                                    const float* row_stats, int64_t n, int32_t H, int32_t C, float* pack,
                                    size_t pack_bytes, float* gsum_part, size_t gsum_part_bytes, float* grad_a_dst,
                                    void* stream) {
@@ -400,10 +417,11 @@ int mp_gat_backward_prep_train_f32(const float* grad_out, int64_t ldg, const flo
   MP_CHECK_ARG((uintptr_t)pack % 16 == 0 && (uintptr_t)grad_out % 16 == 0 && (uintptr_t)agg % 16 == 0 &&
                    (uintptr_t)agg2 % 16 == 0 && ldg % 4 == 0 && lda % 4 == 0,
                "mp_gat_backward_prep_train_f32: 16-byte alignment required");
+  MP_CHECK_ARG((uintptr_t)bias % 16 == 0, "mp_gat_backward_prep_train_f32: bias must be 16-byte aligned");
   MP_CHECK_ARG(ldg >= F && lda >= F, "mp_gat_backward_prep_train_f32: leading dimension < H*C");
   MP_CHECK_ARG(!gsum_part || F <= 256, "mp_gat_backward_prep_train_f32: gsum_part needs H*C <= 256");
   k_gat_bwd_prep_wave<<<(unsigned)mp_gat_bwd_blocks(n), 256, 0, as_stream(stream)>>>(
-      grad_out, ldg, agg, lda, a_dst, row_stats, n, H, C, G, pack, gsum_part, agg2, row_s2, grad_a_dst);
+      grad_out, ldg, agg, lda, a_dst, row_stats, n, H, C, G, pack, gsum_part, bias, agg2, row_s2, grad_a_dst);
   MP_CHECK_LAUNCH();
   return MP_OK;
 }
@@ -431,7 +449,8 @@ int mp_gat_bwd_blocks(int64_t n) {
   return (int)(b < 1 ? 1 : b);
 }
 
-int mp_gat_backward_prep_f32(const float* grad_out, int64_t ldg, const float* agg, int64_t lda, const float* a_dst,
+int mp_gat_backward_prep_f32(const float* grad_out, int64_t ldg, const float* agg, int64_t lda, const float* bias,
+                             const float* a_dst,
                              const float* row_stats, int64_t n, int32_t H, int32_t C, float* pack,
                              size_t pack_bytes, float* gsum_part, size_t gsum_part_bytes, void* stream) {
   MP_DEVICE_GUARD(stream);
@@ -447,14 +466,14 @@ int mp_gat_backward_prep_f32(const float* grad_out, int64_t ldg, const float* ag
   hipStream_t s = as_stream(stream);
   const int G = C / 4;
   const bool v4 = C % 4 == 0 && G <= 64 && (G & (G - 1)) == 0 && (uintptr_t)grad_out % 16 == 0 &&
-                  (uintptr_t)agg % 16 == 0 && ldg % 4 == 0 && lda % 4 == 0;
+                  (uintptr_t)agg % 16 == 0 && ldg % 4 == 0 && lda % 4 == 0 && (uintptr_t)bias % 16 == 0;
   MP_CHECK_ARG(!gsum_part || (v4 && F <= 256), "mp_gat_backward_prep_f32: gsum_part needs C%%4==0 and H*C<=256");
   if (v4) {
     k_gat_bwd_prep_wave<<<(unsigned)mp_gat_bwd_blocks(n), 256, 0, s>>>(grad_out, ldg, agg, lda, a_dst, row_stats, n,
-                                                                      H, C, G, pack, gsum_part);
+                                                                      H, C, G, pack, gsum_part, bias);
   } else {
-    k_gat_bwd_prep_scalar<<<(unsigned)ceil_div(n * H, 256), 256, 0, s>>>(grad_out, ldg, agg, lda, a_dst, row_stats,
-                                                                         n, H, C, pack);
+    k_gat_bwd_prep_scalar<<<(unsigned)ceil_div(n * H, 256), 256, 0, s>>>(grad_out, ldg, agg, lda, bias, a_dst,
+                                                                         row_stats, n, H, C, pack);
   }
   MP_CHECK_LAUNCH();
   return MP_OK;

@@ -14,16 +14,24 @@ namespace mp {
 
 constexpr int kWideWaves = 4;  // waves per block
 
-// sum over a head's features [h*C, h*C + C) of a[.] * b[.] for row pointers a, b
-// (lane partials in chunk order, then the wave tree); every lane gets the sum
+// sum over a head's features [h*C, h*C + C) of a[.] * (b[.] - sub[.]) for row
+// pointers a, b (sub optional: b holds out = agg + bias, sub the bias; lane
+// partials in chunk order, then the wave tree); every lane gets the sum
 __device__ __forceinline__ float head_dot(const float* __restrict__ a, const float* __restrict__ b, int C,
-                                         int lane) {
+                                         int lane, const float* __restrict__ sub = nullptr) {
   float t = 0.f;
   for (int c0 = 0; c0 < C; c0 += 256) {
     const int c = c0 + 4 * lane;
     if (c < C) {
       const f32x4 x = *reinterpret_cast<const f32x4*>(a + c);
-      const f32x4 y = *reinterpret_cast<const f32x4*>(b + c);
+      f32x4 y = *reinterpret_cast<const f32x4*>(b + c);
+      if (sub) {
+        const f32x4 d = *reinterpret_cast<const f32x4*>(sub + c);
+        y.x = __fsub_rn(y.x, d.x);
+        y.y = __fsub_rn(y.y, d.y);
+        y.z = __fsub_rn(y.z, d.z);
+        y.w = __fsub_rn(y.w, d.w);
+      }
       t = __builtin_fmaf(x.x, y.x, t);
       t = __builtin_fmaf(x.y, y.y, t);
       t = __builtin_fmaf(x.z, y.z, t);
@@ -58,10 +66,12 @@ __global__ __launch_bounds__(64 * kWideWaves) void k_gat_node_scores_wide(const 
 
 // Backward prologue after the training forward, per (node n, head h):
 //   rs = <g[n,h,:], agg[n,h,:]>,  pack[n,h] = (a_dst, m, 1/den, rs),
+//   (bias != nullptr: agg holds out = agg + bias, rs over out - bias)
 //   grad_a_dst[n,h] = <g[n,h,:], agg2[n,h,:]> - rs * row_s2[n,h]
 __global__ __launch_bounds__(64 * kWideWaves) void k_gat_bwd_prep_wide(
     const float* __restrict__ g, int64_t ldg, const float* __restrict__ agg, int64_t lda,
-    const float* __restrict__ agg2, const float* __restrict__ s2, const float* __restrict__ a_dst,
+    const float* __restrict__ bias, const float* __restrict__ agg2, const float* __restrict__ s2,
+    const float* __restrict__ a_dst,
     const float* __restrict__ stats, int64_t n, int32_t H, int32_t C, float* __restrict__ pack,
     float* __restrict__ ga_dst) {
   const int lane = lane_id();
@@ -70,7 +80,7 @@ __global__ __launch_bounds__(64 * kWideWaves) void k_gat_bwd_prep_wide(
   for (int64_t r = (int64_t)blockIdx.x * kWideWaves + (threadIdx.x >> 6); r < n; r += nw) {
     for (int h = 0; h < H; ++h) {
       const int64_t o = (int64_t)h * C;
-      const float rs = head_dot(g + r * ldg + o, agg + r * lda + o, C, lane);
+      const float rs = head_dot(g + r * ldg + o, agg + r * lda + o, C, lane, bias ? bias + o : nullptr);
       const float t2 = head_dot(g + r * ldg + o, agg2 + r * HC + o, C, lane);
       if (lane == 0) {
         const int64_t q = r * H + h;
@@ -145,7 +155,7 @@ int mp_gat_node_scores_wide_f32(const float* xw, int64_t n_nodes, int32_t H, int
 }
 
 int mp_gat_backward_prep_wide_f32(const float* grad_out, int64_t ldg, const float* agg, int64_t lda,
-                                  const float* agg2, const float* row_s2, const float* a_dst, const float* row_stats,
+                                  const float* bias, const float* agg2, const float* row_s2, const float* a_dst, const float* row_stats,
                                   int64_t n, int32_t H, int32_t C, float* pack, size_t pack_bytes,
                                   float* grad_a_dst, void* stream) {
   MP_DEVICE_GUARD(stream);
@@ -156,10 +166,10 @@ int mp_gat_backward_prep_wide_f32(const float* grad_out, int64_t ldg, const floa
   MP_CHECK_EXTENT("mp_gat_backward_prep_wide_f32", "pack", pack_bytes, (size_t)n * H * 16);
   const int64_t F = (int64_t)H * C;
   MP_CHECK_ARG(ldg >= F && lda >= F && ldg % 4 == 0 && lda % 4 == 0, "mp_gat_backward_prep_wide_f32: bad ld");
-  MP_CHECK_ARG(al16(grad_out) && al16(agg) && al16(agg2) && al16(pack),
+  MP_CHECK_ARG(al16(grad_out) && al16(agg) && al16(agg2) && al16(pack) && al16(bias),
                "mp_gat_backward_prep_wide_f32: 16-byte alignment required");
   k_gat_bwd_prep_wide<<<wide_blocks(n), 64 * kWideWaves, 0, as_stream(stream)>>>(
-      grad_out, ldg, agg, lda, agg2, row_s2, a_dst, row_stats, n, H, C, pack, grad_a_dst);
+      grad_out, ldg, agg, lda, bias, agg2, row_s2, a_dst, row_stats, n, H, C, pack, grad_a_dst);
   MP_CHECK_LAUNCH();
   return MP_OK;
 }

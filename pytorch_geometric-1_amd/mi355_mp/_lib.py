@@ -106,20 +106,22 @@ SIGNATURES = {
     "mp_gat_dropout_keep": (ctypes.c_int, [u64, f32, i32, i64, c_p, c_p]),
     "mp_gat_wide_ok": (ctypes.c_int, [i32, i32]),
     "mp_gat_node_scores_wide_f32": (ctypes.c_int, [c_p, i64, i32, i32, c_p, c_p, c_p, c_p]),
-    "mp_gat_backward_prep_wide_f32": (ctypes.c_int, [c_p, i64, c_p, i64, c_p, c_p, c_p, c_p, i64, i32, i32, c_p, sz,
-                                                     c_p, c_p]),
+    "mp_gat_backward_prep_wide_f32": (ctypes.c_int, [c_p, i64, c_p, i64, c_p, c_p, c_p, c_p, c_p, i64, i32, i32, c_p,
+                                                     sz, c_p, c_p]),
     "mp_gat_backward_wide_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, i64, c_p, c_p, i32, i32, f32, u64, f32,
                                                 c_p, c_p, sz, c_p, sz, c_p, sz, i32, c_p]),
     "mp_gat_backward_epilogue_wide_f32": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, c_p, i64, i32, i32, c_p]),
     "mp_segment_offset_i64": (ctypes.c_int, [c_p, i64, i32, i64, c_p, c_p, i64, c_p]),
     "mp_segment_ids_i64": (ctypes.c_int, [c_p, i64, c_p, i64, c_p]),
-    "mp_gat_backward_prep_f32": (ctypes.c_int, [c_p, i64, c_p, i64, c_p, c_p, i64, i32, i32, c_p, sz, c_p, sz,
+    "mp_gat_backward_prep_f32": (ctypes.c_int, [c_p, i64, c_p, i64, c_p, c_p, c_p, i64, i32, i32, c_p, sz, c_p, sz,
                                                 c_p]),
-    "mp_gat_backward_prep_train_f32": (ctypes.c_int, [c_p, i64, c_p, i64, c_p, c_p, c_p, c_p, i64, i32, i32, c_p,
-                                                      sz, c_p, sz, c_p, c_p]),
+    "mp_gat_backward_prep_train_f32": (ctypes.c_int, [c_p, i64, c_p, i64, c_p, c_p, c_p, c_p, c_p, i64, i32, i32,
+                                                      c_p, sz, c_p, sz, c_p, c_p]),
     "mp_gat_bwd_blocks": (ctypes.c_int, [i64]),
     "mp_col_sums_f32": (ctypes.c_int, [c_p, i64, i64, i32, c_p, sz, c_p]),
     "mp_gat_backward_finish_f32": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, i64, i32, i32, c_p, sz, c_p]),
+    "mp_gat_merge_partials_f32": (ctypes.c_int, [i64, i32, i32, c_p, c_p, i64, c_p, i64, c_p, c_p, c_p, i64, c_p, c_p,
+                                                 c_p, c_p]),
     "mp_heads_outer_add_f32": (ctypes.c_int, [c_p, i64, c_p, i64, i32, i32, c_p, i64, c_p]),
     "mp_gather_rows_f32": (ctypes.c_int, [c_p, i64, c_p, i64, i32, c_p, i64, c_p]),
     "mp_permute_f32": (ctypes.c_int, [c_p, c_p, i64, c_p, c_p]),

@@ -566,6 +566,11 @@ class HaloCover:
         d_halo = n_own + off_t[d_q] + nS[d_q] + (torch.arange(D.numel(), device=dev) - D_start[d_q])
         self.bnd_src = torch.cat([pull_halo, d_halo])
         self.bnd_dst = torch.cat([r_dst[pull], D - d_q * stride])
+        # kept for GatHaloCover: the remote edges (plan order) and which are pulled,
+        # the halo slot of each pulled one, and per pushed row its destination
+        self.rem, self.pull, self.pull_halo = rem, pull, pull_halo
+        self.push_dst, self.push_halo = D - d_q * stride, d_halo
+        self.n_push_rows_to = nD.tolist()       # pushed rows this rank receives, per owner
         self.bnd_w = torch.cat([r_w[pull], torch.ones(D.numel(), dtype=torch.float32, device=dev)])
         self.n_halo = off[-1]
         self.n_local_src = n_own + self.n_halo
@@ -594,6 +599,7 @@ class HaloCover:
         _a2a(pw, r_w[push][order].contiguous(), snP, nP.tolist(), group)
         # --- the send graph: rows = this rank's send buffer (per peer: pulled rows, then partial rows)
         self.send_counts = [a + b for a, b in zip(snS, snD)]
+        self.send_pull_counts, self.send_push_counts = snS, snD
         base = [0]
         for c in self.send_counts:
             base.append(base[-1] + c)
@@ -1003,6 +1009,7 @@ class ShardedGraph:
         self.deg = None
         self._w = None
         self.cover = None
+        self.gat_cover = None
         self._chunk = None
         return self
 
@@ -1024,6 +1031,12 @@ class ShardedGraph:
         local_gat(graph, edge_index, xw_local, att, H, C, slope, bias,
         return_alpha, dropout) -> (out, alpha): default the HIP path
         (ops.gat_propagate); the gloo CPU tests pass the oracle."""
+        from .gat_cover import cover_ok
+        gc = getattr(self, "gat_cover", None)
+        if gc is not None and not return_alpha and not dropout and local_gat is None \
+                and (not xw_own.is_cuda or cover_ok(heads, out_channels)):
+            from .gat_cover import gat_cover_propagate
+            return gat_cover_propagate(gc, xw_own, att, heads, out_channels, negative_slope, bias), None
         if local_gat is None:
             from . import ops
             local_gat = ops.gat_propagate
@@ -1031,6 +1044,20 @@ class ShardedGraph:
         out, alpha = local_gat(self.g_fwd, self.fwd.local_edge_index, xw_local, att, heads, out_channels,
                                negative_slope, bias, return_alpha, dropout)
         return out, ((self.fwd.edge_gid, alpha) if return_alpha else None)
+
+    def enable_gat_halo_cover(self):
+        """Run gat_propagate (forward AND backward) over the hybrid halo cover
+        (mi355_mp.gat_cover.GatHaloCover: a remote source row is pulled, or its
+        owner pushes its online-softmax piece of the destination row -- 0.57x
+        the pull rows on the config-2 graph) instead of the pull exchange.
+        return_alpha, attention dropout and heads outside gat_cover.cover_ok
+        keep the pull form.  Collective, once (every rank of the group)."""
+        from .gat_cover import GatHaloCover
+        if self.bwd is not None:
+            raise ValueError("mi355_mp.dist: enable_gat_halo_cover needs a graph made by for_gat / "
+                             "for_gat_from_slices")
+        self.gat_cover = GatHaloCover(self.fwd, self.group)
+        return self
 
     def _set_local_weights(self, w_fwd, w_bwd):
         """Per-edge weights already in each plan's local edge order."""

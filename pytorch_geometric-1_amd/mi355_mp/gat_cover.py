@@ -1,0 +1,475 @@
+"""Sharded GATConv over the hybrid halo cover (callers
+/root/reference/ConvexPruning.py:209-224, examples/ppi.py:22-28).
+
+The pull form (ShardedGraph.gat_propagate without a cover) ships X W of every
+remote source of the rank's in-edges.  A GAT destination row is a softmax-
+weighted sum, and softmax sums split into online-softmax pieces that merge
+exactly (GatRed::merge): a cross edge j -> i (j owned by q, i by p) can be
+covered by q pushing its PIECE of row i -- the state (m, den, acc / den) of
+the softmax over q's own sources of i's in-edges -- instead of p pulling
+x_j.  Which edges are pushed is HaloCover's rule (the endpoint with the larger
+cross-degree; on RMAT graphs 0.56-0.57x the pull rows).  One step:
+
+  forward (rank p; every rank is also the "q" of its peers)
+    1. node scores of the own rows; a_dst of every destination some peer pushes
+       a piece of goes to that peer (H floats per row, one all_to_all)
+    2. the send rows: ONE fused GAT aggregation over the send graph (a pulled
+       row is a one-edge row: alpha = 1, the row itself bit for bit; a pushed
+       row is the piece over the push edges, with the received a_dst), then
+       the rows and their (m, den) go out (two all_to_alls)
+    3. the local piece of every own row: the fused GAT aggregation over the
+       interior and pulled edges (global edge order), node scores of the
+       received rows first
+    4. mp_gat_merge_partials_f32: the pieces of each row, local first, then the
+       peers' in rank order, plus the bias.  A row no peer pushes a piece of is
+       the single-GPU kernel's row bit for bit (same edges, same order); merged
+       rows are within the 1e-5 bound (regrouped softmax sums).
+  backward (the global softmax gradient, split by where each edge lives)
+    p: pack (a_dst, M, 1/den, rs) per own row from the MERGED stats (rs over
+       out - bias), the node-wise d a_dst of the local edges (the training
+       forward's agg2 / s2 scaled to the merged rows), the transposed pass
+       over the local edges; then ONE reverse all_to_all of [n_halo, H*C]:
+       a pulled row's slot carries its gradient back to its owner, a pushed
+       piece's slot carries the gradient g_i of its destination (and a second,
+       its pack).
+    q: a pulled row's gradient folds into the own row it copied; the pushed
+       pieces' edges take the GAT backward over the transposed push graph
+       (mp_gat_backward_f32: d xw_j, d a_src_j, de per edge), and the per-row
+       sums of de -- the peer's share of d a_dst_i -- go back to p (one
+       all_to_all of H floats per pushed row).
+    p: d a_dst_i complete; its att_dst term of d xw and the d att partials.
+  Every collective runs in the same order on every rank.
+
+Device path: the HIP kernels (GatHaloCover.forward_device / backward_device,
+wrapped by _GatCoverFn).  Host path (forward_host): the same data flow with
+differentiable torch ops and a differentiable all_to_all -- the gloo CPU tests
+check the distributed algorithm, forward and backward, against the
+single-process oracle with it.  Shapes: C % 4 == 0 with C / 4 a power of two
+<= 64 (the fused transposed pass); other shapes, return_alpha and attention
+dropout take the pull form.
+"""
+import torch
+import torch.distributed as dist
+
+from .dist import HaloCover, _a2a
+
+
+def cover_ok(H, C):
+    """Head shapes the device path takes (mp_gat_train_ok: the fused kernels)."""
+    q = C // 4
+    return H > 0 and C % 4 == 0 and 1 <= q <= 64 and (q & (q - 1)) == 0
+
+
+class _A2A(torch.autograd.Function):
+    """Differentiable all_to_all_single of rows: forward send -> recv with the
+    given splits, backward the reverse exchange of the gradient."""
+
+    @staticmethod
+    def forward(ctx, send, recv_counts, send_counts, group):
+        ctx.counts, ctx.group = (recv_counts, send_counts), group
+        recv = send.new_empty((sum(recv_counts),) + tuple(send.shape[1:]))
+        _a2a(recv, send.contiguous(), recv_counts, send_counts, group)
+        return recv
+
+    @staticmethod
+    def backward(ctx, g):
+        recv_counts, send_counts = ctx.counts
+        gs = g.new_empty((sum(send_counts),) + tuple(g.shape[1:]))
+        _a2a(gs, g.contiguous(), send_counts, recv_counts, ctx.group)
+        return gs, None, None, None
+
+
+def _cat_ranges(starts, lengths, dev):
+    """concatenation of arange(s, s + n) over (s, n) pairs, as an int64 tensor."""
+    parts = [torch.arange(s, s + n, dtype=torch.int64, device=dev) for s, n in zip(starts, lengths) if n]
+    return torch.cat(parts) if parts else torch.zeros(0, dtype=torch.int64, device=dev)
+
+
+class GatHaloCover:
+    """The GAT form of HaloCover for one rank of a ShardedGraph.for_gat plan
+    (built collectively over `group`, like HaloCover).  Index structures:
+
+      loc_src / loc_dst   the local piece's edges, global edge order: interior
+                          edges and pulled edges (source = its halo slot)
+      part_row / part_dst per received piece: its row in the receive buffer and
+                          the own destination row (the merge list)
+      adst_rows           own destination rows whose a_dst the peers need, in
+                          the order of their pushed rows (per owner)
+      send graph          copy edges (own row -> send row) and push edges (own
+                          source -> pushed send row), rows = this rank's send
+                          buffer (per peer: pulled rows, then pieces)
+    Graphs are built lazily on the device of the plan."""
+
+    def __init__(self, plan, group=None):
+        hc = HaloCover(plan, None, group)
+        self.hc, self.plan, self.group = hc, plan, group
+        dev = plan.halo_nodes.device
+        n_own = plan.n_own
+        self.n_own = n_own
+        self.n_halo, self.n_local_src, self.n_send = hc.n_halo, hc.n_local_src, hc.n_send
+        self.recv_counts, self.send_counts = hc.recv_counts, hc.send_counts
+        self.n_pull_rows, self.n_push_rows = hc.n_pull_rows, hc.n_push_rows
+        self.n_pull_edges, self.n_push_edges = hc.n_pull_edges, hc.n_push_edges
+        # the local piece: plan order (= global edge order), pushed edges left out
+        lei = plan.local_edge_index
+        src, dst = lei[0].clone(), lei[1]
+        keep = ~hc.rem
+        rem_idx = torch.nonzero(hc.rem).view(-1)
+        pulled = rem_idx[hc.pull]
+        keep[pulled] = True
+        src[pulled] = hc.pull_halo
+        self.loc_src, self.loc_dst = src[keep].contiguous(), dst[keep].contiguous()
+        self.n_interior = int((~hc.rem).sum())
+        # received pieces -> own destination (the merge list)
+        self.part_row = (hc.push_halo - n_own).contiguous()
+        self.part_dst = hc.push_dst.contiguous()
+        # a_dst requests: the destinations of the pieces this rank receives, grouped by
+        # the pushing owner in its row order (ascending destination within an owner)
+        self.adst_rows = hc.push_dst.contiguous()
+        self.adst_send_counts = list(hc.n_push_rows_to)
+        self.adst_recv_counts = list(hc.send_push_counts)
+        # send buffer positions of this rank's pushed rows, per peer after its pulled rows
+        base = [0]
+        for c in self.send_counts:
+            base.append(base[-1] + c)
+        self.send_push_rows = _cat_ranges([b + s for b, s in zip(base[:-1], hc.send_pull_counts)],
+                                          hc.send_push_counts, dev)
+        n_copy = sum(hc.send_pull_counts)
+        self.copy_src, self.copy_dst = hc.send_src[:n_copy].contiguous(), hc.send_dst[:n_copy].contiguous()
+        self.push_src, self.push_dst = hc.send_src[n_copy:].contiguous(), hc.send_dst[n_copy:].contiguous()
+        self.send_src = hc.send_src.contiguous()
+        self.send_dst = hc.send_dst.contiguous()
+        self._graphs = None
+
+    # ------------------------------------------------------------------ graphs
+    def graphs(self):
+        """(local piece, send graph, merge list, transposed copy graph, push
+        graph) as native Graphs, built once."""
+        if self._graphs is None:
+            from .graph import GAT_TARGET_TASKS, Graph
+            n_own = self.n_own
+            g_loc = Graph(torch.stack([self.loc_src, self.loc_dst]), n_own, self.n_local_src,
+                          target_tasks=GAT_TARGET_TASKS)
+            g_send = Graph(torch.stack([self.send_src, self.send_dst]), self.n_send, n_own,
+                           target_tasks=GAT_TARGET_TASKS)
+            g_merge = Graph(torch.stack([self.part_row, self.part_dst]), n_own, max(self.n_halo, 1))
+            g_copy_t = Graph(torch.stack([self.copy_dst, self.copy_src]), n_own, max(self.n_send, 1))
+            g_push = Graph(torch.stack([self.push_src, self.push_dst]), self.n_send, n_own,
+                           target_tasks=GAT_TARGET_TASKS)
+            self._graphs = (g_loc, g_send, g_merge, g_copy_t, g_push)
+        return self._graphs
+
+    def stats(self):
+        return {"cover_pulled_rows": self.n_pull_rows, "cover_partial_rows": self.n_push_rows,
+                "cover_push_edges": self.n_push_edges, "halo_rows": self.n_halo,
+                "pull_halo_rows": self.plan.n_local_src - self.plan.n_own,
+                "send_rows": self.n_send, "local_piece_edges": int(self.loc_src.numel())}
+
+    # ------------------------------------------------------------ host (oracle)
+    def forward_host(self, xw_own, att, H, C, slope=0.2, bias=None):
+        """The same step with differentiable torch ops (any device, any float
+        dtype): the reference the gloo CPU tests hold the algorithm to, forward
+        and backward (autograd through a differentiable all_to_all).  Returns the
+        rank's rows [n_own, H*C] (+ bias)."""
+        n_own, F = self.n_own, H * C
+        g = self.group
+        att2 = att.reshape(H, 2 * C)
+
+        def scores(x):
+            x3 = x.view(-1, H, C)
+            return (x3 * att2[:, :C]).sum(-1), (x3 * att2[:, C:]).sum(-1)     # a_dst, a_src
+
+        def piece(x_src, a_src, a_dst_rows, src, dst, n_rows):
+            """(out = acc / den, m, den) of the softmax over each row's edges."""
+            e = torch.nn.functional.leaky_relu(a_src[src] + a_dst_rows[dst], slope)
+            m = torch.full((n_rows, H), float("-inf"), dtype=x_src.dtype, device=x_src.device)
+            m = m.scatter_reduce(0, dst.view(-1, 1).expand(-1, H), e.detach(), "amax", include_self=True)
+            p = torch.exp(e - m[dst])
+            den = torch.zeros((n_rows, H), dtype=x_src.dtype, device=x_src.device).index_add(0, dst, p) + 1e-16
+            msg = x_src[src].view(-1, H, C) * p.unsqueeze(-1)
+            acc = torch.zeros((n_rows, H, C), dtype=x_src.dtype, device=x_src.device).index_add(0, dst, msg)
+            return acc / den.unsqueeze(-1), m, den
+
+        a_dst_own, a_src_own = scores(xw_own)
+        # 1. a_dst of the rows the peers push pieces of
+        adst_in = _A2A.apply(a_dst_own[self.adst_rows], self.adst_recv_counts, self.adst_send_counts, g)
+        send_adst = a_dst_own.new_zeros((self.n_send, H)).index_copy(0, self.send_push_rows, adst_in)
+        # 2. the send rows and their stats
+        s_out, s_m, s_den = piece(xw_own, a_src_own, send_adst, self.send_src, self.send_dst, self.n_send)
+        recv = _A2A.apply(s_out.reshape(self.n_send, F), self.recv_counts, self.send_counts, g)
+        r_m = _A2A.apply(s_m, self.recv_counts, self.send_counts, g)
+        r_den = _A2A.apply(s_den, self.recv_counts, self.send_counts, g)
+        # 3. the local piece over [own ; received rows]
+        x_loc = torch.cat([xw_own, recv])
+        _, a_src_loc = scores(x_loc)
+        o, m, den = piece(x_loc, a_src_loc, a_dst_own, self.loc_src, self.loc_dst, n_own)
+        # 4. merge: local piece, then the peers' pieces
+        pm, pden, po = r_m[self.part_row], r_den[self.part_row], recv[self.part_row].view(-1, H, C)
+        M = m.detach().scatter_reduce(0, self.part_dst.view(-1, 1).expand(-1, H), pm.detach(), "amax",
+                                      include_self=True)
+        w_loc = den * torch.exp(m - M)
+        w_p = pden * torch.exp(pm - M[self.part_dst])
+        tot = w_loc.index_add(0, self.part_dst, w_p)
+        out = o * (w_loc / tot).unsqueeze(-1)
+        out = out.index_add(0, self.part_dst, po * (w_p / tot[self.part_dst]).unsqueeze(-1))
+        out = out.reshape(n_own, F)
+        return out + bias if bias is not None else out
+
+    # ---------------------------------------------------------- device (HIP)
+    def forward_device(self, xw_own, att_c, H, C, slope, bias, train, exchange=True):
+        """The step on the fused kernels.  Returns (out [n_own, H*C] with bias,
+        saved) -- saved holds what backward_device needs when train.
+        exchange=False: the compute alone (no collective; the receive buffers
+        hold zeros), for decompose()."""
+        from . import _lib
+        lib = _lib.load()
+        g_loc, g_send, g_merge, _, _ = self.graphs()
+        dev = xw_own.device
+        st = _lib.stream_ptr(dev)
+        n_own, F = self.n_own, H * C
+        grp = self.group
+        xl = torch.empty((self.n_local_src, F), dtype=torch.float32, device=dev)
+        xl[:n_own].copy_(xw_own)
+        a_src = torch.empty((self.n_local_src, H), dtype=torch.float32, device=dev)
+        a_dst = torch.empty((self.n_local_src, H), dtype=torch.float32, device=dev)
+        if n_own:
+            _lib.check(lib.mp_gat_node_scores_f32(xl.data_ptr(), n_own, H, C, att_c.data_ptr(), a_src.data_ptr(),
+                                                  a_dst.data_ptr(), st), "mp_gat_node_scores_f32")
+        # 1. a_dst of the rows the peers push pieces of
+        a2a = _a2a if exchange else (lambda o, *a: o.zero_())
+        adst_in = torch.empty((sum(self.adst_recv_counts), H), dtype=torch.float32, device=dev)
+        a2a(adst_in, a_dst[self.adst_rows].contiguous(), self.adst_recv_counts, self.adst_send_counts, grp)
+        send_adst = torch.zeros((max(self.n_send, 1), H), dtype=torch.float32, device=dev)
+        if adst_in.shape[0]:
+            send_adst[self.send_push_rows] = adst_in
+        # 2. the send rows: one fused aggregation over the send graph, then rows + stats out
+        send = torch.empty((self.n_send, F), dtype=torch.float32, device=dev)
+        send_st = torch.empty((self.n_send, H, 2), dtype=torch.float32, device=dev)
+        if self.n_send:
+            gs = g_send.dst.struct("other")
+            sb = lib.mp_gat_slab_bytes(gs, H, C)
+            slab = torch.empty(sb, dtype=torch.uint8, device=dev)
+            _lib.check(lib.mp_gat_aggregate_att_f32(gs, xl.data_ptr(), a_src.data_ptr(), send_adst.data_ptr(),
+                                                    att_c.data_ptr(), H, C, float(slope), None, send.data_ptr(), F,
+                                                    send_st.data_ptr(), slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
+                       "mp_gat_aggregate_att_f32 (send rows)")
+            del slab
+        r_st = torch.empty((self.n_halo, H, 2), dtype=torch.float32, device=dev)
+        a2a(xl[n_own:], send, self.recv_counts, self.send_counts, grp)
+        a2a(r_st, send_st, self.recv_counts, self.send_counts, grp)
+        if self.n_halo:
+            _lib.check(lib.mp_gat_node_scores_f32(xl[n_own:].data_ptr(), self.n_halo, H, C, att_c.data_ptr(),
+                                                  a_src[n_own:].data_ptr(), a_dst[n_own:].data_ptr(), st),
+                       "mp_gat_node_scores_f32 (received rows)")
+        # 3. the local piece (no bias: the merge adds it)
+        out = torch.empty((n_own, F), dtype=torch.float32, device=dev)
+        stats = torch.empty((n_own, H, 2), dtype=torch.float32, device=dev)
+        agg2 = s2 = None
+        if n_own:
+            gl = g_loc.dst.struct("other")
+            if train:
+                agg2 = torch.empty((n_own, F), dtype=torch.float32, device=dev)
+                s2 = torch.empty((n_own, H), dtype=torch.float32, device=dev)
+                sb = lib.mp_gat_train_slab_bytes(gl, H, C)
+                slab = torch.empty(sb, dtype=torch.uint8, device=dev)
+                _lib.check(lib.mp_gat_aggregate_train_f32(gl, xl.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(),
+                                                          att_c.data_ptr(), H, C, float(slope), None, out.data_ptr(),
+                                                          F, None, stats.data_ptr(), agg2.data_ptr(), s2.data_ptr(),
+                                                          slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
+                           "mp_gat_aggregate_train_f32 (local piece)")
+            else:
+                sb = lib.mp_gat_slab_bytes(gl, H, C)
+                slab = torch.empty(sb, dtype=torch.uint8, device=dev)
+                _lib.check(lib.mp_gat_aggregate_att_f32(gl, xl.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(),
+                                                        att_c.data_ptr(), H, C, float(slope), None, out.data_ptr(), F,
+                                                        stats.data_ptr(), slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
+                           "mp_gat_aggregate_att_f32 (local piece)")
+            del slab
+            # 4. merge the pieces (+ bias; agg2 / s2 scaled to the merged rows)
+            m = g_merge.dst
+            n_parts = int(self.part_row.numel())
+            _lib.check(lib.mp_gat_merge_partials_f32(n_own, H, C, m.rowptr.data_ptr(),
+                                                     m.col.data_ptr() if n_parts else None, n_parts,
+                                                     xl[n_own:].data_ptr() if n_parts else None, F,
+                                                     r_st.data_ptr() if n_parts else None, _lib.ptr(bias),
+                                                     out.data_ptr(), F, stats.data_ptr(), _lib.ptr(agg2),
+                                                     _lib.ptr(s2), st), "mp_gat_merge_partials_f32")
+        saved = (xl, a_src, a_dst, stats, agg2, s2) if train else None
+        return out, saved
+
+    def decompose(self, xw_own, att, H, C, slope, bias, reps=10, barrier=None):
+        """The forward step taken apart on this rank (wall clock over `reps`,
+        the device synchronised after them, ranks lined up by `barrier`):
+        exchange_only_ms -- the three all_to_alls (a_dst requests, rows, stats)
+        with packed buffers; compute_only_ms -- node scores, send rows, local
+        piece and merge with no collective; step_ms -- the step itself;
+        hidden_frac as OverlappedAggregation.decompose (the GAT step runs its
+        pieces in order, so ~0 means nothing is hidden)."""
+        import time
+        H, C = int(H), int(C)
+        att_c = att.reshape(H, 2 * C).contiguous().to(torch.float32)
+        dev = xw_own.device
+        F = H * C
+        grp = self.group
+        adst_s = torch.zeros((sum(self.adst_send_counts), H), dtype=torch.float32, device=dev)
+        adst_r = torch.empty((sum(self.adst_recv_counts), H), dtype=torch.float32, device=dev)
+        rows_s = torch.zeros((self.n_send, F), dtype=torch.float32, device=dev)
+        rows_r = torch.empty((self.n_halo, F), dtype=torch.float32, device=dev)
+        st_s = torch.zeros((self.n_send, H, 2), dtype=torch.float32, device=dev)
+        st_r = torch.empty((self.n_halo, H, 2), dtype=torch.float32, device=dev)
+
+        def exchange():
+            _a2a(adst_r, adst_s, self.adst_recv_counts, self.adst_send_counts, grp)
+            _a2a(rows_r, rows_s, self.recv_counts, self.send_counts, grp)
+            _a2a(st_r, st_s, self.recv_counts, self.send_counts, grp)
+
+        def timed(fn):
+            fn()
+            if barrier is not None:
+                barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                fn()
+            torch.cuda.synchronize()
+            return (time.perf_counter() - t0) / reps * 1e3
+
+        res = {"exchange_only_ms": timed(exchange),
+               "compute_only_ms": timed(lambda: self.forward_device(xw_own, att_c, H, C, slope, bias, False,
+                                                                   exchange=False)),
+               "step_ms": timed(lambda: self.forward_device(xw_own, att_c, H, C, slope, bias, False))}
+        shorter = min(res["exchange_only_ms"], res["compute_only_ms"])
+        res["hidden_frac"] = ((res["exchange_only_ms"] + res["compute_only_ms"] - res["step_ms"]) / shorter
+                              if shorter > 1e-3 else None)
+        return res
+
+    def backward_device(self, g, out, bias, att_c, H, C, slope, saved, want_att, want_bias):
+        """d xw_own, d att (or None), d bias (or None) of forward_device (see the
+        module docstring for the split)."""
+        from . import _lib, ops
+        lib = _lib.load()
+        g_loc, _, g_merge, g_copy_t, g_push = self.graphs()
+        xl, a_src, a_dst, stats, agg2, s2 = saved
+        dev = g.device
+        st = _lib.stream_ptr(dev)
+        n_own, F, grp = self.n_own, H * C, self.group
+        nl = self.n_local_src
+        # p: pack from the merged stats, node-wise d a_dst of the local edges
+        pack = torch.zeros((max(n_own, 1), H, 4), dtype=torch.float32, device=dev)
+        ga_dst = torch.zeros((max(n_own, 1), H), dtype=torch.float32, device=dev)
+        if n_own:
+            _lib.check(lib.mp_gat_backward_prep_train_f32(g.data_ptr(), F, out.data_ptr(), F, _lib.ptr(bias),
+                                                          agg2.data_ptr(), s2.data_ptr(), a_dst.data_ptr(),
+                                                          stats.data_ptr(), n_own, H, C, pack.data_ptr(),
+                                                          _lib.nbytes(pack), None, 0, ga_dst.data_ptr(), st),
+                       "mp_gat_backward_prep_train_f32 (cover)")
+        # p: the transposed pass over the local edges (the att_dst term comes last)
+        gx_l = torch.zeros((nl, F), dtype=torch.float32, device=dev)
+        ga_src_l = torch.zeros((nl, H), dtype=torch.float32, device=dev)
+        if n_own and g_loc.dst.n_edges:
+            gt = g_loc.src_with_dst_slots()
+            gs = gt.struct("dst_slot")
+            zero_gd = torch.zeros((nl, H), dtype=torch.float32, device=dev)
+            sb = lib.mp_gat_slab_bytes(gs, H, C)
+            slab = torch.empty(sb, dtype=torch.uint8, device=dev)
+            _lib.check(lib.mp_gat_backward_train_f32(gs, g.data_ptr(), F, xl.data_ptr(), a_src.data_ptr(),
+                                                     pack.data_ptr(), att_c.data_ptr(), H, C, float(slope),
+                                                     zero_gd.data_ptr(), gx_l.data_ptr(), ga_src_l.data_ptr(),
+                                                     slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
+                       "mp_gat_backward_train_f32 (local piece)")
+            del slab, zero_gd
+        # reverse exchange: a pulled slot returns its row's gradient to the owner, a
+        # piece's slot carries its destination's g and pack to the peer that pushed it
+        rev = gx_l[n_own:]
+        rev_pack = torch.zeros((self.n_halo, H * 4), dtype=torch.float32, device=dev)
+        if self.part_row.numel():
+            rev[self.part_row] = g[self.part_dst]
+            rev_pack[self.part_row] = pack.view(-1, H * 4)[self.part_dst]
+        back = torch.empty((self.n_send, F), dtype=torch.float32, device=dev)
+        back_pack = torch.empty((self.n_send, H * 4), dtype=torch.float32, device=dev)
+        _a2a(back, rev.contiguous(), self.send_counts, self.recv_counts, grp)
+        _a2a(back_pack, rev_pack, self.send_counts, self.recv_counts, grp)
+        # q: pulled rows' gradients fold into the rows they copied
+        gx = gx_l[:n_own].clone()
+        if self.copy_src.numel():
+            gx += ops._aggregate(g_copy_t.dst, "other", back, None, "sum", 0, None)[0]
+        # q: the pushed pieces' edges (global softmax gradient with p's pack)
+        ga_src_push = torch.zeros((max(n_own, 1), H), dtype=torch.float32, device=dev)
+        ga_back = torch.zeros((self.n_send, H), dtype=torch.float32, device=dev)
+        E_push = int(self.push_src.numel())
+        if E_push:
+            gt = g_push.src_with_dst_slots()
+            gs = gt.struct("dst_slot")
+            gx_push = torch.empty((n_own, F), dtype=torch.float32, device=dev)
+            de = torch.empty((E_push, H), dtype=torch.float32, device=dev)
+            sb = lib.mp_gat_slab_bytes(gs, H, C)
+            slab = torch.empty(sb, dtype=torch.uint8, device=dev)
+            _lib.check(lib.mp_gat_backward_f32(gs, back.data_ptr(), F, xl.data_ptr(), a_src.data_ptr(),
+                                               back_pack.data_ptr(), att_c.data_ptr(), H, C, float(slope),
+                                               gx_push.data_ptr(), ga_src_push.data_ptr(), de.data_ptr(),
+                                               _lib.nbytes(de), slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
+                       "mp_gat_backward_f32 (pushed pieces)")
+            del slab
+            gx += gx_push
+            ga_back = ops._aggregate(g_push.dst, "slot", de, None, "sum", 0, None)[0]
+        # the peers' shares of d a_dst come home
+        ga_in = torch.empty((self.n_halo, H), dtype=torch.float32, device=dev)
+        _a2a(ga_in, ga_back.contiguous(), self.recv_counts, self.send_counts, grp)
+        if n_own and self.part_row.numel():
+            ga_dst = ga_dst + ops._aggregate(g_merge.dst, "other", ga_in, None, "sum", 0, None)[0]
+        ga_dst = ga_dst[:n_own]
+        if n_own:
+            _lib.check(lib.mp_heads_outer_add_f32(gx.data_ptr(), F, ga_dst.contiguous().data_ptr(), n_own, H, C,
+                                                  att_c.data_ptr(), 2 * C, st), "mp_heads_outer_add_f32")
+        gatt = None
+        if want_att:
+            x_own3 = xl[:n_own].view(n_own, H, C)
+            d_dst = torch.einsum("nh,nhc->hc", ga_dst, x_own3)
+            d_src = (torch.einsum("nh,nhc->hc", ga_src_l, xl.view(nl, H, C))
+                     + torch.einsum("nh,nhc->hc", ga_src_push[:n_own], x_own3))
+            gatt = torch.cat([d_dst, d_src], dim=-1)
+        gb = ops.col_sums(g) if want_bias else None
+        return gx, gatt, gb
+
+
+class _GatCoverFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, xw_own, att, bias, cover, H, C, slope):
+        att_c = att.reshape(H, 2 * C).contiguous().to(torch.float32)
+        out, saved = cover.forward_device(xw_own.contiguous(), att_c, H, C, slope, bias, True)
+        ctx.cover, ctx.H, ctx.C, ctx.slope = cover, H, C, slope
+        ctx.saved = saved
+        ctx.save_for_backward(out, bias, att_c)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        out, bias, att_c = ctx.saved_tensors
+        g = g.contiguous()
+        if g.data_ptr() % 16:
+            g = g.clone()
+        gx, gatt, gb = ctx.cover.backward_device(g, out, bias, att_c, ctx.H, ctx.C, ctx.slope, ctx.saved,
+                                                 ctx.needs_input_grad[1], bias is not None and ctx.needs_input_grad[2])
+        ctx.saved = None
+        if gatt is not None:
+            gatt = gatt.view(1, ctx.H, 2 * ctx.C)
+        return gx, gatt, gb, None, None, None, None
+
+
+def gat_cover_propagate(cover, xw_own, att, heads, out_channels, negative_slope=0.2, bias=None):
+    """This rank's rows of the fused GATConv aggregation over the cover (+ bias);
+    device tensors take the HIP path with its native backward, host tensors the
+    differentiable torch form (forward_host)."""
+    H, C = int(heads), int(out_channels)
+    if xw_own.shape[0] != cover.n_own:
+        raise ValueError("mi355_mp.gat_cover: xw_own has %d rows, this rank owns %d" % (xw_own.shape[0], cover.n_own))
+    if not xw_own.is_cuda:
+        return cover.forward_host(xw_own, att, H, C, negative_slope, bias)
+    if not cover_ok(H, C):
+        raise ValueError("mi355_mp.gat_cover: heads of %d features take the pull form (cover_ok)" % C)
+    needs = torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in (xw_own, att, bias))
+    if not needs:
+        att_c = att.reshape(H, 2 * C).contiguous().to(torch.float32)
+        out, _ = cover.forward_device(xw_own.contiguous(), att_c, H, C, float(negative_slope), bias, False)
+        return out
+    return _GatCoverFn.apply(xw_own, att, bias, cover, H, C, float(negative_slope))

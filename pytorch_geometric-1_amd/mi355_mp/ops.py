@@ -679,7 +679,8 @@ def gat_dropout_keep(graph, seed, p, H):
 def _gat_forward(graph, edge_index, xw, att, H, C, slope, bias, want_alpha, train2=False, drop=None):
     """Returns (out, alpha, a_src, a_dst, stats, extra).  train2 (callers check
     _gat_train_fwd_ok first): the training forward, out = aggregate + bias and
-    extra = (agg2, s2, agg) with agg the pre-bias aggregate; else extra = None.
+    extra = (agg2, s2); else extra = None.  No pre-bias copy of the aggregate
+    is written: the backward prologues take rs over out - bias (ABI 6).
     drop = (seed, p): attention dropout on the messages (train2 only)."""
     lib = _lib.load()
     dev = xw.device
@@ -706,37 +707,32 @@ def _gat_forward(graph, edge_index, xw, att, H, C, slope, bias, want_alpha, trai
     if train2 and nd:
         agg2 = torch.empty((graph.n_dst, H * C), dtype=torch.float32, device=dev)
         s2 = torch.empty((graph.n_dst, H), dtype=torch.float32, device=dev)
-        agg = torch.empty_like(out) if bias is not None else out
         sb = lib.mp_gat_train_slab_bytes(g, H, C)
         slab = torch.empty(sb, dtype=torch.uint8, device=dev)
         _lib.check(lib.mp_gat_forward_train_f32(g, xw.data_ptr(), att_c.data_ptr(), H, C, float(slope), _lib.ptr(bias),
-                                                out.data_ptr(), out.stride(0),
-                                                agg.data_ptr() if bias is not None else None, stats.data_ptr(),
+                                                out.data_ptr(), out.stride(0), None, stats.data_ptr(),
                                                 agg2.data_ptr(), s2.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(),
                                                 slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st), "mp_gat_forward_train_f32")
-        extra = (agg2, s2, agg)
+        extra = (agg2, s2)
     elif train2:
         agg2 = torch.empty((graph.n_dst, H * C), dtype=torch.float32, device=dev)
         s2 = torch.empty((graph.n_dst, H), dtype=torch.float32, device=dev)
-        agg = torch.empty_like(out) if bias is not None else out
         sb = lib.mp_gat_train_slab_bytes(g, H, C)
         slab = torch.empty(sb, dtype=torch.uint8, device=dev)
         if drop is not None:
             _lib.check(lib.mp_gat_aggregate_train_drop_f32(g, xw.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(),
                                                            att_c.data_ptr(), H, C, float(slope), _lib.ptr(bias),
-                                                           out.data_ptr(), out.stride(0),
-                                                           agg.data_ptr() if bias is not None else None,
+                                                           out.data_ptr(), out.stride(0), None,
                                                            stats.data_ptr(), agg2.data_ptr(), s2.data_ptr(),
                                                            int(drop[0]), float(drop[1]), slab.data_ptr(), sb,
                                                            _lib.MP_STAGE_ALL, st), "mp_gat_aggregate_train_drop_f32")
         else:
             _lib.check(lib.mp_gat_aggregate_train_f32(g, xw.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(),
                                                       att_c.data_ptr(), H, C, float(slope), _lib.ptr(bias),
-                                                      out.data_ptr(), out.stride(0),
-                                                      agg.data_ptr() if bias is not None else None, stats.data_ptr(),
+                                                      out.data_ptr(), out.stride(0), None, stats.data_ptr(),
                                                       agg2.data_ptr(), s2.data_ptr(), slab.data_ptr(), sb,
                                                       _lib.MP_STAGE_ALL, st), "mp_gat_aggregate_train_f32")
-        extra = (agg2, s2, agg)
+        extra = (agg2, s2)
     if extra is None:
         sb = lib.mp_gat_slab_bytes(g, H, C)
         slab = torch.empty(sb, dtype=torch.uint8, device=dev)
@@ -791,13 +787,14 @@ def _gat_bwd_fused_ok(C):
     return (C % 4 == 0 and pow2(C // 4)) or pow2(C)
 
 
-def _gat_backward_wide(graph, g, xw, att, a_src, a_dst, stats, agg, extra, H, C, slope, want_att, want_bias,
-                       drop=None):
+def _gat_backward_wide(graph, g, xw, att, a_src, a_dst, stats, agg, agg_bias, extra, H, C, slope, want_att,
+                       want_bias, drop=None):
     """GATConv backward for heads of any width (C % 4 == 0), after the training
     forward: prep (pack + node-wise d a_dst), one pass over the transposed CSR
     with no per-slot dot product (mp_gat_backward_wide_f32: sum alpha g_i,
     sum lk alpha g_i, sum lk alpha rs_i per source row), then the node-wise
-    epilogue (d a_src = <acc2, xw> - sc, the att terms of d xw).
+    epilogue (d a_src = <acc2, xw> - sc, the att terms of d xw).  agg: the
+    forward's output, agg_bias the bias inside it (None: none).
     Returns (d xw, d att or None, d bias or None)."""
     lib = _lib.load()
     dev = xw.device
@@ -814,9 +811,10 @@ def _gat_backward_wide(graph, g, xw, att, a_src, a_dst, stats, agg, extra, H, C,
     ga_dst = (torch.empty if n_dst == N else torch.zeros)((N, H), dtype=torch.float32, device=dev)
     if n_dst:
         _lib.check(lib.mp_gat_backward_prep_wide_f32(g.data_ptr(), g.stride(0), agg.data_ptr(), agg.stride(0),
-                                                     agg2.data_ptr(), s2.data_ptr(), a_dst.data_ptr(),
-                                                     stats.data_ptr(), n_dst, H, C, pack.data_ptr(), _lib.nbytes(pack),
-                                                     ga_dst.data_ptr(), st), "mp_gat_backward_prep_wide_f32")
+                                                     _lib.ptr(agg_bias), agg2.data_ptr(), s2.data_ptr(),
+                                                     a_dst.data_ptr(), stats.data_ptr(), n_dst, H, C, pack.data_ptr(),
+                                                     _lib.nbytes(pack), ga_dst.data_ptr(), st),
+                   "mp_gat_backward_prep_wide_f32")
     src = graph.src_with_dst_slots()
     gs = src.struct("dst_slot")
     gx = torch.empty((N, F), dtype=torch.float32, device=dev)
@@ -853,12 +851,13 @@ def _att_part_blocks(n_rows, n_dst):
     return int(_lib.load().mp_gat_bwd_blocks(n_rows))
 
 
-def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope, want_att, want_bias,
+def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, agg_bias, H, C, slope, want_att, want_bias,
                         extra=None, drop=None):
     """GATConv backward: prep (packed destination terms + bias-grad partials),
     one gather pass over the transposed CSR (mp_gat_backward_f32), the d a_dst
     row sums over the dst CSR (reading the per-edge d score through the
-    src-slot map), and the epilogue (att_dst term + att-grad partials).
+    src-slot map), and the epilogue (att_dst term + att-grad partials).  agg:
+    the forward's output, agg_bias the bias inside it (None: none).
     Returns (d xw, d att or None, d bias or None)."""
     lib = _lib.load()
     dev = xw.device
@@ -881,15 +880,17 @@ def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope
         ga_dst = (torch.empty if n_dst == N else torch.zeros)((N, H), dtype=torch.float32, device=dev)
         if n_dst:
             _lib.check(lib.mp_gat_backward_prep_train_f32(g.data_ptr(), g.stride(0), agg.data_ptr(), agg.stride(0),
-                                                          agg2.data_ptr(), s2.data_ptr(), a_dst.data_ptr(),
-                                                          stats.data_ptr(), n_dst, H, C, pack.data_ptr(),
+                                                          _lib.ptr(agg_bias), agg2.data_ptr(), s2.data_ptr(),
+                                                          a_dst.data_ptr(), stats.data_ptr(), n_dst, H, C,
+                                                          pack.data_ptr(),
                                                           _lib.nbytes(pack), _lib.ptr(gpart), _lib.nbytes(gpart),
                                                           ga_dst.data_ptr(), st),
                        "mp_gat_backward_prep_train_f32")
     elif n_dst:
         _lib.check(lib.mp_gat_backward_prep_f32(g.data_ptr(), g.stride(0), agg.data_ptr(), agg.stride(0),
-                                                a_dst.data_ptr(), stats.data_ptr(), n_dst, H, C, pack.data_ptr(),
-                                                _lib.nbytes(pack), _lib.ptr(gpart), _lib.nbytes(gpart), st),
+                                                _lib.ptr(agg_bias), a_dst.data_ptr(), stats.data_ptr(), n_dst, H, C,
+                                                pack.data_ptr(), _lib.nbytes(pack), _lib.ptr(gpart), _lib.nbytes(gpart),
+                                                st),
                    "mp_gat_backward_prep_f32")
     gb = None
     if want_bias:
@@ -960,33 +961,25 @@ class _GatPropagate(torch.autograd.Function):
         # or without a backward to follow (training mode under no_grad)
         wide = not _gat_bwd_fused_ok(C) and gat_wide_ok(H, C)
         fused = (train or drop is not None) and (_gat_bwd_fused_ok(C) or wide)
-        # the fused backward needs the pre-bias aggregate (rs_i = <g_i, agg_i>):
-        # the training forward writes it next to the output; otherwise the
-        # bias is added here
+        # the fused backward's rs_i = <g_i, agg_i> comes from the saved output
+        # (agg + bias, bias fused into the forward) and the bias: the prologue
+        # takes rs over out - bias, so no pre-bias copy is written (ABI 6).  The
+        # output is saved, so an in-place change of it before backward raises
+        # torch's usual "modified by an inplace operation" error.
         train2 = fused and _gat_train_fwd_ok(graph, xw, H, C)
         if wide and fused and not train2:
             fused = False  # the wide backward needs the training forward's extras
         if drop is not None and not train2:
             raise ValueError("mi355_mp: fused attention dropout needs the training forward (gat_dropout_ok)")
-        out, alpha, a_src, a_dst, stats, extra = _gat_forward(graph, edge_index, xw, att, H, C, slope,
-                                                              bias if (train2 or not fused) else None, want_alpha,
-                                                              train2=train2, drop=drop)
-        agg = None
-        if train2:
-            agg = extra[2]
-            extra = extra[:2]
-            if bias is None:
-                out = agg.clone()
-        elif fused:
-            agg = out
-            out = agg + bias if bias is not None else agg.clone()
+        out, alpha, a_src, a_dst, stats, extra = _gat_forward(graph, edge_index, xw, att, H, C, slope, bias,
+                                                              want_alpha, train2=train2, drop=drop)
         ctx.graph, ctx.H, ctx.C, ctx.slope, ctx.drop = graph, H, C, slope, drop
         ctx.wide = wide
         ctx.has_bias = bias is not None
         ctx.fused = fused
         ctx.has_extra = extra is not None
-        ctx.save_for_backward(xw, att, edge_index, a_src, a_dst, stats, agg,
-                              *(extra if extra is not None else ()))
+        ctx.save_for_backward(xw, att, edge_index, a_src, a_dst, stats, out if fused else None,
+                              bias if fused else None, *(extra if extra is not None else ()))
         if alpha is not None:
             ctx.mark_non_differentiable(alpha)
         return out, alpha
@@ -1001,8 +994,8 @@ class _GatPropagate(torch.autograd.Function):
           dxw   += d a_src (x) att_src + d a_dst (x) att_dst;  d att = sum_n d a (x) xw
         Only [E, H]-sized arrays are materialised, never [E, H*C]."""
         lib = _lib.load()
-        xw, att, edge_index, a_src, a_dst, stats, agg = ctx.saved_tensors[:7]
-        extra = tuple(ctx.saved_tensors[7:9]) if ctx.has_extra else None
+        xw, att, edge_index, a_src, a_dst, stats, agg, agg_bias = ctx.saved_tensors[:8]
+        extra = tuple(ctx.saved_tensors[8:10]) if ctx.has_extra else None
         graph, H, C, slope = ctx.graph, ctx.H, ctx.C, ctx.slope
         dev = xw.device
         st = _lib.stream_ptr(dev)
@@ -1011,12 +1004,12 @@ class _GatPropagate(torch.autograd.Function):
             g = g.clone()  # a view at an odd offset: the 4-wide transposed pass (the dropout form has no other) needs 16-B rows
         N = xw.shape[0]
         if ctx.fused and ctx.wide:
-            gx, gatt, gb = _gat_backward_wide(graph, g, xw, att, a_src, a_dst, stats, agg, extra, H, C, slope,
-                                              ctx.needs_input_grad[1], ctx.has_bias and ctx.needs_input_grad[2],
+            gx, gatt, gb = _gat_backward_wide(graph, g, xw, att, a_src, a_dst, stats, agg, agg_bias, extra, H, C,
+                                              slope, ctx.needs_input_grad[1], ctx.has_bias and ctx.needs_input_grad[2],
                                               ctx.drop)
             return gx, gatt, gb, None, None, None, None, None, None, None, None
         if ctx.fused:
-            gx, gatt, gb = _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, H, C, slope,
+            gx, gatt, gb = _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, agg_bias, H, C, slope,
                                                ctx.needs_input_grad[1], ctx.has_bias and ctx.needs_input_grad[2],
                                                extra, ctx.drop)
             return gx, gatt, gb, None, None, None, None, None, None, None, None
@@ -1082,6 +1075,7 @@ def dropout_seed(device):
     generator without offsets, a host counter per (device, seed) replaces the
     offset (the captured replay reuses the captured key, as any captured
     constant)."""
+    device = torch.device(device)
     idx = device.index if device.index is not None else torch.cuda.current_device()
     gen = torch.cuda.default_generators[idx]
     base = gen.initial_seed()

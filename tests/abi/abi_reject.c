@@ -85,18 +85,18 @@ static void extents_gat_backward(void) {
 
   /* prep (inference forward) and prep_train: pack [n, H, 4], gsum_part [blocks(n), F] */
   const size_t pack = (size_t)n * H * 16, gsum = (size_t)mp_gat_bwd_blocks(n) * F * 4;
-  REJECT("pack", mp_gat_backward_prep_f32(DEVF, F, DEVF, F, DEVF, DEVF, n, H, C, DEVF, pack - 1, DEVF, gsum, NULL));
-  REJECT("gsum_part", mp_gat_backward_prep_f32(DEVF, F, DEVF, F, DEVF, DEVF, n, H, C, DEVF, pack, DEVF, gsum - 4,
+  REJECT("pack", mp_gat_backward_prep_f32(DEVF, F, DEVF, F, NULL, DEVF, DEVF, n, H, C, DEVF, pack - 1, DEVF, gsum, NULL));
+  REJECT("gsum_part", mp_gat_backward_prep_f32(DEVF, F, DEVF, F, NULL, DEVF, DEVF, n, H, C, DEVF, pack, DEVF, gsum - 4,
                                                NULL));
-  ACCEPT(mp_gat_backward_prep_f32(DEVF, F, DEVF, F, DEVF, DEVF, n, H, C, DEVF, pack, DEVF, gsum, NULL));
-  ACCEPT(mp_gat_backward_prep_f32(DEVF, F, DEVF, F, DEVF, DEVF, n, H, C, DEVF, pack, NULL, 0, NULL));
-  REJECT("pack", mp_gat_backward_prep_train_f32(DEVF, F, DEVF, F, DEVF, DEVF, DEVF, DEVF, n, H, C, DEVF, pack - 16,
+  ACCEPT(mp_gat_backward_prep_f32(DEVF, F, DEVF, F, NULL, DEVF, DEVF, n, H, C, DEVF, pack, DEVF, gsum, NULL));
+  ACCEPT(mp_gat_backward_prep_f32(DEVF, F, DEVF, F, NULL, DEVF, DEVF, n, H, C, DEVF, pack, NULL, 0, NULL));
+  REJECT("pack", mp_gat_backward_prep_train_f32(DEVF, F, DEVF, F, NULL, DEVF, DEVF, DEVF, DEVF, n, H, C, DEVF, pack - 16,
                                                 DEVF, gsum, DEVF, NULL));
-  REJECT("gsum_part", mp_gat_backward_prep_train_f32(DEVF, F, DEVF, F, DEVF, DEVF, DEVF, DEVF, n, H, C, DEVF, pack,
+  REJECT("gsum_part", mp_gat_backward_prep_train_f32(DEVF, F, DEVF, F, NULL, DEVF, DEVF, DEVF, DEVF, n, H, C, DEVF, pack,
                                                      DEVF, mp_gat_bwd_blocks(n_own) * (size_t)F * 4, DEVF, NULL));
-  ACCEPT(mp_gat_backward_prep_train_f32(DEVF, F, DEVF, F, DEVF, DEVF, DEVF, DEVF, n, H, C, DEVF, pack, DEVF, gsum,
+  ACCEPT(mp_gat_backward_prep_train_f32(DEVF, F, DEVF, F, NULL, DEVF, DEVF, DEVF, DEVF, n, H, C, DEVF, pack, DEVF, gsum,
                                         DEVF, NULL));
-  REJECT("null", mp_gat_backward_prep_train_f32(DEVF, F, DEVF, F, DEVF, DEVF, DEVF, DEVF, n, H, C, DEVF, pack, DEVF,
+  REJECT("null", mp_gat_backward_prep_train_f32(DEVF, F, DEVF, F, NULL, DEVF, DEVF, DEVF, DEVF, n, H, C, DEVF, pack, DEVF,
                                                 gsum, NULL, NULL));
 
   /* column sums: part [blocks(n), F] */
@@ -126,9 +126,9 @@ static void extents_gat_backward(void) {
   const int Cw = 36, Fw = H * Cw;
   const size_t wslab = mp_gat_train_slab_bytes(&gt, H, Cw);
   const size_t acc2 = (size_t)gt.n_rows * Fw * 4, sc = (size_t)gt.n_rows * H * 4;
-  REJECT("pack", mp_gat_backward_prep_wide_f32(DEVF, Fw, DEVF, Fw, DEVF, DEVF, DEVF, DEVF, n, H, Cw, DEVF,
+  REJECT("pack", mp_gat_backward_prep_wide_f32(DEVF, Fw, DEVF, Fw, NULL, DEVF, DEVF, DEVF, DEVF, n, H, Cw, DEVF,
                                                (size_t)n_own * H * 16, DEVF, NULL));
-  ACCEPT(mp_gat_backward_prep_wide_f32(DEVF, Fw, DEVF, Fw, DEVF, DEVF, DEVF, DEVF, n, H, Cw, DEVF, (size_t)n * H * 16,
+  ACCEPT(mp_gat_backward_prep_wide_f32(DEVF, Fw, DEVF, Fw, NULL, DEVF, DEVF, DEVF, DEVF, n, H, Cw, DEVF, (size_t)n * H * 16,
                                        DEVF, NULL));
   REJECT("acc2", mp_gat_backward_wide_f32(&gt, DEVF, Fw, DEVF, DEVF, H, Cw, 0.2f, 0, 0.f, DEVF, DEVF, acc2 - 4, DEVF,
                                           sc, DEV, wslab, 7, NULL));
@@ -221,8 +221,13 @@ static void workspaces(void) {
                                       NULL));
   REJECT("slab", mp_gat_aggregate_train_f32(&g, DEVF, DEVF, DEVF, DEVF, H, C, 0.2f, NULL, DEVF, F, NULL, DEVF, DEVF,
                                             DEVF, DEV, gs, 7, NULL));
-  REJECT("agg", mp_gat_aggregate_train_f32(&g, DEVF, DEVF, DEVF, DEVF, H, C, 0.2f, DEVF, DEVF, F, NULL, DEVF, DEVF,
-                                           DEVF, DEV, ts, 7, NULL));
+  /* ABI 6: a bias no longer needs the pre-bias copy (the backward takes out - bias) */
+  ACCEPT(mp_gat_aggregate_train_f32(&g, DEVF, DEVF, DEVF, DEVF, H, C, 0.2f, DEVF, DEVF, F, NULL, DEVF, DEVF, DEVF,
+                                    DEV, ts, 7, NULL));
+  REJECT("16-byte", mp_gat_aggregate_train_f32(&g, DEVF, DEVF, DEVF, DEVF, H, C, 0.2f, (float*)((char*)DEV + 4), DEVF,
+                                               F, NULL, DEVF, DEVF, DEVF, DEV, ts, 7, NULL));
+  REJECT("bias", mp_gat_backward_prep_train_f32(DEVF, F, DEVF, F, (float*)((char*)DEV + 8), DEVF, DEVF, DEVF, DEVF,
+                                                N, H, C, DEVF, (size_t)N * H * 16, NULL, 0, DEVF, NULL));
   ACCEPT(mp_gat_aggregate_train_f32(&g, DEVF, DEVF, DEVF, DEVF, H, C, 0.2f, DEVF, DEVF, F, DEVF, DEVF, DEVF, DEVF,
                                     DEV, ts, 7, NULL));
   REJECT("null", mp_gat_forward_train_f32(&g, DEVF, DEVF, H, C, 0.2f, NULL, DEVF, F, NULL, DEVF, DEVF, DEVF, NULL,
@@ -261,6 +266,15 @@ static void null_pointers(void) {
   REJECT("null", mp_segment_ids_i64(NULL, n, DEVL, 3, NULL));
   REJECT("null", mp_gat_dropout_keep(1, 0.5f, 8, E, NULL, NULL));
   REJECT("dropout p", mp_gat_dropout_keep(1, 1.0f, 8, E, DEVU, NULL));
+  REJECT("C % 4", mp_gat_merge_partials_f32(n, 8, 30, DEVI, DEVI, 10, DEVF, 256, DEVF, NULL, DEVF, 256, DEVF, NULL,
+                                            NULL, NULL));
+  REJECT("null", mp_gat_merge_partials_f32(n, 8, 32, DEVI, NULL, 10, DEVF, 256, DEVF, NULL, DEVF, 256, DEVF, NULL,
+                                           NULL, NULL));
+  REJECT("leading dimension", mp_gat_merge_partials_f32(n, 8, 32, DEVI, DEVI, 10, DEVF, 255, DEVF, NULL, DEVF, 256,
+                                                        DEVF, NULL, NULL, NULL));
+  REJECT("16-byte", mp_gat_merge_partials_f32(n, 8, 32, DEVI, DEVI, 10, DEVF, 256, DEVF, (float*)((char*)DEV + 4),
+                                              DEVF, 256, DEVF, NULL, NULL, NULL));
+  ACCEPT(mp_gat_merge_partials_f32(n, 8, 32, DEVI, NULL, 0, NULL, 0, NULL, NULL, DEVF, 256, DEVF, NULL, NULL, NULL));
   REJECT("bad argument", mp_heads_outer_add_f32(DEVF, 256, NULL, n, 8, 32, DEVF, 64, NULL));
   REJECT("bad argument", mp_gat_alpha_f32(DEVL, NULL, E, 8, DEVF, DEVF, 0.2f, DEVF, DEVF, NULL));
   REJECT("bad arguments", mp_self_loop_count(NULL, DEVL, E, n, DEVL, NULL));

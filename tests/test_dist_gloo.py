@@ -492,3 +492,93 @@ def test_allreduce_gradients_keeps_unused_parameters_gradless(world):
         assert only0 == [3.0, 3.0]
         assert b == [5.0 * world] * 2
         assert w == [[5.0 * s] * 3] * 2
+
+
+def _gat_cover_worker(rank, world, port, result_q, from_slices, cuts):
+    """Sharded GATConv over the hybrid halo cover (mi355_mp.gat_cover) on the
+    CPU in float64: the host form of the distributed algorithm (a_dst requests,
+    pushed online-softmax pieces, the merge; autograd through a differentiable
+    all_to_all) against the single-process oracle, forward rows and every
+    gradient; the cover ships no more rows than the pull plan."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "pytorch_geometric-1_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mi355_mp import dist as mdist
+        from mi355_mp.graphgen import powerlaw_edge_index
+        from oracle import pyg_ref as P
+        torch.set_default_dtype(torch.float64)
+        N, E, Fi = 700, 9000, 6
+        ei = powerlaw_edge_index(N, E, seed=67)
+        g = torch.Generator().manual_seed(67)
+        # hub destinations and hub sources: rows both pushed and pulled
+        ei = torch.cat([ei, torch.stack([torch.randint(0, N, (600,), generator=g), torch.full((600,), 5)]),
+                        torch.stack([torch.full((400,), 650), torch.randint(0, N, (400,), generator=g)])], 1)
+        ei = ei[:, torch.randperm(ei.shape[1], generator=g)]
+        E = ei.shape[1]
+        x = torch.randn(N, Fi, generator=g)
+        res = {}
+        for H, C, concat in ((3, 4, True), (2, 8, False), (1, 6, True)):
+            conv = mdist.ShardedGATConv(Fi, C, heads=H, concat=concat)
+            with torch.no_grad():
+                conv.bias.normal_(generator=g)
+                conv.att.mul_(3.0)          # sharper softmax: the pieces' maxima differ
+            mdist.broadcast_parameters(conv)
+            W, att, b = conv.weight.detach(), conv.att.detach(), conv.bias.detach()
+            if from_slices:
+                s0, s1 = rank * E // world, (rank + 1) * E // world
+                sg = mdist.ShardedGraph.for_gat_from_slices(ei[:, s0:s1].clone(), s0, N, rank, world)
+            else:
+                sg = mdist.ShardedGraph.for_gat(ei, N, rank, world, cuts=cuts)
+            pull_rows = sg.fwd.n_local_src - sg.n_own
+            sg.enable_gat_halo_cover()
+            st = sg.gat_cover.stats()
+            lo, hi = sg.lo, sg.hi
+            Fo = H * C if concat else C
+            gout = torch.randn(N, Fo, generator=g)
+            xo = x[lo:hi].clone().requires_grad_(True)
+            out = conv(xo, sg)
+            (out * gout[lo:hi]).sum().backward()
+            mdist.allreduce_gradients(conv)
+            xr = x.clone().requires_grad_(True)
+            Wr, attr, br = (t.clone().requires_grad_(True) for t in (W, att, b))
+            want = P.gat_conv(xr, ei, Wr, attr, br, H, C, concat=concat)
+            (want * gout).sum().backward()
+            tol = 1e-10
+            r = {"out": float(((out.detach() - want.detach()[lo:hi]).abs()
+                               - tol * want.detach()[lo:hi].abs().clamp(min=1.0)).max()) if hi > lo else -1.0,
+                 "gx": float(((xo.grad - xr.grad[lo:hi]).abs() - tol * xr.grad[lo:hi].abs().clamp(min=1.0)).max())
+                 if hi > lo else -1.0,
+                 "halo_rows": st["halo_rows"], "pull_rows": pull_rows, "pushed": st["cover_partial_rows"]}
+            for k, a, rr in (("gw", conv.weight.grad, Wr.grad), ("gatt", conv.att.grad, attr.grad),
+                             ("gb", conv.bias.grad, br.grad)):
+                r[k] = float((a - rr).abs().max() - tol * rr.abs().max())
+            res[(H, C, concat)] = r
+        result_q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,from_slices,cuts", [(1, False, None), (2, False, None), (3, True, None),
+                                                     (3, False, [0, 0, 350, 700]), (4, False, None)])
+def test_sharded_gat_over_halo_cover_matches_single_process(world, from_slices, cuts):
+    """GAT over the hybrid cover, float64 on the CPU: every rank's rows and the
+    all-reduced d W / d att / d b, and d x of its rows, within 1e-10 of the
+    single-process oracle (pieces merge exactly up to rounding); ranks that own
+    no rows take part; pieces are pushed (the cover is not the pull plan) and
+    the halo is never larger than the pull plan's."""
+    res = run_ranks(_gat_cover_worker, world, timeout=300, args=(from_slices, cuts))
+    pushed = 0
+    for rank, r in res:
+        for key, v in r.items():
+            for k in ("out", "gx", "gw", "gatt", "gb"):
+                assert v[k] <= 0, (rank, key, k, v)
+            assert v["halo_rows"] <= v["pull_rows"], (rank, key, v)
+            pushed += v["pushed"]
+    if world > 1:
+        assert pushed > 0, res

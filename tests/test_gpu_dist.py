@@ -1185,3 +1185,119 @@ def test_sharded_layers_fuzz_random_cuts_on_one_gpu():
                 assert r["exact"], (rank, r)
             else:
                 assert r["out"] < 1e-5 and r["gx"] < 1e-5 and r["gparams"] < 1e-5, (rank, r)
+
+
+def _dyadic_(t, gen, scale):
+    """Fill t with small integers / scale: products of two such values and
+    their sums of a few hundred terms are exact in fp32, so X W is the same bit
+    for bit whatever GEMM kernel computes it (a rank's GEMM has M = n_own rows
+    and hipBLASLt picks its kernel by M).  Equal node scores on both sides keep
+    every leaky_relu branch equal: a score within rounding of 0 would otherwise
+    flip leaky' between 1 and the slope and move the gradient by a real amount."""
+    with torch.no_grad():
+        t.copy_(torch.randint(-4, 5, tuple(t.shape), generator=gen).to(t.dtype) / scale)
+    return t
+
+
+def _gat_cover_gpu_worker(rank, world, port, q, cut_sets):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "pytorch_geometric-1_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=_PG_TIMEOUT)
+    try:
+        from mi355_mp import dist as mdist
+        from mi355_mp.graph import GAT_TARGET_TASKS, Graph
+        from mi355_mp.graphgen import powerlaw_edge_index
+        from torch_geometric.nn import GATConv
+        from torch_geometric.nn.conv._structure import gat_loops
+        dev = torch.device("cuda", 0)
+        N, E, Fi = 2500, 40000, 48
+        gen = torch.Generator().manual_seed(83)
+        ei = powerlaw_edge_index(N, E, seed=83)
+        # a hub destination and a hub source: rows both pushed and pulled
+        ei = torch.cat([ei, torch.stack([torch.randint(0, N, (2000,), generator=gen), torch.full((2000,), 7)]),
+                        torch.stack([torch.full((1500,), N - 3), torch.randint(0, N, (1500,), generator=gen)])], 1)
+        ei = ei[:, torch.randperm(ei.shape[1], generator=gen)].to(dev)
+        E = ei.shape[1]
+        x = _dyadic_(torch.empty(N, Fi), gen, 4.0).to(dev)
+        res = {}
+        for ci, cuts in enumerate(cut_sets):
+            for H, C, concat in ((8, 32, True), (3, 8, False), (2, 4, True)):
+                Fo = H * C if concat else C
+                gout = torch.randn(N, Fo, generator=gen).to(dev)
+                ref = GATConv(Fi, C, heads=H, concat=concat).to(dev)
+                _dyadic_(ref.weight, gen, 16.0)
+                with torch.no_grad():
+                    ref.att.copy_(torch.randn(ref.att.shape, generator=gen) * 0.3)
+                    ref.bias.copy_(torch.randn(ref.bias.shape, generator=gen))
+                xr = x.clone().requires_grad_(True)
+                out_ref = ref(xr, ei)
+                (out_ref * gout).sum().backward()
+                if cuts is None:
+                    s0, s1 = rank * E // world, (rank + 1) * E // world
+                    sg = mdist.ShardedGraph.for_gat_from_slices(ei[:, s0:s1].clone(), s0, N, rank, world)
+                else:
+                    sg = mdist.ShardedGraph.for_gat(ei, N, rank, world, cuts=cuts)
+                pull_rows = sg.fwd.n_local_src - sg.n_own
+                sg.enable_gat_halo_cover()
+                conv = mdist.ShardedGATConv(Fi, C, heads=H, concat=concat).to(dev)
+                conv.load_state_dict(ref.state_dict())
+                lo, hi = sg.lo, sg.hi
+                xo = x[lo:hi].clone().requires_grad_(True)
+                out = conv(xo, sg)
+                (out * gout[lo:hi]).sum().backward()
+                mdist.allreduce_gradients(conv)
+                o, w = out.detach(), out_ref.detach()[lo:hi]
+                r = {"rows": hi - lo, "halo_rows": sg.gat_cover.n_halo, "pull_rows": pull_rows,
+                     "pieces": sg.gat_cover.n_push_rows,
+                     "out": float(((o - w).abs() - 1e-5 * w.abs().clamp(min=1.0)).max()) if hi > lo else -1.0,
+                     "gx": float((xo.grad - xr.grad[lo:hi]).abs().max() / xr.grad.abs().max()) if hi > lo else 0.0}
+                for k in ("weight", "att", "bias"):
+                    a, b = getattr(conv, k).grad, getattr(ref, k).grad
+                    r["g" + k] = float((a - b).abs().max() / b.abs().max())
+                if concat and hi > lo:
+                    # rows no peer pushes a piece of, whole on both schedules: the single-GPU
+                    # kernel's rows bit for bit (same edges, same order, same kernel)
+                    gl = sg.gat_cover.graphs()[0].dst
+                    ei_l = gat_loops(ei, N)
+                    g1 = Graph(ei_l, N, N, target_tasks=GAT_TARGET_TASKS).dst    # as GATConv builds it
+                    deg_l = (gl.rowptr[1:] - gl.rowptr[:-1]).long()
+                    deg_1 = (g1.rowptr[1:] - g1.rowptr[:-1]).long()[lo:hi]
+                    merged = torch.zeros(hi - lo, dtype=torch.bool, device=dev)
+                    merged[sg.gat_cover.part_dst] = True
+                    plain = (~merged) & (deg_l == deg_1) & (deg_l <= min(gl.snap, g1.snap))
+                    r["plain_rows"] = int(plain.sum())
+                    r["plain_bitwise"] = bool(torch.equal(o[plain], w[plain]))
+                res[(ci, H, C, concat)] = r
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_gatconv_over_halo_cover_on_one_gpu(world):
+    """ShardedGATConv over the hybrid halo cover (mi355_mp.gat_cover: pulled rows
+    + pushed online-softmax pieces, merged by mp_gat_merge_partials_f32; the
+    native backward returns g and the pack of every pushed row to its pusher):
+    forward rows, d x and the all-reduced d W / d att / d b against the
+    single-GPU GATConv -- slice-built shards, an empty rank, a one-row rank;
+    config 3's 8 x 32 heads, a mean of heads, C = 4.  Rows no peer pushes a
+    piece of are the single-GPU rows bit for bit; the cover never receives
+    more rows than the pull plan, and pieces are pushed."""
+    N = 2500
+    cut_sets = [None, [0, N, N] if world == 2 else [0, 0, N // 2, N], [0, 1, N] if world == 2 else [0, 1, N // 2, N]]
+    res = _spawn(_gat_cover_gpu_worker, world=world, args=(cut_sets,))
+    pieces = 0
+    for rank, r in res:
+        for key, v in r.items():
+            assert v["out"] <= 0 and v["gx"] < 1e-5, (rank, key, v)
+            assert v["gweight"] < 1e-5 and v["gatt"] < 1e-5 and v["gbias"] < 1e-5, (rank, key, v)
+            assert v["halo_rows"] <= v["pull_rows"], (rank, key, v)
+            if "plain_bitwise" in v:
+                assert v["plain_bitwise"], (rank, key, v)
+            pieces += v["pieces"]
+    assert pieces > 0

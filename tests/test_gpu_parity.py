@@ -1409,7 +1409,8 @@ def test_gat_training_forward_node_wise_d_a_dst(H, C, chunk, monkeypatch):
     agg_inf = ops._gat_forward(graph, ei_l.to(DEV), xw.to(DEV), att.to(DEV), H, C, 0.2, None, False)[0]
     assert extra is not None and none is None
     assert torch.equal(out, out_inf) and torch.equal(st_t, st_i)
-    assert torch.equal(extra[2], agg_inf)  # the pre-bias aggregate
+    assert len(extra) == 2       # ABI 6: no pre-bias copy; the backward takes rs over out - bias
+    assert torch.equal(out, agg_inf + bias)
     x_i = xw[ei_l[1]].view(-1, H, C)
     x_j = xw[ei_l[0]].view(-1, H, C)
     pre = (torch.cat([x_i, x_j], -1) * att).sum(-1)

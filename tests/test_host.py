@@ -119,14 +119,15 @@ def _extent_cases():
     return [
         ("mp_gat_backward_finish_f32", lambda b: (None, D, D, D, D, n, H, C, D, b, None),
          blocks * 2 * F * 4, "att_part"),
-        ("mp_gat_backward_prep_f32", lambda b: (D, F, D, F, D, D, n, H, C, D, b, None, 0, None), n * H * 16, "pack"),
-        ("mp_gat_backward_prep_f32", lambda b: (D, F, D, F, D, D, n, H, C, D, n * H * 16, D, b, None),
+        ("mp_gat_backward_prep_f32", lambda b: (D, F, D, F, None, D, D, n, H, C, D, b, None, 0, None), n * H * 16, "pack"),
+        ("mp_gat_backward_prep_f32", lambda b: (D, F, D, F, None, D, D, n, H, C, D, n * H * 16, D, b, None),
          blocks * F * 4, "gsum_part"),
-        ("mp_gat_backward_prep_train_f32", lambda b: (D, F, D, F, D, D, D, D, n, H, C, D, b, None, 0, D, None),
+        ("mp_gat_backward_prep_train_f32", lambda b: (D, F, D, F, None, D, D, D, D, n, H, C, D, b, None, 0, D, None),
          n * H * 16, "pack"),
-        ("mp_gat_backward_prep_train_f32", lambda b: (D, F, D, F, D, D, D, D, n, H, C, D, n * H * 16, D, b, D, None),
+        ("mp_gat_backward_prep_train_f32",
+         lambda b: (D, F, D, F, None, D, D, D, D, n, H, C, D, n * H * 16, D, b, D, None),
          blocks * F * 4, "gsum_part"),
-        ("mp_gat_backward_prep_wide_f32", lambda b: (D, Fw, D, Fw, D, D, D, D, n, H, Cw, D, b, D, None),
+        ("mp_gat_backward_prep_wide_f32", lambda b: (D, Fw, D, Fw, None, D, D, D, D, n, H, Cw, D, b, D, None),
          n * H * 16, "pack"),
         ("mp_col_sums_f32", lambda b: (D, F, n, F, D, b, None), blocks * F * 4, "part"),
         ("mp_gat_backward_f32", lambda b: (gt, D, F, D, D, D, D, H, C, 0.2, D, D, D, b, D, slab, 7, None),

@@ -1,0 +1,41 @@
+#!/bin/bash
+# One GPU-box session of the round's measurements; every step under its own
+# time limit, the session stops at the first failing step.  Outputs under
+# gpurun_out/ (copied into profiles/ as rNN_* when they are kept):
+#   STEPS="tests bench rccl gloo2 gat_gloo2 prof train" R=r05 bash tools/gpu_round.sh
+#   tests     pytest -m gpu                           -> $R_pytest_gpu.txt
+#   bench     python bench.py (the driver's N=1 line)  -> $R_bench_rmat21.json
+#   rccl      one RCCL rank, --sharded --emulate-peers 8,2 (RCCL beside the aggregation),
+#             rocprofv3 kernel trace of the same command -> $R_bench_sharded_rccl_one_rank.json,
+#             $R_rccl_kernel_trace/ (+ tools/kernel_overlap.py summary)
+#   gloo2     bench.py --gpus 2, gloo ranks sharing the GPU (--verify) -> $R_bench_rmat21_gloo2_rehearsal.json
+#   gat_gloo2 the same for --workload gat                -> $R_bench_gat_gloo2_rehearsal.json
+#   prof      tools/profile.sh (kernel trace + PMC of the default bench)
+#   train     kernel trace of the GCNConv / GATConv layer training steps (tools/bench_configs.py)
+set -u
+export TMPDIR=/tmp
+R=${R:-r05}
+O=gpurun_out
+mkdir -p $O
+run() {  # name seconds cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name $(date +%T)"
+  timeout -k 10 "$t" "$@"
+  local rc=$?
+  echo "== $name rc=$rc $(date +%T)"
+  if [ $rc -ne 0 ]; then exit $rc; fi
+}
+for s in ${STEPS:-tests bench}; do
+  case $s in
+    tests) run tests 900 bash -c "python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/${R}_pytest_gpu.txt 2>&1"; tail -3 $O/${R}_pytest_gpu.txt ;;
+    bench) run bench 400 bash -c "python bench.py > $O/${R}_bench_rmat21.json 2> $O/${R}_bench_rmat21.err"; cut -c1-400 $O/${R}_bench_rmat21.json ;;
+    rccl) run rccl 500 bash -c "python bench.py --sharded --emulate-peers 8,2 --steps 10 --warmup 3 --verify > $O/${R}_bench_sharded_rccl_one_rank.json 2> $O/${R}_bench_sharded_rccl_one_rank.err"
+          run rccl_trace 500 rocprofv3 --kernel-trace --stats -d $O/${R}_rccl_kt -o kt --output-format csv -- python3 bench.py --sharded --emulate-peers 8,2 --steps 5 --warmup 2 --no-cpu-baseline --no-ref-paths --no-build-split
+          python3 tools/kernel_overlap.py $O/${R}_rccl_kt > $O/${R}_rccl_kernel_overlap.json; cat $O/${R}_rccl_kernel_overlap.json | head -40 ;;
+    gloo2) run gloo2 600 bash -c "MP_BENCH_BACKEND=gloo python bench.py --gpus 2 --steps 3 --warmup 1 --verify > $O/${R}_bench_rmat21_gloo2_rehearsal.json 2> $O/${R}_bench_rmat21_gloo2_rehearsal.err"; cut -c1-300 $O/${R}_bench_rmat21_gloo2_rehearsal.json ;;
+    gat_gloo2) run gat_gloo2 600 bash -c "MP_BENCH_BACKEND=gloo python bench.py --gpus 2 --workload gat --steps 3 --warmup 1 --verify > $O/${R}_bench_gat_gloo2_rehearsal.json 2> $O/${R}_bench_gat_gloo2_rehearsal.err"; cut -c1-300 $O/${R}_bench_gat_gloo2_rehearsal.json ;;
+    prof) PROF_OUT=$O/${R}_prof run prof 1100 bash tools/profile.sh ;;
+    train) run train 500 rocprofv3 --kernel-trace --stats -d $O/${R}_train_kt -o kt --output-format csv -- python3 tools/bench_configs.py --configs c2train,c3train ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
