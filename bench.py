@@ -821,15 +821,23 @@ class BuildMeter:
             self.res[name] = {"wall_s": time.perf_counter() - t0}
             return out
         from torch.profiler import ProfilerActivity, profile
+        prof = profile(activities=[ProfilerActivity.CUDA])
+        try:
+            prof.start()
+        except Exception as ex:  # pragma: no cover - a profiler that cannot start: wall time only
+            out = fn()
+            torch.cuda.synchronize()
+            self.res[name] = {"wall_s": time.perf_counter() - t0, "note": "profiler did not start: %s" % ex}
+            return out
         with warnings.catch_warnings(record=True) as caught:
             warnings.simplefilter("always")
             torch.cuda.set_sync_debug_mode("warn")
             try:
-                with profile(activities=[ProfilerActivity.CUDA]) as prof:
-                    out = fn()
-                    torch.cuda.synchronize()
+                out = fn()
+                torch.cuda.synchronize()
             finally:
                 torch.cuda.set_sync_debug_mode("default")
+                prof.stop()
         wall = time.perf_counter() - t0
         syncs = sum(1 for w in caught if "synchroniz" in str(w.message).lower())
         spans = []

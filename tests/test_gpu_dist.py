@@ -231,7 +231,8 @@ def _gat_layer_worker(rank, world, port, q):
         N, E, Fi = 3000, 60000, 64
         ei = powerlaw_edge_index(N, E, seed=47).to(dev)
         gen = torch.Generator().manual_seed(47)
-        x = torch.randn(N, Fi, generator=gen).to(dev)
+        # dyadic x and W: X W exact whatever GEMM kernel the rank's M picks (_dyadic_)
+        x = _dyadic_(torch.empty(N, Fi), gen, 4.0).to(dev)
         res = {}
         # (heads, out_channels, concat): config 3's shape, the reference's heads=1 stacks
         # (ConvexPruning.py:209-214, a wide head), a padded width, and ppi's mean head
@@ -239,8 +240,10 @@ def _gat_layer_worker(rank, world, port, q):
             Fo = H * C if concat else C
             gout = torch.randn(N, Fo, generator=gen).to(dev)
             ref = GATConv(Fi, C, heads=H, concat=concat).to(dev)
+            _dyadic_(ref.weight, gen, 16.0)
             with torch.no_grad():
-                ref.bias.normal_()
+                ref.att.copy_(torch.randn(ref.att.shape, generator=gen) * 0.3)
+                ref.bias.copy_(torch.randn(ref.bias.shape, generator=gen))
             mdist.broadcast_parameters(ref)
             xr = x.clone().requires_grad_(True)
             out_ref = ref(xr, ei)
@@ -352,14 +355,16 @@ def _gat_uneven_worker(rank, world, port, q):
         N, Fi, H, C = 1500, 24, 4, 16
         ei = powerlaw_edge_index(N, 20000, seed=71).to(dev)
         gen = torch.Generator().manual_seed(71)
-        x = torch.randn(N, Fi, generator=gen).to(dev)
+        x = _dyadic_(torch.empty(N, Fi), gen, 4.0).to(dev)       # X W exact on both sides (_dyadic_)
         gout = torch.randn(N, H * C, generator=gen).to(dev)
         res = {}
         # an empty rank (cuts [0, N, N]) and a rank holding a single row
         for name, cuts in (("empty_rank", [0, N, N]), ("one_row", [0, 1, N])):
             ref = GATConv(Fi, C, heads=H).to(dev)
+            _dyadic_(ref.weight, gen, 16.0)
             with torch.no_grad():
-                ref.bias.normal_()
+                ref.att.copy_(torch.randn(ref.att.shape, generator=gen) * 0.3)
+                ref.bias.copy_(torch.randn(ref.bias.shape, generator=gen))
             mdist.broadcast_parameters(ref)
             xr = x.clone().requires_grad_(True)
             out_ref = ref(xr, ei)
@@ -1123,7 +1128,7 @@ def _sharded_fuzz_worker(rank, world, port, q, seeds):
             cuts = [0] + inner + [N]                    # random ranges, empty ones included
             Fi = int(torch.randint(1, 40, (1,), generator=g))
             x = torch.randn(N, Fi, generator=g).to(dev)
-            kind = ["gcn", "gcn_cover", "gat", "max"][seed % 4]
+            kind = ["gcn", "gcn_cover", "gat", "max", "gat_cover"][seed % 5]
             r = {"seed": seed, "kind": kind, "N": N, "E": E, "cuts": cuts}
             torch.manual_seed(seed)
             if kind in ("gcn", "gcn_cover"):
@@ -1132,10 +1137,16 @@ def _sharded_fuzz_worker(rank, world, port, q, seeds):
                 if kind == "gcn_cover":
                     sg.enable_halo_cover()
                 conv = mdist.ShardedGCNConv(Fi, 24).to(dev)
-            elif kind == "gat":
+            elif kind in ("gat", "gat_cover"):
                 H = int(torch.randint(1, 5, (1,), generator=g))
                 ref = GATConv(Fi, 8, heads=H).to(dev)
+                if kind == "gat_cover":
+                    # dyadic x and W: X W exact on both sides, so no leaky_relu branch flips
+                    x = _dyadic_(torch.empty(N, Fi), g, 4.0).to(dev)
+                    _dyadic_(ref.weight, g, 16.0)
                 sg = mdist.ShardedGraph.for_gat(ei, N, rank, world, cuts=cuts)
+                if kind == "gat_cover":
+                    sg.enable_gat_halo_cover()
                 conv = mdist.ShardedGATConv(Fi, 8, heads=H).to(dev)
             if kind != "max":
                 with torch.no_grad():
@@ -1157,7 +1168,7 @@ def _sharded_fuzz_worker(rank, world, port, q, seeds):
                 r["gx"] = float((xo.grad - xr.grad[lo:hi]).abs().max()) / gs if hi > lo else 0.0
                 r["gparams"] = max(float((getattr(conv, k).grad - getattr(ref, k).grad).abs().max())
                                    / max(1.0, float(getattr(ref, k).grad.abs().max()))
-                                   for k in ("weight", "bias") + (("att",) if kind == "gat" else ()))
+                                   for k in ("weight", "bias") + (("att",) if kind.startswith("gat") else ()))
             else:
                 sgm = mdist.ShardedGraph(ei, N, rank, world, cuts=cuts)
                 om, am = sgm.propagate(x[sgm.lo:sgm.hi].contiguous(), "max")
@@ -1172,14 +1183,15 @@ def _sharded_fuzz_worker(rank, world, port, q, seeds):
 def test_sharded_layers_fuzz_random_cuts_on_one_gpu():
     """48 random graphs (hub-heavy sources, 0..12N edges, 1..2000 nodes) at 3
     ranks with random row ranges (empty ranks included): ShardedGCNConv over
-    the pull plan and over the halo cover, ShardedGATConv (1-4 heads), each
+    the pull plan and over the halo cover, ShardedGATConv (1-4 heads) over the
+    pull plan and over the GAT halo cover, each
     forward + backward within 1e-5 (relative to max(1, |ref|)) of the
     single-GPU layer with all-reduced parameter gradients; sharded max with
     global argmax ids bit-equal to the single-GPU kernel."""
     res = _spawn(_sharded_fuzz_worker, world=3, timeout=300, args=(list(range(100, 148)),))
     assert len(res) == 3
     for rank, rows in res:
-        assert len(rows) == 48 and {r["kind"] for r in rows} == {"gcn", "gcn_cover", "gat", "max"}
+        assert len(rows) == 48 and {r["kind"] for r in rows} == {"gcn", "gcn_cover", "gat", "max", "gat_cover"}
         for r in rows:
             if r["kind"] == "max":
                 assert r["exact"], (rank, r)

@@ -1,11 +1,11 @@
 """Diagnostic (round 5): sharded GATConv (3 gloo ranks sharing one GPU) vs the
 single-GPU GATConv vs a float64 CPU oracle, per seed; prints one JSON line per
-(seed, rank).  python tools/dbg/gat_shard_diag.py"""
+(seed, rank).  python tools/gat_shard_diag.py"""
 import json
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (ROOT, os.path.join(ROOT, "pytorch_geometric-1_amd")):
     if p not in sys.path:
         sys.path.insert(0, p)

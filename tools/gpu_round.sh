@@ -11,6 +11,7 @@
 #   gloo2     bench.py --gpus 2, gloo ranks sharing the GPU (--verify) -> $R_bench_rmat21_gloo2_rehearsal.json
 #   gat_gloo2 the same for --workload gat                -> $R_bench_gat_gloo2_rehearsal.json
 #   prof      tools/profile.sh (kernel trace + PMC of the default bench)
+#   diag      tools/gat_shard_diag.py (sharded vs single-GPU vs float64 GAT gradients, per seed)
 #   train     kernel trace of the GCNConv / GATConv layer training steps (tools/bench_configs.py)
 set -u
 export TMPDIR=/tmp
@@ -34,6 +35,7 @@ for s in ${STEPS:-tests bench}; do
           python3 tools/kernel_overlap.py $O/${R}_rccl_kt > $O/${R}_rccl_kernel_overlap.json; cat $O/${R}_rccl_kernel_overlap.json | head -40 ;;
     gloo2) run gloo2 600 bash -c "MP_BENCH_BACKEND=gloo python bench.py --gpus 2 --steps 3 --warmup 1 --verify > $O/${R}_bench_rmat21_gloo2_rehearsal.json 2> $O/${R}_bench_rmat21_gloo2_rehearsal.err"; cut -c1-300 $O/${R}_bench_rmat21_gloo2_rehearsal.json ;;
     gat_gloo2) run gat_gloo2 600 bash -c "MP_BENCH_BACKEND=gloo python bench.py --gpus 2 --workload gat --steps 3 --warmup 1 --verify > $O/${R}_bench_gat_gloo2_rehearsal.json 2> $O/${R}_bench_gat_gloo2_rehearsal.err"; cut -c1-300 $O/${R}_bench_gat_gloo2_rehearsal.json ;;
+    diag) run diag 500 bash -c "python tools/gat_shard_diag.py > $O/${R}_gat_shard_diag.jsonl 2> $O/${R}_gat_shard_diag.err"; cat $O/${R}_gat_shard_diag.jsonl ;;
     prof) PROF_OUT=$O/${R}_prof run prof 1100 bash tools/profile.sh ;;
     train) run train 500 rocprofv3 --kernel-trace --stats -d $O/${R}_train_kt -o kt --output-format csv -- python3 tools/bench_configs.py --configs c2train,c3train ;;
     *) echo "unknown step $s"; exit 2 ;;
