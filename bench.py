@@ -920,7 +920,10 @@ def rccl_contention(sg, P, bias, reps=10, rounds=3):
     split is a device-local copy).  Times (ms, median of `rounds` x `reps`):
     exchange alone, compute alone, the two in a row, and overlapped (the
     collective started async, the aggregation on the compute stream, then its
-    wait); hidden_frac as OverlappedAggregation.decompose."""
+    wait) -- from the legacy default stream and, as OverlappedAggregation
+    issues them, from the device's compute stream (dist.compute_stream);
+    hidden_frac as OverlappedAggregation.decompose; two aggregations on two
+    streams show whether the aggregation leaves any bandwidth to share."""
     from mi355_mp import dist as mdist, ops
     from mi355_mp.graph import Graph
     dev = bias.device
@@ -945,6 +948,10 @@ def rccl_contention(sg, P, bias, reps=10, rounds=3):
     send = torch.randn(rows, F_DIM, device=dev, generator=gen)
     recv = torch.empty_like(send)
 
+    side = torch.cuda.Stream(device=dev)
+    out2 = torch.empty_like(out)
+    assert torch.cuda.current_stream(dev) == torch.cuda.default_stream(dev), "the probe starts on the default stream"
+
     def compute():
         ops._aggregate(g.dst, "other", x_loc, w_csr, "sum", 0, bias, out=out)
 
@@ -959,6 +966,25 @@ def rccl_contention(sg, P, bias, reps=10, rounds=3):
         work = dist.all_to_all_single(recv, send, async_op=True)
         compute()
         work.wait()
+
+    def overlapped_side():
+        # what OverlappedAggregation does (dist.compute_stream): the collective
+        # and the aggregation issued from the device's compute stream, not from
+        # the legacy default stream
+        with mdist.compute_stream(dev):
+            work = dist.all_to_all_single(recv, send, async_op=True)
+            compute()
+            work.wait()
+
+    def two_aggregations():
+        # two aggregations on two streams: whether this GPU runs kernels of
+        # different streams side by side at all
+        cur = torch.cuda.current_stream(dev)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            ops._aggregate(g.dst, "other", x_loc, w_csr, "sum", 0, bias, out=out2)
+        compute()
+        cur.wait_stream(side)
 
     def timed(fn):
         per = []
@@ -975,10 +1001,14 @@ def rccl_contention(sg, P, bias, reps=10, rounds=3):
     res = {"P": P, "rank_rows": n_own, "rank_edges": int(src.numel()), "pull_halo_rows": int(halo.numel()),
            "exchange_rows": rows, "exchange_bytes": rows * F_DIM * 4, "reps": reps, "rounds": rounds,
            "exchange_only_ms": timed(exchange), "compute_only_ms": timed(compute),
-           "serial_step_ms": timed(serial), "overlapped_step_ms": timed(overlapped)}
+           "serial_step_ms": timed(serial), "overlapped_default_stream_ms": timed(overlapped),
+           "overlapped_step_ms": timed(overlapped_side),
+           "two_aggregations_two_streams_ms": timed(two_aggregations)}
     shorter = min(res["exchange_only_ms"], res["compute_only_ms"])
-    res["hidden_frac"] = (res["exchange_only_ms"] + res["compute_only_ms"] - res["overlapped_step_ms"]) / shorter
+    for k, v in (("hidden_frac", "overlapped_step_ms"), ("hidden_frac_default_stream", "overlapped_default_stream_ms")):
+        res[k] = (res["exchange_only_ms"] + res["compute_only_ms"] - res[v]) / shorter
     res["overlap_loss_vs_compute"] = res["overlapped_step_ms"] / res["compute_only_ms"] - 1.0
+    res["contention_ms"] = res["overlapped_step_ms"] - max(res["exchange_only_ms"], res["compute_only_ms"])
     res["note"] = ("self split on one GPU: RCCL's kernels contend with the aggregation for CUs / L2 / HBM; "
                    "the xGMI transfer time is not part of it")
     return res

@@ -631,6 +631,51 @@ class HaloCover:
         return out + aggregate(xl, self.bnd_src, self.bnd_dst, self.bnd_w, self.n_own)
 
 
+_COMPUTE_STREAMS = {}
+
+
+class compute_stream:
+    """Context: run the enclosed device work on this process's compute stream
+    of the device (one non-default HIP stream per device), ordered after
+    everything already queued on the caller's current stream, and make the
+    caller's stream wait for it on exit.
+
+    Why: on ROCm, kernels on the legacy default stream never ran beside
+    RCCL's kernels -- measured at one RCCL rank with a non-empty self split
+    (bench.py --emulate-peers, profiles/r05_rccl_stream_probe.json): an
+    all_to_all started async next to an aggregation on the default stream took
+    as long as the two in a row (hidden_frac -0.05, no concurrent kernel in the
+    trace), while the same aggregation on a stream of its own hid half the
+    exchange (hidden_frac 0.51 / 0.54 at P = 8 / 2, RCCL and k_agg_flat
+    intervals overlapping in the trace).  Host tensors: no-op."""
+
+    def __init__(self, device):
+        self.dev = torch.device(device)
+        self.cs = self.cur = self.ctx = None
+
+    def __enter__(self):
+        if self.dev.type != "cuda":
+            return None
+        idx = self.dev.index if self.dev.index is not None else torch.cuda.current_device()
+        cs = _COMPUTE_STREAMS.get(idx)
+        if cs is None:
+            cs = _COMPUTE_STREAMS[idx] = torch.cuda.Stream(device=idx)
+        self.cur = torch.cuda.current_stream(idx)
+        if self.cur == cs:
+            return cs                     # already on it (nested)
+        self.cs = cs
+        cs.wait_stream(self.cur)
+        self.ctx = torch.cuda.stream(cs)
+        self.ctx.__enter__()
+        return cs
+
+    def __exit__(self, *exc):
+        if self.ctx is not None:
+            self.ctx.__exit__(*exc)
+            self.cur.wait_stream(self.cs)
+        return False
+
+
 class OverlappedAggregation:
     """GCN-style sharded aggregation with the halo exchange hidden behind the
     interior edges.
@@ -710,6 +755,12 @@ class OverlappedAggregation:
         return ops.gather_rows(own, self.plan.send_idx)
 
     def step(self, x_local, out, bias=None, group=None):
+        """(see the class docstring) -- on the device's compute stream
+        (compute_stream: RCCL overlaps it, unlike the default stream)."""
+        with compute_stream(out.device):
+            return self._step(x_local, out, bias, group)
+
+    def _step(self, x_local, out, bias=None, group=None):
         from . import _lib, ops
         plan = self.plan
         own = x_local[:plan.n_own]
@@ -747,7 +798,13 @@ class OverlappedAggregation:
         cover's send graph: copies + partial rows), 'interior' (start, end) of
         the interior passes, 'wait'
         (before, after) around each tile's wait (the exchange time the compute
-        stream is exposed to), 'boundary' (start, end) of each boundary pass."""
+        stream is exposed to), 'boundary' (start, end) of each boundary pass.
+        The whole step runs on the device's compute stream (compute_stream),
+        ordered after the caller's stream and waited for by it."""
+        with compute_stream(out.device):
+            return self._step_tiled(x_tiles, out, bias, group, events)
+
+    def _step_tiled(self, x_tiles, out, bias=None, group=None, events=None):
         def rec(name):
             if events is None:
                 return None
@@ -854,12 +911,14 @@ class OverlappedAggregation:
                 barrier()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            for _ in range(reps):
-                fn()
+            with compute_stream(out.device):      # where step_tiled runs its work
+                for _ in range(reps):
+                    fn()
             torch.cuda.synchronize()
             return (time.perf_counter() - t0) / reps * 1e3
 
-        sends = [self._send(xt[:n_own]) for xt in x_tiles]
+        with compute_stream(out.device):
+            sends = [self._send(xt[:n_own]) for xt in x_tiles]
 
         def exchange_only():
             works = [self._exchange_async(xt, s, group) for xt, s in zip(x_tiles, sends)]
