@@ -226,7 +226,16 @@ def setup_dist(args):
                   % (local, n_dev))
             raise SystemExit(3)
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=timeout)
+        # RCCL on high-priority streams: HIP gives them hardware queues of their own.  With
+        # normal priority the communicator's stream is dealt a queue round-robin among
+        # GPU_MAX_HW_QUEUES (4) and may share one with the aggregation's stream -- measured
+        # at one RCCL rank: an all_to_all on the default stream's queue never ran beside the
+        # aggregation (hidden_frac -0.03), on a queue of its own it hid half the exchange
+        # (0.58; profiles/r05_queue_probe.jsonl).  Priority also lets RCCL's few blocks
+        # start before the aggregation's waves.
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=timeout, pg_options=opts)
     if dist.get_world_size() != args.gpus:
         stage(rank, "ERROR: process group has %d ranks, --gpus %d" % (dist.get_world_size(), args.gpus))
         raise SystemExit(3)

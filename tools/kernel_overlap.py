@@ -4,6 +4,8 @@ kernel trace (tools/gpu_round.sh step `rccl`: bench.py --sharded
   rccl_kernels      instances, total ms, and the ms during which at least one
                     k_agg_* kernel ran at the same time (from the start / end
                     timestamps), per kernel name
+  queues            instances per (kind, hardware queue, stream): kernels on one
+                    queue run one after the other, whatever their streams
   agg_kernels       k_agg_* instances that overlap an RCCL kernel: their
                     duration next to the median duration of the same-named
                     instances in the same duration band that overlap none
@@ -25,7 +27,8 @@ def load(root):
     for f in files:
         with open(f) as fh:
             for r in csv.DictReader(fh):
-                rows.append((r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+                rows.append((r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
+                             r.get("Queue_Id"), r.get("Stream_Id")))
     return files, rows
 
 
@@ -55,8 +58,12 @@ def overlap_ns(a, b, spans):
 
 def main(root):
     files, rows = load(root)
-    rccl = sorted((s, e, n) for n, s, e in rows if is_rccl(n))
-    agg = sorted((s, e, n) for n, s, e in rows if is_agg(n))
+    queues = collections.Counter()
+    for n, s, e, qid, sid in rows:
+        kind = "rccl" if is_rccl(n) else ("agg" if is_agg(n) else "other")
+        queues["%s queue %s stream %s" % (kind, qid, sid)] += 1
+    rccl = sorted((s, e, n) for n, s, e, _, _ in rows if is_rccl(n))
+    agg = sorted((s, e, n) for n, s, e, _, _ in rows if is_agg(n))
     agg_spans = [(s, e) for s, e, _ in agg]
     rccl_spans = [(s, e) for s, e, _ in rccl]
     per = collections.defaultdict(lambda: {"instances": 0, "total_ms": 0.0, "concurrent_with_agg_ms": 0.0})
@@ -80,6 +87,7 @@ def main(root):
                         "median_ms_same_band_alone": base,
                         "slowdown": (dur / base - 1.0) if base else None})
     res = {"trace_files": [os.path.relpath(f, root) for f in files],
+           "queues": dict(sorted(queues.items())),
            "rccl_kernels": dict(per),
            "rccl_total_ms": sum(d["total_ms"] for d in per.values()),
            "rccl_concurrent_with_agg_ms": sum(d["concurrent_with_agg_ms"] for d in per.values()),
