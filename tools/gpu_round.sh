@@ -10,7 +10,8 @@
 #             $R_rccl_kernel_trace/ (+ tools/kernel_overlap.py summary)
 #   gloo2     bench.py --gpus 2, gloo ranks sharing the GPU (--verify) -> $R_bench_rmat21_gloo2_rehearsal.json
 #   gat_gloo2 the same for --workload gat                -> $R_bench_gat_gloo2_rehearsal.json
-#   prof      tools/profile.sh (kernel trace + PMC of the default bench)
+#   prof      tools/profile.sh (kernel trace + PMC of the default bench); prof_gat / prof_products /
+#             prof_reddit the same for the other bench workloads (summarise with tools/pmc_summary.py)
 #   diag      tools/gat_shard_diag.py (sharded vs single-GPU vs float64 GAT gradients, per seed)
 #   train     kernel trace of the GCNConv / GATConv layer training steps (tools/bench_configs.py)
 set -u
@@ -37,6 +38,9 @@ for s in ${STEPS:-tests bench}; do
     gat_gloo2) run gat_gloo2 600 bash -c "MP_BENCH_BACKEND=gloo python bench.py --gpus 2 --workload gat --steps 3 --warmup 1 --verify > $O/${R}_bench_gat_gloo2_rehearsal.json 2> $O/${R}_bench_gat_gloo2_rehearsal.err"; cut -c1-300 $O/${R}_bench_gat_gloo2_rehearsal.json ;;
     diag) run diag 500 bash -c "python tools/gat_shard_diag.py > $O/${R}_gat_shard_diag.jsonl 2> $O/${R}_gat_shard_diag.err"; cat $O/${R}_gat_shard_diag.jsonl ;;
     prof) PROF_OUT=$O/${R}_prof run prof 1100 bash tools/profile.sh ;;
+    prof_gat) PROF_OUT=$O/${R}_prof_gat NO_CALIB=1 BENCH_ARGS="--workload gat" run prof_gat 1100 bash tools/profile.sh ;;
+    prof_products) PROF_OUT=$O/${R}_prof_products NO_CALIB=1 BENCH_ARGS="--workload products" run prof_products 1100 bash tools/profile.sh ;;
+    prof_reddit) PROF_OUT=$O/${R}_prof_reddit NO_CALIB=1 BENCH_ARGS="--workload reddit" run prof_reddit 1100 bash tools/profile.sh ;;
     train) run train 500 rocprofv3 --kernel-trace --stats -d $O/${R}_train_kt -o kt --output-format csv -- python3 tools/bench_configs.py --configs c2train,c3train ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
