@@ -5,6 +5,7 @@
 #   STEPS="tests bench rccl gloo2 gat_gloo2 prof train" R=r05 bash tools/gpu_round.sh
 #   tests     pytest -m gpu                           -> $R_pytest_gpu.txt
 #   bench     python bench.py (the driver's N=1 line)  -> $R_bench_rmat21.json
+#   bench_gat / bench_products / bench_reddit  the other workloads at N=1 (--verify)
 #   rccl      one RCCL rank, --sharded --emulate-peers 8,2 (RCCL beside the aggregation),
 #             rocprofv3 kernel trace of the same command -> $R_bench_sharded_rccl_one_rank.json,
 #             $R_rccl_kernel_trace/ (+ tools/kernel_overlap.py summary)
@@ -31,6 +32,9 @@ for s in ${STEPS:-tests bench}; do
   case $s in
     tests) run tests 900 bash -c "python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/${R}_pytest_gpu.txt 2>&1"; tail -3 $O/${R}_pytest_gpu.txt ;;
     bench) run bench 400 bash -c "python bench.py > $O/${R}_bench_rmat21.json 2> $O/${R}_bench_rmat21.err"; cut -c1-400 $O/${R}_bench_rmat21.json ;;
+    bench_gat) run bench_gat 400 bash -c "python bench.py --workload gat --verify > $O/${R}_bench_gat_n1.json 2> $O/${R}_bench_gat_n1.err"; cut -c1-300 $O/${R}_bench_gat_n1.json ;;
+    bench_products) run bench_products 500 bash -c "python bench.py --workload products --verify > $O/${R}_bench_products_n1.json 2> $O/${R}_bench_products_n1.err"; cut -c1-300 $O/${R}_bench_products_n1.json ;;
+    bench_reddit) run bench_reddit 500 bash -c "python bench.py --workload reddit --verify > $O/${R}_bench_reddit_n1.json 2> $O/${R}_bench_reddit_n1.err"; cut -c1-300 $O/${R}_bench_reddit_n1.json ;;
     rccl) run rccl 500 bash -c "python bench.py --sharded --emulate-peers 8,2 --steps 10 --warmup 3 --verify > $O/${R}_bench_sharded_rccl_one_rank.json 2> $O/${R}_bench_sharded_rccl_one_rank.err"
           run rccl_trace 500 rocprofv3 --kernel-trace --stats -d $O/${R}_rccl_kt -o kt --output-format csv -- python3 bench.py --sharded --emulate-peers 8,2 --steps 5 --warmup 2 --no-cpu-baseline --no-ref-paths --no-build-split
           python3 tools/kernel_overlap.py $O/${R}_rccl_kt > $O/${R}_rccl_kernel_overlap.json; cat $O/${R}_rccl_kernel_overlap.json | head -40 ;;
