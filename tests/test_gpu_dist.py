@@ -894,6 +894,36 @@ def test_bench_sharded_path_over_rccl_one_rank():
     assert dc["exchange_only_ms"] < 0.2 * dc["compute_only_ms"], dc
     # the same kernels over the whole graph: within 2x of the single-GPU step
     assert d["value"] > 4e9, d["value"]
+    # the line explains itself: link model and build split per rank
+    assert p["link_model"]["sets_the_step"].startswith("compute"), p["link_model"]
+    assert set(p["build_split"]) == {"shards", "exchange_plan"}
+    assert all(v["wall_s"] > 0 for v in p["build_split"].values())
+
+
+def test_rccl_runs_beside_the_aggregation_one_rank():
+    """RCCL's kernels next to k_agg_flat: one RCCL rank, no
+    launcher (`--sharded` at --gpus 1 makes its own world-1 group), a self
+    split of the P = 8 rank's cover volume started async beside that rank's
+    aggregation.  Issued as OverlappedAggregation issues it (its compute stream,
+    RCCL on high-priority streams with hardware queues of their own) the
+    exchange must partly hide behind the aggregation: round 5 measured 0.54
+    there and -0.03 while RCCL's stream shared the default stream's queue."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MP_BENCH_BACKEND"):
+        env.pop(k, None)
+    cmd = [sys.executable, "bench.py", "--sharded", "--emulate-peers", "8", "--steps", "2", "--warmup", "1",
+           "--no-cpu-baseline", "--no-ref-paths", "--no-build-split"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    (c,) = d["extra"]["per_rank"][0]["rccl_contention"]
+    assert c["P"] == 8 and c["exchange_rows"] == 313_427, c
+    assert c["serial_step_ms"] > c["overlapped_step_ms"], c
+    assert c["hidden_frac"] > 0.2, c
 
 
 def _cover_worker(rank, world, port, q):
