@@ -1109,8 +1109,8 @@ class ShardedGraph:
         (mi355_mp.gat_cover.GatHaloCover: a remote source row is pulled, or its
         owner pushes its online-softmax piece of the destination row -- 0.57x
         the pull rows on the config-2 graph) instead of the pull exchange.
-        return_alpha, attention dropout and heads outside gat_cover.cover_ok
-        keep the pull form.  Collective, once (every rank of the group)."""
+        return_alpha and attention dropout keep the pull form; heads of any
+        width (C % 4 == 0, GATConv pads to it) take the cover.  Collective, once (every rank of the group)."""
         from .gat_cover import GatHaloCover
         if self.bwd is not None:
             raise ValueError("mi355_mp.dist: enable_gat_halo_cover needs a graph made by for_gat / "

@@ -44,9 +44,12 @@ Device path: the HIP kernels (GatHaloCover.forward_device / backward_device,
 wrapped by _GatCoverFn).  Host path (forward_host): the same data flow with
 differentiable torch ops and a differentiable all_to_all -- the gloo CPU tests
 check the distributed algorithm, forward and backward, against the
-single-process oracle with it.  Shapes: C % 4 == 0 with C / 4 a power of two
-<= 64 (the fused transposed pass); other shapes, return_alpha and attention
-dropout take the pull form.
+single-process oracle with it.  Heads of any width (GATConv pads C to a
+multiple of 4): C / 4 a power of two <= 64 takes the fused transposed pass,
+whose per-edge d score gives a pusher its share of d a_dst; other widths the
+wide kernels, the share then node-wise from the pieces' training accumulators
+(out2, s2) rescaled to the merged row.  return_alpha and attention dropout
+take the pull form.
 """
 import torch
 import torch.distributed as dist
@@ -54,10 +57,18 @@ import torch.distributed as dist
 from .dist import HaloCover, _a2a
 
 
-def cover_ok(H, C):
-    """Head shapes the device path takes (mp_gat_train_ok: the fused kernels)."""
+def fused_heads(H, C):
+    """Heads whose C/4 is a power of two <= 64 (mp_gat_train_ok): the fused
+    transposed pass with per-edge d score serves the pushed pieces' edges.
+    Other widths take the wide kernels (any C % 4 == 0)."""
     q = C // 4
     return H > 0 and C % 4 == 0 and 1 <= q <= 64 and (q & (q - 1)) == 0
+
+
+def cover_ok(H, C):
+    """Head shapes the device path takes: any C % 4 == 0 (GATConv pads every
+    head to it); fused_heads picks the kernels."""
+    return H > 0 and C > 0 and C % 4 == 0
 
 
 class _A2A(torch.autograd.Function):
@@ -228,13 +239,15 @@ class GatHaloCover:
         st = _lib.stream_ptr(dev)
         n_own, F = self.n_own, H * C
         grp = self.group
+        fused = fused_heads(H, C)
+        node_scores = lib.mp_gat_node_scores_f32 if fused else lib.mp_gat_node_scores_wide_f32
         xl = torch.empty((self.n_local_src, F), dtype=torch.float32, device=dev)
         xl[:n_own].copy_(xw_own)
         a_src = torch.empty((self.n_local_src, H), dtype=torch.float32, device=dev)
         a_dst = torch.empty((self.n_local_src, H), dtype=torch.float32, device=dev)
         if n_own:
-            _lib.check(lib.mp_gat_node_scores_f32(xl.data_ptr(), n_own, H, C, att_c.data_ptr(), a_src.data_ptr(),
-                                                  a_dst.data_ptr(), st), "mp_gat_node_scores_f32")
+            _lib.check(node_scores(xl.data_ptr(), n_own, H, C, att_c.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(),
+                                   st), "mp_gat_node_scores (own rows)")
         # 1. a_dst of the rows the peers push pieces of
         a2a = _a2a if exchange else (lambda o, *a: o.zero_())
         adst_in = torch.empty((sum(self.adst_recv_counts), H), dtype=torch.float32, device=dev)
@@ -243,24 +256,38 @@ class GatHaloCover:
         if adst_in.shape[0]:
             send_adst[self.send_push_rows] = adst_in
         # 2. the send rows: one fused aggregation over the send graph, then rows + stats out
+        #    (wide heads in training: the training form, whose out2 / s2 of the pushed
+        #    pieces give this rank's share of d a_dst node-wise in the backward)
         send = torch.empty((self.n_send, F), dtype=torch.float32, device=dev)
         send_st = torch.empty((self.n_send, H, 2), dtype=torch.float32, device=dev)
+        send2 = send_s2 = None
         if self.n_send:
             gs = g_send.dst.struct("other")
-            sb = lib.mp_gat_slab_bytes(gs, H, C)
-            slab = torch.empty(sb, dtype=torch.uint8, device=dev)
-            _lib.check(lib.mp_gat_aggregate_att_f32(gs, xl.data_ptr(), a_src.data_ptr(), send_adst.data_ptr(),
-                                                    att_c.data_ptr(), H, C, float(slope), None, send.data_ptr(), F,
-                                                    send_st.data_ptr(), slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
-                       "mp_gat_aggregate_att_f32 (send rows)")
+            if train and not fused:
+                send2 = torch.empty((self.n_send, F), dtype=torch.float32, device=dev)
+                send_s2 = torch.empty((self.n_send, H), dtype=torch.float32, device=dev)
+                sb = lib.mp_gat_train_slab_bytes(gs, H, C)
+                slab = torch.empty(sb, dtype=torch.uint8, device=dev)
+                _lib.check(lib.mp_gat_aggregate_train_f32(gs, xl.data_ptr(), a_src.data_ptr(), send_adst.data_ptr(),
+                                                          att_c.data_ptr(), H, C, float(slope), None, send.data_ptr(),
+                                                          F, None, send_st.data_ptr(), send2.data_ptr(),
+                                                          send_s2.data_ptr(), slab.data_ptr(), sb, _lib.MP_STAGE_ALL,
+                                                          st), "mp_gat_aggregate_train_f32 (send rows)")
+            else:
+                sb = lib.mp_gat_slab_bytes(gs, H, C)
+                slab = torch.empty(sb, dtype=torch.uint8, device=dev)
+                _lib.check(lib.mp_gat_aggregate_att_f32(gs, xl.data_ptr(), a_src.data_ptr(), send_adst.data_ptr(),
+                                                        att_c.data_ptr(), H, C, float(slope), None, send.data_ptr(),
+                                                        F, send_st.data_ptr(), slab.data_ptr(), sb, _lib.MP_STAGE_ALL,
+                                                        st), "mp_gat_aggregate_att_f32 (send rows)")
             del slab
         r_st = torch.empty((self.n_halo, H, 2), dtype=torch.float32, device=dev)
         a2a(xl[n_own:], send, self.recv_counts, self.send_counts, grp)
         a2a(r_st, send_st, self.recv_counts, self.send_counts, grp)
         if self.n_halo:
-            _lib.check(lib.mp_gat_node_scores_f32(xl[n_own:].data_ptr(), self.n_halo, H, C, att_c.data_ptr(),
-                                                  a_src[n_own:].data_ptr(), a_dst[n_own:].data_ptr(), st),
-                       "mp_gat_node_scores_f32 (received rows)")
+            _lib.check(node_scores(xl[n_own:].data_ptr(), self.n_halo, H, C, att_c.data_ptr(),
+                                   a_src[n_own:].data_ptr(), a_dst[n_own:].data_ptr(), st),
+                       "mp_gat_node_scores (received rows)")
         # 3. the local piece (no bias: the merge adds it)
         out = torch.empty((n_own, F), dtype=torch.float32, device=dev)
         stats = torch.empty((n_own, H, 2), dtype=torch.float32, device=dev)
@@ -294,7 +321,7 @@ class GatHaloCover:
                                                      r_st.data_ptr() if n_parts else None, _lib.ptr(bias),
                                                      out.data_ptr(), F, stats.data_ptr(), _lib.ptr(agg2),
                                                      _lib.ptr(s2), st), "mp_gat_merge_partials_f32")
-        saved = (xl, a_src, a_dst, stats, agg2, s2) if train else None
+        saved = (xl, a_src, a_dst, stats, agg2, s2, send_st, send2, send_s2) if train else None
         return out, saved
 
     def decompose(self, xw_own, att, H, C, slope, bias, reps=10, barrier=None):
@@ -349,35 +376,66 @@ class GatHaloCover:
         from . import _lib, ops
         lib = _lib.load()
         g_loc, _, g_merge, g_copy_t, g_push = self.graphs()
-        xl, a_src, a_dst, stats, agg2, s2 = saved
+        xl, a_src, a_dst, stats, agg2, s2, send_st, send2, send_s2 = saved
         dev = g.device
         st = _lib.stream_ptr(dev)
         n_own, F, grp = self.n_own, H * C, self.group
         nl = self.n_local_src
+        fused = fused_heads(H, C)
+
+        def wide_pass(gt_struct, n_rows, grad_out, pack_, xw_rows, gx_out):
+            """mp_gat_backward_wide_f32 + its epilogue over a transposed graph of
+            n_rows source rows: gx_out += sum alpha g + d a_src att_src; returns d a_src."""
+            acc2 = torch.zeros((n_rows, F), dtype=torch.float32, device=dev)
+            sc = torch.zeros((n_rows, H), dtype=torch.float32, device=dev)
+            sb = lib.mp_gat_train_slab_bytes(gt_struct, H, C)
+            slab = torch.empty(sb, dtype=torch.uint8, device=dev)
+            _lib.check(lib.mp_gat_backward_wide_f32(gt_struct, grad_out.data_ptr(), F, a_src.data_ptr(),
+                                                    pack_.data_ptr(), H, C, float(slope), 0, 0.0, gx_out.data_ptr(),
+                                                    acc2.data_ptr(), _lib.nbytes(acc2), sc.data_ptr(),
+                                                    _lib.nbytes(sc), slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
+                       "mp_gat_backward_wide_f32 (cover)")
+            del slab
+            zero_gd = torch.zeros((n_rows, H), dtype=torch.float32, device=dev)
+            _lib.check(lib.mp_gat_backward_epilogue_wide_f32(gx_out.data_ptr(), acc2.data_ptr(), xw_rows.data_ptr(),
+                                                             att_c.data_ptr(), zero_gd.data_ptr(), sc.data_ptr(),
+                                                             n_rows, H, C, st), "mp_gat_backward_epilogue_wide_f32")
+            return sc
+
         # p: pack from the merged stats, node-wise d a_dst of the local edges
         pack = torch.zeros((max(n_own, 1), H, 4), dtype=torch.float32, device=dev)
         ga_dst = torch.zeros((max(n_own, 1), H), dtype=torch.float32, device=dev)
         if n_own:
-            _lib.check(lib.mp_gat_backward_prep_train_f32(g.data_ptr(), F, out.data_ptr(), F, _lib.ptr(bias),
-                                                          agg2.data_ptr(), s2.data_ptr(), a_dst.data_ptr(),
-                                                          stats.data_ptr(), n_own, H, C, pack.data_ptr(),
-                                                          _lib.nbytes(pack), None, 0, ga_dst.data_ptr(), st),
-                       "mp_gat_backward_prep_train_f32 (cover)")
+            if fused:
+                _lib.check(lib.mp_gat_backward_prep_train_f32(g.data_ptr(), F, out.data_ptr(), F, _lib.ptr(bias),
+                                                              agg2.data_ptr(), s2.data_ptr(), a_dst.data_ptr(),
+                                                              stats.data_ptr(), n_own, H, C, pack.data_ptr(),
+                                                              _lib.nbytes(pack), None, 0, ga_dst.data_ptr(), st),
+                           "mp_gat_backward_prep_train_f32 (cover)")
+            else:
+                _lib.check(lib.mp_gat_backward_prep_wide_f32(g.data_ptr(), F, out.data_ptr(), F, _lib.ptr(bias),
+                                                             agg2.data_ptr(), s2.data_ptr(), a_dst.data_ptr(),
+                                                             stats.data_ptr(), n_own, H, C, pack.data_ptr(),
+                                                             _lib.nbytes(pack), ga_dst.data_ptr(), st),
+                           "mp_gat_backward_prep_wide_f32 (cover)")
         # p: the transposed pass over the local edges (the att_dst term comes last)
         gx_l = torch.zeros((nl, F), dtype=torch.float32, device=dev)
         ga_src_l = torch.zeros((nl, H), dtype=torch.float32, device=dev)
         if n_own and g_loc.dst.n_edges:
             gt = g_loc.src_with_dst_slots()
             gs = gt.struct("dst_slot")
-            zero_gd = torch.zeros((nl, H), dtype=torch.float32, device=dev)
-            sb = lib.mp_gat_slab_bytes(gs, H, C)
-            slab = torch.empty(sb, dtype=torch.uint8, device=dev)
-            _lib.check(lib.mp_gat_backward_train_f32(gs, g.data_ptr(), F, xl.data_ptr(), a_src.data_ptr(),
-                                                     pack.data_ptr(), att_c.data_ptr(), H, C, float(slope),
-                                                     zero_gd.data_ptr(), gx_l.data_ptr(), ga_src_l.data_ptr(),
-                                                     slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
-                       "mp_gat_backward_train_f32 (local piece)")
-            del slab, zero_gd
+            if fused:
+                zero_gd = torch.zeros((nl, H), dtype=torch.float32, device=dev)
+                sb = lib.mp_gat_slab_bytes(gs, H, C)
+                slab = torch.empty(sb, dtype=torch.uint8, device=dev)
+                _lib.check(lib.mp_gat_backward_train_f32(gs, g.data_ptr(), F, xl.data_ptr(), a_src.data_ptr(),
+                                                         pack.data_ptr(), att_c.data_ptr(), H, C, float(slope),
+                                                         zero_gd.data_ptr(), gx_l.data_ptr(), ga_src_l.data_ptr(),
+                                                         slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
+                           "mp_gat_backward_train_f32 (local piece)")
+                del slab, zero_gd
+            else:
+                ga_src_l = wide_pass(gs, nl, g, pack, xl, gx_l)
         # reverse exchange: a pulled slot returns its row's gradient to the owner, a
         # piece's slot carries its destination's g and pack to the peer that pushed it
         rev = gx_l[n_own:]
@@ -397,7 +455,22 @@ class GatHaloCover:
         ga_src_push = torch.zeros((max(n_own, 1), H), dtype=torch.float32, device=dev)
         ga_back = torch.zeros((self.n_send, H), dtype=torch.float32, device=dev)
         E_push = int(self.push_src.numel())
-        if E_push:
+        if E_push and not fused:
+            # wide heads: the fused pass's per-edge d score needs C/4 a power of two, so
+            # this rank's share of d a_dst comes node-wise from its pieces' training
+            # accumulators instead: with c = den_q e^(m_q - M) / den the piece's weight in
+            # the merged row, share = c (<g, out2_q> - rs s2_q)
+            gt = g_push.src_with_dst_slots()
+            gx_push = torch.zeros((n_own, F), dtype=torch.float32, device=dev)
+            ga_src_push = wide_pass(gt.struct("dst_slot"), n_own, back, back_pack, xl[:n_own], gx_push)
+            gx += gx_push
+            pk = back_pack.view(-1, H, 4)
+            c = send_st[..., 1] * torch.exp(send_st[..., 0] - pk[..., 1]) * pk[..., 2]
+            dot = (back.view(-1, H, C) * send2.view(-1, H, C)).sum(-1)
+            share = c * (dot - pk[..., 3] * send_s2)
+            ga_back = torch.zeros_like(share)
+            ga_back[self.send_push_rows] = share[self.send_push_rows]
+        elif E_push:
             gt = g_push.src_with_dst_slots()
             gs = gt.struct("dst_slot")
             gx_push = torch.empty((n_own, F), dtype=torch.float32, device=dev)
@@ -466,7 +539,7 @@ def gat_cover_propagate(cover, xw_own, att, heads, out_channels, negative_slope=
     if not xw_own.is_cuda:
         return cover.forward_host(xw_own, att, H, C, negative_slope, bias)
     if not cover_ok(H, C):
-        raise ValueError("mi355_mp.gat_cover: heads of %d features take the pull form (cover_ok)" % C)
+        raise ValueError("mi355_mp.gat_cover: heads of %d features need C %% 4 == 0 (GATConv pads them)" % C)
     needs = torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in (xw_own, att, bias))
     if not needs:
         att_c = att.reshape(H, 2 * C).contiguous().to(torch.float32)

@@ -1169,7 +1169,8 @@ def _sharded_fuzz_worker(rank, world, port, q, seeds):
                 conv = mdist.ShardedGCNConv(Fi, 24).to(dev)
             elif kind in ("gat", "gat_cover"):
                 H = int(torch.randint(1, 5, (1,), generator=g))
-                ref = GATConv(Fi, 8, heads=H).to(dev)
+                Cg = 8 if kind == "gat" else int(torch.randint(1, 41, (1,), generator=g))   # cover: any width
+                ref = GATConv(Fi, Cg, heads=H).to(dev)
                 if kind == "gat_cover":
                     # dyadic x and W: X W exact on both sides, so no leaky_relu branch flips
                     x = _dyadic_(torch.empty(N, Fi), g, 4.0).to(dev)
@@ -1177,7 +1178,7 @@ def _sharded_fuzz_worker(rank, world, port, q, seeds):
                 sg = mdist.ShardedGraph.for_gat(ei, N, rank, world, cuts=cuts)
                 if kind == "gat_cover":
                     sg.enable_gat_halo_cover()
-                conv = mdist.ShardedGATConv(Fi, 8, heads=H).to(dev)
+                conv = mdist.ShardedGATConv(Fi, Cg, heads=H).to(dev)
             if kind != "max":
                 with torch.no_grad():
                     ref.bias.normal_(generator=None)
@@ -1268,7 +1269,9 @@ def _gat_cover_gpu_worker(rank, world, port, q, cut_sets):
         x = _dyadic_(torch.empty(N, Fi), gen, 4.0).to(dev)
         res = {}
         for ci, cuts in enumerate(cut_sets):
-            for H, C, concat in ((8, 32, True), (3, 8, False), (2, 4, True)):
+            # fused-pass heads (C/4 a power of two) and wide ones (a heads=1 stack's 96, a
+            # padded 10 -> 12: the wide kernels, d a_dst shares from the pieces' out2 / s2)
+            for H, C, concat in ((8, 32, True), (3, 8, False), (2, 4, True), (1, 96, True), (2, 10, True)):
                 Fo = H * C if concat else C
                 gout = torch.randn(N, Fo, generator=gen).to(dev)
                 ref = GATConv(Fi, C, heads=H, concat=concat).to(dev)
@@ -1327,7 +1330,8 @@ def test_sharded_gatconv_over_halo_cover_on_one_gpu(world):
     native backward returns g and the pack of every pushed row to its pusher):
     forward rows, d x and the all-reduced d W / d att / d b against the
     single-GPU GATConv -- slice-built shards, an empty rank, a one-row rank;
-    config 3's 8 x 32 heads, a mean of heads, C = 4.  Rows no peer pushes a
+    config 3's 8 x 32 heads, a mean of heads, C = 4, and wide heads (one head
+    of 96, two padded heads of 10).  Rows no peer pushes a
     piece of are the single-GPU rows bit for bit; the cover never receives
     more rows than the pull plan, and pieces are pushed."""
     N = 2500
