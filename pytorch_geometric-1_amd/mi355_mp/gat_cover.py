@@ -52,7 +52,6 @@ wide kernels, the share then node-wise from the pieces' training accumulators
 take the pull form.
 """
 import torch
-import torch.distributed as dist
 
 from .dist import HaloCover, _a2a
 
