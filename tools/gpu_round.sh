@@ -7,7 +7,7 @@
 #   bench     python bench.py (the driver's N=1 line)  -> $R_bench_rmat21.json
 #   bench_gat / bench_products / bench_reddit  the other workloads at N=1 (--verify)
 #   configs   tools/bench_configs.py (configs 3 / 4 / 5, layer steps, Cora graph) -> $R_bench_configs.jsonl
-#   rccl      one RCCL rank, --sharded --emulate-peers 8,2 (RCCL beside the aggregation),
+#   rccl      one RCCL rank, --sharded --emulate-peers 8,4,2 (RCCL beside the aggregation),
 #             rocprofv3 kernel trace of the same command -> $R_bench_sharded_rccl_one_rank.json,
 #             $R_rccl_kernel_trace/ (+ tools/kernel_overlap.py summary)
 #   gloo2     bench.py --gpus 2, gloo ranks sharing the GPU (--verify) -> $R_bench_rmat21_gloo2_rehearsal.json
@@ -37,8 +37,8 @@ for s in ${STEPS:-tests bench}; do
     bench_products) run bench_products 500 bash -c "python bench.py --workload products --verify > $O/${R}_bench_products_n1.json 2> $O/${R}_bench_products_n1.err"; cut -c1-300 $O/${R}_bench_products_n1.json ;;
     bench_reddit) run bench_reddit 500 bash -c "python bench.py --workload reddit --verify > $O/${R}_bench_reddit_n1.json 2> $O/${R}_bench_reddit_n1.err"; cut -c1-300 $O/${R}_bench_reddit_n1.json ;;
     configs) run configs 700 bash -c "python tools/bench_configs.py --cpu-baseline > $O/${R}_bench_configs.jsonl 2> $O/${R}_bench_configs.err"; cut -c1-200 $O/${R}_bench_configs.jsonl ;;
-    rccl) run rccl 500 bash -c "python bench.py --sharded --emulate-peers 8,2 --steps 10 --warmup 3 --verify > $O/${R}_bench_sharded_rccl_one_rank.json 2> $O/${R}_bench_sharded_rccl_one_rank.err"
-          run rccl_trace 500 rocprofv3 --kernel-trace --stats -d $O/${R}_rccl_kt -o kt --output-format csv -- python3 bench.py --sharded --emulate-peers 8,2 --steps 5 --warmup 2 --no-cpu-baseline --no-ref-paths --no-build-split
+    rccl) run rccl 500 bash -c "python bench.py --sharded --emulate-peers 8,4,2 --steps 10 --warmup 3 --verify > $O/${R}_bench_sharded_rccl_one_rank.json 2> $O/${R}_bench_sharded_rccl_one_rank.err"
+          run rccl_trace 500 rocprofv3 --kernel-trace --stats -d $O/${R}_rccl_kt -o kt --output-format csv -- python3 bench.py --sharded --emulate-peers 8,4,2 --steps 5 --warmup 2 --no-cpu-baseline --no-ref-paths --no-build-split
           python3 tools/kernel_overlap.py $O/${R}_rccl_kt > $O/${R}_rccl_kernel_overlap.json; cat $O/${R}_rccl_kernel_overlap.json | head -40 ;;
     gloo2) run gloo2 600 bash -c "MP_BENCH_BACKEND=gloo python bench.py --gpus 2 --steps 3 --warmup 1 --verify > $O/${R}_bench_rmat21_gloo2_rehearsal.json 2> $O/${R}_bench_rmat21_gloo2_rehearsal.err"; cut -c1-300 $O/${R}_bench_rmat21_gloo2_rehearsal.json ;;
     gat_gloo2) run gat_gloo2 600 bash -c "MP_BENCH_BACKEND=gloo python bench.py --gpus 2 --workload gat --steps 3 --warmup 1 --verify > $O/${R}_bench_gat_gloo2_rehearsal.json 2> $O/${R}_bench_gat_gloo2_rehearsal.err"; cut -c1-300 $O/${R}_bench_gat_gloo2_rehearsal.json ;;
