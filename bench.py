@@ -150,9 +150,28 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
+_LAST_STAGE = ["start"]
+
+
 def stage(rank, msg):
     """One progress line per stage on stderr (the JSON line stays alone on stdout)."""
+    _LAST_STAGE[0] = msg[:80]
     print("[bench rank %s +%.1fs] %s" % (rank, time.perf_counter() - T_START, msg), file=sys.stderr, flush=True)
+
+
+def start_heartbeat(rank, every_s=60.0):
+    """Rank 0 prints one line a minute while it runs (a daemon thread): a long
+    one-time build still shows progress to whoever watches the log."""
+    import threading
+    if rank != 0:
+        return
+
+    def beat():
+        while True:
+            time.sleep(every_s)
+            print("[bench rank %s +%.1fs] running; last stage: %s" % (rank, time.perf_counter() - T_START,
+                                                                       _LAST_STAGE[0]), file=sys.stderr, flush=True)
+    threading.Thread(target=beat, name="bench-heartbeat", daemon=True).start()
 
 
 def _free_port():
@@ -906,6 +925,13 @@ def link_model(mine, rank, n_tiles):
            "measured_exchange_ms": ex_meas,
            "measured_link_GBps": (per_peer / (ex_meas * 1e-3) / 1e9) if ex_meas and per_peer else None,
            "measured_over_predicted_77": (meas / nominal) if meas and nominal else None}
+    cit = mine.get("compute_in_turn")
+    if cit:
+        # the same model on the compute each rank measured with the GPU to
+        # itself (ranks sharing one GPU in a rehearsal: the node's compute)
+        c_pf, c_bl = cit["send_pack_ms"] / T, cit["boundary_ms"] / T
+        res["predicted_in_turn"] = {
+            "%g" % gbs: max(cit["compute_alone_ms"], c_pf + per_peer / (gbs * 1e9) * 1e3 + c_bl) for gbs in LINK_GBS}
     if meas is not None and ex_meas is not None:
         longer = max(comp, ex_meas)
         res["contention_ms"] = meas - longer     # beyond a perfect overlap of the two measured pieces
@@ -1035,6 +1061,8 @@ def main(argv=None):
         sys.exit(launch_ranks(args, argv))
     rank, world, local = setup_dist(args)
     sharded = dist.is_initialized()
+    if sharded:
+        start_heartbeat(rank)
     if args.workload == "gat":
         return main_gat(args, rank, world, local)
     if args.workload == "reddit":
@@ -1081,7 +1109,12 @@ def main(argv=None):
         E_local = E2
     else:
         from mi355_mp import dist as mdist
-        meter = BuildMeter(not args.no_build_split)
+        # more than two ranks per GPU (the gloo rehearsals): eight torch profilers
+        # on one device slowed the shard build past 3 min without a line, so
+        # wall time only (two per GPU: measured fine, 2.6 s)
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+        crowded = local_world > 2 * max(1, torch.cuda.device_count())
+        meter = BuildMeter(not args.no_build_split and not crowded)
         sg = meter.run("shards", lambda: mdist.ShardedGraph.for_gcn_from_slices(ei_slice, s0, N, rank, world,
                                                                                chunk=args.chunk or None))
         del ei_slice
@@ -1325,7 +1358,7 @@ def main(argv=None):
                 "pull_exchange_rows_in": plan.n_local_src - plan.n_own,
                 "peers_in": [int(c) for c in (plan.recv_counts if args.no_overlap else overlap.recv_counts)],
                 "peers_out": [int(c) for c in (plan.send_counts if args.no_overlap else overlap.send_counts)],
-                "build_split": meter.res,
+                "build_split": meter.res, "build_split_profiled": meter.enabled,
                 "step_ms_this_rank": dt_local / args.steps * 1e3}
         if overlap.cover is not None:
             mine.update({"cover_pulled_rows": overlap.cover.n_pull_rows,
@@ -1342,6 +1375,9 @@ def main(argv=None):
             reps_d = max(3, min(args.steps, 10))
             mine["decomposed"] = overlap.decompose(tiles, out_buf, bias, reps_d, barrier=lambda: barrier(world))
             stage(rank, "step decomposition: %s" % json.dumps(mine["decomposed"]))
+            mine["compute_in_turn"] = overlap.compute_in_turn(tiles, out_buf, bias, reps_d,
+                                                              barrier=lambda: barrier(world))
+            stage(rank, "compute in turn: %s" % json.dumps(mine["compute_in_turn"]))
             mine["link_model"] = link_model(mine, rank, len(tiles))
             stage(rank, "link model: %s" % json.dumps(mine["link_model"]))
         if args.emulate_peers:

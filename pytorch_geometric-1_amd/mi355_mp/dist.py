@@ -887,6 +887,45 @@ class OverlappedAggregation:
                 ops._aggregate(self.g_bnd.dst, "other", xt, self.w_bnd, "sum", _lib.MP_FLAG_INIT_FROM_OUT, b,
                                out=out[:, offs[t]:offs[t + 1]])
 
+    def compute_in_turn(self, x_tiles, out, bias=None, reps=5, group=None, barrier=None):
+        """decompose()'s compute alone, one rank at a time: rank r times its
+        send pack, interior and boundary passes with HIP events on the compute
+        stream while every other rank waits at `barrier`.  Ranks that share
+        one GPU (the gloo rehearsal) get the compute time each rank would have
+        on a GPU of its own; on a node it equals compute_only_ms.  Collective
+        over `group` (every rank calls it)."""
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        n_own = self.plan.n_own
+        res = None
+        for r in range(world):
+            if barrier is not None:
+                barrier()
+            if r != rank:
+                continue
+            with compute_stream(out.device):
+                for xt in x_tiles:
+                    self._send(xt[:n_own])
+                self._passes(x_tiles, out, bias)
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+                tot = [0.0, 0.0, 0.0]
+                for _ in range(reps):
+                    ev[0].record()
+                    for xt in x_tiles:
+                        self._send(xt[:n_own])
+                    ev[1].record()
+                    self._passes(x_tiles, out, bias, boundary=False)
+                    ev[2].record()
+                    self._passes(x_tiles, out, bias, interior=False)
+                    ev[3].record()
+                    ev[3].synchronize()
+                    for j in range(3):
+                        tot[j] += ev[j].elapsed_time(ev[j + 1])
+            res = {"reps": reps, "send_pack_ms": tot[0] / reps, "interior_ms": tot[1] / reps,
+                   "boundary_ms": tot[2] / reps, "compute_alone_ms": sum(tot) / reps}
+        if barrier is not None:
+            barrier()
+        return res
+
     def decompose(self, x_tiles, out, bias=None, reps=5, group=None, barrier=None):
         """The overlapped step taken apart on this rank, each piece timed alone
         (wall clock over `reps` repetitions, the device synchronised after

@@ -792,6 +792,12 @@ def test_bench_multi_rank_path_end_to_end():
         dc = p["decomposed"]
         assert dc["exchange_only_ms"] > 0 and dc["compute_only_ms"] > 0
         assert dc["serial_step_ms"] > 0 and dc["overlapped_step_ms"] > 0
+        # the compute timed one rank at a time (the GPU to itself): its parts add up
+        cit = p["compute_in_turn"]
+        parts = cit["send_pack_ms"] + cit["interior_ms"] + cit["boundary_ms"]
+        assert min(cit["send_pack_ms"], cit["interior_ms"], cit["boundary_ms"]) > 0, cit
+        assert abs(parts - cit["compute_alone_ms"]) < 1e-6 * max(1.0, parts), cit
+        assert set(p["link_model"]["predicted_in_turn"]) == {"60", "77", "100"}
     for r in (0, 1):
         for marker in ("process group up", "shards built", "warm-up done", "timed steps done", "done"):
             assert ("[bench rank %d " % r) in err and marker in err, marker
@@ -892,6 +898,8 @@ def test_bench_sharded_path_over_rccl_one_rank():
     assert p["interior_ms"] > 0 and p["exchange_exposed_ms"] >= 0
     dc = p["decomposed"]   # one rank: empty splits, the exchange alone costs ~nothing
     assert dc["exchange_only_ms"] < 0.2 * dc["compute_only_ms"], dc
+    cit = p["compute_in_turn"]   # one rank: the same compute, timed with events
+    assert 0.5 * dc["compute_only_ms"] < cit["compute_alone_ms"] < 2.0 * dc["compute_only_ms"], (cit, dc)
     # the same kernels over the whole graph: within 2x of the single-GPU step
     assert d["value"] > 4e9, d["value"]
     # the line explains itself: link model and build split per rank
