@@ -928,10 +928,12 @@ def link_model(mine, rank, n_tiles):
     cit = mine.get("compute_in_turn")
     if cit:
         # the same model on the compute each rank measured with the GPU to
-        # itself (ranks sharing one GPU in a rehearsal: the node's compute)
+        # itself (ranks sharing one GPU in a rehearsal: the node's compute), in
+        # the form the step runs (interior beside the send packing or after it)
         c_pf, c_bl = cit["send_pack_ms"] / T, cit["boundary_ms"] / T
+        c_all = cit["compute_alone_split_ms"] if mine.get("split_interior") else cit["compute_alone_ms"]
         res["predicted_in_turn"] = {
-            "%g" % gbs: max(cit["compute_alone_ms"], c_pf + per_peer / (gbs * 1e9) * 1e3 + c_bl) for gbs in LINK_GBS}
+            "%g" % gbs: max(c_all, c_pf + per_peer / (gbs * 1e9) * 1e3 + c_bl) for gbs in LINK_GBS}
     if meas is not None and ex_meas is not None:
         longer = max(comp, ex_meas)
         res["contention_ms"] = meas - longer     # beyond a perfect overlap of the two measured pieces
@@ -1147,12 +1149,15 @@ def main(argv=None):
             if args.halo_tile > 0:
                 tiling = mdist.tile_widths(F_DIM, args.halo_tile)
             else:
-                # warm-up autotune: every rank times each tiling (one untimed step, then 3),
-                # the max over ranks decides -- the same choice on every rank
+                # warm-up autotune: every rank times each tiling, with the interior
+                # passes on the compute stream and beside the send packing on a
+                # second stream (split_interior), one untimed step then 3; the max
+                # over ranks decides -- the same choice on every rank
                 tune_out = torch.empty((plan.n_own, F_DIM), device=dev)
                 tile_tune = {}
-                for cand in HALO_TILINGS:
+                for cand, split in [(c, sp) for c in HALO_TILINGS for sp in (False, True)]:
                     tiles = make_tiles(cand)
+                    overlap.split_interior = split
                     overlap.step_tiled(tiles, tune_out, bias)
                     torch.cuda.synchronize()
                     barrier(world)
@@ -1163,12 +1168,14 @@ def main(argv=None):
                     tt = torch.tensor([(time.perf_counter() - t1) / 3 * 1e3], dtype=torch.float64)
                     tt = tt.to(dev) if dist.get_backend() == "nccl" else tt
                     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-                    tile_tune[str(cand)] = float(tt.item())
+                    tile_tune[str(cand) + (" split" if split else "")] = float(tt.item())
                     del tiles
                 del tune_out
-                tiling = min(HALO_TILINGS, key=lambda c: tile_tune[str(c)])
-                stage(rank, "halo tiling chosen in the warm-up: %s (max over ranks, ms/step: %s)"
-                      % (tiling, json.dumps(tile_tune)))
+                best = min(tile_tune, key=tile_tune.get)
+                tiling = next(c for c in HALO_TILINGS if best.split(" split")[0] == str(c))
+                overlap.split_interior = best.endswith(" split")
+                stage(rank, "halo tiling chosen in the warm-up: %s%s (max over ranks, ms/step: %s)"
+                      % (tiling, " + split interior" if overlap.split_interior else "", json.dumps(tile_tune)))
             x_tiles = make_tiles(tiling)
         elif not args.no_overlap:
             x_ov = overlap.local_buffer(F_DIM)
@@ -1375,7 +1382,8 @@ def main(argv=None):
             reps_d = max(3, min(args.steps, 10))
             mine["decomposed"] = overlap.decompose(tiles, out_buf, bias, reps_d, barrier=lambda: barrier(world))
             stage(rank, "step decomposition: %s" % json.dumps(mine["decomposed"]))
-            mine["compute_in_turn"] = overlap.compute_in_turn(tiles, out_buf, bias, reps_d,
+            mine["split_interior"] = bool(overlap.split_interior)
+            mine["compute_in_turn"] = overlap.compute_in_turn(tiles, out_buf, bias, max(7, reps_d),
                                                               barrier=lambda: barrier(world))
             stage(rank, "compute in turn: %s" % json.dumps(mine["compute_in_turn"]))
             mine["link_model"] = link_model(mine, rank, len(tiles))
@@ -1445,6 +1453,7 @@ def main(argv=None):
                       "halo_tile": args.halo_tile if sharded and not args.no_overlap else None,
                       "halo_tiles": [int(t.shape[1]) for t in x_tiles] if sharded and x_tiles is not None else None,
                       "halo_tile_autotune_ms": tile_tune if sharded else None,
+                      "split_interior": bool(overlap.split_interior) if sharded and overlap is not None else None,
                       "collective_timeout_s": COLLECTIVE_TIMEOUT_S if sharded else None,
                       "n_wave_tasks": csr.n_waves,
                       "per_rank": ranks,

@@ -676,6 +676,19 @@ class compute_stream:
         return False
 
 
+_SIDE_STREAMS = {}
+
+
+def _side_stream(device):
+    """A second non-default stream per device: OverlappedAggregation's interior
+    passes beside its send packing (split_interior)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    st = _SIDE_STREAMS.get(idx)
+    if st is None:
+        st = _SIDE_STREAMS[idx] = torch.cuda.Stream(device=idx)
+    return st
+
+
 class OverlappedAggregation:
     """GCN-style sharded aggregation with the halo exchange hidden behind the
     interior edges.
@@ -733,6 +746,11 @@ class OverlappedAggregation:
         self.w_bnd = self.g_bnd.dst.to_csr_order(w_bnd.contiguous()) if w_bnd is not None else None
         self.n_interior = int(ei_int.shape[1])
         self.n_boundary = int(ei_bnd.shape[1])
+        # step_tiled: run the interior passes on a second stream beside the send
+        # packing (both read only the rank's own rows); the boundary passes wait
+        # for them.  Off by default; bench.py's warm-up times both and keeps the
+        # faster (the two streams may land on one hardware queue).
+        self.split_interior = False
 
     def local_buffer(self, F, dtype=torch.float32, device=None):
         """[n_own + n_halo, F]: the owner writes rows [:n_own], the exchange the rest."""
@@ -820,12 +838,17 @@ class OverlappedAggregation:
             offs.append(offs[-1] + xt.shape[1])
         if offs[-1] != out.shape[1]:
             raise ValueError("step_tiled: tiles cover %d features, out has %d" % (offs[-1], out.shape[1]))
-        pending = []
-        rec("send")
         for xt in x_tiles:
             if xt.shape[0] != self.n_local_src:
                 raise ValueError("step_tiled: tiles have %d rows, this exchange needs %d (use local_tiles())"
                                  % (xt.shape[0], self.n_local_src))
+        last = self.n_boundary == 0   # the interior pass is the whole row (see step)
+        split = self.split_interior and out.is_cuda
+        if split:
+            start = torch.cuda.current_stream(out.device).record_event()
+        pending = []
+        rec("send")
+        for xt in x_tiles:
             own = xt[:plan.n_own]
             send = self._send(own)
             halo = xt[plan.n_own:]
@@ -837,13 +860,21 @@ class OverlappedAggregation:
                                               input_split_sizes=self.send_counts, group=group, async_op=True)
                 pending.append((work, send))
         rec("send")
-        rec("interior")
-        last = self.n_boundary == 0   # the interior pass is the whole row (see step)
-        for t, xt in enumerate(x_tiles):
-            b = bias[offs[t]:offs[t + 1]] if (last and bias is not None) else None
-            ops._aggregate(self.g_int.dst, "other", xt[:plan.n_own], self.w_int, "sum", 0, b,
-                           out=out[:, offs[t]:offs[t + 1]])
-        rec("interior")
+        if split:
+            # the interior passes on the side stream, ordered after what preceded
+            # the sends only: they run beside the send packing (the sends were
+            # queued first, so the exchange's inputs are not held back)
+            side = _side_stream(out.device)
+            side.wait_event(start)
+            with torch.cuda.stream(side):
+                rec("interior")
+                self._passes(x_tiles, out, bias, boundary=False)
+                rec("interior")
+            torch.cuda.current_stream(out.device).wait_stream(side)
+        else:
+            rec("interior")
+            self._passes(x_tiles, out, bias, boundary=False)
+            rec("interior")
         for t, xt in enumerate(x_tiles):
             work, _send = pending[t]
             rec("wait")
@@ -887,13 +918,37 @@ class OverlappedAggregation:
                 ops._aggregate(self.g_bnd.dst, "other", xt, self.w_bnd, "sum", _lib.MP_FLAG_INIT_FROM_OUT, b,
                                out=out[:, offs[t]:offs[t + 1]])
 
+    def _compute(self, x_tiles, out, bias, split=None):
+        """The step's device work without the exchange: send packing, interior
+        and boundary passes (the interior beside the packing on the side stream
+        when split, default self.split_interior), on the current stream."""
+        split = self.split_interior if split is None else split
+        n_own = self.plan.n_own
+        if not (split and out.is_cuda):
+            for xt in x_tiles:
+                self._send(xt[:n_own])
+            self._passes(x_tiles, out, bias)
+            return
+        cur = torch.cuda.current_stream(out.device)
+        start = cur.record_event()
+        for xt in x_tiles:
+            self._send(xt[:n_own])
+        side = _side_stream(out.device)
+        side.wait_event(start)
+        with torch.cuda.stream(side):
+            self._passes(x_tiles, out, bias, boundary=False)
+        cur.wait_stream(side)
+        self._passes(x_tiles, out, bias, interior=False)
+
     def compute_in_turn(self, x_tiles, out, bias=None, reps=5, group=None, barrier=None):
         """decompose()'s compute alone, one rank at a time: rank r times its
         send pack, interior and boundary passes with HIP events on the compute
         stream while every other rank waits at `barrier`.  Ranks that share
         one GPU (the gloo rehearsal) get the compute time each rank would have
-        on a GPU of its own; on a node it equals compute_only_ms.  Collective
-        over `group` (every rank calls it)."""
+        on a GPU of its own; on a node it equals compute_only_ms.  Also the
+        same work with the interior passes beside the send packing
+        (compute_alone_split_ms, split_interior).  Collective over `group`
+        (every rank calls it)."""
         rank, world = dist.get_rank(group), dist.get_world_size(group)
         n_own = self.plan.n_own
         res = None
@@ -907,7 +962,7 @@ class OverlappedAggregation:
                     self._send(xt[:n_own])
                 self._passes(x_tiles, out, bias)
                 ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-                tot = [0.0, 0.0, 0.0]
+                parts = [[], [], []]
                 for _ in range(reps):
                     ev[0].record()
                     for xt in x_tiles:
@@ -919,9 +974,22 @@ class OverlappedAggregation:
                     ev[3].record()
                     ev[3].synchronize()
                     for j in range(3):
-                        tot[j] += ev[j].elapsed_time(ev[j + 1])
-            res = {"reps": reps, "send_pack_ms": tot[0] / reps, "interior_ms": tot[1] / reps,
-                   "boundary_ms": tot[2] / reps, "compute_alone_ms": sum(tot) / reps}
+                        parts[j].append(ev[j].elapsed_time(ev[j + 1]))
+                # the same work with the interior passes on the side stream beside
+                # the send packing (split_interior), timed on the compute stream
+                split = []
+                for _ in range(reps):
+                    ev[0].record()
+                    self._compute(x_tiles, out, bias, split=True)
+                    ev[3].record()
+                    ev[3].synchronize()
+                    split.append(ev[0].elapsed_time(ev[3]))
+            # medians over the repetitions: ranks time-sharing one GPU see rare
+            # multi-ms stalls while the others sit idle at the barrier
+            med = [sorted(v)[len(v) // 2] for v in parts]
+            res = {"reps": reps, "send_pack_ms": med[0], "interior_ms": med[1], "boundary_ms": med[2],
+                   "compute_alone_ms": sum(med), "compute_alone_split_ms": sorted(split)[len(split) // 2],
+                   "statistic": "median over reps (per part)"}
         if barrier is not None:
             barrier()
         return res
@@ -934,7 +1002,9 @@ class OverlappedAggregation:
                              buffers packed beforehand: the links alone
                              (at one rank the splits are empty: ~0);
           compute_only_ms    packing + interior + boundary passes and no
-                             exchange (the halo rows keep their last values);
+                             exchange (the halo rows keep their last values;
+                             the interior beside the packing when
+                             split_interior, as the step runs them);
           serial_step_ms     pack, exchange and wait, then the interior and
                              boundary passes: the step without overlap;
           overlapped_step_ms step_tiled itself, timed the same way.
@@ -966,9 +1036,7 @@ class OverlappedAggregation:
                     w.wait()
 
         def compute_only():
-            for xt in x_tiles:
-                self._send(xt[:n_own])
-            self._passes(x_tiles, out, bias)
+            self._compute(x_tiles, out, bias)
 
         def serial():
             works = [self._exchange_async(xt, self._send(xt[:n_own]), group) for xt in x_tiles]

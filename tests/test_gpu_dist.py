@@ -68,6 +68,14 @@ def _worker(rank, world, port, q):
         out3 = torch.empty(plan.n_own, F, device=dev)
         ov.step_tiled(tiles, out3, bias)
         assert torch.equal(out3, out), "step_tiled must equal step"
+        # the interior passes on the side stream beside the send packing: the same
+        # arithmetic, so bitwise the same output, every time (ordering, not luck)
+        ov.split_interior = True
+        for _ in range(3):
+            out4 = torch.full_like(out, float("nan"))
+            ov.step_tiled(tiles, out4, bias)
+            assert torch.equal(out4, out), "split_interior must equal step"
+        ov.split_interior = False
         q.put((rank, err, bool(torch.equal(out2, want)), ov.n_interior, ov.n_boundary))
     finally:
         dist.destroy_process_group()
@@ -665,6 +673,10 @@ def _rccl_worker(rank, world, port, q):
         out_c = torch.empty(plan.n_own, F, device=dev)
         ovc.step_tiled(tc, out_c, bias)
         res["cover_step"] = float((out_c - ref).abs().max())
+        ovc.split_interior = True       # interior passes beside the send packing: bitwise the same
+        out_cs = torch.full_like(out_c, float("nan"))
+        ovc.step_tiled(tc, out_cs, bias)
+        res["cover_split_eq"] = bool(torch.equal(out_cs, out_c))
         # sharded GCNConv forward + backward, RCCL broadcast / all_reduce of the weights
         gout = torch.randn(N, F, generator=gen).to(dev)
         xi = torch.randn(N, Fi, generator=gen).to(dev)
@@ -740,7 +752,7 @@ def test_sharded_path_over_rccl_world_one():
     rows of X W and their gradients' return) -- with empty halo splits,
     against the single-GPU kernel, GCNConv and GATConv."""
     (rank, r), = _spawn(_rccl_worker, world=1, timeout=300)
-    assert r["step"] < 1e-5 and r["tiled_eq_step"], r
+    assert r["step"] < 1e-5 and r["tiled_eq_step"] and r["cover_split_eq"], r
     assert r["layer_out"] < 1e-5 and r["layer_gx"] < 1e-5 and r["layer_gw"] < 1e-5, r
     assert r["max_exact"], r
     assert r["slices_equal"], r
@@ -779,8 +791,10 @@ def test_bench_multi_rank_path_end_to_end():
     assert ex["overlap"] and ex["halo_rows_rank0"] > 0
     # the warm-up times both tilings (max over ranks) and keeps the faster
     tune = ex["halo_tile_autotune_ms"]
-    assert set(tune) == {"[128, 128]", "[64, 128, 64]"} and all(v > 0 for v in tune.values())
-    assert str(ex["halo_tiles"]) == min(tune, key=tune.get)
+    assert set(tune) == {"[128, 128]", "[64, 128, 64]", "[128, 128] split", "[64, 128, 64] split"}
+    assert all(v > 0 for v in tune.values())
+    best = min(tune, key=tune.get)    # tiling, and the interior passes beside the send packing or not
+    assert best.split(" split")[0] == str(ex["halo_tiles"]) and ex["split_interior"] == best.endswith(" split")
     assert ex["collective_timeout_s"] == 300
     assert 0 < ex["interior_edges_rank0"] < ex["edges_local_rank0"] < d["config"]["num_edges"]
     assert ex["verify"]["all_ranks_within_1e-5_bound"], ex["verify"]
@@ -794,6 +808,7 @@ def test_bench_multi_rank_path_end_to_end():
         assert dc["serial_step_ms"] > 0 and dc["overlapped_step_ms"] > 0
         # the compute timed one rank at a time (the GPU to itself): its parts add up
         cit = p["compute_in_turn"]
+        assert cit["compute_alone_split_ms"] > 0
         parts = cit["send_pack_ms"] + cit["interior_ms"] + cit["boundary_ms"]
         assert min(cit["send_pack_ms"], cit["interior_ms"], cit["boundary_ms"]) > 0, cit
         assert abs(parts - cit["compute_alone_ms"]) < 1e-6 * max(1.0, parts), cit
