@@ -151,6 +151,25 @@ def parse(argv=None):
 
 
 _LAST_STAGE = ["start"]
+_JSON_OUT = []
+
+
+def claim_stdout():
+    """Keep file descriptor 1 for the one JSON line: everything else this
+    process writes to stdout -- Python prints and native libraries alike (RCCL
+    prints a version banner on every rank, gloo its connection lines) -- goes
+    to stderr from here on."""
+    if not _JSON_OUT:
+        sys.stdout.flush()
+        _JSON_OUT.append(os.fdopen(os.dup(1), "w"))
+        os.dup2(2, 1)
+
+
+def emit(obj):
+    """The JSON line, alone on the real stdout."""
+    out = _JSON_OUT[0] if _JSON_OUT else sys.stdout
+    out.write(json.dumps(obj) + "\n")
+    out.flush()
 
 
 def stage(rank, msg):
@@ -226,7 +245,7 @@ def setup_dist(args):
         dist.all_gather_object(got, {"rank": rank, "local_rank": local, "world": dist.get_world_size()})
         stage(rank, "launch probe: %s" % got[rank])
         if rank == 0:
-            print(json.dumps({"launch_probe": got, "gpus": args.gpus}), flush=True)
+            emit({"launch_probe": got, "gpus": args.gpus})
         dist.destroy_process_group()
         raise SystemExit(0 if ok else 3)
     if world == 1 and not args.sharded:
@@ -680,7 +699,7 @@ def main_gat(args, rank, world, local):
             "extra": {"one_time_build_s": t_build, "graph_gen_s": t_gen, "per_rank": ranks, "verify": verify,
                       "collective_timeout_s": COLLECTIVE_TIMEOUT_S if sharded else None},
         }
-        print(json.dumps(line), flush=True)
+        emit(line)
     stage(rank, "done")
     if dist.is_initialized():
         dist.destroy_process_group()
@@ -820,7 +839,7 @@ def main_reddit(args, rank, world, local):
                   "n_wave_tasks": csr.n_waves, "verify": verify,
                   "note": "x is 238 MB: it fits the 256 MB Infinity Cache"},
     }
-    print(json.dumps(line), flush=True)
+    emit(line)
     stage(rank, "done")
 
 
@@ -1061,6 +1080,7 @@ def main(argv=None):
         sys.exit(2)
     if args.gpus > 1 and "RANK" not in os.environ:
         sys.exit(launch_ranks(args, argv))
+    claim_stdout()
     rank, world, local = setup_dist(args)
     sharded = dist.is_initialized()
     if sharded:
@@ -1463,7 +1483,7 @@ def main(argv=None):
                       "same_gpu_paths": ref_paths,
                       "agg_only_GBps_incl_fixup": alg_bytes / ((main_avg + fix_avg) * 1e-3) / 1e9},
         }
-        print(json.dumps(line), flush=True)
+        emit(line)
     stage(rank, "done")
     if dist.is_initialized():
         dist.destroy_process_group()

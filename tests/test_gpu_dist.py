@@ -770,8 +770,9 @@ def _run_bench(args, env_extra=None, timeout=540):
         env.pop(k, None)
     r = subprocess.run([sys.executable] + args, cwd=root, env=env, capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, r.stderr[-3000:]
-    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, r.stdout[-2000:]
+    # stdout holds the JSON line and nothing else (gloo's and RCCL's own prints go to stderr)
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout[-2000:]
     return json.loads(lines[0]), r.stderr
 
 
@@ -899,8 +900,9 @@ def test_bench_sharded_path_over_rccl_one_rank():
            "--sharded", "--steps", "3", "--warmup", "1"]
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
-    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, r.stdout[-2000:]
+    # the one JSON line alone on stdout: RCCL's version banner goes to stderr
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout[-2000:]
     d = json.loads(lines[0])
     assert d["n_gpus"] == 1 and d["config"]["num_edges"] == 62_094_512 and d["cpu_baseline"] is None
     assert d["config"]["parallelism"].startswith("dst-range shards x1")
