@@ -1,6 +1,8 @@
 """Print the current-state numbers DESIGN.md section 2 quotes, read from the
 committed round files (profiles/<round>_bench_*.json, _bench_configs.jsonl,
-_pmc_traffic*.json), so every number in those tables can be traced to a file.
+_pmc_traffic*.json), so every number in those tables can be traced to a file;
+and section 5.4's predicted multi-GPU curve from the gloo rehearsals'
+per-rank compute and the one-GPU RCCL contention.
     python tools/design_numbers.py [r04]
 """
 import json
@@ -17,7 +19,11 @@ def load(name):
     with open(path) as f:
         if name.endswith(".jsonl"):
             return {d["config"]: d for d in map(json.loads, f)}
-        return json.load(f)
+        text = f.read()
+        try:
+            return json.loads(text)
+        except ValueError:     # a bench line saved with a library's banner above it
+            return json.loads([ln for ln in text.splitlines() if ln.startswith("{")][-1])
 
 
 def main():
@@ -48,6 +54,32 @@ def main():
         out["cfg_" + k] = {kk: v for kk, v in d.items() if not isinstance(v, (dict, list)) and kk != "desc"}
         if "repeated_layer_first_occurrences" in d:
             out["cfg_" + k]["first_occurrences"] = d["repeated_layer_first_occurrences"]
+    # the predicted multi-GPU curve from the rehearsals' per-rank compute
+    # (GPU to itself), the one-GPU RCCL contention and the link model at 77 GB/s
+    one = load("%s_bench_rmat21.json" % rnd)
+    rc = load("%s_bench_sharded_rccl_one_rank.json" % rnd)
+    cont = {}
+    if rc:
+        for r in rc["extra"]["per_rank"][0].get("rccl_contention", []):
+            cont[r["P"]] = r["contention_ms"]
+    for P in (2, 4, 8):
+        d = load("%s_bench_rmat21_gloo%d_rehearsal.json" % (rnd, P))
+        if not d or "compute_in_turn" not in d["extra"]["per_rank"][0]:
+            continue
+        T = len(d["extra"]["halo_tiles"])
+        rows = []
+        for p in d["extra"]["per_rank"]:
+            c, lm = p["compute_in_turn"], p["link_model"]
+            chain = (c["send_pack_ms"] / T + lm["max_peer_bytes"] / 77e9 * 1e3 + c["boundary_ms"] / T)
+            rows.append((c["compute_alone_ms"], c["compute_alone_split_ms"], chain))
+        serial, split = max(r[0] for r in rows), max(r[1] for r in rows)
+        chain = max(r[2] for r in rows)
+        comp = min(serial, split) + cont.get(P, 0.0)
+        step = max(comp, chain)
+        out["curve_P%d" % P] = {"compute_in_turn_ms": serial, "compute_split_ms": split,
+                                "contention_ms": cont.get(P), "compute_plus_contention_ms": comp,
+                                "link_chain_77_ms": chain, "predicted_step_ms": step,
+                                "speedup_vs_1gpu": (one["ms_per_step"] / step) if one else None}
     print(json.dumps(out, indent=1))
 
 
