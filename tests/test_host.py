@@ -417,8 +417,10 @@ def test_bench_starts_its_own_ranks():
     import json
     r = _bench(["bench.py", "--gpus", "3", "--steps", "1"], {})
     assert r.returncode == 0, r.stderr[-3000:]
-    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, r.stdout
+    # the JSON line alone on stdout: gloo's connection lines (and RCCL's banner on
+    # a node) go to stderr (bench.claim_stdout)
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout
     d = json.loads(lines[0])
     assert d["gpus"] == 3
     assert sorted(p["rank"] for p in d["launch_probe"]) == [0, 1, 2]
