@@ -65,11 +65,12 @@ import torch  # noqa: E402  (importing torch does not initialise the GPU)
 import torch.distributed as dist  # noqa: E402
 
 F_DIM = 256
-# feature tilings the N>1 warm-up times (--halo-tile -1): two 128-feature tiles, or a
-# 64-feature tile first (the exchange starts after a quarter of the send pack) and last
-# (the step ends a quarter-boundary pass after the last exchange) -- the link-bound
-# P = 2 step's chain pack_0 + exchange + boundary_last
-HALO_TILINGS = ([128, 128], [64, 128, 64])
+# step forms the N>1 warm-up times (--halo-tile -1), each with the interior pass after
+# and beside the send packing (split_interior): (tile width, boundary as ONE launch after
+# the last tile arrives).  One launch per pass is the compute-bound P = 8 form; tiles whose
+# boundary pass runs per tile as it arrives pipeline the link-bound P = 2 chain
+# pack + exchange + boundary_last
+HALO_FORMS = ((256, True), (128, True), (128, False), (64, False))
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md chip table)
 # SURVEY 8(d) / BASELINE.md section 2 algorithmic bytes: every gathered x_j row
 # counted at full size, no cache-reuse credit.  Reported, but its ratio to the
@@ -78,6 +79,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md chip table)
 BYTES_PER_EDGE = 4 * F_DIM + 4 + 4   # x_j row + col + norm
 BYTES_PER_NODE = 4 * F_DIM + 4       # out row + rowptr
 COLLECTIVE_TIMEOUT_S = 300
+COMM_INIT_S = [None]     # the process group's first collectives (setup_dist), seconds
 T_START = time.perf_counter()
 
 
@@ -144,9 +146,12 @@ def parse(argv=None):
     ap.add_argument("--no-build-split", action="store_true",
                     help="N>1: do not take the one-time build apart into device-busy and host time")
     ap.add_argument("--halo-tile", type=int, default=-1,
-                    help="N>1: exchange and finish the boundary edges per feature tile of this width "
-                         "(pipelined); 0 = one exchange of whole rows; -1 (default) = chosen in the warm-up "
-                         "among HALO_TILINGS by timing each on this job's links (max over ranks)")
+                    help="N>1: exchange feature tiles of this width (64 / 128 / 256; 256 = whole rows), the "
+                         "boundary pass as one launch (see --boundary-per-tile); 0 = the unfused step of "
+                         "[own ; halo] rows; -1 (default) = the form chosen in the warm-up among HALO_FORMS "
+                         "by timing each on this job's links (max over ranks)")
+    ap.add_argument("--boundary-per-tile", action="store_true",
+                    help="with --halo-tile W: the boundary pass per tile as its halo arrives")
     return ap.parse_args(argv)
 
 
@@ -277,7 +282,22 @@ def setup_dist(args):
     if dist.get_world_size() != args.gpus:
         stage(rank, "ERROR: process group has %d ranks, --gpus %d" % (dist.get_world_size(), args.gpus))
         raise SystemExit(3)
-    stage(rank, "process group up: backend %s, world %d, device cuda:%d" % (dist.get_backend(), world, local))
+    # the communicator is set up here, before the one-time build (whose split
+    # would otherwise charge its creation to the first collective it makes):
+    # one all_reduce, all_gather and all_to_all of a few bytes on every rank
+    t0 = time.perf_counter()
+    dev = torch.device("cuda", local) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.ones(world, dtype=torch.int64, device=dev)
+    dist.all_reduce(t)
+    g = torch.empty(world * world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(g, t)
+    r = torch.empty_like(t)
+    dist.all_to_all_single(r, t)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    COMM_INIT_S[0] = time.perf_counter() - t0
+    stage(rank, "process group up: backend %s, world %d, device cuda:%d (communicator set up in %.2f s)"
+          % (dist.get_backend(), world, local, COMM_INIT_S[0]))
     return rank, world, local
 
 
@@ -914,14 +934,23 @@ class BuildMeter:
         return out
 
 
-def link_model(mine, rank, n_tiles):
+def form_name(width, one_boundary, split):
+    """Name of a fused step form in the bench line / autotune table."""
+    return "%d-wide tiles, boundary %s%s" % (width, "in one launch" if one_boundary else "per tile",
+                                             ", interior beside the packing" if split else "")
+
+
+def link_model(mine, rank, n_tiles, fused=False, boundary_per_tile=True):
     """The link-bandwidth model of this rank's step, from its own
     per-peer halo bytes and the compute it measured: each peer pair has its own
     xGMI link, so the exchange takes max over peers of max(bytes in, bytes out)
     / link rate; the step is the longer of the compute (pack + interior +
     boundary, measured alone) and the chain pack(first tile) + exchange +
-    boundary(last tile).  Predicted at 60 / 77 / 100 GB/s per link direction,
-    next to the measured overlapped step, with the verdict which piece sets it."""
+    boundary(last tile) -- in the fused step every tile is packed by one launch
+    (the first exchange starts after the whole pack) and, with the boundary in
+    one launch, the whole boundary pass follows the last tile.  Predicted at
+    60 / 77 / 100 GB/s per link direction, next to the measured overlapped
+    step, with the verdict which piece sets it."""
     row = F_DIM * 4
     peers = [q for q in range(len(mine["peers_in"])) if q != rank]
     per_peer = max([max(mine["peers_in"][q], mine["peers_out"][q]) * row for q in peers] or [0])
@@ -930,8 +959,10 @@ def link_model(mine, rank, n_tiles):
     if comp is None:
         return None
     T = max(1, n_tiles)
-    pack_first = mine.get("send_pack_ms", 0.0) / T
-    bnd_last = mine.get("boundary_ms", 0.0) / T
+    Tp = 1 if fused else T
+    Tb = T if boundary_per_tile else 1
+    pack_first = mine.get("send_pack_ms", 0.0) / Tp
+    bnd_last = mine.get("boundary_ms", 0.0) / Tb
     pred = {}
     for gbs in LINK_GBS:
         ex = per_peer / (gbs * 1e9) * 1e3
@@ -949,7 +980,7 @@ def link_model(mine, rank, n_tiles):
         # the same model on the compute each rank measured with the GPU to
         # itself (ranks sharing one GPU in a rehearsal: the node's compute), in
         # the form the step runs (interior beside the send packing or after it)
-        c_pf, c_bl = cit["send_pack_ms"] / T, cit["boundary_ms"] / T
+        c_pf, c_bl = cit["send_pack_ms"] / Tp, cit["boundary_ms"] / Tb
         c_all = cit["compute_alone_split_ms"] if mine.get("split_interior") else cit["compute_alone_ms"]
         res["predicted_in_turn"] = {
             "%g" % gbs: max(c_all, c_pf + per_peer / (gbs * 1e9) * 1e3 + c_bl) for gbs in LINK_GBS}
@@ -1155,48 +1186,44 @@ def main(argv=None):
             cover=not (args.no_halo_cover or args.no_overlap)))
         torch.cuda.synchronize()
         t_exchange_plan = time.perf_counter() - t0 - t_shards
-        x_tiles = x_ov = None
+        bufs = x_ov = None
         tile_tune = None
-
-        def make_tiles(tiling):
-            tiles = overlap.local_tiles(F_DIM, tiling)
-            c0 = 0
-            for xt in tiles:
-                xt[:plan.n_own].copy_(x_full[plan.lo:plan.hi, c0:c0 + xt.shape[1]])
-                c0 += xt.shape[1]
-            return tiles
         if args.halo_tile != 0 and not args.no_overlap:
             if args.halo_tile > 0:
-                tiling = mdist.tile_widths(F_DIM, args.halo_tile)
+                form = (args.halo_tile, not args.boundary_per_tile)
             else:
-                # warm-up autotune: every rank times each tiling, with the interior
-                # passes on the compute stream and beside the send packing on a
-                # second stream (split_interior), one untimed step then 3; the max
-                # over ranks decides -- the same choice on every rank
+                # warm-up autotune: every rank times each step form (tile width x
+                # boundary as one launch or per tile), with the interior pass after
+                # and beside the send packing (split_interior), one untimed step
+                # then 3; the max over ranks decides -- the same choice on every rank
                 tune_out = torch.empty((plan.n_own, F_DIM), device=dev)
                 tile_tune = {}
-                for cand, split in [(c, sp) for c in HALO_TILINGS for sp in (False, True)]:
-                    tiles = make_tiles(cand)
-                    overlap.split_interior = split
-                    overlap.step_tiled(tiles, tune_out, bias)
+                for (width, one), split in [(c, sp) for c in HALO_FORMS for sp in (False, True)]:
+                    tb = overlap.halo_buffers(F_DIM, width)
+                    overlap.split_interior, overlap.one_boundary_launch = split, one
+                    overlap.step_fused(x, tb, tune_out, bias)
                     torch.cuda.synchronize()
                     barrier(world)
                     t1 = time.perf_counter()
                     for _ in range(3):
-                        overlap.step_tiled(tiles, tune_out, bias)
+                        overlap.step_fused(x, tb, tune_out, bias)
                     torch.cuda.synchronize()
                     tt = torch.tensor([(time.perf_counter() - t1) / 3 * 1e3], dtype=torch.float64)
                     tt = tt.to(dev) if dist.get_backend() == "nccl" else tt
                     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-                    tile_tune[str(cand) + (" split" if split else "")] = float(tt.item())
-                    del tiles
+                    tile_tune[form_name(width, one, split)] = float(tt.item())
+                    del tb
                 del tune_out
                 best = min(tile_tune, key=tile_tune.get)
-                tiling = next(c for c in HALO_TILINGS if best.split(" split")[0] == str(c))
-                overlap.split_interior = best.endswith(" split")
-                stage(rank, "halo tiling chosen in the warm-up: %s%s (max over ranks, ms/step: %s)"
-                      % (tiling, " + split interior" if overlap.split_interior else "", json.dumps(tile_tune)))
-            x_tiles = make_tiles(tiling)
+                width, one, split = next((w_, o_, s_) for (w_, o_), s_ in
+                                         [(c, sp) for c in HALO_FORMS for sp in (False, True)]
+                                         if form_name(w_, o_, s_) == best)
+                form = (width, one)
+                overlap.split_interior = split
+                stage(rank, "step form chosen in the warm-up: %s (max over ranks, ms/step: %s)"
+                      % (best, json.dumps(tile_tune)))
+            overlap.one_boundary_launch = form[1]
+            bufs = overlap.halo_buffers(F_DIM, form[0])
         elif not args.no_overlap:
             x_ov = overlap.local_buffer(F_DIM)
             x_ov[:plan.n_own].copy_(x_full[plan.lo:plan.hi])
@@ -1241,8 +1268,8 @@ def main(argv=None):
                 ev[i][2].record()
         elif args.no_overlap:
             aggregate(plan.exchange_into(x_local, ops.gather_rows), out=out_buf)
-        elif x_tiles is not None:
-            overlap.step_tiled(x_tiles, out_buf, bias, events=None if i is None else step_events[i])
+        elif bufs is not None:
+            overlap.step_fused(x, bufs, out_buf, bias, events=None if i is None else step_events[i])
         else:
             overlap.step(x_ov, out_buf, bias)
 
@@ -1391,22 +1418,25 @@ def main(argv=None):
             mine.update({"cover_pulled_rows": overlap.cover.n_pull_rows,
                          "cover_partial_rows": overlap.cover.n_push_rows,
                          "cover_push_edges": overlap.cover.n_push_edges})
-        if x_tiles is not None:
+        if bufs is not None:
             n = max(1, len(step_events))
             mine.update({"send_pack_ms": sum(span(e, "send") for e in step_events) / n,
                          "interior_ms": sum(span(e, "interior") for e in step_events) / n,
                          "exchange_exposed_ms": sum(span(e, "wait") for e in step_events) / n,
                          "boundary_ms": sum(span(e, "boundary") for e in step_events) / n})
         if not args.no_overlap:
-            tiles = x_tiles if x_tiles is not None else [x_ov]
+            form = (x, bufs) if bufs is not None else [x_ov]
             reps_d = max(3, min(args.steps, 10))
-            mine["decomposed"] = overlap.decompose(tiles, out_buf, bias, reps_d, barrier=lambda: barrier(world))
+            mine["decomposed"] = overlap.decompose(form, out_buf, bias, reps_d, barrier=lambda: barrier(world))
             stage(rank, "step decomposition: %s" % json.dumps(mine["decomposed"]))
             mine["split_interior"] = bool(overlap.split_interior)
-            mine["compute_in_turn"] = overlap.compute_in_turn(tiles, out_buf, bias, max(7, reps_d),
+            mine["one_boundary_launch"] = bool(overlap.one_boundary_launch) if bufs is not None else None
+            mine["compute_in_turn"] = overlap.compute_in_turn(form, out_buf, bias, max(7, reps_d),
                                                               barrier=lambda: barrier(world))
             stage(rank, "compute in turn: %s" % json.dumps(mine["compute_in_turn"]))
-            mine["link_model"] = link_model(mine, rank, len(tiles))
+            mine["link_model"] = link_model(mine, rank, bufs.n_tiles if bufs is not None else 1,
+                                            fused=bufs is not None,
+                                            boundary_per_tile=bufs is not None and not overlap.one_boundary_launch)
             stage(rank, "link model: %s" % json.dumps(mine["link_model"]))
         if args.emulate_peers:
             if world != 1 or dist.get_backend() != "nccl":
@@ -1471,10 +1501,14 @@ def main(argv=None):
                       "interior_edges_rank0": overlap.n_interior if sharded else E_local,
                       "overlap": sharded and not args.no_overlap,
                       "halo_tile": args.halo_tile if sharded and not args.no_overlap else None,
-                      "halo_tiles": [int(t.shape[1]) for t in x_tiles] if sharded and x_tiles is not None else None,
+                      "halo_tiles": [bufs.width] * bufs.n_tiles if sharded and bufs is not None else None,
+                      "step_form": ("fused: one launch per pass, %s" % form_name(bufs.width, overlap.one_boundary_launch,
+                                                                          overlap.split_interior))
+                      if sharded and bufs is not None else None,
                       "halo_tile_autotune_ms": tile_tune if sharded else None,
                       "split_interior": bool(overlap.split_interior) if sharded and overlap is not None else None,
                       "collective_timeout_s": COLLECTIVE_TIMEOUT_S if sharded else None,
+                      "comm_init_s": COMM_INIT_S[0] if sharded else None,
                       "n_wave_tasks": csr.n_waves,
                       "per_rank": ranks,
                       "verify": verify,

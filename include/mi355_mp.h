@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MP_ABI_VERSION 6
+#define MP_ABI_VERSION 7
 
 /* status codes */
 #define MP_OK 0
@@ -56,6 +56,8 @@ extern "C" {
 #define MP_FLAG_INIT_FROM_OUT 1 /* torch_scatter `out=` given: reduce into out's values */
 #define MP_FLAG_PYG_MASK 2      /* torch_geometric.utils.scatter_: max -> out<-10000 := 0,
                                    min -> out>10000 := 0 */
+#define MP_FLAG_SKIP_EMPTY 4    /* (ABI 7, mp_aggregate_tiles_f32 only) rows with no slot are left
+                                   untouched: no store, no bias */
 
 /* aggregate stages (bench times the main kernel on its own) */
 #define MP_STAGE_MAIN 1
@@ -203,6 +205,30 @@ int mp_aggregate_f32(const mp_csr* g, const float* w, const float* x,
                      const float* bias, float* out, int64_t ldo,
                      int64_t* arg_out, void* slab, size_t slab_bytes,
                      int32_t stages, void* stream);
+
+/* mp_aggregate_f32 for sum / mean over TILE-MAJOR operands (ABI 7): the
+ * sharded step's feature tiles (mi355_mp.dist.OverlappedAggregation) in ONE
+ * launch per pass instead of one launch per tile.  With x_tile_w > 0, feature f
+ * of row r of x lives at x[(f / x_tile_w) * x_tile_stride + r * x_tile_w +
+ * f % x_tile_w] (ldx ignored), else at x[r * ldx + f]; likewise out with
+ * out_tile_w / out_tile_stride (ldo ignored), else out[r * ldo + f].  Tile
+ * widths are multiples of 64 dividing F (F a multiple of 64) and tiles do not
+ * overlap (stride >= rows x width: g->n_cols rows of x, g->n_rows rows of
+ * out); bias is [F] as ever, and bias_rows (NULL, or int32 [g->n_rows])
+ * limits it to the rows r with bias_rows[r] != 0.  flags: MP_FLAG_INIT_FROM_OUT
+ * and / or MP_FLAG_SKIP_EMPTY (rows without slots keep out as it is).  The graph
+ * needs its column array.  Per row and feature the arithmetic is exactly
+ * mp_aggregate_f32's on the same values laid out row-major: the results are
+ * bitwise equal.  Replaces, for one rank's step, the per-tile
+ * scatter_add(norm * x_j) of the reference's propagate (gcn_conv.py [U5]). */
+int mp_aggregate_tiles_f32(const mp_csr* g, const float* w, const float* x,
+                           int64_t ldx, int32_t x_tile_w, int64_t x_tile_stride,
+                           int32_t F, int32_t reduce, int32_t flags,
+                           const float* bias, const int32_t* bias_rows,
+                           float* out, int64_t ldo,
+                           int32_t out_tile_w, int64_t out_tile_stride,
+                           void* slab, size_t slab_bytes, int32_t stages,
+                           void* stream);
 
 /* Name (demangled) of the main kernel mp_aggregate_f32 would launch for these
  * arguments (same shape selection, nothing launched), written to buf.  Lets a
@@ -511,11 +537,16 @@ int mp_gat_alpha_f32(const int64_t* src_idx, const int64_t* dst_idx,
  * (int32, non-decreasing, pptr[n_rows] <= n_parts) and every pidx entry in
  * [0, n_parts) are the caller's contract (device arrays, not read on the host).
  * C % 4 == 0; out, part_out, bias, agg2 16-byte aligned, leading dimensions
- * multiples of 4.  (ABI 6) */
+ * multiples of 4.  Extents (ABI 7): part_out_bytes >= ((n_parts - 1) * ldp +
+ * H*C) * 4 and part_stats_bytes >= n_parts * H * 8 when n_parts > 0 (the
+ * pidx range itself is checked by the host that builds the merge list:
+ * mi355_mp.gat_cover.GatHaloCover).  Head of any width: a head may span two of
+ * the kernel's 256-feature chunks (the merged stats are written after every
+ * chunk of the row has read them). */
 int mp_gat_merge_partials_f32(int64_t n_rows, int32_t H, int32_t C, const int32_t* pptr, const int32_t* pidx,
-                              int64_t n_parts, const float* part_out, int64_t ldp, const float* part_stats,
-                              const float* bias, float* out, int64_t ldo, float* row_stats, float* agg2,
-                              float* row_s2, void* stream);
+                              int64_t n_parts, const float* part_out, size_t part_out_bytes, int64_t ldp,
+                              const float* part_stats, size_t part_stats_bytes, const float* bias, float* out,
+                              int64_t ldo, float* row_stats, float* agg2, float* row_s2, void* stream);
 
 /* ---- self-loop rewrites (PyG 1.4.3 utils.loop [U4]) -----
  * Output edge order is upstream's: the kept edges in original order, then the

@@ -99,6 +99,7 @@ struct AggArgs {
   int32_t smem;      // flat sum/mean kernel: slot columns/weights through scalar loads (k_agg_flat SM)
   int32_t seq_tiles; // flat kernel: feature tiles one after another on all XCDs (no XCD-affine map)
   int32_t far;       // flat SM kernel: x larger than the Infinity Cache (batches of kU_Vec1Far)
+  int32_t force_flat;  // mp_aggregate_tiles_f32: the scalar-batch flat kernel whatever the layout
   // features
   const float* w;
   const float* x;
@@ -143,7 +144,38 @@ struct AggArgs {
   uint64_t drop_seed;
   uint32_t drop_thr;
   float drop_scale;
+  // tile-major operands (mp_aggregate_tiles_f32; 0 = row-major): feature f of
+  // row r at x[(f / x_tw) * x_ts + r * x_tw + f % x_tw], likewise out with o_tw
+  // / o_ts.  Widths are multiples of 64, so a flat-kernel block's 64-feature
+  // tile lies inside one operand tile.
+  int32_t x_tw;
+  int32_t o_tw;
+  int64_t x_ts;
+  int64_t o_ts;
+  // per-row bias flags (mp_aggregate_tiles_f32; NULL = every row): the bias is
+  // added to row r only where bias_rows[r] != 0
+  const int32_t* bias_rows;
 };
+
+// This block's view of tile-major operands: x_tile / ldx_tile / fx0 address
+// feature f of row r at x_tile[r * ldx_tile + f - fx0]; out is rebased in place
+// so that out + r * ldo + f addresses it (fb: the block's first feature).
+__device__ __forceinline__ void tile_view(AggArgs& p, int fb, const float*& x_tile, int64_t& ldx_tile, int& fx0) {
+  x_tile = p.x;
+  ldx_tile = p.ldx;
+  fx0 = 0;
+  if (p.x_tw) {
+    const int t = fb / p.x_tw;
+    x_tile = p.x + (int64_t)t * p.x_ts;
+    ldx_tile = p.x_tw;
+    fx0 = t * p.x_tw;
+  }
+  if (p.o_tw) {
+    const int t = fb / p.o_tw;
+    p.out += (int64_t)t * (p.o_ts - p.o_tw);
+    p.ldo = p.o_tw;
+  }
+}
 
 // ---------------------------------------------------------------------------
 // GAT attention dropout (GATConv training: `F.dropout(alpha, p)` after the
@@ -252,13 +284,13 @@ struct SumRed {
     for (int k = 0; k < VEC; ++k) q.v[k] = acc[k];
     return q;
   }
-  __device__ __forceinline__ void finish(const AggArgs& p, int64_t row, int64_t cnt, int f, bool act) {
+  __device__ __forceinline__ void finish(const AggArgs& p, int64_t row, int64_t cnt, int f, bool act, bool with_bias = true) {
     if (!act) return;
     Frag<VEC> o;
     float c = (float)(cnt > 0 ? cnt : 1);
 #pragma unroll
     for (int k = 0; k < VEC; ++k) o.v[k] = MEAN ? __fdiv_rn(acc[k], c) : acc[k];
-    if (p.bias) {
+    if (p.bias && with_bias) {
       Frag<VEC> b = load_frag<VEC>(p.bias + f);
 #pragma unroll
       for (int k = 0; k < VEC; ++k) o.v[k] = __fadd_rn(o.v[k], b.v[k]);
@@ -358,7 +390,7 @@ struct ArgRed {
     }
     return q;
   }
-  __device__ __forceinline__ void finish(const AggArgs& p, int64_t row, int64_t, int f, bool act) {
+  __device__ __forceinline__ void finish(const AggArgs& p, int64_t row, int64_t, int f, bool act, bool with_bias = true) {
     if (!act) return;
     Frag<VEC> o;
     const bool from_out = (p.flags & MP_FLAG_INIT_FROM_OUT) != 0;
@@ -605,7 +637,7 @@ struct GatRed {
     }
     return q;
   }
-  __device__ __forceinline__ void finish(const AggArgs& p, int64_t row, int64_t, int f, bool act) {
+  __device__ __forceinline__ void finish(const AggArgs& p, int64_t row, int64_t, int f, bool act, bool with_bias = true) {
     if constexpr (ND) {
       if (need_ad) node_scores(p);  // a row without slots (the fix-up never begins a row: need_ad false)
     }
@@ -703,7 +735,7 @@ struct GatMaxRed {
     for (int k = 0; k < VEC; ++k) q.v[k] = acc[k];
     return q;
   }
-  __device__ __forceinline__ void finish(const AggArgs& p, int64_t row, int64_t, int f, bool act) {
+  __device__ __forceinline__ void finish(const AggArgs& p, int64_t row, int64_t, int f, bool act, bool with_bias = true) {
     if (!act) return;
 #pragma unroll
     for (int k = 0; k < VEC; ++k)
@@ -741,7 +773,7 @@ struct GatDenRed : GatMaxRed<VEC> {
 #pragma unroll
     for (int k = 0; k < VEC; ++k) acc[k] = __fadd_rn(acc[k], q.v[k]);
   }
-  __device__ __forceinline__ void finish(const AggArgs& p, int64_t row, int64_t, int f, bool act) {
+  __device__ __forceinline__ void finish(const AggArgs& p, int64_t row, int64_t, int f, bool act, bool with_bias = true) {
     if (!act) return;
 #pragma unroll
     for (int k = 0; k < VEC; ++k)
@@ -875,7 +907,7 @@ struct GatBwdRed {
     q.d = dacc;
     return q;
   }
-  __device__ __forceinline__ void finish(const AggArgs& p, int64_t row, int64_t, int f, bool act) {
+  __device__ __forceinline__ void finish(const AggArgs& p, int64_t row, int64_t, int f, bool act, bool with_bias = true) {
     if (!act) return;
     const float* at = p.att + (int64_t)h * 2 * p.C + p.C + (f % p.C);
     Frag<VEC> o;
@@ -996,7 +1028,7 @@ struct GatBwdWideRed {
     q.s = sc;
     return q;
   }
-  __device__ __forceinline__ void finish(const AggArgs& p, int64_t row, int64_t, int f, bool act) {
+  __device__ __forceinline__ void finish(const AggArgs& p, int64_t row, int64_t, int f, bool act, bool with_bias = true) {
     if (!act) return;
     Frag<VEC> o;
 #pragma unroll
@@ -1505,6 +1537,13 @@ __device__ __forceinline__ void scalar_batch(const T* a, int64_t n, int64_t e, T
   }
 }
 
+// MP_FLAG_SKIP_EMPTY (mp_aggregate_tiles_f32 only): an owned row with no slot
+// is left untouched -- no load, no store, no bias.  The sharded step's boundary
+// pass (INIT_FROM_OUT) skips its rows without boundary edges this way: their
+// read-modify-write of out cost the pass as much as its gathers (measured,
+// tools/exp_boundary.py), and the interior pass adds their bias instead
+// (AggArgs::bias_rows).  (An out prefetch issued with each batch's gathers was
+// also measured there: slower, not kept -- DESIGN Appendix A.)
 template <class Red, int VEC, int U, int L, bool GA = false, bool SM = false>
 __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
   static_assert(!Red::kGat && !Red::kGatB && !Red::kHW, "flat loop: sum/mean/max/min reducers");
@@ -1528,10 +1567,15 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
   if (w >= p.n_waves) return;
   const int f = tile * L * VEC + gl * VEC;
   const bool act = f < p.F;
-  const uint32_t foff = (uint32_t)(act ? f : 0) * 4u;
-  const char* xb = reinterpret_cast<const char*>(p.x);
-  const int64_t ldxb = p.ldx * 4;
+  const float* x_tile;
+  int64_t ldx_tile;
+  int fx0;
+  tile_view(p, tile * L * VEC, x_tile, ldx_tile, fx0);
+  const uint32_t foff = (uint32_t)(act ? f - fx0 : 0) * 4u;
+  const char* xb = reinterpret_cast<const char*>(x_tile);
+  const int64_t ldxb = ldx_tile * 4;
   [[maybe_unused]] __amdgpu_buffer_rsrc_t xr;
+  const bool skip_empty = (p.flags & MP_FLAG_SKIP_EMPTY) != 0;
 
   const int r_first = GR::un(p.wave_row[w]);
   const int r_last = GR::un(p.wave_row[w + 1]);
@@ -1539,6 +1583,12 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
   const int64_t e_end = GR::un(p.wave_slot[w + 1]);
 
   Red red(p, f, act);
+  // an owned row opens (rs_ / re_: its slot range); an empty one is skipped
+  // (no load of out) under MP_FLAG_SKIP_EMPTY
+  auto open_row = [&](int rr, int64_t rs_, int64_t re_) {
+    red.begin(p, rr, !(skip_empty && re_ == rs_), f, act);
+  };
+
   std::conditional_t<GA, GatAlphaWin, SlotWin<Red::kW, Red::kEid, L>> win;
   if constexpr (GA) {
     __shared__ float ga_lds[kWavesPerBlock][64 * 4];
@@ -1548,18 +1598,27 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
   }
   [[maybe_unused]] int c_nxt[U];
   if constexpr (SM) {
-    xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
+    xr = __builtin_amdgcn_make_buffer_rsrc((void*)x_tile, (short)0, (int)p.x_bytes, 0x00020000);
     if (e_begin < e_end) scalar_batch<U>(p.col, p.n_edges, e_begin, c_nxt);
   }
+  // row window: rowptr (and the per-row bias flags, bias_rows) of rows
+  // [rbase, rbase + L) across the lanes.  A refill for row pointer r starts
+  // at r - 1, so the row that r closes -- the one open -- stays in the window
+  // until it finishes (its bias flag is read then).
   int rbase = r_first;
   int rp = (rbase + gl <= p.n_rows) ? p.rowptr[rbase + gl] : 0;
-  // row end / start of row r (r >= rbase), refilling the window when needed
+  int bw = (p.bias_rows && rbase + gl < p.n_rows) ? p.bias_rows[rbase + gl] : 1;
   auto row_ptr = [&](int r) -> int64_t {
     if (r - rbase > L - 1) {
-      rbase = r;
+      rbase = r - 1;
       rp = (rbase + gl <= p.n_rows) ? p.rowptr[rbase + gl] : 0;
+      if (p.bias_rows) bw = (rbase + gl < p.n_rows) ? p.bias_rows[rbase + gl] : 1;
     }
     return GR::bc(rp, r - rbase);
+  };
+  auto finish_row = [&](int rr, int64_t cnt) {
+    if (skip_empty && cnt == 0) return;
+    red.finish(p, rr, cnt, f, act, p.bias_rows == nullptr || GR::bc(bw, rr - rbase) != 0);
   };
 
   // current row: the continuation of an earlier task's row, or an owned row
@@ -1571,7 +1630,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
     red.begin(p, r_first - 1, false, f, act);
   } else if (r < r_last) {
     re = row_ptr(r + 1);
-    red.begin(p, r, true, f, act);
+    open_row(r, rs, re);
   }
   // close the current row at slot k (k >= its end) and open the next one(s)
   auto advance = [&](int64_t k) {
@@ -1580,7 +1639,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
         if (act) red.save(slab_ref(p, 2 * (int64_t)w, f, red), false);
         cont = false;
       } else {
-        red.finish(p, r, re - rs, f, act);
+        finish_row(r, re - rs);
         ++r;
       }
       if (r >= r_last) {  // cannot happen for a valid schedule: never open a row past the task
@@ -1589,7 +1648,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
       }
       rs = re;
       re = row_ptr(r + 1);
-      red.begin(p, r, true, f, act);
+      open_row(r, rs, re);
     }
   };
 
@@ -1655,12 +1714,12 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
     if (r < r_last) {
       rs = ce;
       re = row_ptr(r + 1);
-      red.begin(p, r, true, f, act);
+      open_row(r, rs, re);
     }
   }
   while (r < r_last) {
     if (re <= e_end) {
-      red.finish(p, r, re - rs, f, act);
+      finish_row(r, re - rs);
     } else {
       if (act) red.save(slab_ref(p, 2 * (int64_t)w + 1, f, red), false);
     }
@@ -1668,7 +1727,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
     if (r < r_last) {
       rs = re;
       re = row_ptr(r + 1);
-      red.begin(p, r, true, f, act);
+      open_row(r, rs, re);
     }
   }
 }
@@ -1689,6 +1748,12 @@ __global__ __launch_bounds__(kBlock) void k_agg_fixup(AggArgs p) {
   const int f = (int)blockIdx.y * 64 * VEC + lane * VEC;
   const bool act = f < p.F;
   const int fs = act ? f : 0;
+  if (p.o_tw) {  // tile-major out (the host runs this fix-up 64 features wide then)
+    const float* xt;
+    int64_t ldt;
+    int fx0;
+    tile_view(p, (int)blockIdx.y * 64 * VEC, xt, ldt, fx0);
+  }
   const int last = uni(p.split_waves[i]);
   const int r = uni(p.wave_row[last]) - 1;
   const int64_t rs = uni(p.rowptr[r]);
@@ -1729,7 +1794,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_fixup(AggArgs p) {
   for (int q = 1; q < kWavesPerBlock; ++q)
     if (has[q]) red.merge(lds[q - 1][lane]);
   if constexpr (Red::kGatB) red.row_terms(p, r);
-  red.finish(p, r, re - rs, f, act);
+  red.finish(p, r, re - rs, f, act, p.bias_rows == nullptr || p.bias_rows[r] != 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -1989,6 +2054,18 @@ static void fill_graph(AggArgs& a, const mp_csr* g) {
 static int aggregate_dispatch(AggArgs& a, const mp_csr* g, int reduce, int stages, hipStream_t s) {
   const int F = a.F;
   const bool is_arg = reduce == MP_REDUCE_MAX || reduce == MP_REDUCE_MIN;
+  if (a.x_tw || a.o_tw || a.force_flat) {
+    // tile-major operands (mp_aggregate_tiles_f32, arguments checked there): the
+    // scalar-batch flat kernel with 64-feature tiles, its fix-up 64 wide
+    const int64_t xbytes = (int64_t)g->n_cols * (a.x_tw ? a.x_tw : a.ldx) * 4;
+    a.flat = 1;
+    a.smem = 1;
+    a.x_bytes = (uint32_t)xbytes;
+    a.far = xbytes > tuned(g_tune.flat_far_min_bytes) ? 1 : 0;
+    a.seq_tiles = (int32_t)tuned(g_tune.flat_seq_tiles);
+    a.fix4 = 0;
+    return dispatch_reduce<1>(a, reduce, stages, s, 64);
+  }
   Shape sh = pick_shape(F, a.ldx, a.x, a.ldo, a.out);
   // flat kernel lane width: 64-feature tiles (VEC=1) for sum/mean, where an
   // XCD's L2 holding one narrow tile of the hot rows pays (Reddit-scale x of
@@ -2098,6 +2175,68 @@ int mp_aggregate_f32(const mp_csr* g, const float* w, const float* x, int64_t ld
   size_t v = align_up(2 * (size_t)g->n_waves * (size_t)a.slab_ld * 4, 256);
   a.slab_v = (float*)slab;
   a.slab_a = is_arg ? (int32_t*)((char*)slab + v) : nullptr;
+  return aggregate_dispatch(a, g, reduce, stages, as_stream(stream));
+}
+
+int mp_aggregate_tiles_f32(const mp_csr* g, const float* w, const float* x, int64_t ldx, int32_t x_tile_w,
+                           int64_t x_tile_stride, int32_t F, int32_t reduce, int32_t flags, const float* bias,
+                           const int32_t* bias_rows, float* out, int64_t ldo, int32_t out_tile_w,
+                           int64_t out_tile_stride, void* slab, size_t slab_bytes, int32_t stages, void* stream) {
+  MP_DEVICE_GUARD(stream);
+  int rc = check_graph(g, "mp_aggregate_tiles_f32");
+  if (rc) return rc;
+  MP_CHECK_ARG(reduce == MP_REDUCE_SUM || reduce == MP_REDUCE_MEAN, "mp_aggregate_tiles_f32: sum or mean only");
+  MP_CHECK_ARG(F > 0 && F % 64 == 0, "mp_aggregate_tiles_f32: F must be a positive multiple of 64");
+  MP_CHECK_ARG((flags & ~(MP_FLAG_INIT_FROM_OUT | MP_FLAG_SKIP_EMPTY)) == 0,
+               "mp_aggregate_tiles_f32: flags may only hold INIT_FROM_OUT and SKIP_EMPTY");
+  MP_CHECK_ARG(out != nullptr && (g->n_edges == 0 || (x != nullptr && g->col != nullptr && g->n_cols > 0)),
+               "mp_aggregate_tiles_f32: null x/out or a graph without columns");
+  MP_CHECK_ARG(x_tile_w >= 0 && out_tile_w >= 0, "mp_aggregate_tiles_f32: negative tile width");
+  const int64_t ncols = g->n_cols > 0 ? g->n_cols : 0;
+  if (x_tile_w) {
+    MP_CHECK_ARG(x_tile_w % 64 == 0 && F % x_tile_w == 0 && x_tile_stride >= ncols * x_tile_w,
+                 "mp_aggregate_tiles_f32: x tiles must be 64k features wide, divide F, and not overlap "
+                 "(stride %lld < %lld rows x %d)", (long long)x_tile_stride, (long long)ncols, (int)x_tile_w);
+  } else {
+    MP_CHECK_ARG(ldx >= F, "mp_aggregate_tiles_f32: ldx < F");
+  }
+  MP_CHECK_ARG(ncols * (x_tile_w ? x_tile_w : ldx) * 4 <= 0xFFFFFFF0LL,
+               "mp_aggregate_tiles_f32: one x tile must span < 4 GiB");
+  if (out_tile_w) {
+    MP_CHECK_ARG(out_tile_w % 64 == 0 && F % out_tile_w == 0 && out_tile_stride >= g->n_rows * out_tile_w,
+                 "mp_aggregate_tiles_f32: out tiles must be 64k features wide, divide F, and not overlap "
+                 "(stride %lld < %lld rows x %d)", (long long)out_tile_stride, (long long)g->n_rows,
+                 (int)out_tile_w);
+  } else {
+    MP_CHECK_ARG(ldo >= F, "mp_aggregate_tiles_f32: ldo < F");
+  }
+  MP_CHECK_ARG(slab != nullptr && slab_bytes >= mp_aggregate_slab_bytes(g, F, reduce),
+               "mp_aggregate_tiles_f32: slab workspace too small (%zu < %zu)", slab_bytes,
+               mp_aggregate_slab_bytes(g, F, reduce));
+  AggArgs a{};
+  fill_graph(a, g);
+  a.F = F;
+  a.w = w;
+  a.x = x;
+  a.ldx = x_tile_w ? x_tile_w : ldx;
+  a.x_tw = x_tile_w;
+  a.x_ts = x_tile_stride;
+  a.flags = flags;
+  a.bias = bias;
+  a.bias_rows = bias ? bias_rows : nullptr;
+  a.out = out;
+  a.ldo = out_tile_w ? out_tile_w : ldo;
+  a.o_tw = out_tile_w;
+  a.o_ts = out_tile_stride;
+  a.slab_ld = slab_ld_for(F);
+  a.slab_v = (float*)slab;
+  // row-major both ways: the ordinary dispatch (mp_aggregate_f32's) unless rows are
+  // skipped or the bias is per row, which only the scalar-batch flat kernel
+  // does (forced as for tiles)
+  if (!x_tile_w && !out_tile_w && ((flags & MP_FLAG_SKIP_EMPTY) || a.bias_rows)) {
+    a.x_tw = 0;
+    a.force_flat = 1;
+  }
   return aggregate_dispatch(a, g, reduce, stages, as_stream(stream));
 }
 

@@ -18,6 +18,7 @@ MP_OK = 0
 MP_REDUCE = {"sum": 0, "add": 0, "mean": 1, "max": 2, "min": 3}
 MP_FLAG_INIT_FROM_OUT = 1
 MP_FLAG_PYG_MASK = 2
+MP_FLAG_SKIP_EMPTY = 4
 MP_STAGE_MAIN = 1
 MP_STAGE_FIXUP = 2
 MP_STAGE_STATS = 4
@@ -120,8 +121,10 @@ SIGNATURES = {
     "mp_gat_bwd_blocks": (ctypes.c_int, [i64]),
     "mp_col_sums_f32": (ctypes.c_int, [c_p, i64, i64, i32, c_p, sz, c_p]),
     "mp_gat_backward_finish_f32": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, i64, i32, i32, c_p, sz, c_p]),
-    "mp_gat_merge_partials_f32": (ctypes.c_int, [i64, i32, i32, c_p, c_p, i64, c_p, i64, c_p, c_p, c_p, i64, c_p, c_p,
-                                                 c_p, c_p]),
+    "mp_gat_merge_partials_f32": (ctypes.c_int, [i64, i32, i32, c_p, c_p, i64, c_p, sz, i64, c_p, sz, c_p, c_p, i64,
+                                                 c_p, c_p, c_p, c_p]),
+    "mp_aggregate_tiles_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, i64, i32, i64, i32, i32, i32, c_p,
+                                              c_p, c_p, i64, i32, i64, c_p, sz, i32, c_p]),
     "mp_heads_outer_add_f32": (ctypes.c_int, [c_p, i64, c_p, i64, i32, i32, c_p, i64, c_p]),
     "mp_gather_rows_f32": (ctypes.c_int, [c_p, i64, c_p, i64, i32, c_p, i64, c_p]),
     "mp_permute_f32": (ctypes.c_int, [c_p, c_p, i64, c_p, c_p]),

@@ -22,9 +22,9 @@ examples/data_parallel.py:35-49).  One large graph is sharded here instead:
     aggregation over a send graph.
 
 The plan is built natively on the device (mp_shard_plan: flag + scan, no
-sort); host tensors take its torch-op form (_plan_torch), which the gloo tests
-run on CPU.  The data path calls the native kernels (sharded_propagate takes
-the local aggregation as a callable, so the CPU tests can pass a host one).
+sort).  The data path calls the native kernels; a host tensor raises unless a
+test installed host twins of them (install_host_twins: the gloo tests run the
+distributed logic of this module on CPU that way).
 """
 import torch
 import torch.distributed as dist
@@ -33,15 +33,83 @@ import torch.distributed as dist
 def _a2a(out, inp, out_splits=None, in_splits=None, group=None):
     """all_to_all_single; with the gloo backend (CPU-only collectives: the
     multi-process rehearsal of the RCCL path) device tensors are staged
-    through host memory."""
+    through host memory (one device-to-host copy of the input)."""
     if out.is_cuda and dist.get_backend(group) == "gloo":
-        o = out.cpu()
+        o = torch.empty(out.shape, dtype=out.dtype)
         dist.all_to_all_single(o, inp.cpu(), output_split_sizes=out_splits, input_split_sizes=in_splits,
                                group=group)
         out.copy_(o)
         return out
     dist.all_to_all_single(out, inp, output_split_sizes=out_splits, input_split_sizes=in_splits, group=group)
     return out
+
+
+def _device_collectives(dev, group=None):
+    """True when collectives of `group` take tensors on `dev` (RCCL); gloo
+    takes host tensors."""
+    return dev.type != "cpu" and dist.get_backend(group) != "gloo"
+
+
+def _exchange_counts(send, group=None):
+    """all_to_all of per-peer counts: send [world] or [world, k] int64 (device
+    or host).  Returns (send, recv) as host lists (of lists for k > 1) with ONE
+    host sync -- the splits of the exchanges that follow need them on the host."""
+    world = dist.get_world_size(group)
+    k = 1 if send.dim() == 1 else send.shape[1]
+    if _device_collectives(send.device, group):
+        recv = torch.empty_like(send)
+        dist.all_to_all_single(recv.view(-1), send.reshape(-1).contiguous(), group=group)
+        both = torch.stack([send.reshape(world, k), recv.reshape(world, k)]).tolist()
+    else:
+        sh = send.reshape(world, k).cpu()
+        rh = torch.empty_like(sh)
+        dist.all_to_all_single(rh.view(-1), sh.reshape(-1).contiguous(), group=group)
+        both = [sh.tolist(), rh.tolist()]
+    if send.dim() == 1:
+        return [r[0] for r in both[0]], [r[0] for r in both[1]]
+    return both[0], both[1]
+
+
+def _all_gather_rows(vals, dev, group=None):
+    """[[vals of rank 0], [vals of rank 1], ...]: `vals` a 1-D int64 tensor
+    (device or host, the same length on every rank), gathered with one
+    collective and read with ONE host sync."""
+    world = dist.get_world_size(group)
+    v = vals.to(torch.int64)
+    if _device_collectives(dev, group):
+        v = v.to(dev)
+    else:
+        v = v.cpu()
+    got = torch.empty((world, v.numel()), dtype=torch.int64, device=v.device)
+    dist.all_gather_into_tensor(got.view(-1), v.contiguous(), group=group)
+    return got.tolist()
+
+
+def _dev_ints(lists, dev):
+    """Host int lists -> int64 tensors on `dev` in ONE asynchronous copy
+    (pinned staging: no synchronising host-to-device memcpy per small tensor).
+    Returns one tensor per list (views of one buffer)."""
+    flat = [int(v) for lst in lists for v in lst]
+    buf = torch.tensor(flat if flat else [0], dtype=torch.int64)
+    if dev.type == "cuda":
+        buf = buf.pin_memory().to(dev, non_blocking=True)
+    out, o = [], 0
+    for lst in lists:
+        out.append(buf[o:o + len(lst)])
+        o += len(lst)
+    return out
+
+
+def _nonzero_n(mask, n):
+    """Positions of the n true entries of a 1-D mask, n known on the host: no
+    read-back of the count (torch.nonzero_static)."""
+    return torch.nonzero_static(mask, size=int(n)).view(-1)
+
+
+def _count_by(idx, n):
+    """Integer histogram of idx over [0, n) without a host sync (torch.bincount
+    reads the maximum back): exact in any order."""
+    return torch.zeros(n, dtype=torch.int64, device=idx.device).scatter_add_(0, idx, torch.ones_like(idx))
 
 
 def tile_widths(F, tile):
@@ -56,53 +124,59 @@ def tile_widths(F, tile):
 
 
 def edge_balanced_cuts(in_degree, parts):
-    """Row cut points [0=c_0 <= ... <= c_P = N] with ~equal edges per part."""
+    """Row cut points [0=c_0 <= ... <= c_P = N] with ~equal edges per part
+    (the targets E * p // parts searched in the in-degree prefix sum on the
+    device, read back with one host sync)."""
     N = in_degree.numel()
+    if N == 0 or parts <= 1:
+        return [0] * parts + [N]
     csum = torch.cumsum(in_degree.to(torch.int64), 0)
-    E = int(csum[-1]) if N else 0
+    p = torch.arange(1, parts, dtype=torch.int64, device=csum.device)
+    found = torch.searchsorted(csum, (csum[-1] * p) // parts, right=True).tolist()
     cuts = [0]
-    for p in range(1, parts):
-        target = (E * p) // parts
-        c = int(torch.searchsorted(csum, torch.tensor(target, device=csum.device), right=True))
-        cuts.append(max(c, cuts[-1]))
+    for c in found:
+        cuts.append(max(int(c), cuts[-1]))
     cuts.append(N)
     return cuts
 
 
-def _plan_torch(key, other, num_nodes, cuts, rank, world):
-    """The plan of rank `rank` in torch ops (host tensors: the gloo tests of the
-    plan logic; on the GPU the checker of mp_shard_plan).  Returns (edge_pos,
-    local key, local other, halo_nodes, recv_counts)."""
-    dev = key.device
-    lo, hi = cuts[rank], cuts[rank + 1]
-    mine = (key >= lo) & (key < hi)
-    edge_pos = torch.nonzero(mine).view(-1)                  # positions in the global edge order
-    k = key[edge_pos] - lo
-    o = other[edge_pos]
-    if o.numel() and (int(o.min()) < 0 or int(o.max()) >= num_nodes):
-        raise IndexError("mi355_mp.dist: an edge endpoint lies outside [0, %d)" % num_nodes)
-    owner = torch.searchsorted(torch.tensor(cuts[1:], device=dev), o, right=True)
-    remote = owner != rank
-    halo_nodes = torch.unique(o[remote])                     # sorted, hence grouped by owner
-    halo_owner = torch.searchsorted(torch.tensor(cuts[1:], device=dev), halo_nodes, right=True)
-    recv_counts = [int((halo_owner == q).sum()) for q in range(world)]
-    # local column ids: own rows first, then halo rows in sorted order
-    local_o = torch.empty_like(o)
-    local_o[~remote] = o[~remote] - lo
-    local_o[remote] = (hi - lo) + torch.searchsorted(halo_nodes, o[remote])
-    return edge_pos, k, local_o, halo_nodes, recv_counts
+# ---------------------------------------------------------------------------
+# host tensors: no CPU fallback.  The gloo tests (tests/test_dist_gloo.py) run
+# this module's distributed logic -- plans, covers, slice builds, exchanges --
+# on CPU with host twins of the native kernels they install themselves
+# (tests/_host_twins.py); without them a host tensor raises.
+# ---------------------------------------------------------------------------
+_HOST_TWINS = None
+
+
+def install_host_twins(twins):
+    """Test hook: `twins` provides host forms of the native pieces (plan,
+    gather_rows, sum_returned_rows, segment_sum_in_order, norm_local,
+    gat_loops, gat_cover_forward).  None removes them."""
+    global _HOST_TWINS
+    _HOST_TWINS = twins
+
+
+def _host(what):
+    if _HOST_TWINS is None:
+        raise RuntimeError("mi355_mp.dist: %s on host tensors -- there is no CPU fallback: the engine runs on ROCm "
+                           "device tensors" % what)
+    return getattr(_HOST_TWINS, what)
 
 
 def _plan_native(key, other, num_nodes, cuts, rank, world):
-    """_plan_torch on the device by mp_shard_plan (flag + scan, no sort):
-    bitwise the same outputs."""
+    """The plan of rank `rank` on the device by mp_shard_plan (flag + scan, no
+    sort): (edge_pos, local key, local other, halo_nodes, recv_counts) -- the
+    positions of the rank's edges in the list's order, its destinations and
+    sources renumbered [own rows ; sorted halo rows], the halo's global ids and
+    their count per owner.  One host sync (the sizes)."""
     from . import _lib
     lib = _lib.load()
     dev = key.device
     key = key.to(torch.int64).contiguous()
     other = other.to(torch.int64).contiguous()
     E = key.numel()
-    cuts_d = torch.tensor(cuts, dtype=torch.int64, device=dev)
+    cuts_d = _dev_ints([cuts], dev)[0]
     edge_pos = torch.empty(E, dtype=torch.int64, device=dev)
     lkey = torch.empty_like(edge_pos)
     lother = torch.empty_like(edge_pos)
@@ -137,7 +211,7 @@ class ShardPlan:
         self.rank, self.world = rank, world
         lo, hi = cuts[rank], cuts[rank + 1]
         self.lo, self.hi, self.n_own = lo, hi, hi - lo
-        plan = _plan_native if edge_index.is_cuda else _plan_torch
+        plan = _plan_native if edge_index.is_cuda else _host("plan")
         self.edge_pos, dst, local_src, halo_nodes, self.recv_counts = plan(dst_all, src_all, num_nodes, cuts, rank,
                                                                            world)
         self.halo_nodes = halo_nodes
@@ -148,12 +222,10 @@ class ShardPlan:
         self.send_counts = None
 
     def exchange_requests(self, group=None):
-        """All-to-all of the requested node ids (once per plan)."""
+        """All-to-all of the requested node ids (once per plan; one host sync
+        for the counts)."""
         dev = self.halo_nodes.device
-        recv_counts = torch.tensor(self.recv_counts, dtype=torch.int64, device=dev)
-        send_counts = torch.empty_like(recv_counts)
-        _a2a(send_counts, recv_counts, group=group)
-        self.send_counts = send_counts.tolist()
+        _, self.send_counts = _exchange_counts(_dev_ints([self.recv_counts], dev)[0], group)
         requests = torch.empty(sum(self.send_counts), dtype=torch.int64, device=dev)
         _a2a(requests, self.halo_nodes.contiguous(), self.send_counts, self.recv_counts, group)
         self.send_idx = requests - self.lo     # rows of my own block that peers need
@@ -216,14 +288,14 @@ class ShardPlan:
 def _sum_returned_rows(plan, back):
     """Rows returned by the peers (plan.return_halo: aligned with send_idx, peer
     order, then each peer's request order) summed into this rank's own rows in
-    that fixed order: the native segmented sum keyed on send_idx on the device,
-    torch's serial CPU index_add_ on host tensors.  Deterministic."""
-    if back.is_cuda:
-        from . import ops
-        from .graph import csr_for_index
-        return ops._aggregate(csr_for_index(plan.send_idx, plan.n_own), "eid", back.contiguous(), None, "sum", 0,
-                              None)[0]
-    return torch.zeros((plan.n_own, back.shape[1]), dtype=back.dtype).index_add_(0, plan.send_idx, back)
+    that fixed order: the native segmented sum keyed on send_idx.
+    Deterministic."""
+    if not back.is_cuda:
+        return _host("sum_returned_rows")(plan, back)
+    from . import ops
+    from .graph import csr_for_index
+    return ops._aggregate(csr_for_index(plan.send_idx, plan.n_own), "eid", back.contiguous(), None, "sum", 0,
+                          None)[0]
 
 
 class _HaloRows(torch.autograd.Function):
@@ -240,7 +312,7 @@ class _HaloRows(torch.autograd.Function):
             from . import ops
             plan.exchange_into(x_local, ops.gather_rows, group)
         else:
-            plan.exchange_into(x_local, lambda t, idx: t[idx], group)
+            plan.exchange_into(x_local, _host("gather_rows"), group)
         return x_local
 
     @staticmethod
@@ -290,50 +362,47 @@ def sharded_propagate(plan, x_own, local_aggregate, gather_rows, edge_weight=Non
 # ---------------------------------------------------------------------------
 
 def scatter_edges_by_owner(key, cuts, payloads, group=None):
-    """Route the entries of `payloads` (1-D tensors aligned with `key`) to the
-    rank owning key (range partition `cuts`): one all_to_all per payload.  The
-    result is the concatenation over sender ranks in rank order, each sender's
-    entries in their original order -- so when every rank holds a contiguous
-    slice of the global edge list (rank r before rank r + 1), each rank receives
-    its edges in GLOBAL order."""
+    """Route the entries of `payloads` (1-D int64 / float32 tensors aligned with
+    `key`) to the rank owning key (range partition `cuts`): the counts, then
+    every payload in ONE all_to_all (int64 columns; a float32 payload travels
+    as its bits), one host sync.  The result is the concatenation over sender
+    ranks in rank order, each sender's entries in their original order -- so
+    when every rank holds a contiguous slice of the global edge list (rank r
+    before rank r + 1), each rank receives its edges in GLOBAL order."""
     world = len(cuts) - 1
     dev = key.device
-    owner = torch.searchsorted(torch.tensor(cuts[1:], dtype=key.dtype, device=dev), key, right=True)
-    order = torch.sort(owner, stable=True).indices
-    send = torch.bincount(owner, minlength=world)
-    recv = torch.empty_like(send)
-    _a2a(recv, send, group=group)
-    sc, rc = send.tolist(), recv.tolist()
-    out = []
+    cuts_t, ranks = _dev_ints([cuts[1:], range(world + 1)], dev)
+    owner = torch.searchsorted(cuts_t, key, right=True)
+    srt = torch.sort(owner, stable=True)
+    order = srt.indices
+    # per-owner counts from the sorted owners (no atomics on world-many bins)
+    bounds = torch.searchsorted(srt.values, ranks)
+    sc, rc = _exchange_counts(bounds[1:] - bounds[:-1], group)
+    cols = []
     for p in payloads:
-        buf = p.new_empty(sum(rc))
-        _a2a(buf, p[order].contiguous(), rc, sc, group)
-        out.append(buf)
+        if p.dtype == torch.float32:
+            cols.append(p.view(torch.int32).to(torch.int64))
+        elif p.dtype == torch.int64:
+            cols.append(p)
+        else:
+            raise TypeError("scatter_edges_by_owner: payloads are int64 or float32 (got %s)" % p.dtype)
+    packed = torch.stack(cols, 1)[order].contiguous() if cols else key.new_empty((key.numel(), 0))
+    buf = packed.new_empty((sum(rc), len(cols)))
+    _a2a(buf, packed, rc, sc, group)
+    out = []
+    for j, p in enumerate(payloads):
+        c = buf[:, j].contiguous()
+        out.append(c.to(torch.int32).view(torch.float32) if p.dtype == torch.float32 else c)
     return out
 
 
-def _any_rank(flag, dev, group=None):
-    """True on every rank when `flag` is nonzero on any rank (MAX all_reduce)."""
-    t = torch.tensor([int(flag)], dtype=torch.int64)
-    if dev.type != "cpu" and dist.get_backend(group) != "gloo":
-        t = t.to(dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
-    return bool(t.item())
 
 
-def _all_gather_ints(vals, group=None):
-    """[[vals of rank 0], [vals of rank 1], ...] for a few host ints."""
-    got = [None] * dist.get_world_size(group)
-    dist.all_gather_object(got, list(vals), group=group)
-    return got
-
-
-def _segment_sum_in_order(index, values, n, device_native):
+def _segment_sum_in_order(index, values, n):
     """out[k] = sum of values[index == k] left to right (the CPU scatter_add_'s
-    order): torch's serial CPU scatter_add_ on host tensors, the transposed
-    CSR's serial segment sum (mp_segment_sum_serial_f32) on the device."""
-    if not device_native:
-        return torch.zeros(n, dtype=values.dtype).scatter_add_(0, index, values)
+    order): the transposed CSR's serial segment sum (mp_segment_sum_serial_f32)."""
+    if not values.is_cuda:
+        return _host("segment_sum_in_order")(index, values, n)
     from . import ops
     from .graph import CSR
     return ops.segment_sum_serial(CSR(index, None, n, index.numel()), values)
@@ -371,39 +440,43 @@ def gcn_shards_from_slices(edge_slice, slice_offset, num_nodes, rank, world, gro
     dev = row.device
     N = int(num_nodes)
     n = row.numel()
-    # every rank learns whether ANY rank holds an id outside [0, N) before the
-    # first collective whose size depends on N, and all of them raise together
-    # (a rank with a bad id would otherwise all_reduce a longer degree vector)
-    bad = int(n > 0 and (int(torch.minimum(row.min(), col.min())) < 0
-                         or int(torch.maximum(row.max(), col.max())) >= N))
-    if _any_rank(bad, dev, group):
-        raise IndexError("mi355_mp.dist: an edge of some rank's slice names a node outside [0, %d)" % N)
-    w = (edge_weight.to(torch.float32) if edge_weight is not None
-         else torch.ones(n, dtype=torch.float32, device=dev))
-    fill = 2.0 if improved else 1.0
     keep = row != col
-    kept = torch.nonzero(keep).view(-1)
-    # every rank's offset travels with its sizes, so every rank checks every
-    # offset and all of them raise together (a lone raising rank would leave its
-    # peers waiting in the next collective until the group's timeout)
-    sizes = _all_gather_ints([n, kept.numel(), int(slice_offset)], group)
+    # one gather of (slice size, kept edges, offset, bad-id flag) from every rank,
+    # read with one host sync: every rank learns whether ANY rank holds an id
+    # outside [0, N) before the first collective whose size depends on N, and all
+    # of them raise together (a rank with a bad id would otherwise all_reduce a
+    # longer degree vector); every rank checks every offset the same way (a lone
+    # raising rank would leave its peers waiting in the next collective)
+    if n:
+        bad_t = ((torch.minimum(row.min(), col.min()) < 0) | (torch.maximum(row.max(), col.max()) >= N))
+        n_off = _dev_ints([[n, int(slice_offset)]], dev)[0]
+        mine = torch.stack([n_off[0], keep.sum(), n_off[1], bad_t.to(torch.int64)])
+    else:
+        mine = torch.tensor([0, 0, int(slice_offset), 0], dtype=torch.int64)
+    sizes = _all_gather_rows(mine, dev, group)
+    if any(sz[3] for sz in sizes):
+        raise IndexError("mi355_mp.dist: an edge of some rank's slice names a node outside [0, %d)" % N)
     for r, sz in enumerate(sizes):
         if sz[2] != sum(t[0] for t in sizes[:r]):
             raise ValueError("gcn_shards_from_slices: rank %d's slice offset %d does not follow the earlier slices"
                              % (r, sz[2]))
+    n_kept = sizes[rank][1]
+    w = (edge_weight.to(torch.float32) if edge_weight is not None
+         else torch.ones(n, dtype=torch.float32, device=dev))
+    fill = 2.0 if improved else 1.0
+    kept = _nonzero_n(keep, n_kept)
     k_off = sum(sz[1] for sz in sizes[:rank])
     E_kept = sum(sz[1] for sz in sizes)
     kr, kc, kw = row[kept], col[kept], w[kept]
-    kgid = k_off + torch.arange(kept.numel(), dtype=torch.int64, device=dev)
+    kgid = k_off + torch.arange(n_kept, dtype=torch.int64, device=dev)
     # 2. cuts from the global in-degree (+1: every node gets its loop)
-    deg_in = torch.bincount(kc, minlength=N)
-    deg_in = deg_in.to(dev)
-    if dev.type != "cpu" and dist.get_backend(group) == "gloo":
+    deg_in = _count_by(kc, N)
+    if _device_collectives(dev, group):
+        dist.all_reduce(deg_in, group=group)
+    else:
         h = deg_in.cpu()
         dist.all_reduce(h, group=group)
         deg_in = h.to(dev)
-    else:
-        dist.all_reduce(deg_in, group=group)
     cuts = edge_balanced_cuts(deg_in + 1, world)
     lo, hi = cuts[rank], cuts[rank + 1]
     own = torch.arange(lo, hi, dtype=torch.int64, device=dev)
@@ -413,20 +486,22 @@ def gcn_shards_from_slices(edge_slice, slice_offset, num_nodes, rank, world, gro
                torch.ones(f_row.numel() + hi - lo, dtype=torch.float32, device=dev))
         return {"cuts": cuts, "E": E_kept + N, "deg": None, "fwd": fwd, "bwd": None}
     # 3. pre-existing loops -> the node's owner; the last one (largest position) wins
-    lidx = torch.nonzero(~keep).view(-1)
+    lidx = _nonzero_n(~keep, n - n_kept)
     lv, lw = row[lidx], w[lidx]
-    if lv.numel() and (int(lv.min()) < 0 or int(lv.max()) >= N):
-        raise IndexError("self loops name a node outside [0, %d)" % N)
     rv, rpos, rw = scatter_edges_by_owner(lv, cuts, [lv, lidx + slice_offset, lw], group)
     loop_w = torch.full((hi - lo,), fill, dtype=torch.float32, device=dev)
     if rv.numel():
         best = torch.full((hi - lo,), -1, dtype=torch.int64, device=dev)
         best.scatter_reduce_(0, rv - lo, rpos, "amax")
         last = rpos == best[rv - lo]
-        loop_w[rv[last] - lo] = rw[last]
+        # the winners' weights into their rows; the other entries land in a spare slot
+        slot = torch.where(last, rv - lo, torch.full_like(rv, hi - lo))
+        lw_ext = torch.cat([loop_w, loop_w.new_zeros(1)])
+        lw_ext.scatter_(0, slot, torch.where(last, rw, torch.zeros_like(rw)))
+        loop_w = lw_ext[:hi - lo]
     # 4. out-edges of my rows, global order -> deg = scatter_add(w, row) in edge order, then the loop
     b_row, b_col, b_gid, b_w = scatter_edges_by_owner(kr, cuts, [kr, kc, kgid, kw], group)
-    deg = _segment_sum_in_order(b_row - lo, b_w, hi - lo, dev.type != "cpu")
+    deg = _segment_sum_in_order(b_row - lo, b_w, hi - lo)
     deg = deg + loop_w
     # 5. in-edges of my rows, global order; the loops last
     f_row, f_col, f_gid, f_w = scatter_edges_by_owner(kc, cuts, [kr, kc, kgid, kw], group)
@@ -449,12 +524,11 @@ def _norm_over_plan(plan, deg_own, w_local, group=None):
         from . import ops
         plan.exchange_into(degl, ops.gather_rows, group)
         lei = plan.local_edge_index
-        return ops.norm_from_degree(lei[0], lei[1], degl.view(-1).clone(), w_local)
-    plan.exchange_into(degl, lambda t, idx: t[idx], group)
-    dinv = degl.view(-1).pow(-0.5)
-    dinv[dinv == float("inf")] = 0
+        # local ids < n_own + n_halo by the plan's construction: no range read-back
+        return ops.norm_from_degree(lei[0], lei[1], degl.view(-1).clone(), w_local, trusted=True)
+    plan.exchange_into(degl, _host("gather_rows"), group)
     lei = plan.local_edge_index
-    return dinv[lei[0]] * w_local * dinv[lei[1]]
+    return _host("norm_local")(lei[0], lei[1], degl.view(-1), w_local)
 
 
 class HaloCover:
@@ -494,141 +568,160 @@ class HaloCover:
         n_own = plan.n_own
         lei = plan.local_edge_index
         src_l, dst_l = lei[0], lei[1]
+        E_l = src_l.numel()
         if w_local is None:
-            w_local = torch.ones(src_l.numel(), dtype=torch.float32, device=dev)
+            w_local = torch.ones(E_l, dtype=torch.float32, device=dev)
         w_local = w_local.to(torch.float32)
-        cuts_t = torch.tensor(plan.cuts[1:], dtype=torch.int64, device=dev)
-        interior = src_l < n_own
-        self.int_src, self.int_dst, self.int_w = src_l[interior], dst_l[interior], w_local[interior]
-        rem = ~interior
-        r_src = plan.halo_nodes[src_l[rem] - n_own]          # global source ids, plan (global edge) order
-        r_dst = dst_l[rem]
-        r_w = w_local[rem]
-        r_own = torch.searchsorted(cuts_t, r_src, right=True)
-        stride = max(n_own, 1)
-        # --- the cover: larger cross-degree endpoint, then the two clean-ups.  Dense
-        # O(N + E) counting (bincount / cumsum / nonzero), no sort or unique
         N = plan.cuts[-1]
-        key = r_own * stride + r_dst                          # (owner, destination) of a cross edge
+        cut_all = _dev_ints([plan.cuts], dev)[0]
+        cuts_t = cut_all[1:]
+        stride = max(n_own, 1)
         nkey = world * stride
-        if r_src.numel():
-            cs = torch.bincount(r_src, minlength=N)           # cross out-degree of each remote source
-            cd = torch.bincount(key, minlength=nkey)          # cross in-degree per (owner, destination)
-            pick = cs[r_src] >= cd[key]
-            in_s = torch.bincount(r_src[pick], minlength=N) > 0
-            push = ~in_s[r_src]
-            in_d = torch.bincount(key[push], minlength=nkey) > 0
-            push = in_d[key]
-            # per owner the fewest rows of three covers: this one, pull only, push only
-            # (the degree rule can lose to either on a dense pair)
-            in_s = torch.bincount(r_src[~push], minlength=N) > 0
-            cover_q = (torch.bincount(torch.searchsorted(cuts_t, torch.nonzero(in_s).view(-1), right=True),
-                                      minlength=world)
-                       + torch.bincount(torch.nonzero(in_d).view(-1) // stride, minlength=world))
-            pull_q = torch.bincount(torch.searchsorted(cuts_t, torch.nonzero(cs).view(-1), right=True),
-                                    minlength=world)
-            push_q = torch.bincount(torch.nonzero(cd).view(-1) // stride, minlength=world)
-            mode = torch.where((pull_q <= cover_q) & (pull_q <= push_q), 0, torch.where(push_q < cover_q, 1, 2))
-            m = mode[r_own]
-            push = torch.where(m == 0, torch.zeros_like(push), torch.where(m == 1, torch.ones_like(push), push))
-            pull = ~push
-            in_s = torch.bincount(r_src[pull], minlength=N) > 0
-            in_d = torch.bincount(key[push], minlength=nkey) > 0
-            del cs, cd, pick
+        # Every edge of the plan stays in place and the remote ones are masked (no
+        # compaction before the sizes are known): the whole cover is computed on the
+        # device and its sizes come back in ONE host read, with the request counts
+        # of the peers (three host syncs for the build in all, whatever the graph).
+        remm = src_l >= n_own                                  # remote source (a halo slot)
+        if plan.halo_nodes.numel():
+            gsrc = torch.where(remm, plan.halo_nodes[(src_l - n_own).clamp(min=0)], torch.zeros_like(src_l))
         else:
-            in_s = torch.zeros(N, dtype=torch.bool, device=dev)
-            in_d = torch.zeros(nkey, dtype=torch.bool, device=dev)
-            push = pull = torch.zeros(0, dtype=torch.bool, device=dev)
-        S = torch.nonzero(in_s).view(-1)                      # ascending node ids: grouped by owner
-        D = torch.nonzero(in_d).view(-1)                      # ascending (owner, destination) keys
+            gsrc = torch.zeros_like(src_l)
+        r_own = torch.searchsorted(cuts_t, gsrc, right=True)   # owner of the source (remote edges)
+        key = r_own * stride + dst_l                           # (owner, destination) of a cross edge
+
+        spread = torch.arange(E_l, device=dev) & 1023
+
+        def count(idx, mask, n):
+            # masked-out entries go to 1024 spare bins (not all onto one bin: an
+            # atomic hot spot that held the P = 2 build's device for 1.6 s)
+            i = torch.where(mask, idx, n + spread)
+            return torch.zeros(n + 1024, dtype=torch.int64, device=dev).scatter_add_(0, i, torch.ones_like(i))[:n]
+
+        def per_owner_nodes(flags):      # flagged global nodes per owner (contiguous ranges)
+            cz = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), torch.cumsum(flags.to(torch.int64), 0)])
+            return cz[cut_all[1:]] - cz[cut_all[:-1]]
+
+        def per_owner_keys(flags):       # flagged (owner, destination) keys per owner
+            return flags.to(torch.int64).view(world, stride).sum(1)
+
+        # --- the cover: larger cross-degree endpoint, then the two clean-ups, then per
+        # owner the fewest rows of {this cover, pull only, push only}
+        cs = count(gsrc, remm, N)                              # cross out-degree of each remote source
+        cd = count(key, remm, nkey)                            # cross in-degree per (owner, destination)
+        pick = cs[gsrc] >= cd[key]
+        in_s = count(gsrc, remm & pick, N) > 0
+        push = remm & ~in_s[gsrc]
+        in_d = count(key, push, nkey) > 0
+        push = remm & in_d[key]
+        in_s = count(gsrc, remm & ~push, N) > 0
+        cover_q = per_owner_nodes(in_s) + per_owner_keys(in_d)
+        pull_q = per_owner_nodes(cs > 0)
+        push_q = per_owner_keys(cd > 0)
+        mode = torch.where((pull_q <= cover_q) & (pull_q <= push_q), 0, torch.where(push_q < cover_q, 1, 2))
+        m = mode[r_own]
+        push = remm & torch.where(m == 0, torch.zeros_like(push), torch.where(m == 1, torch.ones_like(push), push))
+        pull = remm & ~push
+        in_s = count(gsrc, pull, N) > 0
+        in_d = count(key, push, nkey) > 0
+        del cs, cd, pick
+        nS = per_owner_nodes(in_s)                             # pulled rows per owner
+        nD = per_owner_keys(in_d)                              # pushed rows per owner
+        nP = per_owner_keys(count(key, push, nkey))            # push edges per owner
+        cnt = torch.stack([nS, nD, nP], 1).contiguous()
+        extra = torch.stack([(~remm).sum(), pull.sum(), push.sum()])
+        # host read 1 (+ the peers' counts): sizes of everything below
+        if _device_collectives(dev, group):
+            cnt_in = torch.empty_like(cnt)
+            dist.all_to_all_single(cnt_in.view(-1), cnt.view(-1), group=group)
+            allv = torch.cat([cnt.view(-1), cnt_in.view(-1), extra]).tolist()
+            mine_c, peer_c = allv[:3 * world], allv[3 * world:6 * world]
+            n_int, n_pull, n_push = allv[6 * world:]
+        else:
+            allv = torch.cat([cnt.view(-1), extra]).tolist()
+            mine_c = allv[:3 * world]
+            n_int, n_pull, n_push = allv[3 * world:]
+            ch = torch.tensor(mine_c, dtype=torch.int64).view(world, 3)
+            rh = torch.empty_like(ch)
+            dist.all_to_all_single(rh.view(-1), ch.view(-1), group=group)
+            peer_c = rh.view(-1).tolist()
+        nS_l, nD_l, nP_l = mine_c[0::3], mine_c[1::3], mine_c[2::3]
+        snS, snD, snP = peer_c[0::3], peer_c[1::3], peer_c[2::3]
+        nS_tot, nD_tot = sum(nS_l), sum(nD_l)
+        # --- the plan's edges by class in plan (= global edge) order: interior,
+        # pulled, pushed (a stable partition)
+        code = torch.where(remm, torch.where(push, 2, 1), 0).to(torch.int8)
+        order3 = torch.argsort(code, stable=True)
+        idx_int = order3[:n_int]
+        idx_pull = order3[n_int:n_int + n_pull]
+        idx_push = order3[n_int + n_pull:]
+        self.int_src, self.int_dst, self.int_w = src_l[idx_int], dst_l[idx_int], w_local[idx_int]
+        S = _nonzero_n(in_s, nS_tot)                           # ascending node ids: grouped by owner
+        D = _nonzero_n(in_d, nD_tot)                           # ascending (owner, destination) keys
         s_rank = torch.cumsum(in_s, 0) - 1                    # position of a pulled node in S
         d_rank = torch.cumsum(in_d, 0) - 1                    # position of a pushed key in D
         del in_s, in_d
         S_own = torch.searchsorted(cuts_t, S, right=True)
         D_own = D // stride
-        nS = torch.bincount(S_own, minlength=world)
-        nD = torch.bincount(D_own, minlength=world)
-        p_own = r_own[push]
-        nP = torch.bincount(p_own, minlength=world)
-        self.recv_counts = (nS + nD).tolist()
+        self.recv_counts = [a_ + b_ for a_, b_ in zip(nS_l, nD_l)]
         off = [0]
         for c in self.recv_counts:
             off.append(off[-1] + c)
-        off_t = torch.tensor(off[:-1], dtype=torch.int64, device=dev)
-        S_start = torch.cumsum(nS, 0) - nS
-        D_start = torch.cumsum(nD, 0) - nD
+        off_t, nS_t, S_start, D_start = _dev_ints([off[:-1], nS_l, [sum(nS_l[:q]) for q in range(world)],
+                                                   [sum(nD_l[:q]) for q in range(world)]], dev)
         # halo slot of each pulled source / pushed destination row: per owner q,
         # [its pulled rows ; its partial rows]
-        s_pos = s_rank[r_src[pull]]
+        s_pos = s_rank[gsrc[idx_pull]]
         s_q = S_own[s_pos]
         pull_halo = n_own + off_t[s_q] + (s_pos - S_start[s_q])
         d_q = D_own
-        d_halo = n_own + off_t[d_q] + nS[d_q] + (torch.arange(D.numel(), device=dev) - D_start[d_q])
+        d_halo = n_own + off_t[d_q] + nS_t[d_q] + (torch.arange(nD_tot, device=dev) - D_start[d_q])
         self.bnd_src = torch.cat([pull_halo, d_halo])
-        self.bnd_dst = torch.cat([r_dst[pull], D - d_q * stride])
-        # kept for GatHaloCover: the remote edges (plan order) and which are pulled,
-        # the halo slot of each pulled one, and per pushed row its destination
-        self.rem, self.pull, self.pull_halo = rem, pull, pull_halo
+        self.bnd_dst = torch.cat([dst_l[idx_pull], D - d_q * stride])
+        self.bnd_w = torch.cat([w_local[idx_pull], torch.ones(nD_tot, dtype=torch.float32, device=dev)])
+        # kept for GatHaloCover: plan positions of the interior and pulled edges, the
+        # halo slot of each pulled one, and per pushed row its destination
+        self.int_pos, self.pull_pos, self.pull_halo = idx_int, idx_pull, pull_halo
         self.push_dst, self.push_halo = D - d_q * stride, d_halo
-        self.n_push_rows_to = nD.tolist()       # pushed rows this rank receives, per owner
-        self.bnd_w = torch.cat([r_w[pull], torch.ones(D.numel(), dtype=torch.float32, device=dev)])
+        self.n_push_rows_to = list(nD_l)     # pushed rows this rank receives, per owner
         self.n_halo = off[-1]
         self.n_local_src = n_own + self.n_halo
-        self.n_pull_rows, self.n_push_rows = int(S.numel()), int(D.numel())
-        self.n_pull_edges, self.n_push_edges = int(pull.sum()), int(push.sum())
-        # --- requests to the owners: pulled ids, and the push edges (source, partial row, weight)
-        p_row = d_rank[key[push]] - D_start[p_own]
+        self.n_pull_rows, self.n_push_rows = nS_tot, nD_tot
+        self.n_pull_edges, self.n_push_edges = n_pull, n_push
+        # --- requests to the owners: pulled ids, and the push edges (source, partial
+        # row, weight) grouped by owner, global edge order inside (a stable sort)
+        p_own = r_own[idx_push]
+        p_key = key[idx_push]
+        p_row = d_rank[p_key] - D_start[p_own]
         del s_rank, d_rank
-        # push edges grouped by owner, global edge order inside (a stable partition)
-        order = torch.cat([torch.nonzero(p_own == q).view(-1) for q in range(world)])
-        cnt = torch.stack([nS, nD, nP], 1).reshape(-1).contiguous()
-        cnt_in = torch.empty_like(cnt)
-        _a2a(cnt_in, cnt, group=group)
-        cin = cnt_in.view(world, 3).tolist()
-        snS = [c[0] for c in cin]
-        snD = [c[1] for c in cin]
-        snP = [c[2] for c in cin]
+        ord_p = torch.argsort(p_own, stable=True)
         req = S.new_empty(sum(snS))
-        _a2a(req, S.contiguous(), snS, nS.tolist(), group)
+        _a2a(req, S.contiguous(), snS, nS_l, group)
         lo = plan.lo
-        ps = S.new_empty(sum(snP))
-        _a2a(ps, r_src[push][order].contiguous(), snP, nP.tolist(), group)
-        pr = S.new_empty(sum(snP))
-        _a2a(pr, p_row[order].contiguous(), snP, nP.tolist(), group)
-        pw = r_w.new_empty(sum(snP))
-        _a2a(pw, r_w[push][order].contiguous(), snP, nP.tolist(), group)
+        # the push edges' (source, partial row, weight bits) in one all_to_all
+        pk = torch.stack([gsrc[idx_push], p_row, w_local[idx_push].view(torch.int32).to(torch.int64)], 1)[ord_p]
+        pk_in = pk.new_empty((sum(snP), 3))
+        _a2a(pk_in, pk.contiguous(), snP, nP_l, group)
+        ps, pr = pk_in[:, 0], pk_in[:, 1]
+        pw = pk_in[:, 2].to(torch.int32).view(torch.float32)
         # --- the send graph: rows = this rank's send buffer (per peer: pulled rows, then partial rows)
-        self.send_counts = [a + b for a, b in zip(snS, snD)]
+        self.send_counts = [a_ + b_ for a_, b_ in zip(snS, snD)]
         self.send_pull_counts, self.send_push_counts = snS, snD
         base = [0]
         for c in self.send_counts:
             base.append(base[-1] + c)
-        peer_s = torch.repeat_interleave(torch.arange(world, device=dev), torch.tensor(snS, device=dev))
-        peer_p = torch.repeat_interleave(torch.arange(world, device=dev), torch.tensor(snP, device=dev))
-        base_t = torch.tensor(base[:-1], dtype=torch.int64, device=dev)
-        sS_start = torch.tensor([sum(snS[:k]) for k in range(world)], dtype=torch.int64, device=dev)
-        snS_t = torch.tensor(snS, dtype=torch.int64, device=dev)
+        ar = torch.arange(world, device=dev)
+        snS_t, snP_t, base_t, sS_start = _dev_ints([snS, snP, base[:-1], [sum(snS[:k]) for k in range(world)]], dev)
+        peer_s = torch.repeat_interleave(ar, snS_t, output_size=sum(snS))
+        peer_p = torch.repeat_interleave(ar, snP_t, output_size=sum(snP))
         pull_rows = base_t[peer_s] + (torch.arange(req.numel(), device=dev) - sS_start[peer_s])
         push_rows = base_t[peer_p] + snS_t[peer_p] + pr
+        # every requested row is one of this rank's own rows by construction (the
+        # requests name sources in [lo, hi) of the shared cuts)
         self.send_src = torch.cat([req - lo, ps - lo])
         self.send_dst = torch.cat([pull_rows, push_rows])
         self.send_w = torch.cat([torch.ones(req.numel(), dtype=torch.float32, device=dev), pw])
         self.n_send = base[-1]
-        if self.send_src.numel() and (int(self.send_src.min()) < 0 or int(self.send_src.max()) >= n_own):
-            raise RuntimeError("HaloCover: a peer requested a row this rank does not own")
         self.n_own = n_own
-
-    def host_step(self, x_own, aggregate, group=None):
-        """Reference form of one step on host tensors: aggregate(x_src, src_idx,
-        dst_idx, w, n_dst) is the serial edge-order sum (the oracle).  Returns
-        the rank's [n_own, F] sum over all its in-edges."""
-        F = x_own.shape[1]
-        send = aggregate(x_own, self.send_src, self.send_dst, self.send_w, self.n_send)
-        xl = x_own.new_empty((self.n_local_src, F))
-        xl[:self.n_own] = x_own
-        _a2a(xl[self.n_own:], send.contiguous(), self.recv_counts, self.send_counts, group)
-        out = aggregate(x_own, self.int_src, self.int_dst, self.int_w, self.n_own)
-        return out + aggregate(xl, self.bnd_src, self.bnd_dst, self.bnd_w, self.n_own)
 
 
 _COMPUTE_STREAMS = {}
@@ -746,11 +839,19 @@ class OverlappedAggregation:
         self.w_bnd = self.g_bnd.dst.to_csr_order(w_bnd.contiguous()) if w_bnd is not None else None
         self.n_interior = int(ei_int.shape[1])
         self.n_boundary = int(ei_bnd.shape[1])
-        # step_tiled: run the interior passes on a second stream beside the send
-        # packing (both read only the rank's own rows); the boundary passes wait
-        # for them.  Off by default; bench.py's warm-up times both and keeps the
-        # faster (the two streams may land on one hardware queue).
+        self.n_halo = self.n_local_src - plan.n_own
+        self._chunk = chunk
+        self._ei_bnd = ei_bnd
+        self._fused = None
+        # step_tiled / step_fused: run the interior pass(es) on a second stream
+        # beside the send packing (both read only the rank's own rows); the
+        # boundary passes wait for them.  Off by default; bench.py's warm-up times
+        # both and keeps the faster (the two streams may land on one hardware queue).
         self.split_interior = False
+        # step_fused: the boundary pass as one launch over every tile after the
+        # last tile's halo arrived (True), or one launch per tile as its halo
+        # arrives (False: tile t's boundary pass overlaps tile t+1's exchange)
+        self.one_boundary_launch = True
 
     def local_buffer(self, F, dtype=torch.float32, device=None):
         """[n_own + n_halo, F]: the owner writes rows [:n_own], the exchange the rest."""
@@ -918,39 +1019,233 @@ class OverlappedAggregation:
                 ops._aggregate(self.g_bnd.dst, "other", xt, self.w_bnd, "sum", _lib.MP_FLAG_INIT_FROM_OUT, b,
                                out=out[:, offs[t]:offs[t + 1]])
 
-    def _compute(self, x_tiles, out, bias, split=None):
+    # ------------------------------------------------------------------
+    # the fused step: own rows from the caller's row-major tensor, tile-major
+    # buffers holding only the exchanged rows, one launch per pass
+    # ------------------------------------------------------------------
+    def halo_buffers(self, F, width=128, device=None):
+        """HaloBuffers for step_fused: the send rows and the received halo rows,
+        tile-major ([T, rows, width], T = F / width), so each tile's rows are
+        contiguous and go over the links on their own, while each pass reads or
+        writes every tile in one launch.  width: 64, 128 or 256 (one tile:
+        whole rows), dividing F."""
+        dev = device or self.plan.halo_nodes.device
+        return HaloBuffers(self.n_send, self.n_halo, F, width, dev)
+
+    def _fused_graphs(self):
+        """(boundary graph over the halo rows alone -- columns = halo slot, the
+        same edges in the same order as g_bnd --, the send graph of the pull
+        exchange: one unweighted edge per requested row, the per-row flags
+        of the own rows with no boundary edge, int32), built once."""
+        if self._fused is None:
+            from .graph import Graph
+            n_own = self.plan.n_own
+            ei = self._ei_bnd
+            g_bh = Graph(torch.stack([ei[0] - n_own, ei[1]]), n_own, max(self.n_halo, 1), chunk=self._chunk)
+            g_sp = None
+            if self.cover is None and self.n_send:
+                si = self.plan.send_idx
+                g_sp = Graph(torch.stack([si, torch.arange(si.numel(), dtype=si.dtype, device=si.device)]),
+                             self.n_send, n_own, chunk=self._chunk)
+            rp = g_bh.dst.rowptr
+            no_bnd = (rp[1:] == rp[:-1]).to(torch.int32)     # per own row: 1 = no boundary edge
+            self._fused = (g_bh, g_sp, no_bnd)
+        return self._fused
+
+    def _pack_fused(self, x_own, bufs):
+        """Every tile's send rows in ONE launch: the cover's send graph (copies +
+        partial rows) or the pull requests, written tile-major into bufs.send."""
+        from . import ops
+        if self.n_send == 0:
+            return
+        g_bh, g_sp, _ = self._fused_graphs()
+        if self.cover is not None:
+            g, w = self.g_send.dst, self.w_send
+        else:
+            g, w = g_sp.dst, None
+        ops.aggregate_tiles(g, "other", x_own, w, bufs.F, bufs.send, "sum", 0, None,
+                            out_tiles=(bufs.width, bufs.n_send * bufs.width))
+
+    def _interior_fused(self, x_own, out, bias):
+        """The interior edges of every feature in one launch, with the bias of
+        the rows the boundary pass leaves untouched (no boundary edge: a per-row
+        flag; every row when no boundary edge follows at all)."""
+        from . import ops
+        if self.n_boundary == 0:
+            ops._aggregate(self.g_int.dst, "other", x_own, self.w_int, "sum", 0, bias, out=out)
+            return
+        F = x_own.shape[1]
+        ops.aggregate_tiles(self.g_int.dst, "other", x_own, self.w_int, F, out, "sum", 0, bias,
+                            bias_rows=self._fused_graphs()[2] if bias is not None else None)
+
+    def _boundary_fused(self, bufs, out, bias, tile=None):
+        """The boundary edges over the received halo rows on top of out
+        (MP_FLAG_INIT_FROM_OUT) + bias, rows without boundary edges untouched
+        (MP_FLAG_SKIP_EMPTY: their bias came with the interior pass): every tile
+        in one launch (tile None), or tile `tile` alone.  Each row's out values
+        are loaded with the gathers of its first slot's batch (the kernel's
+        out prefetch), not when the row opens."""
+        from . import _lib, ops
+        if self.n_boundary == 0:
+            return
+        g_bh, _, _ = self._fused_graphs()
+        flags = _lib.MP_FLAG_INIT_FROM_OUT | _lib.MP_FLAG_SKIP_EMPTY
+        if tile is None:
+            ops.aggregate_tiles(g_bh.dst, "other", bufs.recv, self.w_bnd, bufs.F, out, "sum", flags, bias,
+                                x_tiles=(bufs.width, bufs.n_halo * bufs.width))
+            return
+        c0, c1 = tile * bufs.width, (tile + 1) * bufs.width
+        b = bias[c0:c1] if bias is not None else None
+        ops.aggregate_tiles(g_bh.dst, "other", bufs.recv[tile], self.w_bnd, bufs.width, out[:, c0:c1], "sum", flags, b)
+
+    def _start_exchange(self, bufs, group=None):
+        """Every tile's all_to_all, started in tile order (RCCL runs them back to
+        back on its stream); returns one work handle per tile (None: gloo with
+        device tensors, done synchronously)."""
+        gloo = bufs.recv.is_cuda and dist.get_backend(group) == "gloo"
+        works = []
+        for t in range(bufs.n_tiles):
+            if gloo:
+                _a2a(bufs.recv[t], bufs.send[t], self.recv_counts, self.send_counts, group)
+                works.append(None)
+            else:
+                works.append(dist.all_to_all_single(bufs.recv[t], bufs.send[t], output_split_sizes=self.recv_counts,
+                                                    input_split_sizes=self.send_counts, group=group, async_op=True))
+        return works
+
+    def step_fused(self, x_own, bufs, out, bias=None, group=None, events=None):
+        """The step with one launch per pass:
+          1. pack every tile's send rows in one launch (tile-major bufs.send),
+             then start each tile's all_to_all into bufs.recv,
+          2. the interior edges in one launch over x_own (the caller's
+             row-major [n_own, F] rows: no copy into a tile buffer), beside the
+             packing on a second stream when split_interior,
+          3. the boundary edges over the received halo rows on top (INIT_FROM_OUT)
+             + bias: one launch after the last tile arrived
+             (one_boundary_launch), or per tile as each tile arrives.
+        Per row and feature the arithmetic is step()'s: bitwise the same output.
+        events: as step_tiled ('send', 'interior', 'wait', 'boundary')."""
+        if x_own.shape != (self.n_own, bufs.F) or x_own.stride(1) != 1:
+            raise ValueError("step_fused: x_own must be this rank's [%d, %d] rows (row-major)" % (self.n_own, bufs.F))
+        with compute_stream(out.device):
+            return self._step_fused(x_own, bufs, out, bias, group, events)
+
+    def _step_fused(self, x_own, bufs, out, bias=None, group=None, events=None):
+        def rec(name):
+            if events is None:
+                return None
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            events.setdefault(name, []).append(e)
+            return e
+        split = self.split_interior and out.is_cuda
+        if split:
+            start = torch.cuda.current_stream(out.device).record_event()
+        rec("send")
+        self._pack_fused(x_own, bufs)
+        works = self._start_exchange(bufs, group)
+        rec("send")
+        if split:
+            side = _side_stream(out.device)
+            side.wait_event(start)
+            with torch.cuda.stream(side):
+                rec("interior")
+                self._interior_fused(x_own, out, bias)
+                rec("interior")
+            torch.cuda.current_stream(out.device).wait_stream(side)
+        else:
+            rec("interior")
+            self._interior_fused(x_own, out, bias)
+            rec("interior")
+        if self.one_boundary_launch:
+            rec("wait")
+            for w in works:
+                if w is not None:
+                    w.wait()
+            rec("wait")
+            rec("boundary")
+            self._boundary_fused(bufs, out, bias)
+            rec("boundary")
+        else:
+            for t, w in enumerate(works):
+                rec("wait")
+                if w is not None:
+                    w.wait()
+                rec("wait")
+                rec("boundary")
+                self._boundary_fused(bufs, out, bias, tile=t)
+                rec("boundary")
+        return out
+
+    # ------------------------------------------------------------------
+    # the step's pieces, for either form (step_tiled's list of [own ; halo]
+    # tiles, or step_fused's (x_own, HaloBuffers)): timing and decomposition
+    # ------------------------------------------------------------------
+    def _pieces(self, form, out, bias):
+        """(pack, interior, boundary, exchange(group) -> works) of one form."""
+        n_own = self.plan.n_own
+        if isinstance(form, tuple):
+            x_own, bufs = form
+
+            def boundary():
+                if self.one_boundary_launch:
+                    self._boundary_fused(bufs, out, bias)
+                else:
+                    for t in range(bufs.n_tiles):
+                        self._boundary_fused(bufs, out, bias, tile=t)
+            return (lambda: self._pack_fused(x_own, bufs), lambda: self._interior_fused(x_own, out, bias), boundary,
+                    lambda group: self._start_exchange(bufs, group))
+        x_tiles = form
+        sends = {}
+
+        def pack():
+            sends["s"] = [self._send(xt[:n_own]) for xt in x_tiles]
+
+        def exchange(group):
+            if "s" not in sends:
+                pack()
+            return [self._exchange_async(xt, s, group) for xt, s in zip(x_tiles, sends["s"])]
+        return (pack, lambda: self._passes(x_tiles, out, bias, boundary=False),
+                lambda: self._passes(x_tiles, out, bias, interior=False), exchange)
+
+    def _compute(self, form, out, bias, split=None):
         """The step's device work without the exchange: send packing, interior
         and boundary passes (the interior beside the packing on the side stream
         when split, default self.split_interior), on the current stream."""
         split = self.split_interior if split is None else split
-        n_own = self.plan.n_own
+        pack, interior, boundary, _ = self._pieces(form, out, bias)
         if not (split and out.is_cuda):
-            for xt in x_tiles:
-                self._send(xt[:n_own])
-            self._passes(x_tiles, out, bias)
+            pack()
+            interior()
+            boundary()
             return
         cur = torch.cuda.current_stream(out.device)
         start = cur.record_event()
-        for xt in x_tiles:
-            self._send(xt[:n_own])
+        pack()
         side = _side_stream(out.device)
         side.wait_event(start)
         with torch.cuda.stream(side):
-            self._passes(x_tiles, out, bias, boundary=False)
+            interior()
         cur.wait_stream(side)
-        self._passes(x_tiles, out, bias, interior=False)
+        boundary()
 
-    def compute_in_turn(self, x_tiles, out, bias=None, reps=5, group=None, barrier=None):
+    def _step_form(self, form, out, bias, group=None):
+        if isinstance(form, tuple):
+            return self.step_fused(form[0], form[1], out, bias, group)
+        return self.step_tiled(form, out, bias, group)
+
+    def compute_in_turn(self, form, out, bias=None, reps=5, group=None, barrier=None):
         """decompose()'s compute alone, one rank at a time: rank r times its
         send pack, interior and boundary passes with HIP events on the compute
         stream while every other rank waits at `barrier`.  Ranks that share
         one GPU (the gloo rehearsal) get the compute time each rank would have
         on a GPU of its own; on a node it equals compute_only_ms.  Also the
-        same work with the interior passes beside the send packing
-        (compute_alone_split_ms, split_interior).  Collective over `group`
+        same work with the interior pass(es) beside the send packing
+        (compute_alone_split_ms, split_interior).  form: step_tiled's tile
+        list, or (x_own, HaloBuffers) of step_fused.  Collective over `group`
         (every rank calls it)."""
         rank, world = dist.get_rank(group), dist.get_world_size(group)
-        n_own = self.plan.n_own
+        pack, interior, boundary, _ = self._pieces(form, out, bias)
         res = None
         for r in range(world):
             if barrier is not None:
@@ -958,29 +1253,26 @@ class OverlappedAggregation:
             if r != rank:
                 continue
             with compute_stream(out.device):
-                for xt in x_tiles:
-                    self._send(xt[:n_own])
-                self._passes(x_tiles, out, bias)
+                self._compute(form, out, bias, split=False)
                 ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
                 parts = [[], [], []]
                 for _ in range(reps):
                     ev[0].record()
-                    for xt in x_tiles:
-                        self._send(xt[:n_own])
+                    pack()
                     ev[1].record()
-                    self._passes(x_tiles, out, bias, boundary=False)
+                    interior()
                     ev[2].record()
-                    self._passes(x_tiles, out, bias, interior=False)
+                    boundary()
                     ev[3].record()
                     ev[3].synchronize()
                     for j in range(3):
                         parts[j].append(ev[j].elapsed_time(ev[j + 1]))
-                # the same work with the interior passes on the side stream beside
+                # the same work with the interior pass(es) on the side stream beside
                 # the send packing (split_interior), timed on the compute stream
                 split = []
                 for _ in range(reps):
                     ev[0].record()
-                    self._compute(x_tiles, out, bias, split=True)
+                    self._compute(form, out, bias, split=True)
                     ev[3].record()
                     ev[3].synchronize()
                     split.append(ev[0].elapsed_time(ev[3]))
@@ -994,7 +1286,7 @@ class OverlappedAggregation:
             barrier()
         return res
 
-    def decompose(self, x_tiles, out, bias=None, reps=5, group=None, barrier=None):
+    def decompose(self, form, out, bias=None, reps=5, group=None, barrier=None):
         """The overlapped step taken apart on this rank, each piece timed alone
         (wall clock over `reps` repetitions, the device synchronised after
         them, the ranks lined up by `barrier` before each piece):
@@ -1007,53 +1299,100 @@ class OverlappedAggregation:
                              split_interior, as the step runs them);
           serial_step_ms     pack, exchange and wait, then the interior and
                              boundary passes: the step without overlap;
-          overlapped_step_ms step_tiled itself, timed the same way.
+          overlapped_step_ms the step itself, timed the same way.
         hidden_frac = (exchange + compute - overlapped) / min(exchange, compute)
         is the share of the shorter piece the overlap hides (1 = all of it;
         below 0, the overlapped step is slower than the two pieces in a row,
-        e.g. RCCL's kernels contending with the aggregation for CUs / L2)."""
+        e.g. RCCL's kernels contending with the aggregation for CUs / L2).  It
+        is reported only where the pieces are comparable (hidden_frac_valid):
+        when the exchange alone takes longer than the whole serial step (the
+        gloo rehearsal, whose host staging makes exchange timings swing from
+        one measurement to the next) or the ratio leaves [-1, 1], it is None
+        with the reason in hidden_frac_note.  form: as compute_in_turn."""
         import time
-        n_own = self.plan.n_own
+        pack, interior, boundary, exchange_start = self._pieces(form, out, bias)
 
         def timed(fn):
             if barrier is not None:
                 barrier()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            with compute_stream(out.device):      # where step_tiled runs its work
+            with compute_stream(out.device):      # where the step runs its work
                 for _ in range(reps):
                     fn()
             torch.cuda.synchronize()
             return (time.perf_counter() - t0) / reps * 1e3
 
         with compute_stream(out.device):
-            sends = [self._send(xt[:n_own]) for xt in x_tiles]
+            pack()
 
         def exchange_only():
-            works = [self._exchange_async(xt, s, group) for xt, s in zip(x_tiles, sends)]
-            for w in works:
+            for w in exchange_start(group):
                 if w is not None:
                     w.wait()
 
         def compute_only():
-            self._compute(x_tiles, out, bias)
+            self._compute(form, out, bias)
 
         def serial():
-            works = [self._exchange_async(xt, self._send(xt[:n_own]), group) for xt in x_tiles]
-            for w in works:
+            pack()
+            for w in exchange_start(group):
                 if w is not None:
                     w.wait()
-            self._passes(x_tiles, out, bias)
+            interior()
+            boundary()
 
         res = {"reps": reps,
                "exchange_only_ms": timed(exchange_only),
                "compute_only_ms": timed(compute_only),
                "serial_step_ms": timed(serial),
-               "overlapped_step_ms": timed(lambda: self.step_tiled(x_tiles, out, bias, group))}
-        shorter = min(res["exchange_only_ms"], res["compute_only_ms"])
-        res["hidden_frac"] = ((res["exchange_only_ms"] + res["compute_only_ms"] - res["overlapped_step_ms"]) / shorter
-                              if shorter > 1e-3 else None)
+               "overlapped_step_ms": timed(lambda: self._step_form(form, out, bias, group))}
+        res.update(hidden_fraction(res))
         return res
+
+
+def hidden_fraction(res):
+    """hidden_frac of a decomposition {exchange_only_ms, compute_only_ms,
+    serial_step_ms, overlapped_step_ms} (OverlappedAggregation.decompose), or
+    None with the reason when the pieces are not comparable: the exchange alone
+    longer than the serial step that contains it (host-staged gloo exchanges
+    swing between measurements), a shorter piece of ~0 ms (one rank), or a
+    ratio outside [-1, 1]."""
+    ex, co = res["exchange_only_ms"], res["compute_only_ms"]
+    shorter = min(ex, co)
+    if shorter <= 1e-3:
+        return {"hidden_frac": None, "hidden_frac_valid": False,
+                "hidden_frac_note": "the shorter piece takes ~0 ms (empty splits): nothing to hide"}
+    if "serial_step_ms" in res and ex > res["serial_step_ms"]:
+        return {"hidden_frac": None, "hidden_frac_valid": False,
+                "hidden_frac_note": "exchange alone (%.3f ms) exceeds the serial step (%.3f ms): the exchange "
+                                    "timings are not comparable (host-staged gloo)" % (ex, res["serial_step_ms"])}
+    h = (ex + co - res.get("overlapped_step_ms", res.get("step_ms"))) / shorter
+    if not -1.0 <= h <= 1.0:
+        return {"hidden_frac": None, "hidden_frac_valid": False,
+                "hidden_frac_note": "ratio %.3f outside [-1, 1]: the pieces are not comparable" % h}
+    return {"hidden_frac": h, "hidden_frac_valid": True, "hidden_frac_note": None}
+
+
+class HaloBuffers:
+    """The fused step's exchange buffers (OverlappedAggregation.halo_buffers):
+    send [T, n_send, width] and recv [T, n_halo, width], T = F / width,
+    tile-major -- tile t's rows contiguous (one all_to_all per tile), every
+    tile addressed by the kernel in one launch (mp_aggregate_tiles_f32).  The
+    rank's own rows stay in the caller's row-major tensor."""
+
+    def __init__(self, n_send, n_halo, F, width, device):
+        width = int(width)
+        if width not in (64, 128, 256) or F % width:
+            raise ValueError("HaloBuffers: width %d must be 64, 128 or 256 and divide F = %d" % (width, F))
+        self.F, self.width, self.n_tiles = int(F), width, int(F) // width
+        self.n_send, self.n_halo = int(n_send), int(n_halo)
+        self.send = torch.empty((self.n_tiles, self.n_send, width), dtype=torch.float32, device=device)
+        self.recv = torch.empty((self.n_tiles, self.n_halo, width), dtype=torch.float32, device=device)
+
+    def halo_rows(self):
+        """The received halo rows as one row-major [n_halo, F] tensor (a copy)."""
+        return self.recv.permute(1, 0, 2).reshape(self.n_halo, self.F)
 
 
 def transposed_plan(edge_index, num_nodes, rank, world, cuts, group=None):
@@ -1144,7 +1483,7 @@ class ShardedGraph:
         backward runs over the rank's local transposed CSR, and the gradients of
         its halo rows go back to their owners (halo_rows)."""
         from torch_geometric.nn.conv._structure import gat_loops
-        ei = gat_loops(edge_index, num_nodes) if edge_index.is_cuda else _host_gat_loops(edge_index, num_nodes)
+        ei = gat_loops(edge_index, num_nodes) if edge_index.is_cuda else _host("gat_loops")(edge_index, num_nodes)
         plan = ShardPlan(ei, num_nodes, rank, world, cuts=cuts).exchange_requests(group)
         return cls._for_gat_plan(plan, ei.shape[1], group)
 
@@ -1199,10 +1538,12 @@ class ShardedGraph:
         (ops.gat_propagate); the gloo CPU tests pass the oracle."""
         from .gat_cover import cover_ok
         gc = getattr(self, "gat_cover", None)
-        if gc is not None and not return_alpha and not dropout and local_gat is None \
-                and (not xw_own.is_cuda or cover_ok(heads, out_channels)):
-            from .gat_cover import gat_cover_propagate
-            return gat_cover_propagate(gc, xw_own, att, heads, out_channels, negative_slope, bias), None
+        if gc is not None and not return_alpha and not dropout and local_gat is None:
+            if not xw_own.is_cuda:
+                return _host("gat_cover_forward")(gc, xw_own, att, heads, out_channels, negative_slope, bias), None
+            if cover_ok(heads, out_channels):
+                from .gat_cover import gat_cover_propagate
+                return gat_cover_propagate(gc, xw_own, att, heads, out_channels, negative_slope, bias), None
         if local_gat is None:
             from . import ops
             local_gat = ops.gat_propagate
@@ -1354,13 +1695,6 @@ class _ShardedAggregate(torch.autograd.Function):
         w_bwd = sg._w[1] if sg._w is not None else None
         gx, _ = ops._aggregate(sg.g_bwd.dst, "other", g_local, w_bwd, "sum", 0, None)
         return gx, None, None
-
-
-def _host_gat_loops(edge_index, num_nodes):
-    """remove_self_loops + add_self_loops on host tensors (the gloo CPU tests)."""
-    keep = edge_index[0] != edge_index[1]
-    loops = torch.arange(int(num_nodes), dtype=edge_index.dtype).view(1, -1).repeat(2, 1)
-    return torch.cat([edge_index[:, keep], loops], 1)
 
 
 def broadcast_parameters(module, src=0, group=None):

@@ -41,10 +41,10 @@ cross-degree; on RMAT graphs 0.56-0.57x the pull rows).  One step:
   Every collective runs in the same order on every rank.
 
 Device path: the HIP kernels (GatHaloCover.forward_device / backward_device,
-wrapped by _GatCoverFn).  Host path (forward_host): the same data flow with
-differentiable torch ops and a differentiable all_to_all -- the gloo CPU tests
-check the distributed algorithm, forward and backward, against the
-single-process oracle with it.  Heads of any width (GATConv pads C to a
+wrapped by _GatCoverFn); no CPU fallback.  The gloo CPU tests check the
+distributed algorithm, forward and backward, against the single-process
+oracle with a host twin of the same data flow in differentiable torch ops
+(tests/_host_twins.py, installed through dist.install_host_twins).  Heads of any width (GATConv pads C to a
 multiple of 4): C / 4 a power of two <= 64 takes the fused transposed pass,
 whose per-edge d score gives a pusher its share of d a_dst; other widths the
 wide kernels, the share then node-wise from the pieces' training accumulators
@@ -68,25 +68,6 @@ def cover_ok(H, C):
     """Head shapes the device path takes: any C % 4 == 0 (GATConv pads every
     head to it); fused_heads picks the kernels."""
     return H > 0 and C > 0 and C % 4 == 0
-
-
-class _A2A(torch.autograd.Function):
-    """Differentiable all_to_all_single of rows: forward send -> recv with the
-    given splits, backward the reverse exchange of the gradient."""
-
-    @staticmethod
-    def forward(ctx, send, recv_counts, send_counts, group):
-        ctx.counts, ctx.group = (recv_counts, send_counts), group
-        recv = send.new_empty((sum(recv_counts),) + tuple(send.shape[1:]))
-        _a2a(recv, send.contiguous(), recv_counts, send_counts, group)
-        return recv
-
-    @staticmethod
-    def backward(ctx, g):
-        recv_counts, send_counts = ctx.counts
-        gs = g.new_empty((sum(send_counts),) + tuple(g.shape[1:]))
-        _a2a(gs, g.contiguous(), send_counts, recv_counts, ctx.group)
-        return gs, None, None, None
 
 
 def _cat_ranges(starts, lengths, dev):
@@ -120,16 +101,14 @@ class GatHaloCover:
         self.recv_counts, self.send_counts = hc.recv_counts, hc.send_counts
         self.n_pull_rows, self.n_push_rows = hc.n_pull_rows, hc.n_push_rows
         self.n_pull_edges, self.n_push_edges = hc.n_pull_edges, hc.n_push_edges
-        # the local piece: plan order (= global edge order), pushed edges left out
+        # the local piece: plan order (= global edge order), pushed edges left out,
+        # a pulled edge's source replaced by its halo slot
         lei = plan.local_edge_index
         src, dst = lei[0].clone(), lei[1]
-        keep = ~hc.rem
-        rem_idx = torch.nonzero(hc.rem).view(-1)
-        pulled = rem_idx[hc.pull]
-        keep[pulled] = True
-        src[pulled] = hc.pull_halo
-        self.loc_src, self.loc_dst = src[keep].contiguous(), dst[keep].contiguous()
-        self.n_interior = int((~hc.rem).sum())
+        src[hc.pull_pos] = hc.pull_halo
+        loc = torch.sort(torch.cat([hc.int_pos, hc.pull_pos])).values
+        self.loc_src, self.loc_dst = src[loc].contiguous(), dst[loc].contiguous()
+        self.n_interior = int(hc.int_pos.numel())
         # received pieces -> own destination (the merge list)
         self.part_row = (hc.push_halo - n_own).contiguous()
         self.part_dst = hc.push_dst.contiguous()
@@ -174,56 +153,6 @@ class GatHaloCover:
                 "cover_push_edges": self.n_push_edges, "halo_rows": self.n_halo,
                 "pull_halo_rows": self.plan.n_local_src - self.plan.n_own,
                 "send_rows": self.n_send, "local_piece_edges": int(self.loc_src.numel())}
-
-    # ------------------------------------------------------------ host (oracle)
-    def forward_host(self, xw_own, att, H, C, slope=0.2, bias=None):
-        """The same step with differentiable torch ops (any device, any float
-        dtype): the reference the gloo CPU tests hold the algorithm to, forward
-        and backward (autograd through a differentiable all_to_all).  Returns the
-        rank's rows [n_own, H*C] (+ bias)."""
-        n_own, F = self.n_own, H * C
-        g = self.group
-        att2 = att.reshape(H, 2 * C)
-
-        def scores(x):
-            x3 = x.view(-1, H, C)
-            return (x3 * att2[:, :C]).sum(-1), (x3 * att2[:, C:]).sum(-1)     # a_dst, a_src
-
-        def piece(x_src, a_src, a_dst_rows, src, dst, n_rows):
-            """(out = acc / den, m, den) of the softmax over each row's edges."""
-            e = torch.nn.functional.leaky_relu(a_src[src] + a_dst_rows[dst], slope)
-            m = torch.full((n_rows, H), float("-inf"), dtype=x_src.dtype, device=x_src.device)
-            m = m.scatter_reduce(0, dst.view(-1, 1).expand(-1, H), e.detach(), "amax", include_self=True)
-            p = torch.exp(e - m[dst])
-            den = torch.zeros((n_rows, H), dtype=x_src.dtype, device=x_src.device).index_add(0, dst, p) + 1e-16
-            msg = x_src[src].view(-1, H, C) * p.unsqueeze(-1)
-            acc = torch.zeros((n_rows, H, C), dtype=x_src.dtype, device=x_src.device).index_add(0, dst, msg)
-            return acc / den.unsqueeze(-1), m, den
-
-        a_dst_own, a_src_own = scores(xw_own)
-        # 1. a_dst of the rows the peers push pieces of
-        adst_in = _A2A.apply(a_dst_own[self.adst_rows], self.adst_recv_counts, self.adst_send_counts, g)
-        send_adst = a_dst_own.new_zeros((self.n_send, H)).index_copy(0, self.send_push_rows, adst_in)
-        # 2. the send rows and their stats
-        s_out, s_m, s_den = piece(xw_own, a_src_own, send_adst, self.send_src, self.send_dst, self.n_send)
-        recv = _A2A.apply(s_out.reshape(self.n_send, F), self.recv_counts, self.send_counts, g)
-        r_m = _A2A.apply(s_m, self.recv_counts, self.send_counts, g)
-        r_den = _A2A.apply(s_den, self.recv_counts, self.send_counts, g)
-        # 3. the local piece over [own ; received rows]
-        x_loc = torch.cat([xw_own, recv])
-        _, a_src_loc = scores(x_loc)
-        o, m, den = piece(x_loc, a_src_loc, a_dst_own, self.loc_src, self.loc_dst, n_own)
-        # 4. merge: local piece, then the peers' pieces
-        pm, pden, po = r_m[self.part_row], r_den[self.part_row], recv[self.part_row].view(-1, H, C)
-        M = m.detach().scatter_reduce(0, self.part_dst.view(-1, 1).expand(-1, H), pm.detach(), "amax",
-                                      include_self=True)
-        w_loc = den * torch.exp(m - M)
-        w_p = pden * torch.exp(pm - M[self.part_dst])
-        tot = w_loc.index_add(0, self.part_dst, w_p)
-        out = o * (w_loc / tot).unsqueeze(-1)
-        out = out.index_add(0, self.part_dst, po * (w_p / tot[self.part_dst]).unsqueeze(-1))
-        out = out.reshape(n_own, F)
-        return out + bias if bias is not None else out
 
     # ---------------------------------------------------------- device (HIP)
     def forward_device(self, xw_own, att_c, H, C, slope, bias, train, exchange=True):
@@ -313,11 +242,14 @@ class GatHaloCover:
             del slab
             # 4. merge the pieces (+ bias; agg2 / s2 scaled to the merged rows)
             m = g_merge.dst
-            n_parts = int(self.part_row.numel())
+            merged = self.part_row.numel() > 0
+            n_parts = self.n_halo if merged else 0       # rows of the receive buffer the merge list names
             _lib.check(lib.mp_gat_merge_partials_f32(n_own, H, C, m.rowptr.data_ptr(),
-                                                     m.col.data_ptr() if n_parts else None, n_parts,
-                                                     xl[n_own:].data_ptr() if n_parts else None, F,
-                                                     r_st.data_ptr() if n_parts else None, _lib.ptr(bias),
+                                                     m.col.data_ptr() if merged else None, n_parts,
+                                                     xl[n_own:].data_ptr() if merged else None,
+                                                     _lib.nbytes(xl[n_own:]), F,
+                                                     r_st.data_ptr() if merged else None, _lib.nbytes(r_st),
+                                                     _lib.ptr(bias),
                                                      out.data_ptr(), F, stats.data_ptr(), _lib.ptr(agg2),
                                                      _lib.ptr(s2), st), "mp_gat_merge_partials_f32")
         saved = (xl, a_src, a_dst, stats, agg2, s2, send_st, send2, send_s2) if train else None
@@ -364,9 +296,8 @@ class GatHaloCover:
                "compute_only_ms": timed(lambda: self.forward_device(xw_own, att_c, H, C, slope, bias, False,
                                                                    exchange=False)),
                "step_ms": timed(lambda: self.forward_device(xw_own, att_c, H, C, slope, bias, False))}
-        shorter = min(res["exchange_only_ms"], res["compute_only_ms"])
-        res["hidden_frac"] = ((res["exchange_only_ms"] + res["compute_only_ms"] - res["step_ms"]) / shorter
-                              if shorter > 1e-3 else None)
+        from .dist import hidden_fraction
+        res.update(hidden_fraction(res))
         return res
 
     def backward_device(self, g, out, bias, att_c, H, C, slope, saved, want_att, want_bias):
@@ -529,14 +460,14 @@ class _GatCoverFn(torch.autograd.Function):
 
 
 def gat_cover_propagate(cover, xw_own, att, heads, out_channels, negative_slope=0.2, bias=None):
-    """This rank's rows of the fused GATConv aggregation over the cover (+ bias);
-    device tensors take the HIP path with its native backward, host tensors the
-    differentiable torch form (forward_host)."""
+    """This rank's rows of the fused GATConv aggregation over the cover (+ bias)
+    on the HIP path with its native backward; a host tensor raises."""
     H, C = int(heads), int(out_channels)
     if xw_own.shape[0] != cover.n_own:
         raise ValueError("mi355_mp.gat_cover: xw_own has %d rows, this rank owns %d" % (xw_own.shape[0], cover.n_own))
     if not xw_own.is_cuda:
-        return cover.forward_host(xw_own, att, H, C, negative_slope, bias)
+        raise RuntimeError("mi355_mp.gat_cover: host tensors -- there is no CPU fallback: the engine runs on ROCm "
+                           "device tensors")
     if not cover_ok(H, C):
         raise ValueError("mi355_mp.gat_cover: heads of %d features need C %% 4 == 0 (GATConv pads them)" % C)
     needs = torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in (xw_own, att, bias))

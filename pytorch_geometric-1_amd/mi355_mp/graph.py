@@ -93,15 +93,15 @@ class CSR:
         _lib.check(lib.mp_csr_build(key.data_ptr(), _lib.ptr(other), E, self.n_rows, self.n_other,
                                     self.rowptr.data_ptr(), self.col.data_ptr(), self.eid.data_ptr(),
                                     bad.data_ptr(), ws.data_ptr(), ws_bytes, st), "mp_csr_build")
-        nbad = int(bad.item())
-        if nbad:
-            raise IndexError("mi355_mp: %d edge indices out of range (rows %d, columns %d)"
-                             % (nbad, self.n_rows, self.n_other))
+        # the bad-index count is read together with the schedule's split-row count:
+        # one host sync per CSR (the schedule over a rowptr that skipped bad ids is
+        # still well formed, and is dropped with the raise)
+        self._build_schedule(bad)
         del ws
-        self._build_schedule()
 
-    def _build_schedule(self):
-        """Merge-path schedule over rowptr (tasks of `chunk` rows + slots)."""
+    def _build_schedule(self, bad=None):
+        """Merge-path schedule over rowptr (tasks of `chunk` rows + slots); bad:
+        the CSR build's out-of-range count, read in the same host sync."""
         lib = _lib.load()
         dev, E = self.device, self.n_edges
         st = _lib.stream_ptr(dev)
@@ -116,7 +116,13 @@ class CSR:
                                          self.wave_row.data_ptr(), self.wave_slot.data_ptr(),
                                          self.split_waves.data_ptr(), n_split.data_ptr(),
                                          ws.data_ptr(), sws, st), "mp_schedule_build")
-        self.n_split = int(n_split.item())
+        if bad is None:
+            self.n_split = int(n_split.item())
+        else:
+            nbad, self.n_split = torch.cat([bad, n_split]).tolist()
+            if nbad:
+                raise IndexError("mi355_mp: %d edge indices out of range (rows %d, columns %d)"
+                                 % (nbad, self.n_rows, self.n_other))
         self._structs = {}
         self._deg = None
 

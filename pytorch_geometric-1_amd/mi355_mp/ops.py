@@ -104,6 +104,36 @@ def _aggregate(csr, gather, x, w_csr, reduce, flags, bias, out=None, stages=_lib
     return out, arg
 
 
+def aggregate_tiles(csr, gather, x, w_csr, F, out, reduce="sum", flags=0, bias=None, x_tiles=None, out_tiles=None,
+                    slab=None, stages=_lib.MP_STAGE_ALL, bias_rows=None):
+    """One sum / mean launch (mp_aggregate_tiles_f32) over operands held
+    tile-major: x_tiles / out_tiles = (width, stride in elements) when x / out
+    is a [T, rows, width] buffer (feature f of row r at
+    [f // width][r][f % width]), None when row-major (then x / out is a 2-D
+    tensor and its row stride is used).  bias_rows: None, or int32 [rows]
+    flags -- the bias goes only to rows whose flag is nonzero.  Bitwise the
+    arithmetic of _aggregate on the same values laid out row-major.  Returns
+    out."""
+    lib = _lib.load()
+    dev = out.device
+    if csr.n_rows == 0:
+        return out
+    g = csr.struct(gather)
+    red = _lib.MP_REDUCE[reduce]
+    sb = lib.mp_aggregate_slab_bytes(g, F, red)
+    if slab is None or slab.numel() < sb:
+        slab = torch.empty(sb, dtype=torch.uint8, device=dev)
+    xw, xs = x_tiles if x_tiles is not None else (0, 0)
+    ow, os_ = out_tiles if out_tiles is not None else (0, 0)
+    ldx = 0 if x_tiles is not None else x.stride(0)
+    ldo = 0 if out_tiles is not None else out.stride(0)
+    _lib.check(lib.mp_aggregate_tiles_f32(g, _lib.ptr(w_csr), x.data_ptr() if x.numel() else None, ldx, xw, xs, F, red,
+                                          flags, _lib.ptr(bias), _lib.ptr(bias_rows), out.data_ptr(), ldo, ow, os_,
+                                          slab.data_ptr(), sb,
+                                          stages, _lib.stream_ptr(dev)), "mp_aggregate_tiles_f32")
+    return out
+
+
 def gather_rows(x, idx):
     """out = x[idx] via the native row gather (no autograd; see GatherRows)."""
     lib = _lib.load()
@@ -520,14 +550,17 @@ def segment_sum_serial(csr, values, out=None):
     return out
 
 
-def norm_from_degree(row, col, deg, edge_weight):
+def norm_from_degree(row, col, deg, edge_weight, trusted=False):
     """dinv = deg^-1/2 (inf -> 0, torch's CPU pow(-0.5) rounding), then
     dinv[row] * w * dinv[col] (mp_gcn_norm_from_deg_f32).  deg is consumed.
     The kernel reads deg[row[e]] and deg[col[e]]: an id outside [0, deg.numel())
-    raises IndexError first, as the reference's deg_inv_sqrt[row] / [col] does."""
+    raises IndexError first, as the reference's deg_inv_sqrt[row] / [col] does.
+    trusted=True (ids the caller built in range, e.g. a shard plan's local
+    edges): no range check, so no host read-back."""
     _lib.require_device(row, col, deg, edge_weight)
-    check_row_index(row, deg.numel(), "gcn_norm (row)")
-    check_row_index(col, deg.numel(), "gcn_norm (col)")
+    if not trusted:
+        check_row_index(row, deg.numel(), "gcn_norm (row)")
+        check_row_index(col, deg.numel(), "gcn_norm (col)")
     E = row.numel()
     w = edge_weight.to(torch.float32).contiguous() if edge_weight is not None else None
     norm = torch.empty(E, dtype=torch.float32, device=row.device)

@@ -158,6 +158,39 @@ static void extents_arg_backward(void) {
   ACCEPT(mp_scatter_arg_grad_w_f32(DEVL, DEVL, E, DEVI, DEVU, mask, F, DEVF, F, DEVF, F, DEVF, NULL));
 }
 
+static void abi7(void) {
+  /* the GAT merge list's part_out [n_parts, ldp] / part_stats [n_parts, H, 2] */
+  const int64_t n = 1000, np = 300;
+  const int H = 6, C = 124, F = H * C;
+  const size_t po = (size_t)((np - 1) * F + F) * 4, ps = (size_t)np * H * 2 * 4;
+  REJECT("part_out", mp_gat_merge_partials_f32(n, H, C, DEVI, DEVI, np, DEVF, po - 4, F, DEVF, ps, NULL, DEVF, F, DEVF,
+                                               NULL, NULL, NULL));
+  REJECT("part_stats", mp_gat_merge_partials_f32(n, H, C, DEVI, DEVI, np, DEVF, po, F, DEVF, ps - 1, NULL, DEVF, F,
+                                                 DEVF, NULL, NULL, NULL));
+  ACCEPT(mp_gat_merge_partials_f32(n, H, C, DEVI, DEVI, np, DEVF, po, F, DEVF, ps, NULL, DEVF, F, DEVF, NULL, NULL,
+                                   NULL));
+  /* tile-major sum / mean: tiles of 64k features dividing F, no overlap */
+  const int64_t N = 2000, E = 9000;
+  mp_csr g = graph(N, E, (int32_t)N);
+  const size_t slab = mp_aggregate_slab_bytes(&g, 256, MP_REDUCE_SUM);
+  REJECT("sum or mean", mp_aggregate_tiles_f32(&g, DEVF, DEVF, 0, 128, N * 128, 256, MP_REDUCE_MAX, 0, NULL, NULL, DEVF, 256,
+                                               0, 0, DEV, slab, 7, NULL));
+  REJECT("64k features", mp_aggregate_tiles_f32(&g, DEVF, DEVF, 0, 96, N * 96, 192, MP_REDUCE_SUM, 0, NULL, NULL, DEVF, 192,
+                                                0, 0, DEV, slab, 7, NULL));
+  REJECT("not overlap", mp_aggregate_tiles_f32(&g, DEVF, DEVF, 0, 128, N * 128 - 1, 256, MP_REDUCE_SUM, 0, NULL, NULL, DEVF,
+                                               256, 0, 0, DEV, slab, 7, NULL));
+  REJECT("not overlap", mp_aggregate_tiles_f32(&g, DEVF, DEVF, 256, 0, 0, 256, MP_REDUCE_SUM, 0, NULL, NULL, DEVF, 0, 64,
+                                               N * 64 - 64, DEV, slab, 7, NULL));
+  REJECT("flags", mp_aggregate_tiles_f32(&g, DEVF, DEVF, 256, 0, 0, 256, MP_REDUCE_SUM, MP_FLAG_PYG_MASK, NULL, NULL, DEVF,
+                                         256, 128, N * 128, DEV, slab, 7, NULL));
+  REJECT("slab", mp_aggregate_tiles_f32(&g, DEVF, DEVF, 0, 128, N * 128, 256, MP_REDUCE_SUM, 0, NULL, NULL, DEVF, 256, 0, 0,
+                                        DEV, slab - 1, 7, NULL));
+  ACCEPT(mp_aggregate_tiles_f32(&g, DEVF, DEVF, 0, 128, N * 128, 256, MP_REDUCE_SUM, MP_FLAG_INIT_FROM_OUT, NULL, NULL, DEVF,
+                                256, 0, 0, DEV, slab, 7, NULL));
+  ACCEPT(mp_aggregate_tiles_f32(&g, DEVF, DEVF, 256, 0, 0, 256, MP_REDUCE_MEAN, 0, DEVF, NULL, DEVF, 0, 64, N * 64, DEV, slab,
+                                7, NULL));
+}
+
 static void workspaces(void) {
   /* entry points whose workspace extents predate ABI 6 */
   const int64_t E = 10000, N = 2000;
@@ -266,15 +299,17 @@ static void null_pointers(void) {
   REJECT("null", mp_segment_ids_i64(NULL, n, DEVL, 3, NULL));
   REJECT("null", mp_gat_dropout_keep(1, 0.5f, 8, E, NULL, NULL));
   REJECT("dropout p", mp_gat_dropout_keep(1, 1.0f, 8, E, DEVU, NULL));
-  REJECT("C % 4", mp_gat_merge_partials_f32(n, 8, 30, DEVI, DEVI, 10, DEVF, 256, DEVF, NULL, DEVF, 256, DEVF, NULL,
-                                            NULL, NULL));
-  REJECT("null", mp_gat_merge_partials_f32(n, 8, 32, DEVI, NULL, 10, DEVF, 256, DEVF, NULL, DEVF, 256, DEVF, NULL,
-                                           NULL, NULL));
-  REJECT("leading dimension", mp_gat_merge_partials_f32(n, 8, 32, DEVI, DEVI, 10, DEVF, 255, DEVF, NULL, DEVF, 256,
-                                                        DEVF, NULL, NULL, NULL));
-  REJECT("16-byte", mp_gat_merge_partials_f32(n, 8, 32, DEVI, DEVI, 10, DEVF, 256, DEVF, (float*)((char*)DEV + 4),
-                                              DEVF, 256, DEVF, NULL, NULL, NULL));
-  ACCEPT(mp_gat_merge_partials_f32(n, 8, 32, DEVI, NULL, 0, NULL, 0, NULL, NULL, DEVF, 256, DEVF, NULL, NULL, NULL));
+  const size_t po = 10 * 256 * 4, ps = 10 * 8 * 2 * 4;  /* part_out / part_stats of 10 pieces */
+  REJECT("C % 4", mp_gat_merge_partials_f32(n, 8, 30, DEVI, DEVI, 10, DEVF, po, 256, DEVF, ps, NULL, DEVF, 256, DEVF,
+                                            NULL, NULL, NULL));
+  REJECT("null", mp_gat_merge_partials_f32(n, 8, 32, DEVI, NULL, 10, DEVF, po, 256, DEVF, ps, NULL, DEVF, 256, DEVF,
+                                           NULL, NULL, NULL));
+  REJECT("leading dimension", mp_gat_merge_partials_f32(n, 8, 32, DEVI, DEVI, 10, DEVF, po, 255, DEVF, ps, NULL,
+                                                        DEVF, 256, DEVF, NULL, NULL, NULL));
+  REJECT("16-byte", mp_gat_merge_partials_f32(n, 8, 32, DEVI, DEVI, 10, DEVF, po, 256, DEVF, ps,
+                                              (float*)((char*)DEV + 4), DEVF, 256, DEVF, NULL, NULL, NULL));
+  ACCEPT(mp_gat_merge_partials_f32(n, 8, 32, DEVI, NULL, 0, NULL, 0, 0, NULL, 0, NULL, DEVF, 256, DEVF, NULL, NULL,
+                                   NULL));
   REJECT("bad argument", mp_heads_outer_add_f32(DEVF, 256, NULL, n, 8, 32, DEVF, 64, NULL));
   REJECT("bad argument", mp_gat_alpha_f32(DEVL, NULL, E, 8, DEVF, DEVF, 0.2f, DEVF, DEVF, NULL));
   REJECT("bad arguments", mp_self_loop_count(NULL, DEVL, E, n, DEVL, NULL));
@@ -299,6 +334,7 @@ int main(void) {
   }
   extents_gat_backward();
   extents_arg_backward();
+  abi7();
   workspaces();
   null_pointers();
   printf("abi_reject: %d cases, %d failures\n", n_cases, n_fail);

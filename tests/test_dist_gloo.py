@@ -25,6 +25,8 @@ def _worker(rank, world, port, result_q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from mi355_mp import dist as mdist
+        from tests import _host_twins
+        _host_twins.install()   # host twins of the native kernels (no CPU fallback in mi355_mp)
         from mi355_mp.graphgen import powerlaw_edge_index
         from oracle import scatter_ref as S
         N, E, F = 900, 12000, 7
@@ -110,6 +112,8 @@ def _slices_worker(rank, world, port, result_q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from mi355_mp import dist as mdist
+        from tests import _host_twins
+        _host_twins.install()   # host twins of the native kernels (no CPU fallback in mi355_mp)
         from mi355_mp.graphgen import powerlaw_edge_index
         from oracle import pyg_ref as P, scatter_ref as S
         N, E, F = 700, 9000, 5
@@ -174,6 +178,8 @@ def _cover_worker(rank, world, port, result_q, cuts):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from mi355_mp import dist as mdist
+        from tests import _host_twins
+        _host_twins.install()   # host twins of the native kernels (no CPU fallback in mi355_mp)
         from mi355_mp.graphgen import powerlaw_edge_index
         from oracle import scatter_ref as S
         N, E, F = 1200, 30000, 6
@@ -186,14 +192,14 @@ def _cover_worker(rank, world, port, result_q, cuts):
         def agg(xs, s, d, ws, n):
             return S.gather_sum(xs, s, d, ws, n)
         x = torch.randn(N, F, generator=g)
-        out = hc.host_step(x[plan.lo:plan.hi].contiguous(), agg)
+        out = _host_twins.host_step(hc, x[plan.lo:plan.hi].contiguous(), agg)
         want = S.gather_sum(x, ei[0], ei[1], w, N)[plan.lo:plan.hi]
         terms = S.gather_sum(x.abs(), ei[0], ei[1], w, N)[plan.lo:plan.hi]
         ok_f = bool(((out - want).abs() <= 1e-5 * terms.clamp(min=1.0)).all())
         xi = torch.randint(-8, 9, (N, F), generator=g).to(torch.float32)
         wi = torch.randint(1, 4, (E,), generator=g).to(torch.float32)
         hci = mdist.HaloCover(plan, wi[plan.edge_pos])
-        outi = hci.host_step(xi[plan.lo:plan.hi].contiguous(), agg)
+        outi = _host_twins.host_step(hci, xi[plan.lo:plan.hi].contiguous(), agg)
         ok_i = torch.equal(outi, S.gather_sum(xi, ei[0], ei[1], wi, N)[plan.lo:plan.hi])
         pull_rows = plan.n_local_src - plan.n_own
         edges_ok = (hc.n_pull_edges + hc.n_push_edges + int(hc.int_src.numel()) == int(plan.edge_pos.numel()))
@@ -229,6 +235,8 @@ def _cover_fuzz_worker(rank, world, port, result_q, n_cases):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from mi355_mp import dist as mdist
+        from tests import _host_twins
+        _host_twins.install()   # host twins of the native kernels (no CPU fallback in mi355_mp)
         from oracle import scatter_ref as S
         bad = []
         for case in range(n_cases):
@@ -256,7 +264,7 @@ def _cover_fuzz_worker(rank, world, port, result_q, n_cases):
             x = torch.randint(-8, 9, (N, 3), generator=g).to(torch.float32)
             plan = mdist.ShardPlan(ei, N, rank, world, cuts=cuts).exchange_requests()
             hc = mdist.HaloCover(plan, w[plan.edge_pos])
-            out = hc.host_step(x[plan.lo:plan.hi].contiguous(),
+            out = _host_twins.host_step(hc, x[plan.lo:plan.hi].contiguous(),
                                lambda xs, s, d, ws, n: S.gather_sum(xs, s, d, ws, n))
             want = S.gather_sum(x, ei[0], ei[1], w, N)[plan.lo:plan.hi]
             n_edges = hc.n_pull_edges + hc.n_push_edges + int(hc.int_src.numel())
@@ -307,6 +315,8 @@ def _gat_worker(rank, world, port, result_q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from mi355_mp import dist as mdist
+        from tests import _host_twins
+        _host_twins.install()   # host twins of the native kernels (no CPU fallback in mi355_mp)
         from mi355_mp.graphgen import powerlaw_edge_index
         from oracle import pyg_ref as P
         N, E, Fi, H, C = 600, 8000, 6, 3, 4
@@ -373,6 +383,8 @@ def _bad_slice_worker(rank, world, port, result_q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from mi355_mp import dist as mdist
+        from tests import _host_twins
+        _host_twins.install()   # host twins of the native kernels (no CPU fallback in mi355_mp)
         N = 50
         ei = torch.randint(N, (2, 400), generator=torch.Generator().manual_seed(3))
         ei[1, 390] = N + 4                          # only the LAST rank's slice holds the bad id
@@ -423,6 +435,8 @@ def _tiny_worker(rank, world, port, result_q, N, edges):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from mi355_mp import dist as mdist
+        from tests import _host_twins
+        _host_twins.install()   # host twins of the native kernels (no CPU fallback in mi355_mp)
         from oracle import pyg_ref as P, scatter_ref as S
         ei = torch.tensor(edges, dtype=torch.long).view(2, -1)
         E = ei.shape[1]
@@ -464,6 +478,8 @@ def _grad_flags_worker(rank, world, port, result_q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from mi355_mp import dist as mdist
+        from tests import _host_twins
+        _host_twins.install()   # host twins of the native kernels (no CPU fallback in mi355_mp)
         m = torch.nn.Linear(3, 2)
         m.extra = torch.nn.Parameter(torch.ones(4))      # no rank forms a gradient for it
         m.only0 = torch.nn.Parameter(torch.ones(2))      # only rank 0 does
@@ -510,6 +526,8 @@ def _gat_cover_worker(rank, world, port, result_q, from_slices, cuts):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from mi355_mp import dist as mdist
+        from tests import _host_twins
+        _host_twins.install()   # host twins of the native kernels (no CPU fallback in mi355_mp)
         from mi355_mp.graphgen import powerlaw_edge_index
         from oracle import pyg_ref as P
         torch.set_default_dtype(torch.float64)

@@ -27,6 +27,26 @@ def _free_port():
     return port
 
 
+def _fused_forms_equal(ov, x_own, out_ref, bias, F):
+    """step_fused over every (tile width, boundary in one launch / per tile,
+    interior after / beside the packing) form: bitwise out_ref (step()'s
+    output).  Returns the list of forms that differ (empty: all equal)."""
+    bad = []
+    for width in (64, 128, 256):
+        bufs = ov.halo_buffers(F, width)
+        for one in (True, False):
+            for split in (False, True):
+                ov.one_boundary_launch, ov.split_interior = one, split
+                for _ in range(2):   # twice: the result never depends on the buffers' last contents
+                    o = torch.full_like(out_ref, float("nan"))
+                    ov.step_fused(x_own, bufs, o, bias)
+                    if not torch.equal(o, out_ref):
+                        bad.append((width, one, split))
+                        break
+    ov.one_boundary_launch, ov.split_interior = True, False
+    return bad
+
+
 def _worker(rank, world, port, q):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -76,6 +96,15 @@ def _worker(rank, world, port, q):
             ov.step_tiled(tiles, out4, bias)
             assert torch.equal(out4, out), "split_interior must equal step"
         ov.split_interior = False
+        # the fused step (one launch per pass, own rows read in place, tile-major halo
+        # buffers, out values prefetched with the batch's gathers, rows without
+        # boundary edges skipped): bitwise step()'s output in every form
+        bad = _fused_forms_equal(ov, xl[:plan.n_own], out, bias, F)
+        assert not bad, ("step_fused differs from step", bad)
+        # ... and without a bias (the skipped rows keep the interior sums as they are)
+        out_nb = torch.empty_like(out)
+        ov.step(xl, out_nb, None)
+        assert not _fused_forms_equal(ov, xl[:plan.n_own], out_nb, None, F)
         q.put((rank, err, bool(torch.equal(out2, want)), ov.n_interior, ov.n_boundary))
     finally:
         dist.destroy_process_group()
@@ -602,7 +631,8 @@ def test_native_shard_plan_matches_torch_plan(world, flow):
     for rank in range(world):
         plan = mdist.ShardPlan(ei, N, rank, world, cuts=cuts, flow=flow)
         i, j = (1, 0) if flow == "source_to_target" else (0, 1)
-        want = mdist._plan_torch(ei[i], ei[j], N, cuts, rank, world)
+        from tests import _host_twins
+        want = _host_twins.plan(ei[i], ei[j], N, cuts, rank, world)
         assert torch.equal(plan.edge_pos, want[0])
         loc = plan.local_edge_index
         lk, lo_ = (loc[1], loc[0]) if flow == "source_to_target" else (loc[0], loc[1])
@@ -677,6 +707,10 @@ def _rccl_worker(rank, world, port, q):
         out_cs = torch.full_like(out_c, float("nan"))
         ovc.step_tiled(tc, out_cs, bias)
         res["cover_split_eq"] = bool(torch.equal(out_cs, out_c))
+        ovc.split_interior = False
+        # the fused step over RCCL (async all_to_all per tile into tile-major buffers)
+        res["fused_eq"] = not _fused_forms_equal(ovc, x.contiguous(), out_c, bias, F) and \
+            not _fused_forms_equal(ov, x.contiguous(), out, bias, F)
         # sharded GCNConv forward + backward, RCCL broadcast / all_reduce of the weights
         gout = torch.randn(N, F, generator=gen).to(dev)
         xi = torch.randn(N, Fi, generator=gen).to(dev)
@@ -752,7 +786,7 @@ def test_sharded_path_over_rccl_world_one():
     rows of X W and their gradients' return) -- with empty halo splits,
     against the single-GPU kernel, GCNConv and GATConv."""
     (rank, r), = _spawn(_rccl_worker, world=1, timeout=300)
-    assert r["step"] < 1e-5 and r["tiled_eq_step"] and r["cover_split_eq"], r
+    assert r["step"] < 1e-5 and r["tiled_eq_step"] and r["cover_split_eq"] and r["fused_eq"], r
     assert r["layer_out"] < 1e-5 and r["layer_gx"] < 1e-5 and r["layer_gw"] < 1e-5, r
     assert r["max_exact"], r
     assert r["slices_equal"], r
@@ -989,7 +1023,7 @@ def _cover_worker(rank, world, port, q):
             xt[:plan.n_own].copy_(x[lo:hi, 128 * t:128 * t + xt.shape[1]])
         out_t = torch.empty_like(out)
         ov.step_tiled(tiles, out_t, bias)
-        ok_t = torch.equal(out_t, out)
+        ok_t = torch.equal(out_t, out) and not _fused_forms_equal(ov, x[lo:hi].contiguous(), out, bias, F)
         # integer-valued features and weights: every regrouping is exact -> bitwise
         xi = torch.randint(-8, 9, (N, F), generator=gen).to(torch.float32).to(dev)
         wi = torch.randint(1, 4, (ei2.shape[1],), generator=gen).to(torch.float32).to(dev)
@@ -1136,6 +1170,10 @@ def _tiny_gpu_worker(rank, world, port, q, N, edges):
         out = torch.empty((sg.n_own, 64), device=dev)
         ov.step_tiled(tiles, out)
         res["cover"] = float((out - want).abs().max()) if sg.n_own else 0.0
+        # the fused step on the same degenerate shards (empty buffers, ranks without rows)
+        of = torch.full_like(out, float("nan"))
+        ov.step_fused(x[sg.lo:sg.hi].contiguous(), ov.halo_buffers(64, 64), of)
+        res["fused_eq"] = bool(torch.equal(of, out))
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -1153,7 +1191,7 @@ def test_slice_built_shards_degenerate_graphs_on_one_gpu(world, N, edges):
     res = _spawn(_tiny_gpu_worker, world=world, timeout=300, args=(N, edges))
     assert sum(r["rows"] for _, r in res) == N
     for rank, r in res:
-        assert r["pull"] < 1e-6 and r["cover"] < 1e-6, (rank, r)
+        assert r["pull"] < 1e-6 and r["cover"] < 1e-6 and r["fused_eq"], (rank, r)
 
 
 def _sharded_fuzz_worker(rank, world, port, q, seeds):
@@ -1295,8 +1333,11 @@ def _gat_cover_gpu_worker(rank, world, port, q, cut_sets):
         res = {}
         for ci, cuts in enumerate(cut_sets):
             # fused-pass heads (C/4 a power of two) and wide ones (a heads=1 stack's 96, a
-            # padded 10 -> 12: the wide kernels, d a_dst shares from the pieces' out2 / s2)
-            for H, C, concat in ((8, 32, True), (3, 8, False), (2, 4, True), (1, 96, True), (2, 10, True)):
+            # padded 10 -> 12: the wide kernels, d a_dst shares from the pieces' out2 / s2);
+            # heads that cross the merge kernel's 256-feature chunks: PPI's conv3
+            # (examples/ppi.py: 6 heads of 121 -> 124, concat=False) and one head of 512
+            for H, C, concat in ((8, 32, True), (3, 8, False), (2, 4, True), (1, 96, True), (2, 10, True),
+                                 (6, 121, False), (1, 512, True)):
                 Fo = H * C if concat else C
                 gout = torch.randn(N, Fo, generator=gen).to(dev)
                 ref = GATConv(Fi, C, heads=H, concat=concat).to(dev)
@@ -1356,7 +1397,8 @@ def test_sharded_gatconv_over_halo_cover_on_one_gpu(world):
     forward rows, d x and the all-reduced d W / d att / d b against the
     single-GPU GATConv -- slice-built shards, an empty rank, a one-row rank;
     config 3's 8 x 32 heads, a mean of heads, C = 4, and wide heads (one head
-    of 96, two padded heads of 10).  Rows no peer pushes a
+    of 96, two padded heads of 10), and heads that cross the merge kernel's
+    256-feature chunks (PPI conv3's 6 x 121 -> 124 mean, one head of 512).  Rows no peer pushes a
     piece of are the single-GPU rows bit for bit; the cover never receives
     more rows than the pull plan, and pieces are pushed."""
     N = 2500
@@ -1372,3 +1414,26 @@ def test_sharded_gatconv_over_halo_cover_on_one_gpu(world):
                 assert v["plain_bitwise"], (rank, key, v)
             pieces += v["pieces"]
     assert pieces > 0
+
+
+def test_host_tensors_raise_without_twins():
+    """No CPU fallback in the product package: a shard
+    plan, the GAT cover step and the ordered segment sum on host tensors raise
+    RuntimeError in a process that has not installed the gloo tests' host twins
+    (tests/_host_twins.py) -- this GPU suite's process."""
+    from mi355_mp import dist as mdist
+    from mi355_mp.gat_cover import gat_cover_propagate
+    assert mdist._HOST_TWINS is None
+    ei = torch.tensor([[0, 1, 2], [1, 2, 0]])
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        mdist.ShardPlan(ei, 3, 0, 1)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        mdist._segment_sum_in_order(torch.zeros(3, dtype=torch.long), torch.zeros(3), 2)
+
+    class _Cover:
+        n_own = 3
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        gat_cover_propagate(_Cover(), torch.zeros(3, 8), torch.zeros(1, 1, 16), 1, 8)
+    # the same calls on the device run the engine
+    plan = mdist.ShardPlan(ei.cuda(), 3, 0, 1)
+    assert plan.n_own == 3 and plan.halo_nodes.numel() == 0

@@ -42,7 +42,7 @@ def test_ctypes_signatures_cover_the_header():
 
 
 def test_abi_version_and_error_string(lib):
-    assert lib.mp_abi_version() == 6
+    assert lib.mp_abi_version() == 7
     assert isinstance(lib.mp_last_error(), bytes)
 
 
@@ -139,6 +139,11 @@ def _extent_cases():
         ("mp_arg_winner_mask", lambda b: (D, R, Fa, E, D, D, b, None), E * W * 4, "mask"),
         ("mp_scatter_arg_backward_csr_f32", lambda b: (ga, D, b, D, Fa, Fa, None, D, Fa, None), E * W * 4, "mask"),
         ("mp_scatter_arg_grad_w_f32", lambda b: (D, D, E, D, D, b, Fa, D, Fa, D, Fa, D, None), E * W * 4, "mask"),
+        # ABI 7: the GAT merge list's pieces (PPI conv3's 6 x 124 heads)
+        ("mp_gat_merge_partials_f32", lambda b: (n, 6, 124, D, D, 300, D, b, 744, D, 300 * 6 * 8, None, D, 744, D,
+                                                 None, None, None), 300 * 744 * 4, "part_out"),
+        ("mp_gat_merge_partials_f32", lambda b: (n, 6, 124, D, D, 300, D, 300 * 744 * 4, 744, D, b, None, D, 744, D,
+                                                 None, None, None), 300 * 6 * 8, "part_stats"),
     ]
 
 
@@ -154,7 +159,7 @@ def test_every_partial_array_carries_its_extent(lib):
                                      "mp_gat_backward_prep_train_f32", "mp_gat_backward_prep_wide_f32",
                                      "mp_col_sums_f32", "mp_gat_backward_f32", "mp_gat_backward_wide_f32",
                                      "mp_arg_winner_mask", "mp_scatter_arg_backward_csr_f32",
-                                     "mp_scatter_arg_grad_w_f32"}
+                                     "mp_scatter_arg_grad_w_f32", "mp_gat_merge_partials_f32"}
     for name, args, need, what in cases:
         for short in (need - 1, 0):
             rc = getattr(lib, name)(*args(short))
@@ -176,7 +181,7 @@ def test_extent_arguments_in_the_header():
             "mp_gat_backward_prep_train_f32": ["pack", "gsum_part"], "mp_gat_backward_prep_wide_f32": ["pack"],
             "mp_col_sums_f32": ["part"], "mp_gat_backward_f32": ["de"], "mp_gat_backward_wide_f32": ["acc2", "sc"],
             "mp_arg_winner_mask": ["mask"], "mp_scatter_arg_backward_csr_f32": ["mask"],
-            "mp_scatter_arg_grad_w_f32": ["mask"]}
+            "mp_scatter_arg_grad_w_f32": ["mask"], "mp_gat_merge_partials_f32": ["part_out", "part_stats"]}
     for fn, arrays in want.items():
         decl = re.search(r"\b%s\((.*?)\);" % fn, text, flags=re.S).group(1)
         params = [p.strip() for p in decl.split(",")]
@@ -206,7 +211,7 @@ def test_abi_rejections_under_asan():
     m = re.match(r"abi_reject: (\d+) cases, 0 failures", last)
     assert m and int(m.group(1)) >= 100, last
     # every extent rejection and the matching exact-extent acceptance ran
-    assert r.stdout.count("holds") >= 17
+    assert r.stdout.count("holds") >= 19
     assert "att_part holds 512000 bytes" in r.stdout       # the round-4 own-rows sizing, rejected
 
 
@@ -563,3 +568,22 @@ def test_halo_tile_widths():
     for bad in ([64, 64], [0, 256], [128, 129]):
         with pytest.raises(ValueError):
             mdist.tile_widths(256, bad)
+
+
+def test_hidden_fraction_is_null_when_pieces_are_not_comparable():
+    """The step decomposition's hidden_frac: the r05 P = 2
+    gloo rehearsal's sample -- exchange alone 230 ms, longer than the whole
+    serial step of 212 ms -- gives None with the reason; a ratio outside
+    [-1, 1] and an empty exchange give None too; a node-like sample keeps its
+    number."""
+    from mi355_mp.dist import hidden_fraction
+    gloo = {"exchange_only_ms": 230.4, "compute_only_ms": 4.3, "serial_step_ms": 212.0, "overlapped_step_ms": 215.1}
+    h = hidden_fraction(gloo)
+    assert h["hidden_frac"] is None and not h["hidden_frac_valid"] and "exceeds the serial step" in h["hidden_frac_note"]
+    odd = {"exchange_only_ms": 2.0, "compute_only_ms": 1.0, "serial_step_ms": 3.1, "overlapped_step_ms": 0.5}
+    assert hidden_fraction(odd)["hidden_frac"] is None          # (2 + 1 - 0.5) / 1 = 2.5
+    one_rank = {"exchange_only_ms": 0.0, "compute_only_ms": 6.6, "serial_step_ms": 6.6, "overlapped_step_ms": 6.6}
+    assert hidden_fraction(one_rank)["hidden_frac"] is None
+    node = {"exchange_only_ms": 0.30, "compute_only_ms": 0.91, "serial_step_ms": 1.20, "overlapped_step_ms": 1.04}
+    h = hidden_fraction(node)
+    assert h["hidden_frac_valid"] and abs(h["hidden_frac"] - (0.30 + 0.91 - 1.04) / 0.30) < 1e-12
