@@ -435,7 +435,7 @@ int mp_gat_backward_prep_wide_f32(const float* grad_out, int64_t ldg, const floa
                                   size_t pack_bytes, float* grad_a_dst, void* stream);
 int mp_gat_backward_wide_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, const float* a_src,
                              const float* pack, int32_t H, int32_t C, float slope, uint64_t seed, float p_drop,
-                             float* grad_xw, float* acc2, size_t acc2_bytes, float* sc, size_t sc_bytes,
+                             const int32_t* drop_ids, float* grad_xw, float* acc2, size_t acc2_bytes, float* sc, size_t sc_bytes,
                              void* slab, size_t slab_bytes, int32_t stages, void* stream);
 int mp_gat_backward_epilogue_wide_f32(float* grad_xw, const float* acc2, const float* xw, const float* att,
                                       const float* grad_a_dst, float* sc_grad_a_src, int64_t n, int32_t H,
@@ -460,11 +460,16 @@ int mp_segment_ids_i64(int64_t* ids, int64_t n, const int64_t* starts, int64_t n
  * GATConv.message applies `F.dropout(alpha, p, training)` to the softmax output
  * (PyG 1.4.3 [U6]; the reference's generic path materialises alpha [E, H] and
  * the [E, H*C] messages for it).  Here the mask is a function of the edge's
- * destination-CSR slot s and the head h:
- *   keep(s, h) = hash(seed, s*H + h) >= floor(p * 2^32),  kept alpha * 1/(1-p)
+ * key k and the head h:
+ *   keep(k, h) = hash(seed, k*H + h) >= floor(p * 2^32),  kept alpha * 1/(1-p)
  * (hash: two rounds of the murmur3 32-bit finaliser, oracle/pyg_ref.py
  * restates it), so the forward and the transposed backward evaluate the same
- * mask without storing one.  0 < p < 1, H <= 32.
+ * mask without storing one.  0 < p < 1, H <= 32.  The key (ABI 7): drop_ids[s]
+ * for slot s of the CSR the call walks (int32, one per slot: the forward's
+ * destination CSR, the backward's transposed CSR), or -- drop_ids NULL -- the
+ * edge's destination-CSR slot.  mi355_mp passes edge ids: the layer's on one
+ * GPU, the GLOBAL ones on a shard, so a sharded GATConv draws exactly the mask
+ * of the single-GPU layer.
  *
  * mp_gat_aggregate_train_drop_f32: mp_gat_aggregate_train_f32 with the dropped
  *   alpha on the messages: out / agg / out2 use alpha * keep / (1-p); the
@@ -472,21 +477,22 @@ int mp_segment_ids_i64(int64_t* ids, int64_t n, const int64_t* starts, int64_t n
  * mp_gat_backward_train_drop_f32: mp_gat_backward_train_f32 for that forward
  *   (the transposed CSR's eid channel must hold each edge's dst-CSR slot);
  *   needs C/4 a power of two <= 64 and 16-byte aligned rows.
- * mp_gat_dropout_keep: bits[s] = keep bits of slot s (bit h), s < n_slots. */
+ * mp_gat_dropout_keep: bits[s] = keep bits of slot s (bit h), s < n_slots (key drop_ids[s],
+ *   or s when drop_ids is NULL). */
 int mp_gat_aggregate_train_drop_f32(const mp_csr* g, const float* xw, const float* a_src,
                                     const float* a_dst, const float* att, int32_t H, int32_t C,
                                     float slope, const float* bias, float* out, int64_t ldo,
                                     float* agg, float* row_stats, float* out2, float* row_s2,
-                                    uint64_t seed, float p_drop, void* slab, size_t slab_bytes,
-                                    int32_t stages, void* stream);
+                                    uint64_t seed, float p_drop, const int32_t* drop_ids, void* slab,
+                                    size_t slab_bytes, int32_t stages, void* stream);
 int mp_gat_backward_train_drop_f32(const mp_csr* gt, const float* grad_out, int64_t ldg,
                                    const float* xw, const float* a_src, const float* pack,
                                    const float* att, int32_t H, int32_t C, float slope,
                                    const float* grad_a_dst, uint64_t seed, float p_drop,
-                                   float* grad_xw, float* grad_a_src, void* slab, size_t slab_bytes,
-                                   int32_t stages, void* stream);
-int mp_gat_dropout_keep(uint64_t seed, float p_drop, int32_t H, int64_t n_slots, uint32_t* bits,
-                        void* stream);
+                                   const int32_t* drop_ids, float* grad_xw, float* grad_a_src, void* slab,
+                                   size_t slab_bytes, int32_t stages, void* stream);
+int mp_gat_dropout_keep(uint64_t seed, float p_drop, int32_t H, int64_t n_slots, const int32_t* drop_ids,
+                        uint32_t* bits, void* stream);
 
 /* Per-block column sums of x [n, F] (0 < F <= 256, F % 4 == 0, 16-byte aligned
  * rows): part [mp_gat_bwd_blocks(n), F] (part_bytes >= that * 4; ABI 6);

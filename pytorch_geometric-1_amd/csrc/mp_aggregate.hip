@@ -144,6 +144,7 @@ struct AggArgs {
   uint64_t drop_seed;
   uint32_t drop_thr;
   float drop_scale;
+  const int32_t* drop_ids;  // (ABI 7) the key of each slot of this CSR (an edge id), or NULL: the dst slot
   // tile-major operands (mp_aggregate_tiles_f32; 0 = row-major): feature f of
   // row r at x[(f / x_tw) * x_ts + r * x_tw + f % x_tw], likewise out with o_tw
   // / o_ts.  Widths are multiples of 64, so a flat-kernel block's 64-feature
@@ -179,11 +180,14 @@ __device__ __forceinline__ void tile_view(AggArgs& p, int fb, const float*& x_ti
 
 // ---------------------------------------------------------------------------
 // GAT attention dropout (GATConv training: `F.dropout(alpha, p)` after the
-// softmax [U6]).  The keep bit of (s, h) -- s the edge's slot in the forward's
-// destination CSR, h the head -- is a counter-based hash of (seed, s * H + h)
-// compared with p * 2^32, so the forward (slot s) and the transposed backward
-// (the edge's dst-slot channel) evaluate the same mask without storing it; a
-// kept alpha is scaled by 1 / (1 - p).  oracle/pyg_ref.py restates the hash.
+// softmax [U6]).  The keep bit of (k, h) -- k the edge's key, h the head -- is
+// a counter-based hash of (seed, k * H + h) compared with p * 2^32, so the
+// forward and the transposed backward evaluate the same mask without storing
+// it; a kept alpha is scaled by 1 / (1 - p).  The key (ABI 7) comes from a
+// per-slot array of each pass's CSR (drop_ids): the layer's edge id on one
+// GPU, the GLOBAL edge id on a shard -- so a sharded layer draws the
+// single-GPU mask; without the array it is the edge's destination-CSR slot.
+// oracle/pyg_ref.py restates the hash.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t drop_mix32(uint32_t h) {
   h ^= h >> 16;
@@ -1088,6 +1092,7 @@ template <bool W, bool EID, int L, bool GW = false, bool DR = false>
 struct SlotWin {
   int64_t base, limit;
   int col, col_n, eid, eid_n;
+  int did = 0, did_n = 0;  // DR with drop_ids: the dropout key of each slot of the window
   float w, w_n;
   uint32_t dr = 0;
   // GAT (GW, 64-lane tasks, H a power of two <= 8): a_src rows of the current
@@ -1105,6 +1110,16 @@ struct SlotWin {
     c = ok ? (p.col ? ld_stream(p.col + k) : (int)k) : 0;  // col == nullptr: identity (rows in slot order)
     if (W) wt = ok ? ld_stream(p.w + k) : 0.f;
     if (EID) e = ok ? ld_stream(p.eid + k) : 0;
+  }
+  // the dropout keys of a window's slots (drop_ids; loaded a window ahead, with its columns)
+  __device__ __forceinline__ void fetch_did(const AggArgs& p, int64_t b, int gl, int& d) {
+    if constexpr (DR) {
+      const int64_t k = b + gl;
+      d = (p.drop_ids && k < limit) ? ld_stream(p.drop_ids + k) : 0;
+    }
+  }
+  __device__ __forceinline__ int64_t drop_key(const AggArgs& p, int gl) const {
+    return p.drop_ids ? (int64_t)did : (EID ? (int64_t)eid : base + gl);
   }
   __device__ __forceinline__ void load_as(const AggArgs& p, int c) {
     const float* r = p.a_src + (int64_t)c * p.H;
@@ -1137,7 +1152,9 @@ struct SlotWin {
     limit = lim;
     fetch(p, base, gl, col, w, eid);
     fetch(p, base + L, gl, col_n, w_n, eid_n);
-    if constexpr (DR) dr = drop_bits(p, EID ? (int64_t)eid : base + gl);
+    fetch_did(p, base, gl, did);
+    fetch_did(p, base + L, gl, did_n);
+    if constexpr (DR) dr = drop_bits(p, drop_key(p, gl));
     if constexpr (GW) {
       lds = wave_lds;
       gw = p.H <= 8 && (p.H & (p.H - 1)) == 0;
@@ -1157,7 +1174,9 @@ struct SlotWin {
       col = col_n;
       w = w_n;
       eid = eid_n;
-      if constexpr (DR) dr = drop_bits(p, EID ? (int64_t)eid : base + gl);  // eid_n was loaded a window ago
+      did = did_n;
+      if constexpr (DR) dr = drop_bits(p, drop_key(p, gl));  // eid_n / did_n were loaded a window ago
+      fetch_did(p, base + L, gl, did_n);
       if constexpr (GW) {
         if (gw) {
           col_n = col_nn;
@@ -2117,7 +2136,7 @@ static int aggregate_dispatch(AggArgs& a, const mp_csr* g, int reduce, int stage
 // the dropout keep bits of slots [0, n) (mp_gat_dropout_keep: tests, host-side masks)
 __global__ void k_gat_dropout_keep(AggArgs p, int64_t n, uint32_t* bits) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < n) bits[i] = drop_bits(p, i);
+  if (i < n) bits[i] = drop_bits(p, p.drop_ids ? (int64_t)p.drop_ids[i] : i);
 }
 
 }  // namespace mp
@@ -2422,9 +2441,10 @@ int mp_gat_forward_f32(const mp_csr* g, const float* xw, const float* att, int32
 }
 
 // keep threshold p * 2^32 and scale 1 / (1 - p) (in double, then rounded: F.dropout's scale)
-static void set_drop(AggArgs& a, uint64_t seed, float p_drop) {
+static void set_drop(AggArgs& a, uint64_t seed, float p_drop, const int32_t* drop_ids = nullptr) {
   const double t = std::floor((double)p_drop * 4294967296.0);
   a.drop_seed = seed;
+  a.drop_ids = drop_ids;
   a.drop_thr = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
   a.drop_scale = (float)(1.0 / (1.0 - (double)p_drop));
 }
@@ -2438,7 +2458,8 @@ static int drop_check(float p_drop, int32_t H, const char* who) {
 static int gat_train(const mp_csr* g, const float* xw, const float* a_src, const float* a_dst, const float* att,
                      int32_t H, int32_t C, float slope, const float* bias, float* out, int64_t ldo, float* agg,
                      float* row_stats, float* out2, float* row_s2, void* slab, size_t slab_bytes, int32_t stages,
-                     void* stream, float* as_out, float* ad_out, uint64_t drop_seed = 0, float p_drop = 0.f) {
+                     void* stream, float* as_out, float* ad_out, uint64_t drop_seed = 0, float p_drop = 0.f,
+                     const int32_t* drop_ids = nullptr) {
   MP_DEVICE_GUARD(stream);
   int rc = check_graph(g, "mp_gat_aggregate_train_f32");
   if (rc) return rc;
@@ -2489,13 +2510,13 @@ static int gat_train(const mp_csr* g, const float* xw, const float* a_src, const
   if (!own) {
     a.att = nullptr;
     if (p_drop > 0.f) {
-      set_drop(a, drop_seed, p_drop);
+      set_drop(a, drop_seed, p_drop, drop_ids);
       return launch<GatRed<4, false, true, false, true>, 4>(a, stages, as_stream(stream), lanes);
     }
     return launch<GatRed<4, false, true>, 4>(a, stages, as_stream(stream), lanes);
   }
   if (p_drop > 0.f) {
-    set_drop(a, drop_seed, p_drop);
+    set_drop(a, drop_seed, p_drop, drop_ids);
     return launch<GatRed<4, true, true, false, true>, 4>(a, stages, as_stream(stream), lanes);
   }
   if (a.a_src_out) return launch<GatRed<4, true, true, true>, 4>(a, stages, as_stream(stream), lanes);
@@ -2604,7 +2625,8 @@ int mp_gat_softmax_aggregate_f32(const mp_csr* g, const int32_t* slot_row, const
 static int gat_backward(const mp_csr* gt, const float* grad_out, int64_t ldg, const float* xw, const float* a_src,
                         const float* pack, const float* att, int32_t H, int32_t C, float slope, float* grad_xw,
                         float* grad_a_src, float* de, const float* ga_dst_in, void* slab, size_t slab_bytes,
-                        int32_t stages, void* stream, uint64_t drop_seed = 0, float p_drop = 0.f) {
+                        int32_t stages, void* stream, uint64_t drop_seed = 0, float p_drop = 0.f,
+                        const int32_t* drop_ids = nullptr) {
   MP_DEVICE_GUARD(stream);
   int rc = check_graph(gt, "mp_gat_backward_f32");
   if (rc) return rc;
@@ -2647,13 +2669,13 @@ static int gat_backward(const mp_csr* gt, const float* grad_out, int64_t ldg, co
   if (v4 && bv < 4 && F >= 64 * bv * 2 && pow2(C / bv) && (64 * bv) % C == 0) {
     if (bv == 2) {
       if (p_drop > 0.f) {
-        set_drop(a, drop_seed, p_drop);
+        set_drop(a, drop_seed, p_drop, drop_ids);
         return launch<GatBwdRed<2, true>, 2>(a, stages, s);
       }
       return launch<GatBwdRed<2>, 2>(a, stages, s);
     }
     if (p_drop > 0.f) {
-      set_drop(a, drop_seed, p_drop);
+      set_drop(a, drop_seed, p_drop, drop_ids);
       return launch<GatBwdRed<1, true>, 1>(a, stages, s);
     }
     return launch<GatBwdRed<1>, 1>(a, stages, s);
@@ -2662,7 +2684,7 @@ static int gat_backward(const mp_csr* gt, const float* grad_out, int64_t ldg, co
     int lanes = F >= 256 ? kGatLanes : pick_shape(F, ldg, grad_out, F, grad_xw).lanes;
     if (lanes < C / 4) lanes = C / 4;
     if (p_drop > 0.f) {
-      set_drop(a, drop_seed, p_drop);
+      set_drop(a, drop_seed, p_drop, drop_ids);
       return launch<GatBwdRed<4, true>, 4>(a, stages, s, lanes);
     }
     return launch<GatBwdRed<4>, 4>(a, stages, s, lanes);
@@ -2697,30 +2719,30 @@ int mp_gat_backward_train_f32(const mp_csr* gt, const float* grad_out, int64_t l
 int mp_gat_aggregate_train_drop_f32(const mp_csr* g, const float* xw, const float* a_src, const float* a_dst,
                                     const float* att, int32_t H, int32_t C, float slope, const float* bias,
                                     float* out, int64_t ldo, float* agg, float* row_stats, float* out2,
-                                    float* row_s2, uint64_t seed, float p_drop, void* slab, size_t slab_bytes,
-                                    int32_t stages, void* stream) {
+                                    float* row_s2, uint64_t seed, float p_drop, const int32_t* drop_ids, void* slab,
+                                    size_t slab_bytes, int32_t stages, void* stream) {
   int rc = drop_check(p_drop, H, "mp_gat_aggregate_train_drop_f32");
   if (rc) return rc;
   MP_CHECK_ARG(a_src && a_dst, "mp_gat_aggregate_train_drop_f32: null input");
   return gat_train(g, xw, a_src, a_dst, att, H, C, slope, bias, out, ldo, agg, row_stats, out2, row_s2, slab,
-                   slab_bytes, stages, stream, nullptr, nullptr, seed, p_drop);
+                   slab_bytes, stages, stream, nullptr, nullptr, seed, p_drop, drop_ids);
 }
 
 int mp_gat_backward_train_drop_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, const float* xw,
                                    const float* a_src, const float* pack, const float* att, int32_t H, int32_t C,
                                    float slope, const float* grad_a_dst, uint64_t seed, float p_drop,
-                                   float* grad_xw, float* grad_a_src, void* slab, size_t slab_bytes, int32_t stages,
-                                   void* stream) {
+                                   const int32_t* drop_ids, float* grad_xw, float* grad_a_src, void* slab,
+                                   size_t slab_bytes, int32_t stages, void* stream) {
   int rc = drop_check(p_drop, H, "mp_gat_backward_train_drop_f32");
   if (rc) return rc;
   MP_CHECK_ARG(grad_a_dst != nullptr, "mp_gat_backward_train_drop_f32: null grad_a_dst");
   return gat_backward(gt, grad_out, ldg, xw, a_src, pack, att, H, C, slope, grad_xw, grad_a_src, nullptr,
-                      grad_a_dst, slab, slab_bytes, stages, stream, seed, p_drop);
+                      grad_a_dst, slab, slab_bytes, stages, stream, seed, p_drop, drop_ids);
 }
 
 int mp_gat_backward_wide_f32(const mp_csr* gt, const float* grad_out, int64_t ldg, const float* a_src,
                              const float* pack, int32_t H, int32_t C, float slope, uint64_t seed, float p_drop,
-                             float* grad_xw, float* acc2, size_t acc2_bytes, float* sc, size_t sc_bytes, void* slab,
+                             const int32_t* drop_ids, float* grad_xw, float* acc2, size_t acc2_bytes, float* sc, size_t sc_bytes, void* slab,
                              size_t slab_bytes, int32_t stages, void* stream) {
   MP_DEVICE_GUARD(stream);
   int rc = check_graph(gt, "mp_gat_backward_wide_f32");
@@ -2765,13 +2787,14 @@ int mp_gat_backward_wide_f32(const mp_csr* gt, const float* grad_out, int64_t ld
   hipStream_t s = as_stream(stream);
   const int lanes = F >= 256 ? 64 : (F / 4 <= 4 ? 4 : next_pow2(F / 4));
   if (p_drop > 0.f) {
-    set_drop(a, seed, p_drop);
+    set_drop(a, seed, p_drop, drop_ids);
     return launch<GatBwdWideRed<4, true>, 4>(a, stages, s, lanes);
   }
   return launch<GatBwdWideRed<4>, 4>(a, stages, s, lanes);
 }
 
-int mp_gat_dropout_keep(uint64_t seed, float p_drop, int32_t H, int64_t n_slots, uint32_t* bits, void* stream) {
+int mp_gat_dropout_keep(uint64_t seed, float p_drop, int32_t H, int64_t n_slots, const int32_t* drop_ids,
+                        uint32_t* bits, void* stream) {
   MP_DEVICE_GUARD(stream);
   int rc = drop_check(p_drop, H, "mp_gat_dropout_keep");
   if (rc) return rc;
@@ -2780,7 +2803,7 @@ int mp_gat_dropout_keep(uint64_t seed, float p_drop, int32_t H, int64_t n_slots,
   MP_CHECK_ARG(bits != nullptr, "mp_gat_dropout_keep: null bits");
   AggArgs a{};
   a.H = H;
-  set_drop(a, seed, p_drop);
+  set_drop(a, seed, p_drop, drop_ids);
   hipLaunchKernelGGL(k_gat_dropout_keep, dim3((unsigned)ceil_div(n_slots, 256)), dim3(256), 0, as_stream(stream), a,
                      n_slots, bits);
   MP_CHECK_LAUNCH();

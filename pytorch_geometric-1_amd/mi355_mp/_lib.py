@@ -100,16 +100,16 @@ SIGNATURES = {
     "mp_gat_backward_train_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, i64, c_p, c_p, c_p, c_p, i32, i32,
                                                  ctypes.c_float, c_p, c_p, c_p, c_p, sz, i32, c_p]),
     "mp_gat_aggregate_train_drop_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, c_p, c_p, c_p, i32, i32, f32,
-                                                       c_p, c_p, i64, c_p, c_p, c_p, c_p, u64, f32, c_p, sz, i32,
+                                                       c_p, c_p, i64, c_p, c_p, c_p, c_p, u64, f32, c_p, c_p, sz, i32,
                                                        c_p]),
     "mp_gat_backward_train_drop_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, i64, c_p, c_p, c_p, c_p, i32,
-                                                      i32, f32, c_p, u64, f32, c_p, c_p, c_p, sz, i32, c_p]),
-    "mp_gat_dropout_keep": (ctypes.c_int, [u64, f32, i32, i64, c_p, c_p]),
+                                                      i32, f32, c_p, u64, f32, c_p, c_p, c_p, c_p, sz, i32, c_p]),
+    "mp_gat_dropout_keep": (ctypes.c_int, [u64, f32, i32, i64, c_p, c_p, c_p]),
     "mp_gat_wide_ok": (ctypes.c_int, [i32, i32]),
     "mp_gat_node_scores_wide_f32": (ctypes.c_int, [c_p, i64, i32, i32, c_p, c_p, c_p, c_p]),
     "mp_gat_backward_prep_wide_f32": (ctypes.c_int, [c_p, i64, c_p, i64, c_p, c_p, c_p, c_p, c_p, i64, i32, i32, c_p,
                                                      sz, c_p, c_p]),
-    "mp_gat_backward_wide_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, i64, c_p, c_p, i32, i32, f32, u64, f32,
+    "mp_gat_backward_wide_f32": (ctypes.c_int, [ctypes.POINTER(MpCsr), c_p, i64, c_p, c_p, i32, i32, f32, u64, f32, c_p,
                                                 c_p, c_p, sz, c_p, sz, c_p, sz, i32, c_p]),
     "mp_gat_backward_epilogue_wide_f32": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, c_p, i64, i32, i32, c_p]),
     "mp_segment_offset_i64": (ctypes.c_int, [c_p, i64, i32, i64, c_p, c_p, i64, c_p]),

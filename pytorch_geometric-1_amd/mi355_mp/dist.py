@@ -1347,17 +1347,21 @@ class OverlappedAggregation:
                "compute_only_ms": timed(compute_only),
                "serial_step_ms": timed(serial),
                "overlapped_step_ms": timed(lambda: self._step_form(form, out, bias, group))}
-        res.update(hidden_fraction(res))
+        res.update(hidden_fraction(res, staged=out.is_cuda and dist.get_backend(group) == "gloo"))
         return res
 
 
-def hidden_fraction(res):
+def hidden_fraction(res, staged=False):
     """hidden_frac of a decomposition {exchange_only_ms, compute_only_ms,
     serial_step_ms, overlapped_step_ms} (OverlappedAggregation.decompose), or
-    None with the reason when the pieces are not comparable: the exchange alone
-    longer than the serial step that contains it (host-staged gloo exchanges
-    swing between measurements), a shorter piece of ~0 ms (one rank), or a
-    ratio outside [-1, 1]."""
+    None with the reason when the pieces are not comparable: device tensors
+    exchanged over gloo (staged: the host copies make the exchange a blocking
+    call that cannot overlap, and its time swings between measurements), the
+    exchange alone longer than the serial step that contains it, a shorter
+    piece of ~0 ms (one rank), or a ratio outside [-1, 1]."""
+    if staged:
+        return {"hidden_frac": None, "hidden_frac_valid": False,
+                "hidden_frac_note": "host-staged gloo exchange (a rehearsal): blocking, not the node's links"}
     ex, co = res["exchange_only_ms"], res["compute_only_ms"]
     shorter = min(ex, co)
     if shorter <= 1e-3:
@@ -1510,6 +1514,8 @@ class ShardedGraph:
         # destination rows = own rows, sources = [own rows ; halo rows]: the fused
         # GAT kernels' sharded form (ops._gat_rows_ok); built lazily on first use
         self.g_fwd = Graph(plan.local_edge_index, self.n_own, plan.n_local_src, target_tasks=GAT_TARGET_TASKS)
+        # attention dropout keyed on the GLOBAL edge id: the single-GPU layer's mask
+        self.g_fwd.edge_key = plan.edge_gid
         self.g_bwd = None
         self.deg = None
         self._w = None

@@ -296,8 +296,9 @@ class GatHaloCover:
                "compute_only_ms": timed(lambda: self.forward_device(xw_own, att_c, H, C, slope, bias, False,
                                                                    exchange=False)),
                "step_ms": timed(lambda: self.forward_device(xw_own, att_c, H, C, slope, bias, False))}
+        import torch.distributed as tdist
         from .dist import hidden_fraction
-        res.update(hidden_fraction(res))
+        res.update(hidden_fraction(res, staged=xw_own.is_cuda and tdist.get_backend(grp) == "gloo"))
         return res
 
     def backward_device(self, g, out, bias, att_c, H, C, slope, saved, want_att, want_bias):
@@ -321,7 +322,8 @@ class GatHaloCover:
             sb = lib.mp_gat_train_slab_bytes(gt_struct, H, C)
             slab = torch.empty(sb, dtype=torch.uint8, device=dev)
             _lib.check(lib.mp_gat_backward_wide_f32(gt_struct, grad_out.data_ptr(), F, a_src.data_ptr(),
-                                                    pack_.data_ptr(), H, C, float(slope), 0, 0.0, gx_out.data_ptr(),
+                                                    pack_.data_ptr(), H, C, float(slope), 0, 0.0, None,
+                                                    gx_out.data_ptr(),
                                                     acc2.data_ptr(), _lib.nbytes(acc2), sc.data_ptr(),
                                                     _lib.nbytes(sc), slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
                        "mp_gat_backward_wide_f32 (cover)")

@@ -276,6 +276,26 @@ class Graph:
         self.target_tasks = target_tasks
         self._dst = None
         self._src = None
+        # attention-dropout keys: None = the edge's id in this edge list; a
+        # shard's local graph sets the GLOBAL edge ids (dist.ShardedGraph)
+        self.edge_key = None
+        self._drop_ids = {}
+
+    def drop_ids(self, side):
+        """Per-slot attention-dropout keys (int32) of the 'dst' CSR (the forward)
+        or the 'src' CSR (the transposed backward): each slot's edge id in this
+        edge list, or edge_key of it.  The keep mask is then a function of the
+        edge, not of where a CSR puts it (ABI 7 drop_ids)."""
+        ids = self._drop_ids.get(side)
+        if ids is None:
+            csr = self.dst if side == "dst" else self.src
+            E = csr.n_edges
+            if self.edge_key is None:
+                ids = csr.eid                                    # int32 edge ids, slot order
+            else:
+                ids = self.edge_key[csr.eid[:E].long()].to(torch.int32).contiguous() if E else csr.eid
+            self._drop_ids[side] = ids
+        return ids
 
     def _edge_index(self):
         ei = self._ei()

@@ -687,20 +687,23 @@ def gat_wide_ok(H, C):
 def gat_dropout_ok(H, C, p):
     """The fused path carries GATConv's attention dropout (training, 0 < p < 1):
     the training forward and its transposed backward evaluate one hashed keep
-    mask per (destination-CSR slot, head) (mp_gat_aggregate_train_drop_f32)."""
+    mask per (edge, head) (mp_gat_aggregate_train_drop_f32; the edge's key is
+    its id -- the global id on a shard: Graph.drop_ids)."""
     return (0.0 < float(p) < 1.0 and GAT_TRAIN_FWD and GAT_OWN_A_SRC and 1 <= H <= 32 and gat_wide_ok(H, C))
 
 
 def gat_dropout_keep(graph, seed, p, H):
     """The attention-dropout keep mask [E, H] (bool, the graph's edge order) that
     the fused GAT kernels apply for (seed, p): mp_gat_dropout_keep over the
-    destination-CSR slots, mapped back through the CSR's edge ids."""
+    destination-CSR slots with their keys (Graph.drop_ids), mapped back through
+    the CSR's edge ids."""
     lib = _lib.load()
     csr = graph.dst
     E = csr.n_edges
     dev = csr.rowptr.device
     bits = torch.empty(max(E, 1), dtype=torch.int32, device=dev)
-    _lib.check(lib.mp_gat_dropout_keep(int(seed) & 0xFFFFFFFFFFFFFFFF, float(p), int(H), E, bits.data_ptr(),
+    _lib.check(lib.mp_gat_dropout_keep(int(seed) & 0xFFFFFFFFFFFFFFFF, float(p), int(H), E,
+                                       graph.drop_ids("dst").data_ptr(), bits.data_ptr(),
                                        _lib.stream_ptr(dev)), "mp_gat_dropout_keep")
     shifts = torch.arange(H, dtype=torch.int32, device=dev)
     keep_slot = ((bits[:E].unsqueeze(1) >> shifts) & 1).bool()
@@ -757,7 +760,8 @@ def _gat_forward(graph, edge_index, xw, att, H, C, slope, bias, want_alpha, trai
                                                            att_c.data_ptr(), H, C, float(slope), _lib.ptr(bias),
                                                            out.data_ptr(), out.stride(0), None,
                                                            stats.data_ptr(), agg2.data_ptr(), s2.data_ptr(),
-                                                           int(drop[0]), float(drop[1]), slab.data_ptr(), sb,
+                                                           int(drop[0]), float(drop[1]),
+                                                           graph.drop_ids("dst").data_ptr(), slab.data_ptr(), sb,
                                                            _lib.MP_STAGE_ALL, st), "mp_gat_aggregate_train_drop_f32")
         else:
             _lib.check(lib.mp_gat_aggregate_train_f32(g, xw.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(),
@@ -856,8 +860,10 @@ def _gat_backward_wide(graph, g, xw, att, a_src, a_dst, stats, agg, agg_bias, ex
     sb = lib.mp_gat_train_slab_bytes(gs, H, C)
     slab = torch.empty(sb, dtype=torch.uint8, device=dev)
     seed, p = (0, 0.0) if drop is None else (int(drop[0]), float(drop[1]))
+    ids = graph.drop_ids("src").data_ptr() if drop is not None else None
     _lib.check(lib.mp_gat_backward_wide_f32(gs, g.data_ptr(), g.stride(0), a_src.data_ptr(), pack.data_ptr(), H, C,
-                                            float(slope), seed, p, gx.data_ptr(), acc2.data_ptr(), _lib.nbytes(acc2),
+                                            float(slope), seed, p, ids, gx.data_ptr(), acc2.data_ptr(),
+                                            _lib.nbytes(acc2),
                                             sc.data_ptr(), _lib.nbytes(sc), slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
                "mp_gat_backward_wide_f32")
     del slab, pack
@@ -943,7 +949,8 @@ def _gat_backward_fused(graph, g, xw, att, a_src, a_dst, stats, agg, agg_bias, H
             raise ValueError("mi355_mp: the attention-dropout backward needs the training forward's extras")
         _lib.check(lib.mp_gat_backward_train_drop_f32(gs, g.data_ptr(), g.stride(0), xw.data_ptr(), a_src.data_ptr(),
                                                       pack.data_ptr(), att_c.data_ptr(), H, C, float(slope),
-                                                      ga_dst.data_ptr(), int(drop[0]), float(drop[1]), gx.data_ptr(),
+                                                      ga_dst.data_ptr(), int(drop[0]), float(drop[1]),
+                                                      graph.drop_ids("src").data_ptr(), gx.data_ptr(),
                                                       ga_src.data_ptr(), slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
                    "mp_gat_backward_train_drop_f32")
     elif fused_dst:

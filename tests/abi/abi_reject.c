@@ -119,7 +119,7 @@ static void extents_gat_backward(void) {
                              NULL));
   REJECT("grad_a_dst", mp_gat_backward_train_f32(&gt, DEVF, F, DEVF, DEVF, DEVF, DEVF, H, C, 0.2f, NULL, DEVF, DEVF,
                                                  DEV, slab, 7, NULL));
-  REJECT("dropout p", mp_gat_backward_train_drop_f32(&gt, DEVF, F, DEVF, DEVF, DEVF, DEVF, H, C, 0.2f, DEVF, 1, 1.5f,
+  REJECT("dropout p", mp_gat_backward_train_drop_f32(&gt, DEVF, F, DEVF, DEVF, DEVF, DEVF, H, C, 0.2f, DEVF, 1, 1.5f, NULL,
                                                       DEVF, DEVF, DEV, slab, 7, NULL));
 
   /* heads of any width: pack, acc2 [gt.n_rows, F], sc [gt.n_rows, H] */
@@ -130,13 +130,13 @@ static void extents_gat_backward(void) {
                                                (size_t)n_own * H * 16, DEVF, NULL));
   ACCEPT(mp_gat_backward_prep_wide_f32(DEVF, Fw, DEVF, Fw, NULL, DEVF, DEVF, DEVF, DEVF, n, H, Cw, DEVF, (size_t)n * H * 16,
                                        DEVF, NULL));
-  REJECT("acc2", mp_gat_backward_wide_f32(&gt, DEVF, Fw, DEVF, DEVF, H, Cw, 0.2f, 0, 0.f, DEVF, DEVF, acc2 - 4, DEVF,
+  REJECT("acc2", mp_gat_backward_wide_f32(&gt, DEVF, Fw, DEVF, DEVF, H, Cw, 0.2f, 0, 0.f, NULL, DEVF, DEVF, acc2 - 4, DEVF,
                                           sc, DEV, wslab, 7, NULL));
-  REJECT("sc", mp_gat_backward_wide_f32(&gt, DEVF, Fw, DEVF, DEVF, H, Cw, 0.2f, 0, 0.f, DEVF, DEVF, acc2, DEVF,
+  REJECT("sc", mp_gat_backward_wide_f32(&gt, DEVF, Fw, DEVF, DEVF, H, Cw, 0.2f, 0, 0.f, NULL, DEVF, DEVF, acc2, DEVF,
                                         (size_t)n_own * H * 4, DEV, wslab, 7, NULL));
-  ACCEPT(mp_gat_backward_wide_f32(&gt, DEVF, Fw, DEVF, DEVF, H, Cw, 0.2f, 0, 0.f, DEVF, DEVF, acc2, DEVF, sc, DEV,
+  ACCEPT(mp_gat_backward_wide_f32(&gt, DEVF, Fw, DEVF, DEVF, H, Cw, 0.2f, 0, 0.f, NULL, DEVF, DEVF, acc2, DEVF, sc, DEV,
                                   wslab, 7, NULL));
-  REJECT("C % 4", mp_gat_backward_wide_f32(&gt, DEVF, Fw, DEVF, DEVF, H, 35, 0.2f, 0, 0.f, DEVF, DEVF, acc2, DEVF, sc,
+  REJECT("C % 4", mp_gat_backward_wide_f32(&gt, DEVF, Fw, DEVF, DEVF, H, 35, 0.2f, 0, 0.f, NULL, DEVF, DEVF, acc2, DEVF, sc,
                                            DEV, wslab, 7, NULL));
   REJECT("null", mp_gat_backward_epilogue_wide_f32(DEVF, NULL, DEVF, DEVF, DEVF, DEVF, n, H, Cw, NULL));
 }
@@ -266,9 +266,9 @@ static void workspaces(void) {
   REJECT("null", mp_gat_forward_train_f32(&g, DEVF, DEVF, H, C, 0.2f, NULL, DEVF, F, NULL, DEVF, DEVF, DEVF, NULL,
                                           DEVF, DEV, ts, 7, NULL));
   REJECT("dropout p", mp_gat_aggregate_train_drop_f32(&g, DEVF, DEVF, DEVF, DEVF, H, C, 0.2f, NULL, DEVF, F, NULL,
-                                                       DEVF, DEVF, DEVF, 1, 0.f, DEV, ts, 7, NULL));
+                                                       DEVF, DEVF, DEVF, 1, 0.f, NULL, DEV, ts, 7, NULL));
   REJECT("H <= 32", mp_gat_aggregate_train_drop_f32(&g, DEVF, DEVF, DEVF, DEVF, 64, 4, 0.2f, NULL, DEVF, F, NULL,
-                                                     DEVF, DEVF, DEVF, 1, 0.5f, DEV, ts, 7, NULL));
+                                                     DEVF, DEVF, DEVF, 1, 0.5f, NULL, DEV, ts, 7, NULL));
   REJECT("H <= 16", mp_gat_softmax_aggregate_f32(&g, DEVI, DEVF, DEVF, DEVF, 32, 8, 0.2f, NULL, DEVF, F, DEVF, DEV,
                                                   gs, 7, NULL));
   REJECT("slab", mp_gat_softmax_aggregate_f32(&g, DEVI, DEVF, DEVF, DEVF, H, C, 0.2f, NULL, DEVF, F, DEVF, DEV,
@@ -297,8 +297,8 @@ static void null_pointers(void) {
   REJECT("leading dimension", mp_gat_sddmm_f32(&g, DEVI, DEVF, 255, DEVF, 256, 8, 32, DEVF, NULL));
   REJECT("null", mp_segment_offset_i64(NULL, n, 2, n, DEVL, DEVL, 3, NULL));
   REJECT("null", mp_segment_ids_i64(NULL, n, DEVL, 3, NULL));
-  REJECT("null", mp_gat_dropout_keep(1, 0.5f, 8, E, NULL, NULL));
-  REJECT("dropout p", mp_gat_dropout_keep(1, 1.0f, 8, E, DEVU, NULL));
+  REJECT("null", mp_gat_dropout_keep(1, 0.5f, 8, E, NULL, NULL, NULL));
+  REJECT("dropout p", mp_gat_dropout_keep(1, 1.0f, 8, E, NULL, DEVU, NULL));
   const size_t po = 10 * 256 * 4, ps = 10 * 8 * 2 * 4;  /* part_out / part_stats of 10 pieces */
   REJECT("C % 4", mp_gat_merge_partials_f32(n, 8, 30, DEVI, DEVI, 10, DEVF, po, 256, DEVF, ps, NULL, DEVF, 256, DEVF,
                                             NULL, NULL, NULL));

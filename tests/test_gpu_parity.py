@@ -1157,11 +1157,10 @@ def test_gat_attention_dropout_fused_vs_masked_reference(H, C):
     ei_l = gat_loops(eid, N)
     graph = graph_for(ei_l, N, N, conv.flow, target_tasks=GAT_TARGET_TASKS)
     keep = ops.gat_dropout_keep(graph, seed, p, H).cpu()
-    # the device mask == the oracle's restatement of the hash (slot order -> edge order)
+    # the device mask == the oracle's restatement of the hash, keyed on the edge id
+    # (ABI 7: the layer's edge id; a sharded layer passes the same global id)
     E = ei_l.shape[1]
-    ks = P.gat_dropout_keep_slots(seed, p, H, E)
-    want_keep = torch.empty_like(ks)
-    want_keep[graph.dst.eid[:E].long().cpu()] = ks
+    want_keep = P.gat_dropout_keep_slots(seed, p, H, E)
     assert torch.equal(keep, want_keep)
     frac = keep.float().mean().item()
     assert abs(frac - (1 - p)) < 0.01, frac

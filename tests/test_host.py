@@ -132,9 +132,9 @@ def _extent_cases():
         ("mp_col_sums_f32", lambda b: (D, F, n, F, D, b, None), blocks * F * 4, "part"),
         ("mp_gat_backward_f32", lambda b: (gt, D, F, D, D, D, D, H, C, 0.2, D, D, D, b, D, slab, 7, None),
          9000 * H * 4, "de"),
-        ("mp_gat_backward_wide_f32", lambda b: (gt, D, Fw, D, D, H, Cw, 0.2, 0, 0.0, D, D, b, D, n * H * 4, D, wslab,
+        ("mp_gat_backward_wide_f32", lambda b: (gt, D, Fw, D, D, H, Cw, 0.2, 0, 0.0, None, D, D, b, D, n * H * 4, D, wslab,
                                                 7, None), n * Fw * 4, "acc2"),
-        ("mp_gat_backward_wide_f32", lambda b: (gt, D, Fw, D, D, H, Cw, 0.2, 0, 0.0, D, D, n * Fw * 4, D, b, D, wslab,
+        ("mp_gat_backward_wide_f32", lambda b: (gt, D, Fw, D, D, H, Cw, 0.2, 0, 0.0, None, D, D, n * Fw * 4, D, b, D, wslab,
                                                 7, None), n * H * 4, "sc"),
         ("mp_arg_winner_mask", lambda b: (D, R, Fa, E, D, D, b, None), E * W * 4, "mask"),
         ("mp_scatter_arg_backward_csr_f32", lambda b: (ga, D, b, D, Fa, Fa, None, D, Fa, None), E * W * 4, "mask"),
@@ -584,6 +584,9 @@ def test_hidden_fraction_is_null_when_pieces_are_not_comparable():
     assert hidden_fraction(odd)["hidden_frac"] is None          # (2 + 1 - 0.5) / 1 = 2.5
     one_rank = {"exchange_only_ms": 0.0, "compute_only_ms": 6.6, "serial_step_ms": 6.6, "overlapped_step_ms": 6.6}
     assert hidden_fraction(one_rank)["hidden_frac"] is None
+    staged = hidden_fraction({"exchange_only_ms": 100.0, "compute_only_ms": 4.3, "serial_step_ms": 120.0,
+                              "overlapped_step_ms": 101.0}, staged=True)
+    assert staged["hidden_frac"] is None and "gloo" in staged["hidden_frac_note"]
     node = {"exchange_only_ms": 0.30, "compute_only_ms": 0.91, "serial_step_ms": 1.20, "overlapped_step_ms": 1.04}
     h = hidden_fraction(node)
     assert h["hidden_frac_valid"] and abs(h["hidden_frac"] - (0.30 + 0.91 - 1.04) / 0.30) < 1e-12

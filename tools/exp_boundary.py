@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--empty", type=float, default=0.47)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--tiles-only", action="store_true",
+                    help="only the feature-tile order A/B (XCD-affine vs one tile after another) of plain sums")
     args = ap.parse_args()
     from mi355_mp import _lib, ops
     from mi355_mp.graph import Graph
@@ -72,6 +74,17 @@ def main():
 
     gr, wc = make()
     out = out0.clone()
+    if args.tiles_only:
+        res = {"rows": n, "edges": E, "x_rows": h, "x_MB": h * F * 4 / 2**20}
+        for seq in (0, 1):
+            prev = lib.mp_tune(_lib.MP_TUNE_FLAT_SEQ_TILES, seq)
+            try:
+                res["seq_tiles_%d_ms" % seq] = timed(lambda: ops.aggregate_tiles(gr.dst, "other", x, wc, F, out, "sum",
+                                                                               0, bias))
+            finally:
+                lib.mp_tune(_lib.MP_TUNE_FLAT_SEQ_TILES, prev)
+        print(json.dumps(res), flush=True)
+        return
     INIT, SKIP = _lib.MP_FLAG_INIT_FROM_OUT, _lib.MP_FLAG_SKIP_EMPTY
 
     def run(flags, chunk_graph=None, u16=False):
