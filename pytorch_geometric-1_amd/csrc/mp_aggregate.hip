@@ -57,6 +57,7 @@ constexpr bool kNtIdx = true;   // non-temporal col/weight/eid stream loads (A/B
 constexpr bool kXcdTiles = true;  // feature tile = (block % 8) % tiles when tiles divide 8: each XCD's L2
                                   // holds one tile (A/B: -1.5%)
 constexpr int kLaneMaxF = 8;    // rows of 2..this many features: one task per lane (A/B: wins at F=4,8)
+constexpr int64_t kSeqTilesMin = 384ll << 20;  // mp_aggregate_tiles_f32: sequential feature tiles above this x
 constexpr int kULane = 8;       // slots in flight per lane task
 }  // namespace mp
 
@@ -100,6 +101,7 @@ struct AggArgs {
   int32_t seq_tiles; // flat kernel: feature tiles one after another on all XCDs (no XCD-affine map)
   int32_t far;       // flat SM kernel: x larger than the Infinity Cache (batches of kU_Vec1Far)
   int32_t force_flat;  // mp_aggregate_tiles_f32: the scalar-batch flat kernel whatever the layout
+  int32_t xr;          // ... and its XR instance (tile-major operands, skipped rows, per-row bias)
   // features
   const float* w;
   const float* x;
@@ -287,6 +289,22 @@ struct SumRed {
 #pragma unroll
     for (int k = 0; k < VEC; ++k) q.v[k] = acc[k];
     return q;
+  }
+  // sum with the bias scaled by a per-row 0 / 1 flag (k_agg_flat XM 1): o + b * 1
+  // is o + b bit for bit; o + b * 0 is o (a -0 row reads +0: equal values)
+  __device__ __forceinline__ void finish_scaled_bias(const AggArgs& p, int64_t row, int64_t cnt, int f, bool act,
+                                                     float bs) {
+    if (!act) return;
+    Frag<VEC> o;
+    float c = (float)(cnt > 0 ? cnt : 1);
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) o.v[k] = MEAN ? __fdiv_rn(acc[k], c) : acc[k];
+    if (p.bias) {
+      Frag<VEC> b = load_frag<VEC>(p.bias + f);
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) o.v[k] = __fadd_rn(o.v[k], __fmul_rn(b.v[k], bs));
+    }
+    store_out<VEC>(p.out + row * p.ldo + f, o);
   }
   __device__ __forceinline__ void finish(const AggArgs& p, int64_t row, int64_t cnt, int f, bool act, bool with_bias = true) {
     if (!act) return;
@@ -1563,11 +1581,18 @@ __device__ __forceinline__ void scalar_batch(const T* a, int64_t n, int64_t e, T
 // tools/exp_boundary.py), and the interior pass adds their bias instead
 // (AggArgs::bias_rows).  (An out prefetch issued with each batch's gathers was
 // also measured there: slower, not kept -- DESIGN Appendix A.)
-template <class Red, int VEC, int U, int L, bool GA = false, bool SM = false>
+// XM (mp_aggregate_tiles_f32's launches only): 1 = per-row bias flags (the
+// sharded interior pass), 2 = MP_FLAG_SKIP_EMPTY (the boundary pass); TM:
+// tile-major operands.  Compile-time, one feature per instance, so every other
+// launch runs the kernel without their per-block and per-row work (measured:
+// both features as run-time branches of one instance cost short-row passes 13 %).
+template <class Red, int VEC, int U, int L, bool GA = false, bool SM = false, int XM = 0, bool TM = false>
 __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
   static_assert(!Red::kGat && !Red::kGatB && !Red::kHW, "flat loop: sum/mean/max/min reducers");
   static_assert(!GA || (L == 64 && VEC == 1 && Red::kW), "two-pass GAT: 64-lane tasks, 64-feature tiles");
   static_assert(!SM || (L == 64 && !GA && !Red::kEid), "scalar batches: 64-lane sum/mean tasks");
+  static_assert(!(XM || TM) || (SM && VEC == 1), "tile-major / skipped rows: the scalar-batch kernel, 64-feature tiles");
+  constexpr bool kSkip = XM == 2, kFlags = XM == 1;
   using GR = Grp<L>;
   const int lane = lane_id();
   const int gl = lane & (L - 1);
@@ -1586,15 +1611,15 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
   if (w >= p.n_waves) return;
   const int f = tile * L * VEC + gl * VEC;
   const bool act = f < p.F;
-  const float* x_tile;
-  int64_t ldx_tile;
-  int fx0;
-  tile_view(p, tile * L * VEC, x_tile, ldx_tile, fx0);
+  const float* x_tile = p.x;
+  int64_t ldx_tile = p.ldx;
+  int fx0 = 0;
+  if constexpr (TM) tile_view(p, tile * L * VEC, x_tile, ldx_tile, fx0);
   const uint32_t foff = (uint32_t)(act ? f - fx0 : 0) * 4u;
   const char* xb = reinterpret_cast<const char*>(x_tile);
   const int64_t ldxb = ldx_tile * 4;
   [[maybe_unused]] __amdgpu_buffer_rsrc_t xr;
-  const bool skip_empty = (p.flags & MP_FLAG_SKIP_EMPTY) != 0;
+
 
   const int r_first = GR::un(p.wave_row[w]);
   const int r_last = GR::un(p.wave_row[w + 1]);
@@ -1605,7 +1630,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
   // an owned row opens (rs_ / re_: its slot range); an empty one is skipped
   // (no load of out) under MP_FLAG_SKIP_EMPTY
   auto open_row = [&](int rr, int64_t rs_, int64_t re_) {
-    red.begin(p, rr, !(skip_empty && re_ == rs_), f, act);
+    red.begin(p, rr, !(kSkip && re_ == rs_), f, act);
   };
 
   std::conditional_t<GA, GatAlphaWin, SlotWin<Red::kW, Red::kEid, L>> win;
@@ -1620,24 +1645,31 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
     xr = __builtin_amdgcn_make_buffer_rsrc((void*)x_tile, (short)0, (int)p.x_bytes, 0x00020000);
     if (e_begin < e_end) scalar_batch<U>(p.col, p.n_edges, e_begin, c_nxt);
   }
-  // row window: rowptr (and the per-row bias flags, bias_rows) of rows
-  // [rbase, rbase + L) across the lanes.  A refill for row pointer r starts
-  // at r - 1, so the row that r closes -- the one open -- stays in the window
+  // row window: rowptr (and, kFlags, the per-row bias flags) of rows [rbase,
+  // rbase + L) across the lanes.  A kFlags refill for row pointer r starts at
+  // r - 1, so the row that r closes -- the one open -- stays in the window
   // until it finishes (its bias flag is read then).
   int rbase = r_first;
   int rp = (rbase + gl <= p.n_rows) ? p.rowptr[rbase + gl] : 0;
-  int bw = (p.bias_rows && rbase + gl < p.n_rows) ? p.bias_rows[rbase + gl] : 1;
+  [[maybe_unused]] int bw = 1;
+  if constexpr (kFlags) bw = (rbase + gl < p.n_rows) ? p.bias_rows[rbase + gl] : 1;
   auto row_ptr = [&](int r) -> int64_t {
     if (r - rbase > L - 1) {
-      rbase = r - 1;
+      rbase = kFlags ? r - 1 : r;
       rp = (rbase + gl <= p.n_rows) ? p.rowptr[rbase + gl] : 0;
-      if (p.bias_rows) bw = (rbase + gl < p.n_rows) ? p.bias_rows[rbase + gl] : 1;
+      if constexpr (kFlags) bw = (rbase + gl < p.n_rows) ? p.bias_rows[rbase + gl] : 1;
     }
     return GR::bc(rp, r - rbase);
   };
   auto finish_row = [&](int rr, int64_t cnt) {
-    if (skip_empty && cnt == 0) return;
-    red.finish(p, rr, cnt, f, act, p.bias_rows == nullptr || GR::bc(bw, rr - rbase) != 0);
+    if constexpr (kSkip) {
+      if (cnt == 0) return;
+    }
+    if constexpr (kFlags) {
+      red.finish_scaled_bias(p, rr, cnt, f, act, GR::bc(bw, rr - rbase) != 0 ? 1.f : 0.f);
+    } else {
+      red.finish(p, rr, cnt, f, act);
+    }
   };
 
   // current row: the continuation of an earlier task's row, or an owned row
@@ -1877,6 +1909,24 @@ static int launch_main(void (*k)(AggArgs), dim3 grid, hipStream_t s, const AggAr
   return MP_OK;
 }
 
+// the mp_aggregate_tiles_f32 instances: XM from the call (per-row bias flags /
+// skipped rows / neither), TM when an operand is tile-major
+template <class Red, int U, int XM>
+static int launch_xm(const AggArgs& a, dim3 grid, hipStream_t s, bool far) {
+  const bool tm = a.x_tw || a.o_tw;
+  if (tm)
+    return far ? launch_main(k_agg_flat<Red, 1, kU_Vec1Far, 64, false, true, XM, true>, grid, s, a)
+               : launch_main(k_agg_flat<Red, 1, U, 64, false, true, XM, true>, grid, s, a);
+  return far ? launch_main(k_agg_flat<Red, 1, kU_Vec1Far, 64, false, true, XM>, grid, s, a)
+             : launch_main(k_agg_flat<Red, 1, U, 64, false, true, XM>, grid, s, a);
+}
+template <class Red, int U>
+static int launch_xr(const AggArgs& a, dim3 grid, hipStream_t s, bool far) {
+  if (a.bias_rows) return launch_xm<Red, U, 1>(a, grid, s, far);
+  if (a.flags & MP_FLAG_SKIP_EMPTY) return launch_xm<Red, U, 2>(a, grid, s, far);
+  return launch_xm<Red, U, 0>(a, grid, s, far);
+}
+
 template <class Red, int VEC, int L>
 static int launch_l(const AggArgs& a, int stages, hipStream_t s) {
   // the GAT backward holds a 16-B destination pack per slot in flight: U = 8 at every width
@@ -1895,9 +1945,13 @@ static int launch_l(const AggArgs& a, int stages, hipStream_t s) {
           bool far = false;
           if constexpr (VEC == 1) {
             far = a.smem && a.far;
-            if (far) rc = launch_main(k_agg_flat<Red, 1, kU_Vec1Far, 64, false, true>, grid, s, a);
+            if (far && !a.xr) rc = launch_main(k_agg_flat<Red, 1, kU_Vec1Far, 64, false, true>, grid, s, a);
           }
-          if (far) {
+          if constexpr (VEC == 1) {
+            // mp_aggregate_tiles_f32 (scalar batches, 64-feature tiles by construction)
+            if (a.xr) rc = launch_xr<Red, U>(a, grid, s, far);
+          }
+          if (far || a.xr) {
           } else if (a.smem) rc = launch_main(k_agg_flat<Red, VEC, U, 64, false, true>, grid, s, a);
           else rc = launch_main(k_agg_flat<Red, VEC, U, L>, grid, s, a);
         } else {
@@ -2081,8 +2135,15 @@ static int aggregate_dispatch(AggArgs& a, const mp_csr* g, int reduce, int stage
     a.smem = 1;
     a.x_bytes = (uint32_t)xbytes;
     a.far = xbytes > tuned(g_tune.flat_far_min_bytes) ? 1 : 0;
-    a.seq_tiles = (int32_t)tuned(g_tune.flat_seq_tiles);
+    // feature tiles one after another when x outgrows the Infinity Cache by up to 4x: then
+    // each 64-feature tile of it (a quarter) fits, and the tiles take turns in it (the
+    // sharded step's P = 4 passes: interior 0.68 -> 0.65 ms, send 1.26 -> 1.22 ms; at P = 8,
+    // x fits whole and XCD-affine tiles stay ahead by 1-2 %; tools/exp_boundary.py)
+    const int64_t x_all = (int64_t)g->n_cols * F * 4;
+    a.seq_tiles = (tuned(g_tune.flat_seq_tiles) || (x_all > kSeqTilesMin && x_all <= 4 * tuned(g_tune.flat_far_min_bytes)))
+                      ? 1 : 0;
     a.fix4 = 0;
+    a.xr = 1;
     return dispatch_reduce<1>(a, reduce, stages, s, 64);
   }
   Shape sh = pick_shape(F, a.ldx, a.x, a.ldo, a.out);
@@ -2208,6 +2269,8 @@ int mp_aggregate_tiles_f32(const mp_csr* g, const float* w, const float* x, int6
   MP_CHECK_ARG(F > 0 && F % 64 == 0, "mp_aggregate_tiles_f32: F must be a positive multiple of 64");
   MP_CHECK_ARG((flags & ~(MP_FLAG_INIT_FROM_OUT | MP_FLAG_SKIP_EMPTY)) == 0,
                "mp_aggregate_tiles_f32: flags may only hold INIT_FROM_OUT and SKIP_EMPTY");
+  MP_CHECK_ARG(!(bias_rows && bias && (flags & MP_FLAG_SKIP_EMPTY)),
+               "mp_aggregate_tiles_f32: per-row bias flags and SKIP_EMPTY are separate calls (one kernel each)");
   MP_CHECK_ARG(out != nullptr && (g->n_edges == 0 || (x != nullptr && g->col != nullptr && g->n_cols > 0)),
                "mp_aggregate_tiles_f32: null x/out or a graph without columns");
   MP_CHECK_ARG(x_tile_w >= 0 && out_tile_w >= 0, "mp_aggregate_tiles_f32: negative tile width");
@@ -2242,20 +2305,18 @@ int mp_aggregate_tiles_f32(const mp_csr* g, const float* w, const float* x, int6
   a.x_ts = x_tile_stride;
   a.flags = flags;
   a.bias = bias;
-  a.bias_rows = bias ? bias_rows : nullptr;
+  a.bias_rows = bias ? bias_rows : nullptr;  // the flags matter only with a bias
   a.out = out;
   a.ldo = out_tile_w ? out_tile_w : ldo;
   a.o_tw = out_tile_w;
   a.o_ts = out_tile_stride;
   a.slab_ld = slab_ld_for(F);
   a.slab_v = (float*)slab;
-  // row-major both ways: the ordinary dispatch (mp_aggregate_f32's) unless rows are
-  // skipped or the bias is per row, which only the scalar-batch flat kernel
-  // does (forced as for tiles)
-  if (!x_tile_w && !out_tile_w && ((flags & MP_FLAG_SKIP_EMPTY) || a.bias_rows)) {
-    a.x_tw = 0;
-    a.force_flat = 1;
-  }
+  // every call takes the scalar-batch flat kernel with 64-feature tiles (its
+  // instance chosen by the operands' layout and the call's options), row-major
+  // operands included: the same kernel mp_aggregate_f32 picks for such rows,
+  // with the feature-tile order chosen for the pass's x (see aggregate_dispatch)
+  a.force_flat = 1;
   return aggregate_dispatch(a, g, reduce, stages, as_stream(stream));
 }
 

@@ -1063,8 +1063,11 @@ class OverlappedAggregation:
             g, w = self.g_send.dst, self.w_send
         else:
             g, w = g_sp.dst, None
-        ops.aggregate_tiles(g, "other", x_own, w, bufs.F, bufs.send, "sum", 0, None,
-                            out_tiles=(bufs.width, bufs.n_send * bufs.width))
+        if bufs.n_tiles == 1:        # whole rows: the send buffer is row-major
+            ops.aggregate_tiles(g, "other", x_own, w, bufs.F, bufs.send[0], "sum", 0, None)
+        else:
+            ops.aggregate_tiles(g, "other", x_own, w, bufs.F, bufs.send, "sum", 0, None,
+                                out_tiles=(bufs.width, bufs.n_send * bufs.width))
 
     def _interior_fused(self, x_own, out, bias):
         """The interior edges of every feature in one launch, with the bias of
@@ -1091,8 +1094,11 @@ class OverlappedAggregation:
         g_bh, _, _ = self._fused_graphs()
         flags = _lib.MP_FLAG_INIT_FROM_OUT | _lib.MP_FLAG_SKIP_EMPTY
         if tile is None:
-            ops.aggregate_tiles(g_bh.dst, "other", bufs.recv, self.w_bnd, bufs.F, out, "sum", flags, bias,
-                                x_tiles=(bufs.width, bufs.n_halo * bufs.width))
+            if bufs.n_tiles == 1:    # whole rows: the halo buffer is row-major
+                ops.aggregate_tiles(g_bh.dst, "other", bufs.recv[0], self.w_bnd, bufs.F, out, "sum", flags, bias)
+            else:
+                ops.aggregate_tiles(g_bh.dst, "other", bufs.recv, self.w_bnd, bufs.F, out, "sum", flags, bias,
+                                    x_tiles=(bufs.width, bufs.n_halo * bufs.width))
             return
         c0, c1 = tile * bufs.width, (tile + 1) * bufs.width
         b = bias[c0:c1] if bias is not None else None

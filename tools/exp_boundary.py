@@ -83,6 +83,14 @@ def main():
                                                                                0, bias))
             finally:
                 lib.mp_tune(_lib.MP_TUNE_FLAT_SEQ_TILES, prev)
+        # the XR kernel instance (per-row bias flags: every row flagged) against the plain launch
+        ones = torch.ones(n, dtype=torch.int32, device=dev)
+        res["plain_bias_ms"] = timed(lambda: ops.aggregate_tiles(gr.dst, "other", x, wc, F, out, "sum", 0, bias))
+        res["xr_bias_rows_ms"] = timed(lambda: ops.aggregate_tiles(gr.dst, "other", x, wc, F, out, "sum", 0, bias,
+                                                                   bias_rows=ones))
+        # XR without the bias flags (MP_FLAG_SKIP_EMPTY alone forces the XR instance)
+        res["xr_skip_only_ms"] = timed(lambda: ops.aggregate_tiles(gr.dst, "other", x, wc, F, out, "sum",
+                                                                   _lib.MP_FLAG_SKIP_EMPTY, bias))
         print(json.dumps(res), flush=True)
         return
     INIT, SKIP = _lib.MP_FLAG_INIT_FROM_OUT, _lib.MP_FLAG_SKIP_EMPTY
