@@ -871,8 +871,12 @@ class BuildMeter:
     driver's first 8-GPU run): wall time, the time the device was busy (union
     of the kernel / copy intervals the torch profiler records, device activity
     only), the rest = host work and host-device round trips, and the number of
-    synchronising calls (torch's sync debug mode, counted as warnings).
-    enabled=False: wall time only."""
+    synchronising calls (torch's sync debug mode, counted as warnings, with
+    the source line of each: sync_sites).  The gloo rehearsal stages every
+    all_to_all through host memory: those syncs (mdist._stage_to_host) and the
+    host time inside the staged all_to_alls are given apart -- over RCCL
+    neither exists.  The profiler's start-up and trace processing lie outside
+    the wall time.  enabled=False: wall time only."""
 
     def __init__(self, enabled):
         self.enabled = enabled
@@ -888,9 +892,11 @@ class BuildMeter:
             self.res[name] = {"wall_s": time.perf_counter() - t0}
             return out
         from torch.profiler import ProfilerActivity, profile
+        import inspect
+        import mi355_mp.dist as mdist
         prof = profile(activities=[ProfilerActivity.CUDA])
         try:
-            prof.start()
+            prof.start()            # the profiler's own start-up is not charged to the phase
         except Exception as ex:  # pragma: no cover - a profiler that cannot start: wall time only
             out = fn()
             torch.cuda.synchronize()
@@ -898,15 +904,29 @@ class BuildMeter:
             return out
         with warnings.catch_warnings(record=True) as caught:
             warnings.simplefilter("always")
+            torch.cuda.synchronize()
+            staged0 = mdist.GLOO_STAGED_S[0]
+            t0 = time.perf_counter()
             torch.cuda.set_sync_debug_mode("warn")
             try:
                 out = fn()
-                torch.cuda.synchronize()
             finally:
-                torch.cuda.set_sync_debug_mode("default")
-                prof.stop()
-        wall = time.perf_counter() - t0
-        syncs = sum(1 for w in caught if "synchroniz" in str(w.message).lower())
+                torch.cuda.set_sync_debug_mode("default")    # the phase's end below is not one of its syncs
+            torch.cuda.synchronize()
+            wall = time.perf_counter() - t0           # before the profiler's stop / trace processing
+            prof.stop()
+        src, first = inspect.getsourcelines(mdist._stage_to_host)
+        stage_lines = set(range(first, first + len(src)))
+        sites = {}
+        n_stage = 0
+        for w in caught:
+            if "synchroniz" not in str(w.message).lower():
+                continue
+            where = "%s:%d" % (os.path.basename(w.filename), w.lineno)
+            sites[where] = sites.get(where, 0) + 1
+            if os.path.basename(w.filename) == "dist.py" and w.lineno in stage_lines:
+                n_stage += 1
+        syncs = sum(sites.values())
         spans = []
         try:
             for e in prof.events():
@@ -930,7 +950,10 @@ class BuildMeter:
         busy_s = busy * 1e-6
         self.res[name] = {"wall_s": wall, "device_busy_s": busy_s if spans else None,
                           "host_and_sync_s": (wall - busy_s) if spans else None,
-                          "device_ops": len(spans), "host_syncs": syncs}
+                          "device_ops": len(spans), "host_syncs": syncs,
+                          "host_syncs_without_gloo_staging": syncs - n_stage,
+                          "gloo_staged_all_to_all_s": mdist.GLOO_STAGED_S[0] - staged0,
+                          "sync_sites": dict(sorted(sites.items(), key=lambda kv: -kv[1]))}
         return out
 
 

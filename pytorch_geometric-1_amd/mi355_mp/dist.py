@@ -30,15 +30,29 @@ import torch
 import torch.distributed as dist
 
 
+GLOO_STAGED_S = [0.0]     # host time inside staged (gloo) all_to_alls: copies + host transfer
+
+
+def _stage_to_host(t):
+    """gloo staging (the multi-process rehearsal of the RCCL path on a shared
+    GPU): a device tensor's copy in host memory -- the one host sync of a
+    staged collective (bench.py's build split counts the syncs on this line
+    apart).  A host tensor is returned as it is."""
+    return t.cpu()
+
+
 def _a2a(out, inp, out_splits=None, in_splits=None, group=None):
-    """all_to_all_single; with the gloo backend (CPU-only collectives: the
-    multi-process rehearsal of the RCCL path) device tensors are staged
-    through host memory (one device-to-host copy of the input)."""
+    """all_to_all_single; with the gloo backend (CPU-only collectives) device
+    tensors are staged through host memory: one device-to-host copy of the
+    input, the result lands in pinned memory and goes back without a sync."""
     if out.is_cuda and dist.get_backend(group) == "gloo":
-        o = torch.empty(out.shape, dtype=out.dtype)
-        dist.all_to_all_single(o, inp.cpu(), output_split_sizes=out_splits, input_split_sizes=in_splits,
+        import time
+        t0 = time.perf_counter()
+        o = torch.empty(out.shape, dtype=out.dtype, pin_memory=True)
+        dist.all_to_all_single(o, _stage_to_host(inp), output_split_sizes=out_splits, input_split_sizes=in_splits,
                                group=group)
-        out.copy_(o)
+        out.copy_(o, non_blocking=True)
+        GLOO_STAGED_S[0] += time.perf_counter() - t0
         return out
     dist.all_to_all_single(out, inp, output_split_sizes=out_splits, input_split_sizes=in_splits, group=group)
     return out
@@ -61,28 +75,13 @@ def _exchange_counts(send, group=None):
         dist.all_to_all_single(recv.view(-1), send.reshape(-1).contiguous(), group=group)
         both = torch.stack([send.reshape(world, k), recv.reshape(world, k)]).tolist()
     else:
-        sh = send.reshape(world, k).cpu()
+        sh = _stage_to_host(send.reshape(world, k))
         rh = torch.empty_like(sh)
         dist.all_to_all_single(rh.view(-1), sh.reshape(-1).contiguous(), group=group)
         both = [sh.tolist(), rh.tolist()]
     if send.dim() == 1:
         return [r[0] for r in both[0]], [r[0] for r in both[1]]
     return both[0], both[1]
-
-
-def _all_gather_rows(vals, dev, group=None):
-    """[[vals of rank 0], [vals of rank 1], ...]: `vals` a 1-D int64 tensor
-    (device or host, the same length on every rank), gathered with one
-    collective and read with ONE host sync."""
-    world = dist.get_world_size(group)
-    v = vals.to(torch.int64)
-    if _device_collectives(dev, group):
-        v = v.to(dev)
-    else:
-        v = v.cpu()
-    got = torch.empty((world, v.numel()), dtype=torch.int64, device=v.device)
-    dist.all_gather_into_tensor(got.view(-1), v.contiguous(), group=group)
-    return got.tolist()
 
 
 def _dev_ints(lists, dev):
@@ -123,21 +122,26 @@ def tile_widths(F, tile):
     return [min(int(tile), F - c0) for c0 in range(0, F, int(tile))]
 
 
+def balanced_cut_points(in_degree, parts):
+    """edge_balanced_cuts on the device, without a read-back: an int64 tensor
+    [0 = c_0 <= ... <= c_P = N] (the targets E * p // parts searched in the
+    in-degree prefix sum, made monotone)."""
+    N = in_degree.numel()
+    dev = in_degree.device
+    if N == 0 or parts <= 1:
+        return _dev_ints([[0] * parts + [N]], dev)[0]
+    csum = torch.cumsum(in_degree.to(torch.int64), 0)
+    p = torch.arange(1, parts, dtype=torch.int64, device=dev)
+    found = torch.searchsorted(csum, (csum[-1] * p) // parts, right=True)
+    found = torch.cummax(found, 0).values
+    ends = torch.tensor([0, N], dtype=torch.int64, device=dev)
+    return torch.cat([ends[:1], found, ends[1:]])
+
+
 def edge_balanced_cuts(in_degree, parts):
     """Row cut points [0=c_0 <= ... <= c_P = N] with ~equal edges per part
-    (the targets E * p // parts searched in the in-degree prefix sum on the
-    device, read back with one host sync)."""
-    N = in_degree.numel()
-    if N == 0 or parts <= 1:
-        return [0] * parts + [N]
-    csum = torch.cumsum(in_degree.to(torch.int64), 0)
-    p = torch.arange(1, parts, dtype=torch.int64, device=csum.device)
-    found = torch.searchsorted(csum, (csum[-1] * p) // parts, right=True).tolist()
-    cuts = [0]
-    for c in found:
-        cuts.append(max(int(c), cuts[-1]))
-    cuts.append(N)
-    return cuts
+    (balanced_cut_points, read back with one host sync)."""
+    return [int(c) for c in balanced_cut_points(in_degree, parts).tolist()]
 
 
 # ---------------------------------------------------------------------------
@@ -164,19 +168,16 @@ def _host(what):
     return getattr(_HOST_TWINS, what)
 
 
-def _plan_native(key, other, num_nodes, cuts, rank, world):
-    """The plan of rank `rank` on the device by mp_shard_plan (flag + scan, no
-    sort): (edge_pos, local key, local other, halo_nodes, recv_counts) -- the
-    positions of the rank's edges in the list's order, its destinations and
-    sources renumbered [own rows ; sorted halo rows], the halo's global ids and
-    their count per owner.  One host sync (the sizes)."""
+def _plan_launch(key, other, num_nodes, cuts, cuts_d, rank, world):
+    """mp_shard_plan of rank `rank` on the device, without a read-back: the
+    full-size outputs (edge_pos, local key, local other, halo_nodes) and the
+    device count vector [n edges, n halo, per-owner halo counts...]."""
     from . import _lib
     lib = _lib.load()
     dev = key.device
     key = key.to(torch.int64).contiguous()
     other = other.to(torch.int64).contiguous()
     E = key.numel()
-    cuts_d = _dev_ints([cuts], dev)[0]
     edge_pos = torch.empty(E, dtype=torch.int64, device=dev)
     lkey = torch.empty_like(edge_pos)
     lother = torch.empty_like(edge_pos)
@@ -187,17 +188,33 @@ def _plan_native(key, other, num_nodes, cuts, rank, world):
                                  cuts[rank], cuts[rank + 1], edge_pos.data_ptr(), lkey.data_ptr(),
                                  lother.data_ptr(), halo.data_ptr(), counts.data_ptr(), ws.data_ptr(),
                                  ws.numel(), _lib.stream_ptr(dev)), "mp_shard_plan")
-    c = counts.tolist()
+    return edge_pos, lkey, lother, halo, counts
+
+
+def _plan_finish(launched, c, num_nodes):
+    """The compact plan from _plan_launch's outputs and its counts read back."""
     if c[1] < 0:
         raise IndexError("mi355_mp.dist: an edge endpoint lies outside [0, %d)" % num_nodes)
+    edge_pos, lkey, lother, halo, _ = launched
     n = c[0]
-    return edge_pos[:n].clone(), lkey[:n].clone(), lother[:n].clone(), halo[:c[1]].clone(), c[2:]
+    return edge_pos[:n].clone(), lkey[:n].clone(), lother[:n].clone(), halo[:c[1]].clone(), list(c[2:])
+
+
+def _plan_native(key, other, num_nodes, cuts, rank, world):
+    """The plan of rank `rank` on the device by mp_shard_plan (flag + scan, no
+    sort): (edge_pos, local key, local other, halo_nodes, recv_counts) -- the
+    positions of the rank's edges in the list's order, its destinations and
+    sources renumbered [own rows ; sorted halo rows], the halo's global ids and
+    their count per owner.  One host sync (the sizes)."""
+    launched = _plan_launch(key, other, num_nodes, cuts, _dev_ints([cuts], key.device)[0], rank, world)
+    return _plan_finish(launched, launched[4].tolist(), num_nodes)
 
 
 class ShardPlan:
     """Everything rank `rank` needs to aggregate its destination rows."""
 
-    def __init__(self, edge_index, num_nodes, rank, world, cuts=None, flow="source_to_target", edge_ids=None):
+    def __init__(self, edge_index, num_nodes, rank, world, cuts=None, flow="source_to_target", edge_ids=None,
+                 _planned=None):
         """edge_index: the global edge list, or any list holding (at least) this
         rank's edges in global order -- e.g. the rank's own in-edges from
         scatter_edges_by_owner; edge_ids then gives each listed edge's GLOBAL id
@@ -211,15 +228,75 @@ class ShardPlan:
         self.rank, self.world = rank, world
         lo, hi = cuts[rank], cuts[rank + 1]
         self.lo, self.hi, self.n_own = lo, hi, hi - lo
-        plan = _plan_native if edge_index.is_cuda else _host("plan")
-        self.edge_pos, dst, local_src, halo_nodes, self.recv_counts = plan(dst_all, src_all, num_nodes, cuts, rank,
-                                                                           world)
+        if _planned is None:
+            plan = _plan_native if edge_index.is_cuda else _host("plan")
+            _planned = plan(dst_all, src_all, num_nodes, cuts, rank, world)
+        self.edge_pos, dst, local_src, halo_nodes, self.recv_counts = _planned
         self.halo_nodes = halo_nodes
         self.edge_gid = edge_ids[self.edge_pos] if edge_ids is not None else self.edge_pos
         self.local_edge_index = torch.stack([local_src, dst]) if i == 1 else torch.stack([dst, local_src])
         self.n_local_src = self.n_own + halo_nodes.numel()
         self.send_idx = None
         self.send_counts = None
+
+    @classmethod
+    def many(cls, edge_lists, num_nodes, rank, world, cuts, flows, edge_ids, group=None):
+        """Several plans of one partition (e.g. GCN's forward and backward
+        plans) built and their requests exchanged together: every plan's sizes
+        and the peers' request counts come back in ONE host read, and all the
+        requests travel in one all_to_all (per peer: plan 0's, plan 1's, ...).
+        Each plan equals ShardPlan(...).exchange_requests(group)."""
+        K = len(edge_lists)
+        specs = []
+        for ei, flow in zip(edge_lists, flows):
+            i, j = (1, 0) if flow == "source_to_target" else (0, 1)
+            specs.append((ei[i], ei[j]))
+        dev = edge_lists[0].device
+        if dev.type == "cuda":
+            cuts_d = _dev_ints([cuts], dev)[0]
+            launched = [_plan_launch(k, o, num_nodes, cuts, cuts_d, rank, world) for k, o in specs]
+            cnt = torch.stack([l[4] for l in launched])                 # [K, 2 + world]
+        else:
+            host = [_host("plan")(k, o, num_nodes, cuts, rank, world) for k, o in specs]
+            cnt = torch.tensor([[h[0].numel(), h[3].numel()] + list(h[4]) for h in host], dtype=torch.int64)
+        W = 2 + world
+        if _device_collectives(dev, group):
+            rc_d = cnt[:, 2:].t().contiguous()                          # [world, K] rows requested per owner
+            sc_d = torch.empty_like(rc_d)
+            dist.all_to_all_single(sc_d.view(-1), rc_d.view(-1), group=group)
+            allv = torch.cat([cnt.view(-1), sc_d.view(-1)]).tolist()
+        else:
+            ch = _stage_to_host(cnt)
+            rc_h = ch[:, 2:].t().contiguous()
+            sc_h = torch.empty_like(rc_h)
+            dist.all_to_all_single(sc_h.view(-1), rc_h.view(-1), group=group)
+            allv = ch.view(-1).tolist() + sc_h.view(-1).tolist()
+        plans = []
+        for k in range(K):
+            c = allv[k * W:(k + 1) * W]
+            planned = _plan_finish(launched[k], c, num_nodes) if dev.type == "cuda" else host[k]
+            plans.append(cls(edge_lists[k], num_nodes, rank, world, cuts=cuts, flow=flows[k],
+                             edge_ids=edge_ids[k], _planned=planned))
+        sc = [allv[K * W + q * K:K * W + (q + 1) * K] for q in range(world)]    # [peer][plan]
+        for k, p in enumerate(plans):
+            p.send_counts = [sc[q][k] for q in range(world)]
+        segs, offs = [], [0] * K
+        for q in range(world):
+            for k, p in enumerate(plans):
+                segs.append(p.halo_nodes[offs[k]:offs[k] + p.recv_counts[q]])
+                offs[k] += p.recv_counts[q]
+        send = torch.cat(segs) if segs else torch.empty(0, dtype=torch.int64, device=dev)
+        requests = torch.empty(sum(map(sum, sc)), dtype=torch.int64, device=dev)
+        _a2a(requests, send.contiguous(), [sum(r) for r in sc],
+             [sum(p.recv_counts[q] for p in plans) for q in range(world)], group)
+        got, pos = [[] for _ in range(K)], 0
+        for q in range(world):
+            for k in range(K):
+                got[k].append(requests[pos:pos + sc[q][k]])
+                pos += sc[q][k]
+        for k, p in enumerate(plans):
+            p.send_idx = torch.cat(got[k]) - p.lo      # rows of my own block that peers need
+        return plans
 
     def exchange_requests(self, group=None):
         """All-to-all of the requested node ids (once per plan; one host sync
@@ -369,33 +446,55 @@ def scatter_edges_by_owner(key, cuts, payloads, group=None):
     ranks in rank order, each sender's entries in their original order -- so
     when every rank holds a contiguous slice of the global edge list (rank r
     before rank r + 1), each rank receives its edges in GLOBAL order."""
+    return scatter_edges_by_owner_many([(key, payloads)], cuts, group)[0]
+
+
+def scatter_edges_by_owner_many(jobs, cuts, group=None):
+    """scatter_edges_by_owner for several (key, payloads) jobs in one exchange:
+    one all_to_all of the counts ([world, jobs], one host sync) and one of all
+    the payloads (columns padded to the widest job; to each peer the jobs
+    follow one another).  Returns one list of payloads per job, each exactly
+    what scatter_edges_by_owner(key, cuts, payloads) returns."""
     world = len(cuts) - 1
-    dev = key.device
-    cuts_t, ranks = _dev_ints([cuts[1:], range(world + 1)], dev)
-    owner = torch.searchsorted(cuts_t, key, right=True)
-    srt = torch.sort(owner, stable=True)
-    order = srt.indices
-    # per-owner counts from the sorted owners (no atomics on world-many bins)
-    bounds = torch.searchsorted(srt.values, ranks)
-    sc, rc = _exchange_counts(bounds[1:] - bounds[:-1], group)
-    cols = []
-    for p in payloads:
-        if p.dtype == torch.float32:
-            cols.append(p.view(torch.int32).to(torch.int64))
-        elif p.dtype == torch.int64:
-            cols.append(p)
-        else:
-            raise TypeError("scatter_edges_by_owner: payloads are int64 or float32 (got %s)" % p.dtype)
-    packed = torch.stack(cols, 1)[order].contiguous() if cols else key.new_empty((key.numel(), 0))
-    buf = packed.new_empty((sum(rc), len(cols)))
-    _a2a(buf, packed, rc, sc, group)
-    out = []
-    for j, p in enumerate(payloads):
-        c = buf[:, j].contiguous()
-        out.append(c.to(torch.int32).view(torch.float32) if p.dtype == torch.float32 else c)
-    return out
-
-
+    K = len(jobs)
+    dev = jobs[0][0].device
+    ncol = max(len(p) for _, p in jobs)
+    cuts_t, bins = _dev_ints([cuts[1:], range(world * K + 1)], dev)
+    keys, packs = [], []
+    for k, (key, payloads) in enumerate(jobs):
+        cols = []
+        for p in payloads:
+            if p.dtype == torch.float32:
+                cols.append(p.view(torch.int32).to(torch.int64))
+            elif p.dtype == torch.int64:
+                cols.append(p)
+            else:
+                raise TypeError("scatter_edges_by_owner: payloads are int64 or float32 (got %s)" % p.dtype)
+        cols += [key.new_zeros(key.shape, dtype=torch.int64)] * (ncol - len(cols))
+        keys.append(torch.searchsorted(cuts_t, key, right=True) * K + k)
+        packs.append(torch.stack(cols, 1) if ncol else key.new_empty((key.numel(), 0), dtype=torch.int64))
+    ck = torch.cat(keys) if K > 1 else keys[0]
+    srt = torch.sort(ck, stable=True)      # by owner, then job; each job's entries keep their order
+    # per (owner, job) counts from the sorted keys (no atomics on world * K bins)
+    bounds = torch.searchsorted(srt.values, bins)
+    sc, rc = _exchange_counts((bounds[1:] - bounds[:-1]).view(world, K), group)
+    packed = (torch.cat(packs) if K > 1 else packs[0])[srt.indices].contiguous()
+    buf = packed.new_empty((sum(map(sum, rc)), ncol))
+    _a2a(buf, packed, [sum(r) for r in rc], [sum(r) for r in sc], group)
+    outs, pos = [[] for _ in range(K)], 0
+    for q in range(world):            # from sender q: job 0's entries, job 1's, ...
+        for k in range(K):
+            outs[k].append(buf[pos:pos + rc[q][k]])
+            pos += rc[q][k]
+    res = []
+    for k, (key, payloads) in enumerate(jobs):
+        got = torch.cat(outs[k]) if world > 1 else outs[k][0]
+        one = []
+        for j, p in enumerate(payloads):
+            c = got[:, j].contiguous()
+            one.append(c.to(torch.int32).view(torch.float32) if p.dtype == torch.float32 else c)
+        res.append(one)
+    return res
 
 
 def _segment_sum_in_order(index, values, n):
@@ -441,19 +540,38 @@ def gcn_shards_from_slices(edge_slice, slice_offset, num_nodes, rank, world, gro
     N = int(num_nodes)
     n = row.numel()
     keep = row != col
-    # one gather of (slice size, kept edges, offset, bad-id flag) from every rank,
-    # read with one host sync: every rank learns whether ANY rank holds an id
-    # outside [0, N) before the first collective whose size depends on N, and all
-    # of them raise together (a rank with a bad id would otherwise all_reduce a
-    # longer degree vector); every rank checks every offset the same way (a lone
-    # raising rank would leave its peers waiting in the next collective)
+    # 1-2. one gather of (slice size, kept edges, offset, bad-id flag) from every
+    # rank and the all-reduced in-degree (+1 for every node's loop) -> cuts, all
+    # read back with ONE host sync: every rank learns whether ANY rank holds an
+    # id outside [0, N) before the first collective whose size depends on the
+    # data, and all of them raise together (a lone raising rank would leave its
+    # peers waiting in the next collective); every rank checks every offset the
+    # same way.  Ids outside [0, N) are counted in a spare bin of the degree.
     if n:
         bad_t = ((torch.minimum(row.min(), col.min()) < 0) | (torch.maximum(row.max(), col.max()) >= N))
         n_off = _dev_ints([[n, int(slice_offset)]], dev)[0]
         mine = torch.stack([n_off[0], keep.sum(), n_off[1], bad_t.to(torch.int64)])
+        inr = keep & (col >= 0) & (col < N)
+        deg_in = _count_by(torch.where(inr, col, torch.full_like(col, N)), N + 1)[:N]
     else:
-        mine = torch.tensor([0, 0, int(slice_offset), 0], dtype=torch.int64)
-    sizes = _all_gather_rows(mine, dev, group)
+        mine = torch.tensor([0, 0, int(slice_offset), 0], dtype=torch.int64, device=dev)
+        deg_in = torch.zeros(N, dtype=torch.int64, device=dev)
+    if _device_collectives(dev, group):
+        got = torch.empty((world, 4), dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(got.view(-1), mine, group=group)
+        dist.all_reduce(deg_in, group=group)
+        allv = torch.cat([got.view(-1), balanced_cut_points(deg_in + 1, world)]).tolist()
+        sizes = [allv[4 * r:4 * r + 4] for r in range(world)]
+        cuts = allv[4 * world:]
+    else:
+        h = _stage_to_host(torch.cat([mine, deg_in]))
+        got = torch.empty((world, 4), dtype=torch.int64)
+        dist.all_gather_into_tensor(got.view(-1), h[:4].clone(), group=group)
+        deg_h = h[4:].clone()
+        dist.all_reduce(deg_h, group=group)
+        sizes = got.tolist()
+        cuts = edge_balanced_cuts(deg_h + 1, world)
+    del deg_in
     if any(sz[3] for sz in sizes):
         raise IndexError("mi355_mp.dist: an edge of some rank's slice names a node outside [0, %d)" % N)
     for r, sz in enumerate(sizes):
@@ -469,15 +587,6 @@ def gcn_shards_from_slices(edge_slice, slice_offset, num_nodes, rank, world, gro
     E_kept = sum(sz[1] for sz in sizes)
     kr, kc, kw = row[kept], col[kept], w[kept]
     kgid = k_off + torch.arange(n_kept, dtype=torch.int64, device=dev)
-    # 2. cuts from the global in-degree (+1: every node gets its loop)
-    deg_in = _count_by(kc, N)
-    if _device_collectives(dev, group):
-        dist.all_reduce(deg_in, group=group)
-    else:
-        h = deg_in.cpu()
-        dist.all_reduce(h, group=group)
-        deg_in = h.to(dev)
-    cuts = edge_balanced_cuts(deg_in + 1, world)
     lo, hi = cuts[rank], cuts[rank + 1]
     own = torch.arange(lo, hi, dtype=torch.int64, device=dev)
     if structure_only:
@@ -485,10 +594,14 @@ def gcn_shards_from_slices(edge_slice, slice_offset, num_nodes, rank, world, gro
         fwd = (torch.stack([torch.cat([f_row, own]), torch.cat([f_col, own])]), torch.cat([f_gid, E_kept + own]),
                torch.ones(f_row.numel() + hi - lo, dtype=torch.float32, device=dev))
         return {"cuts": cuts, "E": E_kept + N, "deg": None, "fwd": fwd, "bwd": None}
-    # 3. pre-existing loops -> the node's owner; the last one (largest position) wins
+    # 3-5 in ONE exchange: the pre-existing loops to the node's owner, the
+    # out-edges of each rank's rows (by source) and its in-edges (by destination),
+    # each in global order
     lidx = _nonzero_n(~keep, n - n_kept)
     lv, lw = row[lidx], w[lidx]
-    rv, rpos, rw = scatter_edges_by_owner(lv, cuts, [lv, lidx + slice_offset, lw], group)
+    (rv, rpos, rw), (b_row, b_col, b_gid, b_w), (f_row, f_col, f_gid, f_w) = scatter_edges_by_owner_many(
+        [(lv, [lv, lidx + slice_offset, lw]), (kr, [kr, kc, kgid, kw]), (kc, [kr, kc, kgid, kw])], cuts, group)
+    # 3. pre-existing loops -> the node's owner; the last one (largest position) wins
     loop_w = torch.full((hi - lo,), fill, dtype=torch.float32, device=dev)
     if rv.numel():
         best = torch.full((hi - lo,), -1, dtype=torch.int64, device=dev)
@@ -500,11 +613,9 @@ def gcn_shards_from_slices(edge_slice, slice_offset, num_nodes, rank, world, gro
         lw_ext.scatter_(0, slot, torch.where(last, rw, torch.zeros_like(rw)))
         loop_w = lw_ext[:hi - lo]
     # 4. out-edges of my rows, global order -> deg = scatter_add(w, row) in edge order, then the loop
-    b_row, b_col, b_gid, b_w = scatter_edges_by_owner(kr, cuts, [kr, kc, kgid, kw], group)
     deg = _segment_sum_in_order(b_row - lo, b_w, hi - lo)
     deg = deg + loop_w
     # 5. in-edges of my rows, global order; the loops last
-    f_row, f_col, f_gid, f_w = scatter_edges_by_owner(kc, cuts, [kr, kc, kgid, kw], group)
     loop_gid = E_kept + own
     fwd = (torch.stack([torch.cat([f_row, own]), torch.cat([f_col, own])]), torch.cat([f_gid, loop_gid]),
            torch.cat([f_w, loop_w]))
@@ -513,22 +624,52 @@ def gcn_shards_from_slices(edge_slice, slice_offset, num_nodes, rank, world, gro
     return {"cuts": cuts, "E": E_kept + N, "deg": deg, "fwd": fwd, "bwd": bwd}
 
 
-def _norm_over_plan(plan, deg_own, w_local, group=None):
-    """GCN norm dinv[row] * w * dinv[col] of a plan's local edges: the degrees of
-    the halo endpoints come over the plan's own exchange (one float per halo
-    node), dinv = deg^-1/2 with inf -> 0 (torch's CPU pow(-0.5) rounding: the
-    native mp_gcn_norm_from_deg_f32 on the device)."""
-    degl = deg_own.new_empty((plan.n_local_src, 1))
-    degl[:plan.n_own, 0] = deg_own
+def _exchange_into_many(plans, bufs, gather_rows, group=None):
+    """exchange_into() of several plans of one group in ONE all_to_all (per
+    peer: plan 0's rows, plan 1's, ...): bufs[k] is plans[k]'s [n_local_src, F]
+    buffer, its own rows filled; its halo rows are written."""
+    world = plans[0].world
+    sends = [gather_rows(b[:p.n_own], p.send_idx) if p.send_idx.numel() else b.new_empty((0, b.shape[1]))
+             for p, b in zip(plans, bufs)]
+    segs, offs = [], [0] * len(plans)
+    for q in range(world):
+        for k, p in enumerate(plans):
+            segs.append(sends[k][offs[k]:offs[k] + p.send_counts[q]])
+            offs[k] += p.send_counts[q]
+    recv = bufs[0].new_empty((sum(p.n_local_src - p.n_own for p in plans), bufs[0].shape[1]))
+    _a2a(recv, torch.cat(segs).contiguous(), [sum(p.recv_counts[q] for p in plans) for q in range(world)],
+         [sum(p.send_counts[q] for p in plans) for q in range(world)], group)
+    pos, offs = 0, [p.n_own for p in plans]
+    for q in range(world):
+        for k, p in enumerate(plans):
+            n = p.recv_counts[q]
+            if n:
+                bufs[k][offs[k]:offs[k] + n].copy_(recv[pos:pos + n])
+            pos += n
+            offs[k] += n
+    return bufs
+
+
+def _norms_over_plans(plans, deg_own, w_locals, group=None):
+    """GCN norm dinv[row] * w * dinv[col] of each plan's local edges: the
+    degrees of the halo endpoints come over the plans' exchanges (one float
+    per halo node, all plans in one all_to_all), dinv = deg^-1/2 with inf -> 0
+    (torch's CPU pow(-0.5) rounding: the native mp_gcn_norm_from_deg_f32 on
+    the device)."""
+    bufs = []
+    for p in plans:
+        degl = deg_own.new_empty((p.n_local_src, 1))
+        degl[:p.n_own, 0] = deg_own
+        bufs.append(degl)
     if deg_own.is_cuda:
         from . import ops
-        plan.exchange_into(degl, ops.gather_rows, group)
-        lei = plan.local_edge_index
-        # local ids < n_own + n_halo by the plan's construction: no range read-back
-        return ops.norm_from_degree(lei[0], lei[1], degl.view(-1).clone(), w_local, trusted=True)
-    plan.exchange_into(degl, _host("gather_rows"), group)
-    lei = plan.local_edge_index
-    return _host("norm_local")(lei[0], lei[1], degl.view(-1), w_local)
+        _exchange_into_many(plans, bufs, ops.gather_rows, group)
+        # local ids < n_own + n_halo by the plans' construction: no range read-back
+        return [ops.norm_from_degree(p.local_edge_index[0], p.local_edge_index[1], b.view(-1).clone(), w,
+                                     trusted=True) for p, b, w in zip(plans, bufs, w_locals)]
+    _exchange_into_many(plans, bufs, _host("gather_rows"), group)
+    return [_host("norm_local")(p.local_edge_index[0], p.local_edge_index[1], b.view(-1), w)
+            for p, b, w in zip(plans, bufs, w_locals)]
 
 
 class HaloCover:
@@ -1431,8 +1572,10 @@ class ShardedGraph:
         self.group = group
         self.num_nodes = int(num_nodes)
         self.n_edges = int(edge_index.shape[1])
-        self.fwd = ShardPlan(edge_index, num_nodes, rank, world, cuts=cuts).exchange_requests(group)
-        self.bwd = transposed_plan(edge_index, num_nodes, rank, world, self.fwd.cuts, group)
+        if cuts is None:
+            cuts = edge_balanced_cuts(_count_by(edge_index[1].to(torch.int64), num_nodes), world)
+        self.fwd, self.bwd = ShardPlan.many([edge_index, edge_index], num_nodes, rank, world, cuts,
+                                            ["source_to_target", "target_to_source"], [None, None], group)
         self.lo, self.hi, self.n_own = self.fwd.lo, self.fwd.hi, self.fwd.n_own
         self.g_fwd = Graph(self.fwd.local_edge_index, self.n_own, self.fwd.n_local_src, chunk=chunk)
         # bwd.local_edge_index = [local row (= source j), local column (= destination i)]
@@ -1469,9 +1612,8 @@ class ShardedGraph:
         self.n_edges = int(d["E"])
         f_ei, f_gid, f_w = d["fwd"]
         b_ei, b_gid, b_w = d["bwd"]
-        self.fwd = ShardPlan(f_ei, num_nodes, rank, world, cuts=d["cuts"], edge_ids=f_gid).exchange_requests(group)
-        self.bwd = ShardPlan(b_ei, num_nodes, rank, world, cuts=d["cuts"], flow="target_to_source",
-                             edge_ids=b_gid).exchange_requests(group)
+        self.fwd, self.bwd = ShardPlan.many([f_ei, b_ei], num_nodes, rank, world, d["cuts"],
+                                            ["source_to_target", "target_to_source"], [f_gid, b_gid], group)
         self.lo, self.hi, self.n_own = self.fwd.lo, self.fwd.hi, self.fwd.n_own
         self.g_fwd = Graph(self.fwd.local_edge_index, self.n_own, self.fwd.n_local_src, chunk=chunk)
         self.g_bwd = Graph(self.bwd.local_edge_index, self.n_own, self.bwd.n_local_src,
@@ -1479,8 +1621,8 @@ class ShardedGraph:
         self.deg = d["deg"]
         self.cover = None
         self._chunk = chunk
-        self.norm_fwd = _norm_over_plan(self.fwd, d["deg"], f_w[self.fwd.edge_pos], group)
-        self.norm_bwd = _norm_over_plan(self.bwd, d["deg"], b_w[self.bwd.edge_pos], group)
+        self.norm_fwd, self.norm_bwd = _norms_over_plans([self.fwd, self.bwd], d["deg"],
+                                                         [f_w[self.fwd.edge_pos], b_w[self.bwd.edge_pos]], group)
         self._w = None
         if self.norm_fwd.is_cuda:
             self._set_local_weights(self.norm_fwd, self.norm_bwd)

@@ -13,6 +13,7 @@
 #   gloo2     bench.py --gpus 2, gloo ranks sharing the GPU (--verify) -> $R_bench_rmat21_gloo2_rehearsal.json
 #   gloo8 / gloo4  bench.py --gpus 8 / 4 as gloo ranks sharing the GPU (per-rank compute_in_turn:
 #             each rank's compute with the GPU to itself) -> $R_bench_rmat21_gloo{8,4}_rehearsal.json
+#   products_gloo4 / products_gloo8  config 5 (--workload products) as 4 / 8 gloo ranks sharing the GPU (--verify)
 #   gat_gloo2 the same for --workload gat                -> $R_bench_gat_gloo2_rehearsal.json
 #   prof      tools/profile.sh (kernel trace + PMC of the default bench); prof_gat / prof_products /
 #             prof_reddit the same for the other bench workloads (summarise with tools/pmc_summary.py)
@@ -20,7 +21,7 @@
 #   train     kernel trace of the GCNConv / GATConv layer training steps (tools/bench_configs.py)
 set -u
 export TMPDIR=/tmp
-R=${R:-r05}
+R=${R:-r06}
 O=gpurun_out
 mkdir -p $O
 run() {  # name seconds cmd...
@@ -45,6 +46,8 @@ for s in ${STEPS:-tests bench}; do
     gloo2) run gloo2 600 bash -c "MP_BENCH_BACKEND=gloo python bench.py --gpus 2 --steps 3 --warmup 1 --verify > $O/${R}_bench_rmat21_gloo2_rehearsal.json 2> $O/${R}_bench_rmat21_gloo2_rehearsal.err"; cut -c1-300 $O/${R}_bench_rmat21_gloo2_rehearsal.json ;;
     gloo8) run gloo8 1100 bash -c "MP_BENCH_BACKEND=gloo python bench.py --gpus 8 --steps 3 --warmup 1 > $O/${R}_bench_rmat21_gloo8_rehearsal.json 2> $O/${R}_bench_rmat21_gloo8_rehearsal.err"; cut -c1-300 $O/${R}_bench_rmat21_gloo8_rehearsal.json ;;
     gloo4) run gloo4 900 bash -c "MP_BENCH_BACKEND=gloo python bench.py --gpus 4 --steps 3 --warmup 1 > $O/${R}_bench_rmat21_gloo4_rehearsal.json 2> $O/${R}_bench_rmat21_gloo4_rehearsal.err"; cut -c1-300 $O/${R}_bench_rmat21_gloo4_rehearsal.json ;;
+    products_gloo4) run products_gloo4 1100 bash -c "MP_BENCH_BACKEND=gloo python bench.py --workload products --gpus 4 --steps 3 --warmup 1 --verify > $O/${R}_bench_products_gloo4_rehearsal.json 2> $O/${R}_bench_products_gloo4_rehearsal.err"; cut -c1-300 $O/${R}_bench_products_gloo4_rehearsal.json ;;
+    products_gloo8) run products_gloo8 1150 bash -c "MP_BENCH_BACKEND=gloo python bench.py --workload products --gpus 8 --steps 3 --warmup 1 --verify > $O/${R}_bench_products_gloo8_rehearsal.json 2> $O/${R}_bench_products_gloo8_rehearsal.err"; cut -c1-300 $O/${R}_bench_products_gloo8_rehearsal.json ;;
     gat_gloo2) run gat_gloo2 600 bash -c "MP_BENCH_BACKEND=gloo python bench.py --gpus 2 --workload gat --steps 3 --warmup 1 --verify > $O/${R}_bench_gat_gloo2_rehearsal.json 2> $O/${R}_bench_gat_gloo2_rehearsal.err"; cut -c1-300 $O/${R}_bench_gat_gloo2_rehearsal.json ;;
     diag) run diag 500 bash -c "python tools/gat_shard_diag.py > $O/${R}_gat_shard_diag.jsonl 2> $O/${R}_gat_shard_diag.err"; cat $O/${R}_gat_shard_diag.jsonl ;;
     prof) PROF_OUT=$O/${R}_prof run prof 1100 bash tools/profile.sh ;;
