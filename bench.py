@@ -256,6 +256,13 @@ def setup_dist(args):
     if world == 1 and not args.sharded:
         return 0, 1, local
     backend = os.environ.get("MP_BENCH_BACKEND", "nccl")
+    # the node's host threads are shared by its ranks: each rank's intra-op pool
+    # gets its share of OMP_NUM_THREADS (eight ranks x 16 spinning OpenMP threads
+    # on a 16-thread share stalled the shared-GPU rehearsal's builds)
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+    if local_world > 1:
+        share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+        torch.set_num_threads(max(1, share // local_world))
     if backend == "gloo":
         # rehearsal of the multi-GPU path on a box with fewer GPUs than ranks:
         # ranks share devices, halo rows are staged through the host
@@ -927,11 +934,12 @@ class BuildMeter:
             if os.path.basename(w.filename) == "dist.py" and w.lineno in stage_lines:
                 n_stage += 1
         syncs = sum(sites.values())
-        spans = []
+        spans, longest = [], []
         try:
             for e in prof.events():
                 if getattr(e, "device_type", None) == torch.autograd.DeviceType.CUDA:
                     spans.append((e.time_range.start, e.time_range.end))
+                    longest.append(((e.time_range.end - e.time_range.start) * 1e-3, e.name[:90]))
         except Exception as ex:  # pragma: no cover - profiler without device events
             self.res[name] = {"wall_s": wall, "host_syncs": syncs, "device_busy_s": None,
                               "note": "profiler gave no device events: %s" % ex}
@@ -953,7 +961,8 @@ class BuildMeter:
                           "device_ops": len(spans), "host_syncs": syncs,
                           "host_syncs_without_gloo_staging": syncs - n_stage,
                           "gloo_staged_all_to_all_s": mdist.GLOO_STAGED_S[0] - staged0,
-                          "sync_sites": dict(sorted(sites.items(), key=lambda kv: -kv[1]))}
+                          "sync_sites": dict(sorted(sites.items(), key=lambda kv: -kv[1])),
+                          "longest_device_ops_ms": [[round(ms, 3), nm] for ms, nm in sorted(longest, reverse=True)[:4]]}
         return out
 
 
@@ -1185,11 +1194,13 @@ def main(argv=None):
         E_local = E2
     else:
         from mi355_mp import dist as mdist
-        # more than two ranks per GPU (the gloo rehearsals): eight torch profilers
-        # on one device slowed the shard build past 3 min without a line, so
-        # wall time only (two per GPU: measured fine, 2.6 s)
+        # more than two ranks per GPU with the default four hardware queues per
+        # process: the queues oversubscribe the GPU's queue slots and the build
+        # crawls (61 s instead of 1.1 s at 4 ranks) -- wall time only
+        # there; the rehearsals run with GPU_MAX_HW_QUEUES=1 and are profiled
         local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
-        crowded = local_world > 2 * max(1, torch.cuda.device_count())
+        crowded = (local_world > 2 * max(1, torch.cuda.device_count())
+                   and os.environ.get("GPU_MAX_HW_QUEUES") != "1")
         meter = BuildMeter(not args.no_build_split and not crowded)
         sg = meter.run("shards", lambda: mdist.ShardedGraph.for_gcn_from_slices(ei_slice, s0, N, rank, world,
                                                                                chunk=args.chunk or None))
@@ -1218,12 +1229,32 @@ def main(argv=None):
                 # warm-up autotune: every rank times each step form (tile width x
                 # boundary as one launch or per tile), with the interior pass after
                 # and beside the send packing (split_interior), one untimed step
-                # then 3; the max over ranks decides -- the same choice on every rank
+                # then 3; the max over ranks decides -- the same choice on every rank.
+                # A gloo rehearsal (ranks sharing a GPU, every exchange staged through
+                # host memory) ranks the forms by each rank's compute in turn instead:
+                # its step time is the host staging's, not the forms'.  With one
+                # hardware queue per process (the rehearsals' GPU_MAX_HW_QUEUES=1,
+                # DESIGN 5.5) the side stream cannot run beside the compute stream,
+                # so the split forms are left out there.
                 tune_out = torch.empty((plan.n_own, F_DIM), device=dev)
                 tile_tune = {}
-                for (width, one), split in [(c, sp) for c in HALO_FORMS for sp in (False, True)]:
+                staged = dist.get_backend() == "gloo"
+                one_queue = os.environ.get("GPU_MAX_HW_QUEUES") == "1"
+                forms = [(c, sp) for c in HALO_FORMS for sp in ((False,) if one_queue else (False, True))]
+                for (width, one), split in forms:
+                    if staged and split:
+                        continue                  # timed with its non-split twin below
                     tb = overlap.halo_buffers(F_DIM, width)
                     overlap.split_interior, overlap.one_boundary_launch = split, one
+                    if staged:
+                        cit = overlap.compute_in_turn((x, tb), tune_out, bias, reps=5, barrier=lambda: barrier(world))
+                        tt = torch.tensor([cit["compute_alone_ms"], cit["compute_alone_split_ms"]], dtype=torch.float64)
+                        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+                        tile_tune[form_name(width, one, False)] = float(tt[0])
+                        if not one_queue:
+                            tile_tune[form_name(width, one, True)] = float(tt[1])
+                        del tb
+                        continue
                     overlap.step_fused(x, tb, tune_out, bias)
                     torch.cuda.synchronize()
                     barrier(world)
@@ -1243,8 +1274,8 @@ def main(argv=None):
                                          if form_name(w_, o_, s_) == best)
                 form = (width, one)
                 overlap.split_interior = split
-                stage(rank, "step form chosen in the warm-up: %s (max over ranks, ms/step: %s)"
-                      % (best, json.dumps(tile_tune)))
+                stage(rank, "step form chosen in the warm-up: %s (max over ranks, %s: %s)"
+                      % (best, "compute in turn, ms" if staged else "ms/step", json.dumps(tile_tune)))
             overlap.one_boundary_launch = form[1]
             bufs = overlap.halo_buffers(F_DIM, form[0])
         elif not args.no_overlap:
@@ -1529,6 +1560,9 @@ def main(argv=None):
                                                                           overlap.split_interior))
                       if sharded and bufs is not None else None,
                       "halo_tile_autotune_ms": tile_tune if sharded else None,
+                      "halo_tile_autotune_basis": (None if not sharded or tile_tune is None else
+                                                   "compute in turn, max over ranks (gloo rehearsal)"
+                                                   if dist.get_backend() == "gloo" else "step time, max over ranks"),
                       "split_interior": bool(overlap.split_interior) if sharded and overlap is not None else None,
                       "collective_timeout_s": COLLECTIVE_TIMEOUT_S if sharded else None,
                       "comm_init_s": COMM_INIT_S[0] if sharded else None,

@@ -789,12 +789,11 @@ class HaloCover:
         snS, snD, snP = peer_c[0::3], peer_c[1::3], peer_c[2::3]
         nS_tot, nD_tot = sum(nS_l), sum(nD_l)
         # --- the plan's edges by class in plan (= global edge) order: interior,
-        # pulled, pushed (a stable partition)
-        code = torch.where(remm, torch.where(push, 2, 1), 0).to(torch.int8)
-        order3 = torch.argsort(code, stable=True)
-        idx_int = order3[:n_int]
-        idx_pull = order3[n_int:n_int + n_pull]
-        idx_push = order3[n_int + n_pull:]
+        # pulled, pushed (a stable partition: each class's positions ascending, the
+        # sizes known from the read above -- no sort)
+        idx_int = _nonzero_n(~remm, n_int)
+        idx_pull = _nonzero_n(remm & ~push, n_pull)
+        idx_push = _nonzero_n(push, n_push)
         self.int_src, self.int_dst, self.int_w = src_l[idx_int], dst_l[idx_int], w_local[idx_int]
         S = _nonzero_n(in_s, nS_tot)                           # ascending node ids: grouped by owner
         D = _nonzero_n(in_d, nD_tot)                           # ascending (owner, destination) keys
@@ -834,7 +833,8 @@ class HaloCover:
         p_key = key[idx_push]
         p_row = d_rank[p_key] - D_start[p_own]
         del s_rank, d_rank
-        ord_p = torch.argsort(p_own, stable=True)
+        # grouped by owner, each group in edge order (per-owner counts known: no sort)
+        ord_p = torch.cat([_nonzero_n(p_own == q, nP_l[q]) for q in range(world)]) if world else p_own
         req = S.new_empty(sum(snS))
         _a2a(req, S.contiguous(), snS, nS_l, group)
         lo = plan.lo

@@ -12,7 +12,9 @@
 #             $R_rccl_kernel_trace/ (+ tools/kernel_overlap.py summary)
 #   gloo2     bench.py --gpus 2, gloo ranks sharing the GPU (--verify) -> $R_bench_rmat21_gloo2_rehearsal.json
 #   gloo8 / gloo4  bench.py --gpus 8 / 4 as gloo ranks sharing the GPU (per-rank compute_in_turn:
-#             each rank's compute with the GPU to itself) -> $R_bench_rmat21_gloo{8,4}_rehearsal.json
+#             each rank's compute with the GPU to itself) -> $R_bench_rmat21_gloo{8,4}_rehearsal.json;
+#             one hardware queue per process (GPU_MAX_HW_QUEUES=1): 4 x 4 queues oversubscribe the
+#             GPU's queue slots and stretch a 1 s build to 60 s
 #   products_gloo4 / products_gloo8  config 5 (--workload products) as 4 / 8 gloo ranks sharing the GPU (--verify)
 #   gat_gloo2 the same for --workload gat                -> $R_bench_gat_gloo2_rehearsal.json
 #   prof      tools/profile.sh (kernel trace + PMC of the default bench); prof_gat / prof_products /
@@ -44,10 +46,10 @@ for s in ${STEPS:-tests bench}; do
           run rccl_trace 500 rocprofv3 --kernel-trace --stats -d $O/${R}_rccl_kt -o kt --output-format csv -- python3 bench.py --sharded --emulate-peers 8,4,2 --steps 5 --warmup 2 --no-cpu-baseline --no-ref-paths --no-build-split
           python3 tools/kernel_overlap.py $O/${R}_rccl_kt > $O/${R}_rccl_kernel_overlap.json; cat $O/${R}_rccl_kernel_overlap.json | head -40 ;;
     gloo2) run gloo2 600 bash -c "MP_BENCH_BACKEND=gloo python bench.py --gpus 2 --steps 3 --warmup 1 --verify > $O/${R}_bench_rmat21_gloo2_rehearsal.json 2> $O/${R}_bench_rmat21_gloo2_rehearsal.err"; cut -c1-300 $O/${R}_bench_rmat21_gloo2_rehearsal.json ;;
-    gloo8) run gloo8 1100 bash -c "MP_BENCH_BACKEND=gloo python bench.py --gpus 8 --steps 3 --warmup 1 > $O/${R}_bench_rmat21_gloo8_rehearsal.json 2> $O/${R}_bench_rmat21_gloo8_rehearsal.err"; cut -c1-300 $O/${R}_bench_rmat21_gloo8_rehearsal.json ;;
-    gloo4) run gloo4 900 bash -c "MP_BENCH_BACKEND=gloo python bench.py --gpus 4 --steps 3 --warmup 1 > $O/${R}_bench_rmat21_gloo4_rehearsal.json 2> $O/${R}_bench_rmat21_gloo4_rehearsal.err"; cut -c1-300 $O/${R}_bench_rmat21_gloo4_rehearsal.json ;;
-    products_gloo4) run products_gloo4 1100 bash -c "MP_BENCH_BACKEND=gloo python bench.py --workload products --gpus 4 --steps 3 --warmup 1 --verify > $O/${R}_bench_products_gloo4_rehearsal.json 2> $O/${R}_bench_products_gloo4_rehearsal.err"; cut -c1-300 $O/${R}_bench_products_gloo4_rehearsal.json ;;
-    products_gloo8) run products_gloo8 1150 bash -c "MP_BENCH_BACKEND=gloo python bench.py --workload products --gpus 8 --steps 3 --warmup 1 --verify > $O/${R}_bench_products_gloo8_rehearsal.json 2> $O/${R}_bench_products_gloo8_rehearsal.err"; cut -c1-300 $O/${R}_bench_products_gloo8_rehearsal.json ;;
+    gloo8) run gloo8 1100 bash -c "GPU_MAX_HW_QUEUES=1 MP_BENCH_BACKEND=gloo python bench.py --gpus 8 --steps 3 --warmup 1 > $O/${R}_bench_rmat21_gloo8_rehearsal.json 2> $O/${R}_bench_rmat21_gloo8_rehearsal.err"; cut -c1-300 $O/${R}_bench_rmat21_gloo8_rehearsal.json ;;
+    gloo4) run gloo4 900 bash -c "GPU_MAX_HW_QUEUES=1 MP_BENCH_BACKEND=gloo python bench.py --gpus 4 --steps 3 --warmup 1 > $O/${R}_bench_rmat21_gloo4_rehearsal.json 2> $O/${R}_bench_rmat21_gloo4_rehearsal.err"; cut -c1-300 $O/${R}_bench_rmat21_gloo4_rehearsal.json ;;
+    products_gloo4) run products_gloo4 1100 bash -c "GPU_MAX_HW_QUEUES=1 MP_BENCH_BACKEND=gloo python bench.py --workload products --gpus 4 --steps 3 --warmup 1 --verify > $O/${R}_bench_products_gloo4_rehearsal.json 2> $O/${R}_bench_products_gloo4_rehearsal.err"; cut -c1-300 $O/${R}_bench_products_gloo4_rehearsal.json ;;
+    products_gloo8) run products_gloo8 1150 bash -c "GPU_MAX_HW_QUEUES=1 MP_BENCH_BACKEND=gloo python bench.py --workload products --gpus 8 --steps 3 --warmup 1 --verify > $O/${R}_bench_products_gloo8_rehearsal.json 2> $O/${R}_bench_products_gloo8_rehearsal.err"; cut -c1-300 $O/${R}_bench_products_gloo8_rehearsal.json ;;
     gat_gloo2) run gat_gloo2 600 bash -c "MP_BENCH_BACKEND=gloo python bench.py --gpus 2 --workload gat --steps 3 --warmup 1 --verify > $O/${R}_bench_gat_gloo2_rehearsal.json 2> $O/${R}_bench_gat_gloo2_rehearsal.err"; cut -c1-300 $O/${R}_bench_gat_gloo2_rehearsal.json ;;
     diag) run diag 500 bash -c "python tools/gat_shard_diag.py > $O/${R}_gat_shard_diag.jsonl 2> $O/${R}_gat_shard_diag.err"; cat $O/${R}_gat_shard_diag.jsonl ;;
     prof) PROF_OUT=$O/${R}_prof run prof 1100 bash tools/profile.sh ;;
