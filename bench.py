@@ -70,7 +70,9 @@ F_DIM = 256
 # the last tile arrives).  One launch per pass is the compute-bound P = 8 form; tiles whose
 # boundary pass runs per tile as it arrives pipeline the link-bound P = 2 chain
 # pack + exchange + boundary_last
-HALO_FORMS = ((256, True), (128, True), (128, False), (64, False))
+# (tile width, boundary in one launch, send rows packed per tile)
+HALO_FORMS = ((256, True, False), (128, True, False), (128, False, False), (64, False, False),
+              (128, True, True), (128, False, True), (64, False, True))
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md chip table)
 # SURVEY 8(d) / BASELINE.md section 2 algorithmic bytes: every gathered x_j row
 # counted at full size, no cache-reuse credit.  Reported, but its ratio to the
@@ -152,6 +154,9 @@ def parse(argv=None):
                          "by timing each on this job's links (max over ranks)")
     ap.add_argument("--boundary-per-tile", action="store_true",
                     help="with --halo-tile W: the boundary pass per tile as its halo arrives")
+    ap.add_argument("--pack-per-tile", action="store_true",
+                    help="with --halo-tile W: the send rows packed per tile, each tile's exchange started "
+                         "right after its packing")
     return ap.parse_args(argv)
 
 
@@ -966,13 +971,14 @@ class BuildMeter:
         return out
 
 
-def form_name(width, one_boundary, split):
+def form_name(width, one_boundary, split, pack_per_tile=False):
     """Name of a fused step form in the bench line / autotune table."""
-    return "%d-wide tiles, boundary %s%s" % (width, "in one launch" if one_boundary else "per tile",
-                                             ", interior beside the packing" if split else "")
+    return "%d-wide tiles, %sboundary %s%s" % (width, "packed per tile, " if pack_per_tile else "",
+                                               "in one launch" if one_boundary else "per tile",
+                                               ", interior beside the packing" if split else "")
 
 
-def link_model(mine, rank, n_tiles, fused=False, boundary_per_tile=True):
+def link_model(mine, rank, n_tiles, fused=False, boundary_per_tile=True, pack_per_tile=False):
     """The link-bandwidth model of this rank's step, from its own
     per-peer halo bytes and the compute it measured: each peer pair has its own
     xGMI link, so the exchange takes max over peers of max(bytes in, bytes out)
@@ -991,7 +997,7 @@ def link_model(mine, rank, n_tiles, fused=False, boundary_per_tile=True):
     if comp is None:
         return None
     T = max(1, n_tiles)
-    Tp = 1 if fused else T
+    Tp = 1 if fused and not pack_per_tile else T
     Tb = T if boundary_per_tile else 1
     pack_first = mine.get("send_pack_ms", 0.0) / Tp
     bnd_last = mine.get("boundary_ms", 0.0) / Tb
@@ -1224,14 +1230,17 @@ def main(argv=None):
         tile_tune = None
         if args.halo_tile != 0 and not args.no_overlap:
             if args.halo_tile > 0:
-                form = (args.halo_tile, not args.boundary_per_tile)
+                form = (args.halo_tile, not args.boundary_per_tile, args.pack_per_tile)
             else:
                 # warm-up autotune: every rank times each step form (tile width x
-                # boundary as one launch or per tile), with the interior pass after
-                # and beside the send packing (split_interior), one untimed step
-                # then 3; the max over ranks decides -- the same choice on every rank.
-                # A gloo rehearsal (ranks sharing a GPU, every exchange staged through
-                # host memory) ranks the forms by each rank's compute in turn instead:
+                # boundary as one launch or per tile x send rows packed in one launch
+                # or per tile), with the interior pass after and beside the send
+                # packing (split_interior), one untimed step then 3; the max over
+                # ranks decides -- the same choice on every rank.  A gloo rehearsal
+                # (ranks sharing a GPU, every exchange staged through host memory)
+                # ranks the forms by the node step its own measurements predict
+                # instead: the longer of its compute in turn and the link chain
+                # pack(first) + exchange at 77 GB/s + boundary(last) (link_model) --
                 # its step time is the host staging's, not the forms'.  With one
                 # hardware queue per process (the rehearsals' GPU_MAX_HW_QUEUES=1,
                 # DESIGN 5.5) the side stream cannot run beside the compute stream,
@@ -1240,19 +1249,25 @@ def main(argv=None):
                 tile_tune = {}
                 staged = dist.get_backend() == "gloo"
                 one_queue = os.environ.get("GPU_MAX_HW_QUEUES") == "1"
+                peer_bytes = max([max(overlap.recv_counts[q], overlap.send_counts[q]) * F_DIM * 4
+                                  for q in range(world) if q != rank] or [0])
                 forms = [(c, sp) for c in HALO_FORMS for sp in ((False,) if one_queue else (False, True))]
-                for (width, one), split in forms:
+                for (width, one, ppt), split in forms:
                     if staged and split:
                         continue                  # timed with its non-split twin below
                     tb = overlap.halo_buffers(F_DIM, width)
-                    overlap.split_interior, overlap.one_boundary_launch = split, one
+                    overlap.split_interior, overlap.one_boundary_launch, overlap.pack_per_tile = split, one, ppt
                     if staged:
                         cit = overlap.compute_in_turn((x, tb), tune_out, bias, reps=5, barrier=lambda: barrier(world))
-                        tt = torch.tensor([cit["compute_alone_ms"], cit["compute_alone_split_ms"]], dtype=torch.float64)
+                        T = tb.n_tiles
+                        chain = (cit["send_pack_ms"] / (T if ppt else 1) + peer_bytes / 77e9 * 1e3
+                                 + cit["boundary_ms"] / (1 if one else T))
+                        tt = torch.tensor([max(cit["compute_alone_ms"], chain),
+                                           max(cit["compute_alone_split_ms"], chain)], dtype=torch.float64)
                         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-                        tile_tune[form_name(width, one, False)] = float(tt[0])
+                        tile_tune[form_name(width, one, False, ppt)] = float(tt[0])
                         if not one_queue:
-                            tile_tune[form_name(width, one, True)] = float(tt[1])
+                            tile_tune[form_name(width, one, True, ppt)] = float(tt[1])
                         del tb
                         continue
                     overlap.step_fused(x, tb, tune_out, bias)
@@ -1265,18 +1280,18 @@ def main(argv=None):
                     tt = torch.tensor([(time.perf_counter() - t1) / 3 * 1e3], dtype=torch.float64)
                     tt = tt.to(dev) if dist.get_backend() == "nccl" else tt
                     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-                    tile_tune[form_name(width, one, split)] = float(tt.item())
+                    tile_tune[form_name(width, one, split, ppt)] = float(tt.item())
                     del tb
                 del tune_out
                 best = min(tile_tune, key=tile_tune.get)
-                width, one, split = next((w_, o_, s_) for (w_, o_), s_ in
-                                         [(c, sp) for c in HALO_FORMS for sp in (False, True)]
-                                         if form_name(w_, o_, s_) == best)
-                form = (width, one)
+                (width, one, ppt), split = next(f for f in [(c, sp) for c in HALO_FORMS for sp in (False, True)]
+                                                if form_name(f[0][0], f[0][1], f[1], f[0][2]) == best)
+                form = (width, one, ppt)
                 overlap.split_interior = split
                 stage(rank, "step form chosen in the warm-up: %s (max over ranks, %s: %s)"
-                      % (best, "compute in turn, ms" if staged else "ms/step", json.dumps(tile_tune)))
-            overlap.one_boundary_launch = form[1]
+                      % (best, "predicted node step from the compute in turn, ms" if staged else "ms/step",
+                         json.dumps(tile_tune)))
+            overlap.one_boundary_launch, overlap.pack_per_tile = form[1], form[2]
             bufs = overlap.halo_buffers(F_DIM, form[0])
         elif not args.no_overlap:
             x_ov = overlap.local_buffer(F_DIM)
@@ -1490,7 +1505,8 @@ def main(argv=None):
             stage(rank, "compute in turn: %s" % json.dumps(mine["compute_in_turn"]))
             mine["link_model"] = link_model(mine, rank, bufs.n_tiles if bufs is not None else 1,
                                             fused=bufs is not None,
-                                            boundary_per_tile=bufs is not None and not overlap.one_boundary_launch)
+                                            boundary_per_tile=bufs is not None and not overlap.one_boundary_launch,
+                                            pack_per_tile=bufs is not None and overlap.pack_per_tile)
             stage(rank, "link model: %s" % json.dumps(mine["link_model"]))
         if args.emulate_peers:
             if world != 1 or dist.get_backend() != "nccl":
@@ -1557,11 +1573,12 @@ def main(argv=None):
                       "halo_tile": args.halo_tile if sharded and not args.no_overlap else None,
                       "halo_tiles": [bufs.width] * bufs.n_tiles if sharded and bufs is not None else None,
                       "step_form": ("fused: one launch per pass, %s" % form_name(bufs.width, overlap.one_boundary_launch,
-                                                                          overlap.split_interior))
+                                                                          overlap.split_interior, overlap.pack_per_tile))
                       if sharded and bufs is not None else None,
                       "halo_tile_autotune_ms": tile_tune if sharded else None,
                       "halo_tile_autotune_basis": (None if not sharded or tile_tune is None else
-                                                   "compute in turn, max over ranks (gloo rehearsal)"
+                                                   "max over ranks of max(compute in turn, link chain at 77 GB/s)"
+                                                   " (gloo rehearsal)"
                                                    if dist.get_backend() == "gloo" else "step time, max over ranks"),
                       "split_interior": bool(overlap.split_interior) if sharded and overlap is not None else None,
                       "collective_timeout_s": COLLECTIVE_TIMEOUT_S if sharded else None,

@@ -703,7 +703,7 @@ class HaloCover:
     edge weights; every rank of `group` builds its cover together (three
     all_to_alls of the requests)."""
 
-    def __init__(self, plan, w_local, group=None):
+    def __init__(self, plan, w_local, group=None, edge_ids=False):
         dev = plan.halo_nodes.device
         world, rank = plan.world, plan.rank
         n_own = plan.n_own
@@ -838,12 +838,18 @@ class HaloCover:
         req = S.new_empty(sum(snS))
         _a2a(req, S.contiguous(), snS, nS_l, group)
         lo = plan.lo
-        # the push edges' (source, partial row, weight bits) in one all_to_all
-        pk = torch.stack([gsrc[idx_push], p_row, w_local[idx_push].view(torch.int32).to(torch.int64)], 1)[ord_p]
-        pk_in = pk.new_empty((sum(snP), 3))
+        # the push edges' (source, partial row, weight bits[, global edge id]) in one all_to_all
+        cols = [gsrc[idx_push], p_row, w_local[idx_push].view(torch.int32).to(torch.int64)]
+        if edge_ids:
+            cols.append(plan.edge_gid[idx_push].to(torch.int64))
+        pk = torch.stack(cols, 1)[ord_p]
+        pk_in = pk.new_empty((sum(snP), len(cols)))
         _a2a(pk_in, pk.contiguous(), snP, nP_l, group)
         ps, pr = pk_in[:, 0], pk_in[:, 1]
         pw = pk_in[:, 2].to(torch.int32).view(torch.float32)
+        # edge_ids: the GLOBAL id of every push edge this rank sums for its peers, in
+        # send-graph order (the attention-dropout key of a pushed GAT piece's edges)
+        self.push_gid = pk_in[:, 3].contiguous() if edge_ids else None
         # --- the send graph: rows = this rank's send buffer (per peer: pulled rows, then partial rows)
         self.send_counts = [a_ + b_ for a_, b_ in zip(snS, snD)]
         self.send_pull_counts, self.send_push_counts = snS, snD
@@ -993,6 +999,12 @@ class OverlappedAggregation:
         # last tile's halo arrived (True), or one launch per tile as its halo
         # arrives (False: tile t's boundary pass overlaps tile t+1's exchange)
         self.one_boundary_launch = True
+        # step_fused: the send rows packed by one launch over every tile (False),
+        # or one launch per tile with that tile's all_to_all started right after
+        # it (True: the exchange starts after 1/T of the packing instead of all
+        # of it -- the link chain pack + exchange + boundary is shorter, the
+        # compute a few launches longer)
+        self.pack_per_tile = False
 
     def local_buffer(self, F, dtype=torch.float32, device=None):
         """[n_own + n_halo, F]: the owner writes rows [:n_own], the exchange the rest."""
@@ -1210,6 +1222,29 @@ class OverlappedAggregation:
             ops.aggregate_tiles(g, "other", x_own, w, bufs.F, bufs.send, "sum", 0, None,
                                 out_tiles=(bufs.width, bufs.n_send * bufs.width))
 
+    def _pack_tile(self, x_own, bufs, t):
+        """Tile t's send rows alone (pack_per_tile): features [t*width, (t+1)*width)
+        of x_own's rows into bufs.send[t], the same per-row arithmetic."""
+        from . import ops
+        if self.n_send == 0:
+            return
+        g_bh, g_sp, _ = self._fused_graphs()
+        g, w = (self.g_send.dst, self.w_send) if self.cover is not None else (g_sp.dst, None)
+        c0 = t * bufs.width
+        ops.aggregate_tiles(g, "other", x_own[:, c0:c0 + bufs.width], w, bufs.width, bufs.send[t], "sum", 0, None)
+
+    def _pack_and_exchange(self, x_own, bufs, group=None):
+        """The send packing and every tile's all_to_all: one packing launch then
+        the tiles' exchanges, or (pack_per_tile) tile by tile."""
+        if self.pack_per_tile and bufs.n_tiles > 1:
+            works = []
+            for t in range(bufs.n_tiles):
+                self._pack_tile(x_own, bufs, t)
+                works += self._start_exchange(bufs, group, tiles=[t])
+            return works
+        self._pack_fused(x_own, bufs)
+        return self._start_exchange(bufs, group)
+
     def _interior_fused(self, x_own, out, bias):
         """The interior edges of every feature in one launch, with the bias of
         the rows the boundary pass leaves untouched (no boundary edge: a per-row
@@ -1245,13 +1280,13 @@ class OverlappedAggregation:
         b = bias[c0:c1] if bias is not None else None
         ops.aggregate_tiles(g_bh.dst, "other", bufs.recv[tile], self.w_bnd, bufs.width, out[:, c0:c1], "sum", flags, b)
 
-    def _start_exchange(self, bufs, group=None):
-        """Every tile's all_to_all, started in tile order (RCCL runs them back to
-        back on its stream); returns one work handle per tile (None: gloo with
-        device tensors, done synchronously)."""
+    def _start_exchange(self, bufs, group=None, tiles=None):
+        """Every tile's all_to_all (or those of `tiles`), started in tile order
+        (RCCL runs them back to back on its stream); returns one work handle per
+        tile (None: gloo with device tensors, done synchronously)."""
         gloo = bufs.recv.is_cuda and dist.get_backend(group) == "gloo"
         works = []
-        for t in range(bufs.n_tiles):
+        for t in (range(bufs.n_tiles) if tiles is None else tiles):
             if gloo:
                 _a2a(bufs.recv[t], bufs.send[t], self.recv_counts, self.send_counts, group)
                 works.append(None)
@@ -1263,7 +1298,8 @@ class OverlappedAggregation:
     def step_fused(self, x_own, bufs, out, bias=None, group=None, events=None):
         """The step with one launch per pass:
           1. pack every tile's send rows in one launch (tile-major bufs.send),
-             then start each tile's all_to_all into bufs.recv,
+             then start each tile's all_to_all into bufs.recv (pack_per_tile:
+             one launch per tile, its all_to_all started right after it),
           2. the interior edges in one launch over x_own (the caller's
              row-major [n_own, F] rows: no copy into a tile buffer), beside the
              packing on a second stream when split_interior,
@@ -1289,8 +1325,7 @@ class OverlappedAggregation:
         if split:
             start = torch.cuda.current_stream(out.device).record_event()
         rec("send")
-        self._pack_fused(x_own, bufs)
-        works = self._start_exchange(bufs, group)
+        works = self._pack_and_exchange(x_own, bufs, group)
         rec("send")
         if split:
             side = _side_stream(out.device)
@@ -1340,7 +1375,13 @@ class OverlappedAggregation:
                 else:
                     for t in range(bufs.n_tiles):
                         self._boundary_fused(bufs, out, bias, tile=t)
-            return (lambda: self._pack_fused(x_own, bufs), lambda: self._interior_fused(x_own, out, bias), boundary,
+            def pack():
+                if self.pack_per_tile and bufs.n_tiles > 1:
+                    for t in range(bufs.n_tiles):
+                        self._pack_tile(x_own, bufs, t)
+                else:
+                    self._pack_fused(x_own, bufs)
+            return (pack, lambda: self._interior_fused(x_own, out, bias), boundary,
                     lambda group: self._start_exchange(bufs, group))
         x_tiles = form
         sends = {}
@@ -1685,19 +1726,21 @@ class ShardedGraph:
         weighted sum of a row run over the same edges in the same (global)
         order as on one GPU: no extra collective, alpha bit-equal on rows no
         merge-path task splits.  return_alpha: (global edge ids, alpha [m, H])
-        of this rank's in-edges.  dropout: the fused attention dropout (its keep
-        mask hashes the rank's local CSR slots, so it differs from one GPU's).
+        of this rank's in-edges (the pull form).  dropout: the fused attention
+        dropout, its keep mask keyed on the GLOBAL edge ids -- the single-GPU
+        layer's mask (over the cover too).
         local_gat(graph, edge_index, xw_local, att, H, C, slope, bias,
         return_alpha, dropout) -> (out, alpha): default the HIP path
         (ops.gat_propagate); the gloo CPU tests pass the oracle."""
         from .gat_cover import cover_ok
         gc = getattr(self, "gat_cover", None)
-        if gc is not None and not return_alpha and not dropout and local_gat is None:
+        if gc is not None and not return_alpha and local_gat is None:
             if not xw_own.is_cuda:
-                return _host("gat_cover_forward")(gc, xw_own, att, heads, out_channels, negative_slope, bias), None
-            if cover_ok(heads, out_channels):
+                if not dropout:
+                    return _host("gat_cover_forward")(gc, xw_own, att, heads, out_channels, negative_slope, bias), None
+            elif cover_ok(heads, out_channels):
                 from .gat_cover import gat_cover_propagate
-                return gat_cover_propagate(gc, xw_own, att, heads, out_channels, negative_slope, bias), None
+                return gat_cover_propagate(gc, xw_own, att, heads, out_channels, negative_slope, bias, dropout), None
         if local_gat is None:
             from . import ops
             local_gat = ops.gat_propagate
@@ -1711,8 +1754,9 @@ class ShardedGraph:
         (mi355_mp.gat_cover.GatHaloCover: a remote source row is pulled, or its
         owner pushes its online-softmax piece of the destination row -- 0.57x
         the pull rows on the config-2 graph) instead of the pull exchange.
-        return_alpha and attention dropout keep the pull form; heads of any
-        width (C % 4 == 0, GATConv pads to it) take the cover.  Collective, once (every rank of the group)."""
+        Attention dropout runs over the cover too (keys: global edge ids);
+        return_alpha keeps the pull form; heads of any width (C % 4 == 0,
+        GATConv pads to it) take the cover.  Collective, once (every rank of the group)."""
         from .gat_cover import GatHaloCover
         if self.bwd is not None:
             raise ValueError("mi355_mp.dist: enable_gat_halo_cover needs a graph made by for_gat / "

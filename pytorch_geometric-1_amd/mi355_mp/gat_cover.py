@@ -48,8 +48,17 @@ oracle with a host twin of the same data flow in differentiable torch ops
 multiple of 4): C / 4 a power of two <= 64 takes the fused transposed pass,
 whose per-edge d score gives a pusher its share of d a_dst; other widths the
 wide kernels, the share then node-wise from the pieces' training accumulators
-(out2, s2) rescaled to the merged row.  return_alpha and attention dropout
-take the pull form.
+(out2, s2) rescaled to the merged row.
+
+Attention dropout (training) keys its hashed keep mask on each edge's GLOBAL
+id, as the single-GPU layer does (ABI 7 drop_ids): the local piece's edges
+carry their plan's global ids, the pushed pieces' edges the ids their owner
+sent with them (HaloCover(edge_ids=True)).  A piece keeps the undropped
+softmax statistics and the dropped weights on its sum, so the merge rule is
+unchanged; the pulled rows are plain copies (no attention edge, no mask);
+a pusher's share of d a_dst comes node-wise from its pieces' (out2, s2)
+whatever the head width.  return_alpha takes the pull form (the alpha of a
+pushed edge lives on its pusher).
 """
 import torch
 
@@ -92,7 +101,7 @@ class GatHaloCover:
     Graphs are built lazily on the device of the plan."""
 
     def __init__(self, plan, group=None):
-        hc = HaloCover(plan, None, group)
+        hc = HaloCover(plan, None, group, edge_ids=True)
         self.hc, self.plan, self.group = hc, plan, group
         dev = plan.halo_nodes.device
         n_own = plan.n_own
@@ -108,6 +117,8 @@ class GatHaloCover:
         src[hc.pull_pos] = hc.pull_halo
         loc = torch.sort(torch.cat([hc.int_pos, hc.pull_pos])).values
         self.loc_src, self.loc_dst = src[loc].contiguous(), dst[loc].contiguous()
+        self.loc_gid = plan.edge_gid[loc].contiguous()        # attention-dropout keys
+        self.push_gid = hc.push_gid
         self.n_interior = int(hc.int_pos.numel())
         # received pieces -> own destination (the merge list)
         self.part_row = (hc.push_halo - n_own).contiguous()
@@ -145,6 +156,8 @@ class GatHaloCover:
             g_copy_t = Graph(torch.stack([self.copy_dst, self.copy_src]), n_own, max(self.n_send, 1))
             g_push = Graph(torch.stack([self.push_src, self.push_dst]), self.n_send, n_own,
                            target_tasks=GAT_TARGET_TASKS)
+            # attention dropout keyed on the global edge ids (Graph.drop_ids)
+            g_loc.edge_key, g_push.edge_key = self.loc_gid, self.push_gid
             self._graphs = (g_loc, g_send, g_merge, g_copy_t, g_push)
         return self._graphs
 
@@ -155,14 +168,16 @@ class GatHaloCover:
                 "send_rows": self.n_send, "local_piece_edges": int(self.loc_src.numel())}
 
     # ---------------------------------------------------------- device (HIP)
-    def forward_device(self, xw_own, att_c, H, C, slope, bias, train, exchange=True):
+    def forward_device(self, xw_own, att_c, H, C, slope, bias, train, exchange=True, drop=None):
         """The step on the fused kernels.  Returns (out [n_own, H*C] with bias,
         saved) -- saved holds what backward_device needs when train.
         exchange=False: the compute alone (no collective; the receive buffers
-        hold zeros), for decompose()."""
+        hold zeros), for decompose().  drop = (seed, p): attention dropout
+        (training form)."""
         from . import _lib
         lib = _lib.load()
-        g_loc, g_send, g_merge, _, _ = self.graphs()
+        g_loc, g_send, g_merge, _, g_push = self.graphs()
+        train = train or drop is not None
         dev = xw_own.device
         st = _lib.stream_ptr(dev)
         n_own, F = self.n_own, H * C
@@ -189,7 +204,32 @@ class GatHaloCover:
         send = torch.empty((self.n_send, F), dtype=torch.float32, device=dev)
         send_st = torch.empty((self.n_send, H, 2), dtype=torch.float32, device=dev)
         send2 = send_s2 = None
-        if self.n_send:
+        if self.n_send and drop is not None:
+            # the pushed pieces over the push graph with the keep mask of their
+            # global edge ids (training form: out2 / s2 give this rank's share of
+            # d a_dst), then the pulled rows copied in -- a copy is not an
+            # attention edge; alpha = 1 would give the row itself bit for bit
+            send2 = torch.zeros((self.n_send, F), dtype=torch.float32, device=dev)
+            send_s2 = torch.zeros((self.n_send, H), dtype=torch.float32, device=dev)
+            if self.push_src.numel():
+                gp = g_push.dst.struct("other")
+                sb = lib.mp_gat_train_slab_bytes(gp, H, C)
+                slab = torch.empty(sb, dtype=torch.uint8, device=dev)
+                _lib.check(lib.mp_gat_aggregate_train_drop_f32(gp, xl.data_ptr(), a_src.data_ptr(),
+                                                               send_adst.data_ptr(), att_c.data_ptr(), H, C,
+                                                               float(slope), None, send.data_ptr(), F, None,
+                                                               send_st.data_ptr(), send2.data_ptr(),
+                                                               send_s2.data_ptr(), int(drop[0]), float(drop[1]),
+                                                               g_push.drop_ids("dst").data_ptr(), slab.data_ptr(), sb,
+                                                               _lib.MP_STAGE_ALL, st),
+                           "mp_gat_aggregate_train_drop_f32 (pushed pieces)")
+                del slab
+            else:
+                send.zero_()
+                send_st.zero_()
+            if self.copy_src.numel():
+                send[self.copy_dst] = xl[self.copy_src]
+        elif self.n_send:
             gs = g_send.dst.struct("other")
             if train and not fused:
                 send2 = torch.empty((self.n_send, F), dtype=torch.float32, device=dev)
@@ -222,7 +262,19 @@ class GatHaloCover:
         agg2 = s2 = None
         if n_own:
             gl = g_loc.dst.struct("other")
-            if train:
+            if drop is not None:
+                agg2 = torch.empty((n_own, F), dtype=torch.float32, device=dev)
+                s2 = torch.empty((n_own, H), dtype=torch.float32, device=dev)
+                sb = lib.mp_gat_train_slab_bytes(gl, H, C)
+                slab = torch.empty(sb, dtype=torch.uint8, device=dev)
+                _lib.check(lib.mp_gat_aggregate_train_drop_f32(gl, xl.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(),
+                                                               att_c.data_ptr(), H, C, float(slope), None,
+                                                               out.data_ptr(), F, None, stats.data_ptr(),
+                                                               agg2.data_ptr(), s2.data_ptr(), int(drop[0]),
+                                                               float(drop[1]), g_loc.drop_ids("dst").data_ptr(),
+                                                               slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
+                           "mp_gat_aggregate_train_drop_f32 (local piece)")
+            elif train:
                 agg2 = torch.empty((n_own, F), dtype=torch.float32, device=dev)
                 s2 = torch.empty((n_own, H), dtype=torch.float32, device=dev)
                 sb = lib.mp_gat_train_slab_bytes(gl, H, C)
@@ -252,7 +304,7 @@ class GatHaloCover:
                                                      _lib.ptr(bias),
                                                      out.data_ptr(), F, stats.data_ptr(), _lib.ptr(agg2),
                                                      _lib.ptr(s2), st), "mp_gat_merge_partials_f32")
-        saved = (xl, a_src, a_dst, stats, agg2, s2, send_st, send2, send_s2) if train else None
+        saved = (xl, a_src, a_dst, stats, agg2, s2, send_st, send2, send_s2, drop) if train else None
         return out, saved
 
     def decompose(self, xw_own, att, H, C, slope, bias, reps=10, barrier=None):
@@ -307,22 +359,25 @@ class GatHaloCover:
         from . import _lib, ops
         lib = _lib.load()
         g_loc, _, g_merge, g_copy_t, g_push = self.graphs()
-        xl, a_src, a_dst, stats, agg2, s2, send_st, send2, send_s2 = saved
+        xl, a_src, a_dst, stats, agg2, s2, send_st, send2, send_s2, drop = saved
+        seed, p_drop = (0, 0.0) if drop is None else (int(drop[0]), float(drop[1]))
         dev = g.device
         st = _lib.stream_ptr(dev)
         n_own, F, grp = self.n_own, H * C, self.group
         nl = self.n_local_src
         fused = fused_heads(H, C)
 
-        def wide_pass(gt_struct, n_rows, grad_out, pack_, xw_rows, gx_out):
+        def wide_pass(gt_struct, n_rows, grad_out, pack_, xw_rows, gx_out, graph):
             """mp_gat_backward_wide_f32 + its epilogue over a transposed graph of
-            n_rows source rows: gx_out += sum alpha g + d a_src att_src; returns d a_src."""
+            n_rows source rows (graph: its Graph, for the dropout keys):
+            gx_out += sum alpha g + d a_src att_src; returns d a_src."""
             acc2 = torch.zeros((n_rows, F), dtype=torch.float32, device=dev)
             sc = torch.zeros((n_rows, H), dtype=torch.float32, device=dev)
             sb = lib.mp_gat_train_slab_bytes(gt_struct, H, C)
             slab = torch.empty(sb, dtype=torch.uint8, device=dev)
             _lib.check(lib.mp_gat_backward_wide_f32(gt_struct, grad_out.data_ptr(), F, a_src.data_ptr(),
-                                                    pack_.data_ptr(), H, C, float(slope), 0, 0.0, None,
+                                                    pack_.data_ptr(), H, C, float(slope), seed, p_drop,
+                                                    graph.drop_ids("src").data_ptr() if drop is not None else None,
                                                     gx_out.data_ptr(),
                                                     acc2.data_ptr(), _lib.nbytes(acc2), sc.data_ptr(),
                                                     _lib.nbytes(sc), slab.data_ptr(), sb, _lib.MP_STAGE_ALL, st),
@@ -356,7 +411,19 @@ class GatHaloCover:
         if n_own and g_loc.dst.n_edges:
             gt = g_loc.src_with_dst_slots()
             gs = gt.struct("dst_slot")
-            if fused:
+            if fused and drop is not None:
+                zero_gd = torch.zeros((nl, H), dtype=torch.float32, device=dev)
+                sb = lib.mp_gat_slab_bytes(gs, H, C)
+                slab = torch.empty(sb, dtype=torch.uint8, device=dev)
+                _lib.check(lib.mp_gat_backward_train_drop_f32(gs, g.data_ptr(), F, xl.data_ptr(), a_src.data_ptr(),
+                                                              pack.data_ptr(), att_c.data_ptr(), H, C, float(slope),
+                                                              zero_gd.data_ptr(), seed, p_drop,
+                                                              g_loc.drop_ids("src").data_ptr(), gx_l.data_ptr(),
+                                                              ga_src_l.data_ptr(), slab.data_ptr(), sb,
+                                                              _lib.MP_STAGE_ALL, st),
+                           "mp_gat_backward_train_drop_f32 (local piece)")
+                del slab, zero_gd
+            elif fused:
                 zero_gd = torch.zeros((nl, H), dtype=torch.float32, device=dev)
                 sb = lib.mp_gat_slab_bytes(gs, H, C)
                 slab = torch.empty(sb, dtype=torch.uint8, device=dev)
@@ -367,7 +434,7 @@ class GatHaloCover:
                            "mp_gat_backward_train_f32 (local piece)")
                 del slab, zero_gd
             else:
-                ga_src_l = wide_pass(gs, nl, g, pack, xl, gx_l)
+                ga_src_l = wide_pass(gs, nl, g, pack, xl, gx_l, g_loc)
         # reverse exchange: a pulled slot returns its row's gradient to the owner, a
         # piece's slot carries its destination's g and pack to the peer that pushed it
         rev = gx_l[n_own:]
@@ -387,14 +454,15 @@ class GatHaloCover:
         ga_src_push = torch.zeros((max(n_own, 1), H), dtype=torch.float32, device=dev)
         ga_back = torch.zeros((self.n_send, H), dtype=torch.float32, device=dev)
         E_push = int(self.push_src.numel())
-        if E_push and not fused:
-            # wide heads: the fused pass's per-edge d score needs C/4 a power of two, so
-            # this rank's share of d a_dst comes node-wise from its pieces' training
-            # accumulators instead: with c = den_q e^(m_q - M) / den the piece's weight in
-            # the merged row, share = c (<g, out2_q> - rs s2_q)
+        if E_push and (not fused or drop is not None):
+            # wide heads (the fused pass's per-edge d score needs C/4 a power of two) and
+            # attention dropout (that pass has no dropout form): this rank's share of
+            # d a_dst comes node-wise from its pieces' training accumulators instead:
+            # with c = den_q e^(m_q - M) / den the piece's weight in the merged row,
+            # share = c (<g, out2_q> - rs s2_q)
             gt = g_push.src_with_dst_slots()
             gx_push = torch.zeros((n_own, F), dtype=torch.float32, device=dev)
-            ga_src_push = wide_pass(gt.struct("dst_slot"), n_own, back, back_pack, xl[:n_own], gx_push)
+            ga_src_push = wide_pass(gt.struct("dst_slot"), n_own, back, back_pack, xl[:n_own], gx_push, g_push)
             gx += gx_push
             pk = back_pack.view(-1, H, 4)
             c = send_st[..., 1] * torch.exp(send_st[..., 0] - pk[..., 1]) * pk[..., 2]
@@ -439,9 +507,9 @@ class GatHaloCover:
 
 class _GatCoverFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, xw_own, att, bias, cover, H, C, slope):
+    def forward(ctx, xw_own, att, bias, cover, H, C, slope, drop):
         att_c = att.reshape(H, 2 * C).contiguous().to(torch.float32)
-        out, saved = cover.forward_device(xw_own.contiguous(), att_c, H, C, slope, bias, True)
+        out, saved = cover.forward_device(xw_own.contiguous(), att_c, H, C, slope, bias, True, drop=drop)
         ctx.cover, ctx.H, ctx.C, ctx.slope = cover, H, C, slope
         ctx.saved = saved
         ctx.save_for_backward(out, bias, att_c)
@@ -458,12 +526,16 @@ class _GatCoverFn(torch.autograd.Function):
         ctx.saved = None
         if gatt is not None:
             gatt = gatt.view(1, ctx.H, 2 * ctx.C)
-        return gx, gatt, gb, None, None, None, None
+        return gx, gatt, gb, None, None, None, None, None
 
 
-def gat_cover_propagate(cover, xw_own, att, heads, out_channels, negative_slope=0.2, bias=None):
+def gat_cover_propagate(cover, xw_own, att, heads, out_channels, negative_slope=0.2, bias=None, dropout=0.0,
+                        seed=None):
     """This rank's rows of the fused GATConv aggregation over the cover (+ bias)
-    on the HIP path with its native backward; a host tensor raises."""
+    on the HIP path with its native backward; a host tensor raises.
+    dropout > 0: GATConv's training-mode attention dropout, its keep mask keyed
+    on the global edge ids (seed from the device's generator unless given):
+    the single-GPU layer's mask."""
     H, C = int(heads), int(out_channels)
     if xw_own.shape[0] != cover.n_own:
         raise ValueError("mi355_mp.gat_cover: xw_own has %d rows, this rank owns %d" % (xw_own.shape[0], cover.n_own))
@@ -472,9 +544,18 @@ def gat_cover_propagate(cover, xw_own, att, heads, out_channels, negative_slope=
                            "device tensors")
     if not cover_ok(H, C):
         raise ValueError("mi355_mp.gat_cover: heads of %d features need C %% 4 == 0 (GATConv pads them)" % C)
+    drop = None
+    if dropout > 0:
+        from . import ops
+        if not ops.gat_dropout_ok(H, C, dropout):
+            raise ValueError("mi355_mp.gat_cover: attention dropout needs 0 < p < 1 and H <= 32 (got p=%g, H=%d)"
+                             % (dropout, H))
+        if seed is None:
+            seed = ops.dropout_seed(xw_own.device)
+        drop = (int(seed) & 0xFFFFFFFFFFFFFFFF, float(dropout))
     needs = torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in (xw_own, att, bias))
     if not needs:
         att_c = att.reshape(H, 2 * C).contiguous().to(torch.float32)
-        out, _ = cover.forward_device(xw_own.contiguous(), att_c, H, C, float(negative_slope), bias, False)
+        out, _ = cover.forward_device(xw_own.contiguous(), att_c, H, C, float(negative_slope), bias, False, drop=drop)
         return out
-    return _GatCoverFn.apply(xw_own, att, bias, cover, H, C, float(negative_slope))
+    return _GatCoverFn.apply(xw_own, att, bias, cover, H, C, float(negative_slope), drop)

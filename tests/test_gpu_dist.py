@@ -29,21 +29,23 @@ def _free_port():
 
 def _fused_forms_equal(ov, x_own, out_ref, bias, F):
     """step_fused over every (tile width, boundary in one launch / per tile,
-    interior after / beside the packing) form: bitwise out_ref (step()'s
-    output).  Returns the list of forms that differ (empty: all equal)."""
+    interior after / beside the packing, send rows packed in one launch / per
+    tile) form: bitwise out_ref (step()'s output).  Returns the list of forms
+    that differ (empty: all equal)."""
     bad = []
     for width in (64, 128, 256):
         bufs = ov.halo_buffers(F, width)
         for one in (True, False):
             for split in (False, True):
-                ov.one_boundary_launch, ov.split_interior = one, split
-                for _ in range(2):   # twice: the result never depends on the buffers' last contents
-                    o = torch.full_like(out_ref, float("nan"))
-                    ov.step_fused(x_own, bufs, o, bias)
-                    if not torch.equal(o, out_ref):
-                        bad.append((width, one, split))
-                        break
-    ov.one_boundary_launch, ov.split_interior = True, False
+                for ppt in ((False, True) if width < F else (False,)):
+                    ov.one_boundary_launch, ov.split_interior, ov.pack_per_tile = one, split, ppt
+                    for _ in range(2):   # twice: the result never depends on the buffers' last contents
+                        o = torch.full_like(out_ref, float("nan"))
+                        ov.step_fused(x_own, bufs, o, bias)
+                        if not torch.equal(o, out_ref):
+                            bad.append((width, one, split, ppt))
+                            break
+    ov.one_boundary_launch, ov.split_interior, ov.pack_per_tile = True, False, False
     return bad
 
 
@@ -490,52 +492,62 @@ def _gat_dropout_worker(rank, world, port, q, cut_sets):
         from mi355_mp.graphgen import powerlaw_edge_index
         from torch_geometric.nn import GATConv
         dev = torch.device("cuda", 0)
-        N, Fi, H, C, p = 1500, 24, 4, 16, 0.3
+        N, Fi, p = 1500, 24, 0.3
         ei = powerlaw_edge_index(N, 20000, seed=73).to(dev)
         gen = torch.Generator().manual_seed(73)
         x = _dyadic_(torch.empty(N, Fi), gen, 4.0).to(dev)
-        gout = torch.randn(N, H * C, generator=gen).to(dev)
         res = {}
-        for ci, cuts in enumerate(cut_sets):
-            ref = GATConv(Fi, C, heads=H, dropout=p).to(dev).train()
-            _dyadic_(ref.weight, gen, 16.0)
-            with torch.no_grad():
-                ref.att.copy_(torch.randn(ref.att.shape, generator=gen) * 0.3)
-                ref.bias.copy_(torch.randn(ref.bias.shape, generator=gen))
-            xr = x.clone().requires_grad_(True)
-            torch.manual_seed(11 + ci)                 # the dropout key both layers draw
-            out_ref = ref(xr, ei)
-            (out_ref * gout).sum().backward()
-            if cuts is None:
-                E = ei.shape[1]
-                s0, s1 = rank * E // world, (rank + 1) * E // world
-                sg = mdist.ShardedGraph.for_gat_from_slices(ei[:, s0:s1].clone(), s0, N, rank, world)
-            else:
-                sg = mdist.ShardedGraph.for_gat(ei, N, rank, world, cuts=cuts)
-            conv = mdist.ShardedGATConv(Fi, C, heads=H, dropout=p).to(dev).train()
-            conv.load_state_dict(ref.state_dict())
-            lo, hi = sg.lo, sg.hi
-            xo = x[lo:hi].clone().requires_grad_(True)
-            torch.manual_seed(11 + ci)
-            out = conv(xo, sg)
-            (out * gout[lo:hi]).sum().backward()
-            mdist.allreduce_gradients(conv)
-            o, w = out.detach(), out_ref.detach()[lo:hi]
-            r = {"rows": hi - lo,
-                 "out": float(((o - w).abs() - 1e-5 * w.abs().clamp(min=1.0)).max()) if hi > lo else -1.0,
-                 "gx": float((xo.grad - xr.grad[lo:hi]).abs().max() / xr.grad.abs().max()) if hi > lo else 0.0}
-            for k in ("weight", "att", "bias"):
-                a, b = getattr(conv, k).grad, getattr(ref, k).grad
-                r["g" + k] = float((a - b).abs().max() / b.abs().max())
-            # the rank's keep mask IS the single-GPU mask on its edges (global edge ids)
-            from mi355_mp.graph import GAT_TARGET_TASKS, Graph
-            from torch_geometric.nn.conv._structure import gat_loops
-            g1 = Graph(gat_loops(ei, N), N, N, target_tasks=GAT_TARGET_TASKS)
-            k1 = ops.gat_dropout_keep(g1, 99, p, H)
-            kr = ops.gat_dropout_keep(sg.g_fwd, 99, p, H)
-            r["mask_equal"] = bool(torch.equal(kr, k1[sg.fwd.edge_gid]))
-            r["dropped_frac"] = float(1.0 - kr.float().mean()) if kr.numel() else p
-            res[ci] = r
+        # heads 4 x 16 (the fused transposed pass) and 2 x 24 (the wide kernels), over
+        # the pull exchange and over the hybrid cover
+        for H, C in ((4, 16), (2, 24)):
+            gout = torch.randn(N, H * C, generator=gen).to(dev)
+            for ci, cuts in enumerate(cut_sets):
+                for cover in (False, True):
+                    ref = GATConv(Fi, C, heads=H, dropout=p).to(dev).train()
+                    _dyadic_(ref.weight, gen, 16.0)
+                    with torch.no_grad():
+                        ref.att.copy_(torch.randn(ref.att.shape, generator=gen) * 0.3)
+                        ref.bias.copy_(torch.randn(ref.bias.shape, generator=gen))
+                    xr = x.clone().requires_grad_(True)
+                    torch.manual_seed(11 + ci)                 # the dropout key both layers draw
+                    out_ref = ref(xr, ei)
+                    (out_ref * gout).sum().backward()
+                    if cuts is None:
+                        E = ei.shape[1]
+                        s0, s1 = rank * E // world, (rank + 1) * E // world
+                        sg = mdist.ShardedGraph.for_gat_from_slices(ei[:, s0:s1].clone(), s0, N, rank, world)
+                    else:
+                        sg = mdist.ShardedGraph.for_gat(ei, N, rank, world, cuts=cuts)
+                    if cover:
+                        sg.enable_gat_halo_cover()
+                    conv = mdist.ShardedGATConv(Fi, C, heads=H, dropout=p).to(dev).train()
+                    conv.load_state_dict(ref.state_dict())
+                    lo, hi = sg.lo, sg.hi
+                    xo = x[lo:hi].clone().requires_grad_(True)
+                    torch.manual_seed(11 + ci)
+                    out = conv(xo, sg)
+                    (out * gout[lo:hi]).sum().backward()
+                    mdist.allreduce_gradients(conv)
+                    o, w = out.detach(), out_ref.detach()[lo:hi]
+                    r = {"rows": hi - lo,
+                         "out": float(((o - w).abs() - 1e-5 * w.abs().clamp(min=1.0)).max()) if hi > lo else -1.0,
+                         "gx": float((xo.grad - xr.grad[lo:hi]).abs().max() / xr.grad.abs().max()) if hi > lo else 0.0}
+                    for k in ("weight", "att", "bias"):
+                        a, b = getattr(conv, k).grad, getattr(ref, k).grad
+                        r["g" + k] = float((a - b).abs().max() / b.abs().max())
+                    if cover:
+                        st = sg.gat_cover.stats()
+                        r["cover_rows"], r["pull_rows"] = st["halo_rows"], st["pull_halo_rows"]
+                    else:
+                        # the rank's keep mask IS the single-GPU mask on its edges (global edge ids)
+                        from mi355_mp.graph import GAT_TARGET_TASKS, Graph
+                        from torch_geometric.nn.conv._structure import gat_loops
+                        g1 = Graph(gat_loops(ei, N), N, N, target_tasks=GAT_TARGET_TASKS)
+                        k1 = ops.gat_dropout_keep(g1, 99, p, H)
+                        kr = ops.gat_dropout_keep(sg.g_fwd, 99, p, H)
+                        r["mask_equal"] = bool(torch.equal(kr, k1[sg.fwd.edge_gid]))
+                        r["dropped_frac"] = float(1.0 - kr.float().mean()) if kr.numel() else p
+                    res["%dx%d cuts %d %s" % (H, C, ci, "cover" if cover else "pull")] = r
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -548,18 +560,26 @@ def test_sharded_gatconv_attention_dropout_matches_one_gpu(world):
     keyed on the GLOBAL edge id (ABI 7 drop_ids), so every rank drops exactly
     the single-GPU layer's (edge, head) pairs -- its keep mask equals the
     single-GPU mask on its edges, and the forward rows, d x and the all-reduced
-    d W / d att / d b agree within the bound.  Slice-built shards, edge-balanced
-    cuts, and a rank that owns no rows."""
+    d W / d att / d b agree within the bound, over the pull exchange AND over
+    the hybrid halo cover (pieces with the dropped weights, keys sent with the
+    push edges), fused (4 x 16) and wide (2 x 24) heads.  Slice-built shards,
+    edge-balanced cuts, and a rank that owns no rows."""
     N = 1500
     cut_sets = [None, [0, N // 3, N] if world == 2 else [0, N // 3, 2 * N // 3, N],
                 [0, N, N] if world == 2 else [0, 0, N // 2, N]]
     res = _spawn(_gat_dropout_worker, world=world, args=(cut_sets,))
+    covered = 0
     for rank, r in res:
-        for ci, v in r.items():
-            assert v["mask_equal"], (rank, ci, v)
-            assert v["out"] <= 0 and v["gx"] < 1e-5, (rank, ci, v)
-            assert v["gweight"] < 1e-5 and v["gatt"] < 1e-5 and v["gbias"] < 1e-5, (rank, ci, v)
-            assert abs(v["dropped_frac"] - 0.3) < 0.05, (rank, ci, v)
+        for key, v in r.items():
+            if "mask_equal" in v:
+                assert v["mask_equal"], (rank, key, v)
+                assert abs(v["dropped_frac"] - 0.3) < 0.05, (rank, key, v)
+            assert v["out"] <= 0 and v["gx"] < 1e-5, (rank, key, v)
+            assert v["gweight"] < 1e-5 and v["gatt"] < 1e-5 and v["gbias"] < 1e-5, (rank, key, v)
+            if "cover_rows" in v:
+                assert v["cover_rows"] <= v["pull_rows"], (rank, key, v)
+                covered += v["pull_rows"] > 0
+    assert covered > 0
 
 def _products_worker(rank, world, port, q):
     import sys
@@ -894,8 +914,8 @@ def test_bench_multi_rank_path_end_to_end():
     # the warm-up times every fused step form (max over ranks) and keeps the fastest
     import bench
     tune = ex["halo_tile_autotune_ms"]
-    forms = {bench.form_name(w, one, sp) for (w, one) in bench.HALO_FORMS for sp in (False, True)}
-    assert set(tune) == forms and len(forms) == 8
+    forms = {bench.form_name(w, one, sp, ppt) for (w, one, ppt) in bench.HALO_FORMS for sp in (False, True)}
+    assert set(tune) == forms and len(forms) == 2 * len(bench.HALO_FORMS)
     assert all(v > 0 for v in tune.values())
     best = min(tune, key=tune.get)    # tile width, boundary in one launch or per tile, interior beside the packing
     assert ex["step_form"].endswith(best), (ex["step_form"], best)

@@ -27,7 +27,7 @@ def load(name):
 
 
 def main():
-    rnd = sys.argv[1] if len(sys.argv) > 1 else "r04"
+    rnd = sys.argv[1] if len(sys.argv) > 1 else "r06"
     out = {}
     for wl, f in (("c2", "bench_rmat21"), ("c5", "bench_products_n1"), ("c3", "bench_gat_n1"),
                   ("c5_gloo2", "bench_products_gloo2")):
@@ -55,31 +55,45 @@ def main():
         if "repeated_layer_first_occurrences" in d:
             out["cfg_" + k]["first_occurrences"] = d["repeated_layer_first_occurrences"]
     # the predicted multi-GPU curve from the rehearsals' per-rank compute
-    # (GPU to itself), the one-GPU RCCL contention and the link model at 77 GB/s
-    one = load("%s_bench_rmat21.json" % rnd)
+    # (GPU to itself), the one-GPU RCCL contention and the link model at 77 GB/s:
+    # per rank the bench's link_model.predicted_in_turn["77"] = max(compute in turn
+    # of the chosen form, pack(first) + exchange + boundary(last)), max over ranks,
+    # + the contention; config 2 (rmat21) and config 5 (products)
     rc = load("%s_bench_sharded_rccl_one_rank.json" % rnd)
     cont = {}
     if rc:
         for r in rc["extra"]["per_rank"][0].get("rccl_contention", []):
             cont[r["P"]] = r["contention_ms"]
-    for P in (2, 4, 8):
-        d = load("%s_bench_rmat21_gloo%d_rehearsal.json" % (rnd, P))
-        if not d or "compute_in_turn" not in d["extra"]["per_rank"][0]:
-            continue
-        T = len(d["extra"]["halo_tiles"])
-        rows = []
-        for p in d["extra"]["per_rank"]:
-            c, lm = p["compute_in_turn"], p["link_model"]
-            chain = (c["send_pack_ms"] / T + lm["max_peer_bytes"] / 77e9 * 1e3 + c["boundary_ms"] / T)
-            rows.append((c["compute_alone_ms"], c["compute_alone_split_ms"], chain))
-        serial, split = max(r[0] for r in rows), max(r[1] for r in rows)
-        chain = max(r[2] for r in rows)
-        comp = min(serial, split) + cont.get(P, 0.0)
-        step = max(comp, chain)
-        out["curve_P%d" % P] = {"compute_in_turn_ms": serial, "compute_split_ms": split,
-                                "contention_ms": cont.get(P), "compute_plus_contention_ms": comp,
-                                "link_chain_77_ms": chain, "predicted_step_ms": step,
-                                "speedup_vs_1gpu": (one["ms_per_step"] / step) if one else None}
+    for wl, one_name, pre in (("c2", "bench_rmat21", "bench_rmat21_gloo"),
+                              ("c5", "bench_products_n1", "bench_products_gloo")):
+        one = load("%s_%s.json" % (rnd, one_name)) or load("r05_%s.json" % one_name)
+        for P in (2, 4, 8):
+            d = load("%s_%s%d_rehearsal.json" % (rnd, pre, P))
+            if not d or "compute_in_turn" not in d["extra"]["per_rank"][0]:
+                continue
+            ranks = d["extra"]["per_rank"]
+            slow = max(ranks, key=lambda p: p["compute_in_turn"]["compute_alone_ms"])
+            c = slow["compute_in_turn"]
+            pred = max(p["link_model"]["predicted_in_turn"]["77"] for p in ranks)
+            form = d["extra"].get("step_form") or ""
+            T = len(d["extra"]["halo_tiles"])
+            tp = T if "packed per tile" in form else 1
+            tb = 1 if "boundary in one launch" in form else T
+            chain = max(p["compute_in_turn"]["send_pack_ms"] / tp + p["link_model"]["max_peer_bytes"] / 77e9 * 1e3
+                        + p["compute_in_turn"]["boundary_ms"] / tb for p in ranks)
+            step = pred + cont.get(P, 0.0)
+            out["curve_%s_P%d" % (wl, P)] = {
+                "step_form": d["extra"].get("step_form"),
+                "compute_in_turn_slowest_ms": c["compute_alone_ms"],
+                "slowest_parts_ms": [c["send_pack_ms"], c["interior_ms"], c["boundary_ms"]],
+                "compute_split_slowest_ms": max(p["compute_in_turn"]["compute_alone_split_ms"] for p in ranks),
+                "link_chain_77_ms": chain, "predicted_in_turn_77_ms": pred,
+                "contention_ms": cont.get(P), "predicted_step_ms": step,
+                "one_gpu_ms": one["ms_per_step"] if one else None,
+                "ideal_split_ms": one["ms_per_step"] / P if one else None,
+                "speedup_vs_1gpu": (one["ms_per_step"] / step) if one else None,
+                "verify": (d["extra"].get("verify") or {}).get("all_ranks_within_1e-5_bound"),
+                "build_s": d["extra"].get("one_time_build_s")}
     print(json.dumps(out, indent=1))
 
 
