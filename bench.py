@@ -71,6 +71,7 @@ F_DIM = 256
 # boundary pass runs per tile as it arrives pipeline the link-bound P = 2 chain
 # pack + exchange + boundary_last
 # (tile width, boundary in one launch, send rows packed per tile)
+GAT_DROP_SEED = 1234          # --gat-dropout's key
 HALO_FORMS = ((256, True, False), (128, True, False), (128, False, False), (64, False, False),
               (128, True, True), (128, False, True), (64, False, True))
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md chip table)
@@ -154,6 +155,8 @@ def parse(argv=None):
                          "by timing each on this job's links (max over ranks)")
     ap.add_argument("--boundary-per-tile", action="store_true",
                     help="with --halo-tile W: the boundary pass per tile as its halo arrives")
+    ap.add_argument("--gat-dropout", type=float, default=0.0,
+                    help="--workload gat: GATConv's training-mode attention dropout p in every step")
     ap.add_argument("--pack-per-tile", action="store_true",
                     help="with --halo-tile W: the send rows packed per tile, each tile's exchange started "
                          "right after its packing")
@@ -542,6 +545,9 @@ def main_gat(args, rank, world, local):
     dev = torch.device("cuda", local)
     N, H, C = wl["num_nodes"], 8, 32
     F = H * C
+    # --gat-dropout p: GATConv's training-mode attention dropout in every step (one
+    # fixed key, so --verify can apply the same keep mask in float64)
+    drop_p = float(args.gat_dropout)
     t0 = time.perf_counter()
     ei = wl["gen"](dev)
     g = torch.Generator(device=dev).manual_seed(wl["seed"])
@@ -562,7 +568,7 @@ def main_gat(args, rank, world, local):
         n_rows, n_src = N, N
 
         def step():
-            return ops.gat_propagate(graph, ei2, xw, att, H, C, 0.2, bias)[0]
+            return ops.gat_propagate(graph, ei2, xw, att, H, C, 0.2, bias, dropout=drop_p, seed=GAT_DROP_SEED)[0]
     else:
         from mi355_mp import dist as mdist
         E_raw = ei.shape[1]
@@ -588,7 +594,7 @@ def main_gat(args, rank, world, local):
                                                                   cover_stats["cover_partial_rows"])))
 
         def step():
-            return sg.gat_propagate(xw, att, H, C, 0.2, bias)[0]
+            return sg.gat_propagate(xw, att, H, C, 0.2, bias, dropout=drop_p, seed=GAT_DROP_SEED)[0]
     del xw_full
     torch.cuda.synchronize()
     t_build = time.perf_counter() - t0
@@ -648,6 +654,10 @@ def main_gat(args, rank, world, local):
             a_dst = (x3 * att[:, :, :C].double()).sum(-1)
             a_src = (x3 * att[:, :, C:].double()).sum(-1)
             del x3
+            keep = None
+            if drop_p > 0:       # the kernels' keep mask of these edges (global edge ids on a shard)
+                keep = ops.gat_dropout_keep(sg.g_fwd if sharded else graph, GAT_DROP_SEED, drop_p, H).double() \
+                    / (1.0 - drop_p)
             m = torch.full((n_rows, H), float("-inf"), device=dev, dtype=torch.float64)
             den = torch.zeros(n_rows, H, device=dev, dtype=torch.float64)
             ref = torch.zeros(n_rows, H, C, device=dev, dtype=torch.float64)
@@ -663,6 +673,8 @@ def main_gat(args, rank, world, local):
                         den.index_add_(0, dst[sl], torch.exp(sc - m[dst[sl]]))
                     else:
                         a = torch.exp(sc - m[dst[sl]]) / (den[dst[sl]] + 1e-16)
+                        if keep is not None:
+                            a = a * keep[sl]
                         msg = a.unsqueeze(-1) * xs.view(-1, H, C)[src[sl]].double()
                         ref.index_add_(0, dst[sl], msg)
                         terms.index_add_(0, dst[sl], msg.abs())
@@ -714,6 +726,7 @@ def main_gat(args, rank, world, local):
             "data": "synthetic rmat21 graph (seeded, generated on device), random X W / att / bias",
             "config": {"workload": wl["name"], "baseline_config": wl["baseline_config"], "graph": wl["graph"],
                        "num_nodes": N, "num_edges": E2, "heads": H, "out_channels": C, "seed": wl["seed"],
+                       "attention_dropout": drop_p,
                        "parallelism": ("dst-range shards x%d, RCCL halo all_to_all (%s)"
                                        % (world, "pull" if args.no_halo_cover else "hybrid cover")) if sharded
                        else "single GPU"},

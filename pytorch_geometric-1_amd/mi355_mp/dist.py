@@ -1714,7 +1714,7 @@ class ShardedGraph:
         return self
 
     def gat_propagate(self, xw_own, att, heads, out_channels, negative_slope=0.2, bias=None,
-                      return_alpha=False, dropout=0.0, local_gat=None):
+                      return_alpha=False, dropout=0.0, local_gat=None, seed=None):
         """Sharded fused GATConv aggregation (GATConv.message + utils.softmax +
         scatter_add + update, [U3, U6]): this rank's rows [n_own, H*C] (+ bias).
 
@@ -1731,7 +1731,8 @@ class ShardedGraph:
         layer's mask (over the cover too).
         local_gat(graph, edge_index, xw_local, att, H, C, slope, bias,
         return_alpha, dropout) -> (out, alpha): default the HIP path
-        (ops.gat_propagate); the gloo CPU tests pass the oracle."""
+        (ops.gat_propagate); the gloo CPU tests pass the oracle.  seed: the
+        dropout key (default: drawn from the device's generator)."""
         from .gat_cover import cover_ok
         gc = getattr(self, "gat_cover", None)
         if gc is not None and not return_alpha and local_gat is None:
@@ -1740,10 +1741,14 @@ class ShardedGraph:
                     return _host("gat_cover_forward")(gc, xw_own, att, heads, out_channels, negative_slope, bias), None
             elif cover_ok(heads, out_channels):
                 from .gat_cover import gat_cover_propagate
-                return gat_cover_propagate(gc, xw_own, att, heads, out_channels, negative_slope, bias, dropout), None
+                return gat_cover_propagate(gc, xw_own, att, heads, out_channels, negative_slope, bias, dropout,
+                                           seed), None
         if local_gat is None:
             from . import ops
             local_gat = ops.gat_propagate
+            if seed is not None:
+                def local_gat(*a, _seed=seed):
+                    return ops.gat_propagate(*a, seed=_seed)
         xw_local = halo_rows(xw_own, self.fwd, self.group)
         out, alpha = local_gat(self.g_fwd, self.fwd.local_edge_index, xw_local, att, heads, out_channels,
                                negative_slope, bias, return_alpha, dropout)

@@ -17,6 +17,7 @@
 #             GPU's queue slots and stretch a 1 s build to 60 s
 #   products_gloo4 / products_gloo8  config 5 (--workload products) as 4 / 8 gloo ranks sharing the GPU (--verify)
 #   gat_gloo2 the same for --workload gat                -> $R_bench_gat_gloo2_rehearsal.json
+#   gat_drop_gloo2  the same with attention dropout 0.3 over the cover (--verify with the keep mask)
 #   prof      tools/profile.sh (kernel trace + PMC of the default bench); prof_gat / prof_products /
 #             prof_reddit the same for the other bench workloads (summarise with tools/pmc_summary.py)
 #   diag      tools/gat_shard_diag.py (sharded vs single-GPU vs float64 GAT gradients, per seed)
@@ -51,6 +52,7 @@ for s in ${STEPS:-tests bench}; do
     products_gloo4) run products_gloo4 1100 bash -c "GPU_MAX_HW_QUEUES=1 MP_BENCH_BACKEND=gloo python bench.py --workload products --gpus 4 --steps 3 --warmup 1 --verify > $O/${R}_bench_products_gloo4_rehearsal.json 2> $O/${R}_bench_products_gloo4_rehearsal.err"; cut -c1-300 $O/${R}_bench_products_gloo4_rehearsal.json ;;
     products_gloo8) run products_gloo8 1150 bash -c "GPU_MAX_HW_QUEUES=1 MP_BENCH_BACKEND=gloo python bench.py --workload products --gpus 8 --steps 3 --warmup 1 --verify > $O/${R}_bench_products_gloo8_rehearsal.json 2> $O/${R}_bench_products_gloo8_rehearsal.err"; cut -c1-300 $O/${R}_bench_products_gloo8_rehearsal.json ;;
     gat_gloo2) run gat_gloo2 600 bash -c "MP_BENCH_BACKEND=gloo python bench.py --gpus 2 --workload gat --steps 3 --warmup 1 --verify > $O/${R}_bench_gat_gloo2_rehearsal.json 2> $O/${R}_bench_gat_gloo2_rehearsal.err"; cut -c1-300 $O/${R}_bench_gat_gloo2_rehearsal.json ;;
+    gat_drop_gloo2) run gat_drop_gloo2 600 bash -c "MP_BENCH_BACKEND=gloo python bench.py --gpus 2 --workload gat --gat-dropout 0.3 --steps 3 --warmup 1 --verify > $O/${R}_bench_gat_dropout_gloo2_rehearsal.json 2> $O/${R}_bench_gat_dropout_gloo2_rehearsal.err"; cut -c1-300 $O/${R}_bench_gat_dropout_gloo2_rehearsal.json ;;
     diag) run diag 500 bash -c "python tools/gat_shard_diag.py > $O/${R}_gat_shard_diag.jsonl 2> $O/${R}_gat_shard_diag.err"; cat $O/${R}_gat_shard_diag.jsonl ;;
     prof) PROF_OUT=$O/${R}_prof run prof 1100 bash tools/profile.sh ;;
     prof_gat) PROF_OUT=$O/${R}_prof_gat NO_CALIB=1 BENCH_ARGS="--workload gat" run prof_gat 1100 bash tools/profile.sh ;;
