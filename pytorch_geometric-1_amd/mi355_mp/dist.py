@@ -1915,37 +1915,48 @@ def broadcast_parameters(module, src=0, group=None):
 
 def allreduce_gradients(module, group=None):
     """Sum the gradients of replicated parameters over the ranks (each rank's
-    weight gradient covers its own rows only), as DDP would.  The ranks first
-    sum one has-grad flag per parameter (one collective); every parameter some
-    rank has a gradient for then takes part on every rank, in the same order: a
-    rank whose rows never reached it (e.g. a rank that owns no rows, whose
-    empty output does not involve GATConv's att) contributes zeros -- skipping
-    it there would pair different tensors in the collectives of different
-    ranks.  A parameter no rank has a gradient for keeps grad None on every
-    rank (an optimizer with momentum or weight decay leaves it alone, as it
-    does on one GPU)."""
+    weight gradient covers its own rows only), as DDP would, in ONE bucketed
+    all_reduce: [one has-grad flag per parameter ; every gradient flattened].
+    A parameter some rank has no gradient for contributes zeros there (e.g. a
+    rank that owns no rows, whose empty output does not involve GATConv's
+    att), so every rank reduces the same bucket; a parameter NO rank has a
+    gradient for keeps grad None on every rank (an optimizer with momentum or
+    weight decay leaves it alone, as on one GPU) -- only a rank that lacks a
+    gradient reads the summed flags back (the host waits for the reduction
+    there and nowhere else; with every gradient present nothing syncs)."""
     params = [p for p in module.parameters() if p.requires_grad]
     if not params:
         return
-    # one has-grad flag per parameter, summed over the ranks in one collective:
-    # a parameter no rank formed a gradient for keeps grad None everywhere (an
-    # optimizer with momentum / weight decay then leaves it alone, as on one GPU)
     gloo = dist.get_backend(group) == "gloo"
     dev = params[0].device
-    flags = torch.tensor([p.grad is not None for p in params], dtype=torch.int32,
-                         device="cpu" if gloo else dev)
-    dist.all_reduce(flags, group=group)
-    for p, f in zip(params, flags.tolist()):
-        if f == 0:
-            continue
+    dtype = params[0].dtype
+    if any(p.dtype != dtype or p.device != dev for p in params):
+        raise ValueError("mi355_mp.dist.allreduce_gradients: replicated parameters of one dtype and device")
+    have = [p.grad is not None for p in params]
+    # flags built on the device (fills, no host-to-device copy)
+    parts = [torch.full((1,), 1.0 if h else 0.0, dtype=dtype, device=dev) for h in have]
+    parts += [(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in params]
+    flat = torch.cat(parts)
+    if flat.is_cuda and gloo:
+        t = _stage_to_host(flat)
+        dist.all_reduce(t, group=group)
+        flat.copy_(t)
+    else:
+        dist.all_reduce(flat, group=group)
+    k = len(params)
+    flags = flat[:k].tolist() if not all(have) else None
+    o = k
+    for i, p in enumerate(params):
+        n = p.numel()
+        if flags is not None and flags[i] == 0:
+            o += n
+            continue                           # no rank formed it: None everywhere
+        g = flat[o:o + n].view_as(p)
         if p.grad is None:
-            p.grad = torch.zeros_like(p)
-        if p.grad.is_cuda and gloo:
-            t = p.grad.cpu()
-            dist.all_reduce(t, group=group)
-            p.grad.copy_(t)
+            p.grad = g.clone()
         else:
-            dist.all_reduce(p.grad, group=group)
+            p.grad.copy_(g)
+        o += n
 
 
 class ShardedGCNConv(torch.nn.Module):

@@ -702,6 +702,60 @@ def test_gat_backward_matches_float64_autograd(H=4, C=8):
         assert torch.allclose(got.cpu().double(), want, rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("scale", [1e2, 1e4])
+def test_gat_backward_large_bias_precision(scale, capsys):
+    """the fused backward prologue forms rs_i = <g_i, out_i - bias>
+    from the saved output (no pre-bias copy).  With |bias| >> |agg| the fp32
+    output out = fl(agg + bias) holds agg only to ulp(|out|), so rs carries an
+    absolute error up to e_rs = C max|g| ulp(max|out|) per head (out - bias is
+    exact by Sterbenz there; the loss is in out itself), and the terms through
+    rs inherit it: d score = lk alpha (<g, xw_j> - rs_i), summed over a
+    source's out-edges (total attention a_in = max_j sum_i alpha_ij) and, for
+    d a_dst_i, over a row's in-edges (sum alpha = 1).  Per entry of d xw:
+    delta = e_rs (a_in + 1) max(1, max|att|); then d x <= H C max|W| delta,
+    d W <= N max|x| delta, d att <= N max|xw| e_rs (a_in + 1), d b none.
+    Checked: |got - want| <= 1e-4 max(1, |want|) + 2 x that bound."""
+    from torch_geometric.nn import GATConv
+    _, _, _, _, pl = _mods()
+    N, E, Fi, H, C = 300, 4000, 10, 4, 8
+    ei = pl(N, E, seed=15)
+    g = torch.Generator().manual_seed(15)
+    x = torch.randn(N, Fi, generator=g)
+    conv = GATConv(Fi, C, heads=H).to(DEV)
+    with torch.no_grad():
+        conv.bias.copy_(torch.randn(H * C, generator=g) * scale)
+    xd = x.to(DEV).requires_grad_(True)
+    gout = torch.randn(N, H * C, generator=g)
+    out = conv(xd, ei.to(DEV))
+    out.backward(gout.to(DEV))
+    W = conv.weight.detach().cpu().double().requires_grad_(True)
+    att = conv.att.detach().cpu().double().requires_grad_(True)
+    b = conv.bias.detach().cpu().double().requires_grad_(True)
+    x64 = x.double().requires_grad_(True)
+    out64, ei_l, alpha = P.gat_conv(x64, ei, W, att, b, H, C, return_alpha=True)
+    out64.backward(gout.double())
+    # the largest total attention a source receives (float64, over the layer's edges)
+    src = ei_l[0]
+    alpha = alpha.detach()
+    a = att.detach().view(H, 2 * C)
+    a_in = float(torch.zeros(N, H, dtype=torch.float64).index_add_(0, src, alpha).max())
+    ulp = float(torch.finfo(torch.float32).eps) * 2.0 ** float(torch.log2(out.detach().abs().max().cpu().double()).floor())
+    e_rs = C * float(gout.abs().max()) * ulp
+    delta = e_rs * (a_in + 1) * max(1.0, float(a.abs().max()))
+    xw_max = float((x.double() @ W.detach()).abs().max())
+    bound = {"x": H * C * float(W.detach().abs().max()) * delta, "W": N * float(x.abs().max()) * delta,
+             "att": N * xw_max * e_rs * (a_in + 1), "b": 0.0}
+    worst = {}
+    for name, got, want in (("x", xd.grad, x64.grad), ("W", conv.weight.grad, W.grad), ("att", conv.att.grad, att.grad),
+                            ("b", conv.bias.grad, b.grad)):
+        err = (got.cpu().double() - want).abs()
+        tol = 1e-4 * want.abs().clamp(min=1.0) + 2 * bound[name]
+        worst[name] = (float(err.max()), 2 * bound[name])
+        assert (err <= tol).all(), (name, worst[name], e_rs, a_in)
+    with capsys.disabled():
+        print("large bias x%g: e_rs %.3g, a_in %.3g, (max err, rs bound) per gradient %s" % (scale, e_rs, a_in, worst))
+
+
 def test_graphconv_max_and_edgeconv_generic_path():
     from torch_geometric.nn import GraphConv, MessagePassing
     _, _, _, _, pl = _mods()
