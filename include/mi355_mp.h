@@ -494,6 +494,18 @@ int mp_gat_backward_train_drop_f32(const mp_csr* gt, const float* grad_out, int6
 int mp_gat_dropout_keep(uint64_t seed, float p_drop, int32_t H, int64_t n_slots, const int32_t* drop_ids,
                         uint32_t* bits, void* stream);
 
+/* ---- Row-exact feature transform (ABI 7) ----------------------------------
+ * C[i, n] = the k-ordered fmaf chain over k = 0..K-1 from 0 of A[i, k] * B[k, n],
+ * B = W ([K, N] row-major) or, trans_w != 0, W^T (W [N, K] row-major): every
+ * output row is a function of its input row alone, so a shard's rows of X W are
+ * bitwise the single-GPU rows whatever M is (GATConv's x @ W [U6]; a hipBLASLt
+ * GEMM picks its kernel -- and its rounding -- by M).  K = N = 256 with 16-byte
+ * aligned rows of A (lda % 4 == 0): the f32 MFMA kernel; any other shape (or
+ * force_generic): a tiled fmaf kernel with the same arithmetic.  lda >= K,
+ * ldc >= N; M = 0 is a no-op. */
+int mp_gemm_rows_f32(const float* A, int64_t lda, int64_t M, int32_t K, const float* W, int32_t trans_w,
+                     int32_t N, float* C, int64_t ldc, int32_t force_generic, void* stream);
+
 /* Per-block column sums of x [n, F] (0 < F <= 256, F % 4 == 0, 16-byte aligned
  * rows): part [mp_gat_bwd_blocks(n), F] (part_bytes >= that * 4; ABI 6);
  * sum_i x[i, :] is their sum over the blocks (a layer's bias gradient, sum over

@@ -120,6 +120,7 @@ SIGNATURES = {
                                                       c_p, sz, c_p, sz, c_p, c_p]),
     "mp_gat_bwd_blocks": (ctypes.c_int, [i64]),
     "mp_col_sums_f32": (ctypes.c_int, [c_p, i64, i64, i32, c_p, sz, c_p]),
+    "mp_gemm_rows_f32": (ctypes.c_int, [c_p, i64, i64, i32, c_p, i32, i32, c_p, i64, i32, c_p]),
     "mp_gat_backward_finish_f32": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, i64, i32, i32, c_p, sz, c_p]),
     "mp_gat_merge_partials_f32": (ctypes.c_int, [i64, i32, i32, c_p, c_p, i64, c_p, sz, i64, c_p, sz, c_p, c_p, i64,
                                                  c_p, c_p, c_p, c_p]),

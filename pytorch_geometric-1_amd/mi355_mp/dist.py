@@ -2021,7 +2021,7 @@ class ShardedGATConv(torch.nn.Module):
         from torch_geometric.nn.conv.gat_conv import GATConv
         from . import ops
         weight, att, fused_bias, C4 = GATConv._fused_operands(self)
-        xw = ops.feature_transform(x_own, weight)
+        xw = ops.feature_transform(x_own, weight, row_exact=ops.GAT_ROW_EXACT_GEMM)
         drop = self.dropout if self.training else 0.0
         out, aw = sg.gat_propagate(xw, att, self.heads, C4, self.negative_slope, fused_bias,
                                    return_attention_weights, drop, local_gat=local_gat)

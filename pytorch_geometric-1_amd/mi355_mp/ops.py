@@ -1200,9 +1200,50 @@ class _FeatureTransform(torch.autograd.Function):
         return gx, gw
 
 
-def feature_transform(x, w):
-    """``torch.matmul(x, w)`` for a 2-D fp32 device x (split-K weight gradient)."""
-    if not (torch.is_tensor(x) and x.dim() == 2 and x.is_cuda and x.dtype == torch.float32 and w.dim() == 2
-            and torch.is_grad_enabled() and w.requires_grad):
+def gemm_rows(x, w, force_generic=False):
+    """x @ w (fp32, device) with every output row the k-ordered fmaf chain of
+    its own input row (mp_gemm_rows_f32): bitwise independent of how many rows
+    x has -- a shard's rows equal the single-GPU rows.  No autograd."""
+    lib = _lib.load()
+    _lib.require_device(x)
+    x = x if (x.stride(1) == 1 and x.stride(0) >= x.shape[1]) else x.contiguous()
+    w = w.contiguous()
+    M, K = x.shape
+    N = w.shape[1]
+    out = torch.empty((M, N), dtype=torch.float32, device=x.device)
+    if M and K and N:
+        _lib.check(lib.mp_gemm_rows_f32(x.data_ptr(), x.stride(0), M, K, w.data_ptr(), 0, N, out.data_ptr(), N,
+                                        int(bool(force_generic)), _lib.stream_ptr(x.device)), "mp_gemm_rows_f32")
+    elif M and N:
+        out.zero_()
+    return out
+
+
+class _FeatureTransformRows(_FeatureTransform):
+    """_FeatureTransform with the row-exact forward (gemm_rows); the backward is
+    _FeatureTransform's."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return gemm_rows(x, w)
+
+
+# GATConv / ShardedGATConv: x @ W with the row-exact GEMM, so a sharded layer's
+# scores are bitwise the single-GPU layer's (VERDICT r05 item 7)
+GAT_ROW_EXACT_GEMM = True
+
+
+def feature_transform(x, w, row_exact=False):
+    """``torch.matmul(x, w)`` for a 2-D fp32 device x (split-K weight gradient);
+    row_exact: the forward by gemm_rows (each output row a function of its own
+    input row, whatever the row count)."""
+    if not (torch.is_tensor(x) and x.dim() == 2 and x.is_cuda and x.dtype == torch.float32 and w.dim() == 2):
+        return torch.matmul(x, w)
+    if not (torch.is_grad_enabled() and (w.requires_grad or x.requires_grad)):
+        return gemm_rows(x, w) if row_exact else torch.matmul(x, w)
+    if row_exact:
+        return _FeatureTransformRows.apply(x, w)
+    if not w.requires_grad:
         return torch.matmul(x, w)
     return _FeatureTransform.apply(x, w)

@@ -86,7 +86,7 @@ class GATConv(MessagePassing):
 
         if self._can_fuse(x, size):
             weight, att, fused_bias, C4 = self._fused_operands()
-            xw = _ops.feature_transform(x, weight)
+            xw = _ops.feature_transform(x, weight, row_exact=_ops.GAT_ROW_EXACT_GEMM)
             N = xw.size(0)
             graph = graph_for(edge_index, N, N, self.flow, target_tasks=GAT_TARGET_TASKS)
             drop = self.dropout if self.training else 0.0

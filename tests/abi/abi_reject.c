@@ -189,6 +189,13 @@ static void abi7(void) {
                                 256, 0, 0, DEV, slab, 7, NULL));
   ACCEPT(mp_aggregate_tiles_f32(&g, DEVF, DEVF, 256, 0, 0, 256, MP_REDUCE_MEAN, 0, DEVF, NULL, DEVF, 0, 64, N * 64, DEV, slab,
                                 7, NULL));
+  /* the row-exact feature transform */
+  REJECT("null", mp_gemm_rows_f32(NULL, 256, 10, 256, DEVF, 0, 256, DEVF, 256, 0, NULL));
+  REJECT("lda >= K", mp_gemm_rows_f32(DEVF, 100, 10, 256, DEVF, 0, 256, DEVF, 256, 0, NULL));
+  REJECT("ldc >= N", mp_gemm_rows_f32(DEVF, 256, 10, 256, DEVF, 0, 256, DEVF, 255, 0, NULL));
+  REJECT("K > 0", mp_gemm_rows_f32(DEVF, 256, 10, 0, DEVF, 0, 256, DEVF, 256, 0, NULL));
+  ACCEPT(mp_gemm_rows_f32(NULL, 256, 0, 256, NULL, 0, 256, NULL, 256, 0, NULL)); /* M = 0: a no-op */
+  ACCEPT(mp_gemm_rows_f32(DEVF, 24, 10, 24, DEVF, 0, 64, DEVF, 64, 0, NULL));
 }
 
 static void workspaces(void) {

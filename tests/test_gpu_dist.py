@@ -270,8 +270,8 @@ def _gat_layer_worker(rank, world, port, q):
         N, E, Fi = 3000, 60000, 64
         ei = powerlaw_edge_index(N, E, seed=47).to(dev)
         gen = torch.Generator().manual_seed(47)
-        # dyadic x and W: X W exact whatever GEMM kernel the rank's M picks (_dyadic_)
-        x = _dyadic_(torch.empty(N, Fi), gen, 4.0).to(dev)
+        # Gaussian x and W: the row-exact GEMM gives the rank the single-GPU rows of X W (_gauss_)
+        x = _gauss_(torch.empty(N, Fi), gen, 4.0).to(dev)
         res = {}
         # (heads, out_channels, concat): config 3's shape, the reference's heads=1 stacks
         # (ConvexPruning.py:209-214, a wide head), a padded width, and ppi's mean head
@@ -279,7 +279,7 @@ def _gat_layer_worker(rank, world, port, q):
             Fo = H * C if concat else C
             gout = torch.randn(N, Fo, generator=gen).to(dev)
             ref = GATConv(Fi, C, heads=H, concat=concat).to(dev)
-            _dyadic_(ref.weight, gen, 16.0)
+            _gauss_(ref.weight, gen, 16.0)
             with torch.no_grad():
                 ref.att.copy_(torch.randn(ref.att.shape, generator=gen) * 0.3)
                 ref.bias.copy_(torch.randn(ref.bias.shape, generator=gen))
@@ -394,13 +394,13 @@ def _gat_uneven_worker(rank, world, port, q):
         N, Fi, H, C = 1500, 24, 4, 16
         ei = powerlaw_edge_index(N, 20000, seed=71).to(dev)
         gen = torch.Generator().manual_seed(71)
-        x = _dyadic_(torch.empty(N, Fi), gen, 4.0).to(dev)       # X W exact on both sides (_dyadic_)
+        x = _gauss_(torch.empty(N, Fi), gen, 4.0).to(dev)       # X W bitwise on both sides (_gauss_)
         gout = torch.randn(N, H * C, generator=gen).to(dev)
         res = {}
         # an empty rank (cuts [0, N, N]) and a rank holding a single row
         for name, cuts in (("empty_rank", [0, N, N]), ("one_row", [0, 1, N])):
             ref = GATConv(Fi, C, heads=H).to(dev)
-            _dyadic_(ref.weight, gen, 16.0)
+            _gauss_(ref.weight, gen, 16.0)
             with torch.no_grad():
                 ref.att.copy_(torch.randn(ref.att.shape, generator=gen) * 0.3)
                 ref.bias.copy_(torch.randn(ref.bias.shape, generator=gen))
@@ -495,7 +495,7 @@ def _gat_dropout_worker(rank, world, port, q, cut_sets):
         N, Fi, p = 1500, 24, 0.3
         ei = powerlaw_edge_index(N, 20000, seed=73).to(dev)
         gen = torch.Generator().manual_seed(73)
-        x = _dyadic_(torch.empty(N, Fi), gen, 4.0).to(dev)
+        x = _gauss_(torch.empty(N, Fi), gen, 4.0).to(dev)
         res = {}
         # heads 4 x 16 (the fused transposed pass) and 2 x 24 (the wide kernels), over
         # the pull exchange and over the hybrid cover
@@ -504,7 +504,7 @@ def _gat_dropout_worker(rank, world, port, q, cut_sets):
             for ci, cuts in enumerate(cut_sets):
                 for cover in (False, True):
                     ref = GATConv(Fi, C, heads=H, dropout=p).to(dev).train()
-                    _dyadic_(ref.weight, gen, 16.0)
+                    _gauss_(ref.weight, gen, 16.0)
                     with torch.no_grad():
                         ref.att.copy_(torch.randn(ref.att.shape, generator=gen) * 0.3)
                         ref.bias.copy_(torch.randn(ref.bias.shape, generator=gen))
@@ -1329,9 +1329,9 @@ def _sharded_fuzz_worker(rank, world, port, q, seeds):
                 Cg = 8 if kind == "gat" else int(torch.randint(1, 41, (1,), generator=g))   # cover: any width
                 ref = GATConv(Fi, Cg, heads=H).to(dev)
                 if kind == "gat_cover":
-                    # dyadic x and W: X W exact on both sides, so no leaky_relu branch flips
-                    x = _dyadic_(torch.empty(N, Fi), g, 4.0).to(dev)
-                    _dyadic_(ref.weight, g, 16.0)
+                    # Gaussian x and W: the row-exact GEMM keeps X W bitwise on both sides, so no leaky_relu branch flips
+                    x = _gauss_(torch.empty(N, Fi), g, 4.0).to(dev)
+                    _gauss_(ref.weight, g, 16.0)
                 sg = mdist.ShardedGraph.for_gat(ei, N, rank, world, cuts=cuts)
                 if kind == "gat_cover":
                     sg.enable_gat_halo_cover()
@@ -1387,15 +1387,17 @@ def test_sharded_layers_fuzz_random_cuts_on_one_gpu():
                 assert r["out"] < 1e-5 and r["gx"] < 1e-5 and r["gparams"] < 1e-5, (rank, r)
 
 
-def _dyadic_(t, gen, scale):
-    """Fill t with small integers / scale: products of two such values and
-    their sums of a few hundred terms are exact in fp32, so X W is the same bit
-    for bit whatever GEMM kernel computes it (a rank's GEMM has M = n_own rows
-    and hipBLASLt picks its kernel by M).  Equal node scores on both sides keep
-    every leaky_relu branch equal: a score within rounding of 0 would otherwise
-    flip leaky' between 1 and the slope and move the gradient by a real amount."""
+def _gauss_(t, gen, scale):
+    """Fill t with N(0, 1) / (2 scale) draws.  Round 5 drew X and W on a dyadic
+    grid here, so that X W came out exact whatever GEMM kernel computed it
+    (hipBLASLt picks its kernel, and so its rounding, by the row count M, and a
+    rank's M is n_own): a score within rounding of 0 would otherwise flip
+    leaky' between 1 and the slope on one side only.  GATConv and
+    ShardedGATConv now compute X W with the row-exact GEMM (ops.gemm_rows:
+    each output row a function of its own input row), so Gaussian inputs give
+    a rank bitwise the single-GPU rows of X W."""
     with torch.no_grad():
-        t.copy_(torch.randint(-4, 5, tuple(t.shape), generator=gen).to(t.dtype) / scale)
+        t.copy_(torch.randn(tuple(t.shape), generator=gen).to(t.dtype) / (2.0 * scale))
     return t
 
 
@@ -1423,7 +1425,7 @@ def _gat_cover_gpu_worker(rank, world, port, q, cut_sets):
                         torch.stack([torch.full((1500,), N - 3), torch.randint(0, N, (1500,), generator=gen)])], 1)
         ei = ei[:, torch.randperm(ei.shape[1], generator=gen)].to(dev)
         E = ei.shape[1]
-        x = _dyadic_(torch.empty(N, Fi), gen, 4.0).to(dev)
+        x = _gauss_(torch.empty(N, Fi), gen, 4.0).to(dev)
         res = {}
         for ci, cuts in enumerate(cut_sets):
             # fused-pass heads (C/4 a power of two) and wide ones (a heads=1 stack's 96, a
@@ -1435,7 +1437,7 @@ def _gat_cover_gpu_worker(rank, world, port, q, cut_sets):
                 Fo = H * C if concat else C
                 gout = torch.randn(N, Fo, generator=gen).to(dev)
                 ref = GATConv(Fi, C, heads=H, concat=concat).to(dev)
-                _dyadic_(ref.weight, gen, 16.0)
+                _gauss_(ref.weight, gen, 16.0)
                 with torch.no_grad():
                     ref.att.copy_(torch.randn(ref.att.shape, generator=gen) * 0.3)
                     ref.bias.copy_(torch.randn(ref.bias.shape, generator=gen))

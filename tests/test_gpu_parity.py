@@ -702,6 +702,35 @@ def test_gat_backward_matches_float64_autograd(H=4, C=8):
         assert torch.allclose(got.cpu().double(), want, rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("K,N", [(256, 256), (24, 64), (1433, 16), (50, 1024), (256, 128)])
+def test_gemm_rows_row_exact(K, N):
+    """ops.gemm_rows (mp_gemm_rows_f32, GATConv's x @ W): every output row is
+    the k-ordered fmaf chain of its own input row -- bitwise the same for any
+    slice of the rows (a shard's M), the MFMA kernel (K = N = 256) bitwise the
+    generic one, and within 1e-5 sum|x w| of float64."""
+    from mi355_mp import ops
+    g = torch.Generator().manual_seed(K * 7 + N)
+    x = torch.randn(3001, K, generator=g).to(DEV)
+    w = (torch.randn(K, N, generator=g) / K ** 0.5).to(DEV)
+    full = ops.gemm_rows(x, w)
+    for a, b in ((0, 1), (5, 700), (1000, 3001), (17, 18), (64, 128)):
+        assert torch.equal(ops.gemm_rows(x[a:b], w), full[a:b]), (a, b)
+        assert torch.equal(ops.gemm_rows(x[a:b].clone(), w), full[a:b]), (a, b)
+    assert torch.equal(ops.gemm_rows(x, w, force_generic=True), full)
+    ref = x.double() @ w.double()
+    bound = 1e-5 * (x.abs().double() @ w.abs().double()).clamp(min=1.0)
+    assert ((full.double() - ref).abs() <= bound).all()
+    # autograd: the forward row-exact, the backward _FeatureTransform's
+    xr = x[:500].clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    y = ops.feature_transform(xr, wr, row_exact=True)
+    assert torch.equal(y.detach(), full[:500])
+    gy = torch.randn(500, N, generator=g).to(DEV)
+    y.backward(gy)
+    assert torch.allclose(xr.grad, gy @ w.t(), rtol=1e-5, atol=1e-5)
+    assert torch.allclose(wr.grad, x[:500].t() @ gy, rtol=1e-4, atol=1e-4)
+
+
 @pytest.mark.parametrize("scale", [1e2, 1e4])
 def test_gat_backward_large_bias_precision(scale, capsys):
     """the fused backward prologue forms rs_i = <g_i, out_i - bias>
