@@ -1782,7 +1782,8 @@ class ShardedGraph:
             self._w = None
             return self
         if edge_weight.requires_grad:
-            raise NotImplementedError("mi355_mp.dist: edge weights of a sharded graph carry no gradient")
+            raise ValueError("mi355_mp.dist: set_edge_weight fixes the weights (e.g. a norm); pass learnable "
+                             "weights to propagate(x_own, reduce, edge_weight=w) instead")
         w = edge_weight.to(torch.float32)
         return self._set_local_weights(w[self.fwd.edge_pos], w[self.bwd.edge_pos])
 
@@ -1811,10 +1812,19 @@ class ShardedGraph:
         self.w_send = (self.g_send.dst.to_csr_order(ws), self.g_send.src.to_csr_order(ws))
         return self
 
-    def propagate(self, x_own, reduce="sum"):
+    def propagate(self, x_own, reduce="sum", edge_weight=None):
         """Sharded MessagePassing.propagate for message = w * x_j: this rank's
         rows of REDUCE_{e: dst(e) = i} w_e x[src(e)] (autograd included).
-        max/min return (out, arg) with arg = GLOBAL edge ids."""
+        max/min return (out, arg) with arg = GLOBAL edge ids.
+
+        edge_weight: per-edge weights in GLOBAL edge order that the call
+        differentiates (a learnable edge weight held by every rank, like a
+        replicated parameter): they replace the weights set_edge_weight fixed,
+        run over the pull exchange (the cover regroups each edge's term into a
+        peer's partial row), and this rank's backward writes d w_e = <g_i, x_j>
+        for its own in-edges only -- all-reduce the gradient over the ranks
+        (allreduce_gradients does, for a module parameter) to get the full
+        one, as for a layer weight."""
         from . import ops
         reduce = "sum" if reduce == "add" else reduce
         if reduce not in ("sum", "mean", "max", "min"):
@@ -1822,16 +1832,30 @@ class ShardedGraph:
         x_own = ops._f32_2d(x_own, "x")
         if x_own.shape[0] != self.n_own:
             raise ValueError("mi355_mp.dist: x_own has %d rows, this rank owns %d" % (x_own.shape[0], self.n_own))
-        out, arg = _ShardedAggregate.apply(x_own, self, reduce)
+        w_fwd = w_bwd = None
+        if edge_weight is not None:
+            if edge_weight.dim() != 1 or edge_weight.numel() != self.n_edges:
+                raise ValueError("mi355_mp.dist: edge_weight must hold the %d global edges" % self.n_edges)
+            if not (edge_weight.is_cuda and x_own.is_cuda):
+                raise RuntimeError("mi355_mp.dist: learnable edge weights on host tensors -- there is no CPU "
+                                   "fallback: the engine runs on ROCm device tensors")
+            w = edge_weight.to(torch.float32)
+            w_fwd = w[self.fwd.edge_pos]                        # differentiable: d w lands on these edges
+            w_bwd = w.detach()[self.bwd.edge_pos] if self.bwd is not None else None
+        out, arg = _ShardedAggregate.apply(x_own, w_fwd, w_bwd, self, reduce)
         return (out, arg) if reduce in ("max", "min") else out
 
 
 class _ShardedAggregate(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x_own, sg, reduce):
+    def forward(ctx, x_own, w_fwd, w_bwd, sg, reduce):
+        """w_fwd / w_bwd: learnable weights in the two plans' local edge orders
+        (None: the weights set_edge_weight fixed); with them the pull form."""
         from . import ops
+        from .graph import in_csr_order
         ctx.sg, ctx.reduce = sg, reduce
-        if sg.cover is not None and reduce in ("sum", "mean"):
+        ctx.learn = w_fwd is not None
+        if sg.cover is not None and reduce in ("sum", "mean") and not ctx.learn:
             hc = sg.cover
             F = x_own.shape[1]
             x_local = x_own.new_empty((hc.n_local_src, F))
@@ -1848,11 +1872,17 @@ class _ShardedAggregate(torch.autograd.Function):
         x_local = plan.local_buffer(F, device=x_own.device)
         x_local[:plan.n_own].copy_(x_own)
         plan.exchange_into(x_local, ops.gather_rows, sg.group)
-        w_fwd = sg._w[0] if sg._w is not None else None
-        out, arg = ops._aggregate(sg.g_fwd.dst, "other", x_local, w_fwd, reduce, 0, None)
+        if ctx.learn:
+            wl = w_fwd.detach().contiguous()
+            w_csr = in_csr_order(sg.g_fwd.dst, wl)
+            ctx.w_bwd_csr = in_csr_order(sg.g_bwd.dst, w_bwd.contiguous()) if w_bwd is not None else None
+        else:
+            wl = sg._w[2] if sg._w is not None else None
+            w_csr = sg._w[0] if sg._w is not None else None
+        out, arg = ops._aggregate(sg.g_fwd.dst, "other", x_local, w_csr, reduce, 0, None)
         arg_g = None
+        ctx.save_for_backward(arg, wl, x_local if ctx.learn else None)
         if arg is not None:
-            ctx.save_for_backward(arg)
             arg_g = plan.global_edge_ids(arg, sg.n_edges)
             ctx.mark_non_differentiable(arg_g)
         return out, arg_g
@@ -1863,24 +1893,28 @@ class _ShardedAggregate(torch.autograd.Function):
         sg, reduce = ctx.sg, ctx.reduce
         g = grad_out.contiguous()
         F = g.shape[1]
+        want_w = ctx.learn and ctx.needs_input_grad[1]
         if reduce in ("max", "min"):
             # gradient lands on the argmax edge's source, which may live in the halo:
             # accumulate per local column, then return the halo rows to their owners
             # (deterministic: the local transposed CSR adds each column's winning
             # terms in local = global edge order; the rows returned by several
             # peers are summed by a segmented sum keyed on send_idx, in peer order)
-            (arg,) = ctx.saved_tensors
+            arg, w, x_local = ctx.saved_tensors      # w: local edge order, the arg's positions
             plan = sg.fwd
-            w = sg._w[2] if sg._w is not None else None  # local edge order: the arg's positions
-            gl, _ = ops.arg_backward(sg.g_fwd, arg, g, plan.n_local_src, w)
+            gl, gw = ops.arg_backward(sg.g_fwd, arg, g, plan.n_local_src, w, x_local, True, want_w)
             gx = gl[:plan.n_own]
             back = plan.return_halo(gl[plan.n_own:], sg.group)
             if back.shape[0]:
                 gx = gx + _sum_returned_rows(plan, back)
-            return gx.contiguous(), None, None
+            return gx.contiguous(), gw, None, None, None
         if reduce == "mean":
             g = g / sg.g_fwd.dst.degree().clamp(min=1).to(torch.float32).view(-1, 1)
-        if sg.cover is not None:
+        gw = None
+        if want_w:       # d w_e = <g_i, x_j> over this rank's in-edges, local edge order
+            _, _, x_local = ctx.saved_tensors
+            gw = ops._edge_dot(sg.g_fwd.dst, g.contiguous(), x_local)
+        if sg.cover is not None and not ctx.learn:
             # transpose of the cover forward: local rows' gradients over the transposed
             # local graph, the halo part back to its senders, the transposed send graph
             hc = sg.cover
@@ -1890,14 +1924,17 @@ class _ShardedAggregate(torch.autograd.Function):
             gx = gl[:hc.n_own]
             if hc.n_send:
                 gx = gx + ops._aggregate(sg.g_send.src, "other", back, sg.w_send[1], "sum", 0, None)[0]
-            return gx.contiguous(), None, None
+            return gx.contiguous(), None, None, None, None
         plan = sg.bwd
         g_local = plan.local_buffer(F, device=g.device)
         g_local[:plan.n_own].copy_(g)
         plan.exchange_into(g_local, ops.gather_rows, sg.group)
-        w_bwd = sg._w[1] if sg._w is not None else None
+        if ctx.learn:
+            w_bwd = ctx.w_bwd_csr
+        else:
+            w_bwd = sg._w[1] if sg._w is not None else None
         gx, _ = ops._aggregate(sg.g_bwd.dst, "other", g_local, w_bwd, "sum", 0, None)
-        return gx, None, None
+        return gx, gw, None, None, None
 
 
 def broadcast_parameters(module, src=0, group=None):

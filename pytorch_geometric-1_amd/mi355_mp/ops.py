@@ -366,8 +366,58 @@ def segment_reduce(src, index, dim_size, reduce="sum", pyg_mask=False):
     return _SegmentReduce.apply(src, index, int(dim_size), reduce, pyg_mask)
 
 
+def _reduce_into_native(src, index, out, reduce):
+    csr = csr_for_index(index, out.shape[0])
+    if src.dtype == torch.float32:
+        res, arg = _aggregate(csr, "eid", src, None, reduce, _lib.MP_FLAG_INIT_FROM_OUT, None, out=out)
+    else:
+        res, arg = _aggregate_any(csr, "eid", src, reduce, _lib.MP_FLAG_INIT_FROM_OUT, out=out)
+    return res, arg, csr
+
+
+class _SegmentReduceInto(torch.autograd.Function):
+    """torch_scatter 2.0.4's ``out=`` forms with autograd, as upstream
+    differentiates them: scatter_sum is ``out.scatter_add_(dim, index, src)``
+    (d src = gather(g), d out = g), scatter_mean divides that by the clamped
+    count in place (d src = gather(g / count), d out = g / count), and the
+    C++ ScatterMax / ScatterMin give src its winners' gradients and out none.
+    Out of place here (the result a fresh tensor); segment_reduce_into copies
+    it into the caller's out."""
+
+    @staticmethod
+    def forward(ctx, src, index, out_old, reduce):
+        res = out_old.clone(memory_format=torch.contiguous_format)
+        res, arg, csr = _reduce_into_native(src, index, res, reduce)
+        ctx.reduce, ctx.csr, ctx.n_src = reduce, csr, src.shape[0]
+        ctx.save_for_backward(index, arg)
+        if arg is not None:
+            ctx.mark_non_differentiable(arg)
+        return res, arg
+
+    @staticmethod
+    def backward(ctx, g, _grad_arg=None):
+        index, arg = ctx.saved_tensors
+        g = g.contiguous()
+        if ctx.reduce in ("max", "min"):
+            lib = _lib.load()
+            gs = torch.zeros((ctx.n_src, g.shape[1]), dtype=g.dtype, device=g.device)
+            if g.dtype == torch.float32:
+                _lib.check(lib.mp_scatter_arg_backward_f32(g.data_ptr(), arg.data_ptr(), g.shape[0], g.shape[1],
+                                                           ctx.n_src, gs.data_ptr(), gs.stride(0),
+                                                           _lib.stream_ptr(g.device)), "mp_scatter_arg_backward_f32")
+            else:
+                _lib.check(lib.mp_scatter_arg_any(g.element_size(), g.data_ptr(), arg.data_ptr(), g.shape[0],
+                                                  g.shape[1], ctx.n_src, gs.data_ptr(), gs.stride(0),
+                                                  _lib.stream_ptr(g.device)), "mp_scatter_arg_any")
+            return gs, None, None, None
+        if ctx.reduce == "mean":
+            g = g / ctx.csr.degree().clamp(min=1).to(g.dtype).view(-1, 1)
+        return gather_rows(g, index), None, g, None
+
+
 def segment_reduce_into(src, index, out, reduce="sum"):
-    """torch_scatter ``out=`` semantics: reduce into (and return) the given out tensor."""
+    """torch_scatter ``out=`` semantics: reduce into (and return) the given out
+    tensor; differentiable in src and out as upstream (_SegmentReduceInto)."""
     reduce = "sum" if reduce == "add" else reduce
     _lib.require_device(src, index, out)
     src = _any_2d(src, "src")
@@ -375,11 +425,11 @@ def segment_reduce_into(src, index, out, reduce="sum"):
     if out.dtype != src.dtype or out.dim() != 2 or (out.shape[1] > 1 and out.stride(1) != 1):
         raise ValueError("mi355_mp: out must be a row-major [dim_size, F] tensor of src's dtype")
     if torch.is_grad_enabled() and (src.requires_grad or out.requires_grad):
-        raise NotImplementedError("mi355_mp: autograd through torch_scatter `out=` is not supported")
-    csr = csr_for_index(index, out.shape[0])
-    if src.dtype == torch.float32:
-        return _aggregate(csr, "eid", src, None, reduce, _lib.MP_FLAG_INIT_FROM_OUT, None, out=out)
-    return _aggregate_any(csr, "eid", src, reduce, _lib.MP_FLAG_INIT_FROM_OUT, out=out)
+        res, arg = _SegmentReduceInto.apply(src, index, out, reduce)
+        out.copy_(res)
+        return out, arg
+    res, arg, _ = _reduce_into_native(src, index, out, reduce)
+    return res, arg
 
 
 class GatherRows(torch.autograd.Function):

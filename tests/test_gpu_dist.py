@@ -233,6 +233,74 @@ def test_sharded_gcnconv_forward_backward_on_one_gpu():
         assert r["gmax_exact"] and r["gmax_repeat"], r   # deterministic on both sides (round 3)
 
 
+def _learn_w_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "pytorch_geometric-1_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=_PG_TIMEOUT)
+    try:
+        from mi355_mp import dist as mdist, ops
+        from mi355_mp.graph import Graph
+        from mi355_mp.graphgen import powerlaw_edge_index
+        dev = torch.device("cuda", 0)
+        N, E, F = 2000, 30000, 32
+        ei = powerlaw_edge_index(N, E, seed=57).to(dev)
+        gen = torch.Generator().manual_seed(57)
+        x = torch.randn(N, F, generator=gen).to(dev)
+        w0 = torch.rand(E, generator=gen).to(dev) + 0.5
+        gout = torch.randn(N, F, generator=gen).to(dev)
+        g1 = Graph(ei, N, N)
+        res = {}
+        for red in ("sum", "mean", "max", "min"):
+            # single GPU: the fused propagate with the weights differentiated
+            xr, wr = x.clone().requires_grad_(True), w0.clone().requires_grad_(True)
+            ref = ops.fused_propagate(g1, xr, ei, wr, red)
+            ref = ref[0] if isinstance(ref, tuple) else ref
+            (ref * gout).sum().backward()
+            sg = mdist.ShardedGraph(ei, N, rank, world)
+            lo, hi = sg.lo, sg.hi
+            xo, w = x[lo:hi].clone().requires_grad_(True), w0.clone().requires_grad_(True)
+            o = sg.propagate(xo, red, edge_weight=w)
+            o = o[0] if isinstance(o, tuple) else o
+            (o * gout[lo:hi]).sum().backward()
+            # regrouped sums on hub rows (the two graphs' merge-path tasks split them
+            # differently): relative to the largest magnitude; max / min bit-exact
+            sc_o = float(ref.detach().abs().max().clamp(min=1.0))
+            sc_g = float(xr.grad.abs().max().clamp(min=1.0))
+            res[red] = {"out": float((o.detach() - ref.detach()[lo:hi]).abs().max()) / sc_o if hi > lo else 0.0,
+                        "gx": float((xo.grad - xr.grad[lo:hi]).abs().max()) / sc_g if hi > lo else 0.0,
+                        "out_exact": bool(torch.equal(o.detach(), ref.detach()[lo:hi]))}
+            # the rank's own in-edges carry its share; the sum over ranks is the full gradient
+            gw_h = w.grad.cpu()
+            dist.all_reduce(gw_h)
+            res[red]["gw"] = float((gw_h.to(dev) - wr.grad).abs().max() / wr.grad.abs().max().clamp(min=1e-30))
+            res[red]["own_edges_only"] = bool((w.grad[~torch.isin(torch.arange(E, device=dev), sg.fwd.edge_pos)]
+                                               == 0).all())
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_propagate_learnable_edge_weights():
+    """ShardedGraph.propagate(x, reduce, edge_weight=w) with w requiring grad
+    (VERDICT r05 missing 5): forward rows and d x against the single-GPU fused
+    propagate with the same weights differentiated; each rank writes d w on its
+    own in-edges only, and their sum over the ranks is the single-GPU d w --
+    sum, mean and max / min (winning edges), 2 ranks sharing the GPU."""
+    res = _spawn(_learn_w_worker)
+    for rank, r in res:
+        for red, v in r.items():
+            assert v["out"] < 1e-5 and v["gx"] < 1e-5, (rank, red, v)
+            assert v["gw"] < 1e-5, (rank, red, v)
+            assert v["own_edges_only"], (rank, red, v)
+            if red in ("max", "min"):
+                assert v["out_exact"], (rank, red, v)
+
+
 def _unsplit_equal(sg, g1, alpha, alpha_ref, out, out_ref):
     """Bit-equality of the sharded GAT and the single-GPU kernel where both
     schedules keep a row whole: a row of <= snap in-edges is never split across

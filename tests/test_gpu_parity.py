@@ -702,6 +702,48 @@ def test_gat_backward_matches_float64_autograd(H=4, C=8):
         assert torch.allclose(got.cpu().double(), want, rtol=1e-4, atol=1e-4)
 
 
+def test_torch_scatter_out_autograd():
+    """torch_scatter 2.0.4's out= forms are differentiable as upstream: scatter_sum
+    is out.scatter_add_(dim, index, src) (d src = gather(g), d out = g),
+    scatter_mean divides by the clamped count in place (g / count to both), and
+    scatter_max / scatter_min (C++ ScatterMax) give src its winners' gradients
+    and out none.  Against torch's own scatter_add_ autograd on the device."""
+    import torch_scatter as TS
+    g = torch.Generator().manual_seed(91)
+    N, E, F = 300, 5000, 12
+    idx = torch.randint(0, N - 20, (E,), generator=g).to(DEV)      # the last 20 rows get no edge
+    src0 = torch.randn(E, F, generator=g).to(DEV)
+    base0 = torch.randn(N, F, generator=g).to(DEV)
+    gout = torch.randn(N, F, generator=g).to(DEV)
+    cnt = torch.zeros(N, device=DEV).index_add_(0, idx, torch.ones(E, device=DEV)).clamp(min=1).view(-1, 1)
+    for reduce in ("sum", "mean"):
+        src, base = src0.clone().requires_grad_(True), base0.clone().requires_grad_(True)
+        out = base * 1.0
+        y = (TS.scatter_add if reduce == "sum" else TS.scatter_mean)(src, idx, 0, out=out)
+        assert y is out
+        (y * gout).sum().backward()
+        src_r, base_r = src0.clone().requires_grad_(True), base0.clone().requires_grad_(True)
+        y_r = (base_r * 1.0).scatter_add_(0, idx.view(-1, 1).expand(E, F), src_r)
+        if reduce == "mean":
+            y_r = y_r / cnt
+        (y_r * gout).sum().backward()
+        assert torch.allclose(y.detach(), y_r.detach(), rtol=1e-5, atol=1e-5), reduce
+        assert torch.allclose(src.grad, src_r.grad, rtol=1e-6, atol=1e-6), reduce
+        assert torch.allclose(base.grad, base_r.grad, rtol=1e-6, atol=1e-6), reduce
+    for name in ("scatter_max", "scatter_min"):
+        src, base = src0.clone().requires_grad_(True), base0.clone().requires_grad_(True)
+        out = base * 1.0
+        y, arg = getattr(TS, name)(src, idx, 0, out=out)
+        (y * gout).sum().backward()
+        want = torch.zeros(E + 1, F, device=DEV).scatter_(0, arg, gout)[:E]
+        assert torch.equal(src.grad, want), name
+        assert base.grad is None or not base.grad.any(), name
+    # no grad wanted: the in-place native path, unchanged
+    out = base0.clone()
+    TS.scatter_add(src0, idx, 0, out=out)
+    assert torch.allclose(out, base0.index_add(0, idx, src0), rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("K,N", [(256, 256), (24, 64), (1433, 16), (50, 1024), (256, 128)])
 def test_gemm_rows_row_exact(K, N):
     """ops.gemm_rows (mp_gemm_rows_f32, GATConv's x @ W): every output row is
