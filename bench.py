@@ -1043,12 +1043,14 @@ def link_model(mine, rank, n_tiles, fused=False, boundary_per_tile=True, pack_pe
     return res
 
 
-# rank 0's halo rows in under the hybrid cover, RMAT21 config 2 (DESIGN 5.4,
-# profiles/r03_halo_cover_p{2,4,8}.jsonl): the exchange volume --emulate-peers moves
-EMULATED_COVER_ROWS = {2: 288_668, 4: 346_920, 8: 313_427}
+# rank 0's halo rows in under the hybrid cover: the exchange volume
+# --emulate-peers moves -- config 2 (profiles/r03_halo_cover_p{2,4,8}.jsonl) and
+# config 5 (profiles/r06_bench_products_gloo{4,8}_rehearsal.json)
+EMULATED_COVER_ROWS = {"rmat21": {2: 288_668, 4: 346_920, 8: 313_427},
+                       "products": {4: 619_964, 8: 570_164}}
 
 
-def rccl_contention(sg, P, bias, reps=10, rounds=3):
+def rccl_contention(sg, P, bias, reps=10, rounds=3, workload="rmat21"):
     """RCCL beside the aggregation on one GPU (world 1, RCCL): rank 0 of a P-way
     destination-range partition (edge-balanced cuts of this graph) aggregates
     its in-edges over [own rows ; halo rows] while all_to_all_single moves that
@@ -1082,7 +1084,7 @@ def rccl_contention(sg, P, bias, reps=10, rounds=3):
     gen = torch.Generator(device=dev).manual_seed(11)
     x_loc = torch.randn(n_own + halo.numel(), F_DIM, device=dev, generator=gen)
     out = torch.empty(n_own, F_DIM, device=dev)
-    rows = EMULATED_COVER_ROWS.get(P, int(halo.numel()))
+    rows = EMULATED_COVER_ROWS.get(workload, {}).get(P, int(halo.numel()))
     send = torch.randn(rows, F_DIM, device=dev, generator=gen)
     recv = torch.empty_like(send)
 
@@ -1526,7 +1528,7 @@ def main(argv=None):
                 raise SystemExit("--emulate-peers needs --sharded at one RCCL rank")
             mine["rccl_contention"] = []
             for P in [int(p) for p in args.emulate_peers.split(",") if p]:
-                r = rccl_contention(sg, P, bias)
+                r = rccl_contention(sg, P, bias, workload=args.workload)
                 mine["rccl_contention"].append(r)
                 stage(rank, "RCCL beside the aggregation (P = %d): %s" % (P, json.dumps(r)))
         if verify is not None:

@@ -59,13 +59,17 @@ def main():
     # per rank the bench's link_model.predicted_in_turn["77"] = max(compute in turn
     # of the chosen form, pack(first) + exchange + boundary(last)), max over ranks,
     # + the contention; config 2 (rmat21) and config 5 (products)
-    rc = load("%s_bench_sharded_rccl_one_rank.json" % rnd)
-    cont = {}
-    if rc:
-        for r in rc["extra"]["per_rank"][0].get("rccl_contention", []):
-            cont[r["P"]] = r["contention_ms"]
+    conts = {}
+    for wl, f in (("c2", "bench_sharded_rccl_one_rank"), ("c5", "bench_sharded_rccl_one_rank_products")):
+        rc = load("%s_%s.json" % (rnd, f))
+        conts[wl] = {}
+        if rc:
+            for r in rc["extra"]["per_rank"][0].get("rccl_contention", []):
+                conts[wl][r["P"]] = r["contention_ms"]
     for wl, one_name, pre in (("c2", "bench_rmat21", "bench_rmat21_gloo"),
                               ("c5", "bench_products_n1", "bench_products_gloo")):
+        # config 5 without its own contention run: config 2's at the same P
+        cont = {**conts["c2"], **conts[wl]}
         one = load("%s_%s.json" % (rnd, one_name)) or load("r05_%s.json" % one_name)
         for P in (2, 4, 8):
             d = load("%s_%s%d_rehearsal.json" % (rnd, pre, P))
