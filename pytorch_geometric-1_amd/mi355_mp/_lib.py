@@ -162,6 +162,10 @@ class NativeLibraryStale(RuntimeError):
     pass
 
 
+# the C-ABI version these bindings are written for (include/mi355_mp.h MP_ABI_VERSION)
+ABI_VERSION = 7
+
+
 def load(path=None):
     """Load (once) and return the native library; raise if it is absent, or
     (the in-tree library) if it was built from other sources than the ones
@@ -190,6 +194,9 @@ def load(path=None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.mp_abi_version() != ABI_VERSION:
+        raise NativeLibraryStale("mi355_mp: %s has C-ABI %d, these bindings need %d" % (p, lib.mp_abi_version(),
+                                                                                       ABI_VERSION))
     if path is None:
         _lib = lib
     return lib

@@ -42,8 +42,16 @@ def test_ctypes_signatures_cover_the_header():
 
 
 def test_abi_version_and_error_string(lib):
+    import re
+    from mi355_mp import _lib
     assert lib.mp_abi_version() == 7
     assert isinstance(lib.mp_last_error(), bytes)
+    # the header, the bindings and __graft_entry__.build()'s check agree (round 6:
+    # build() still asserted ABI 6 after the bump)
+    hdr = open(os.path.join(ROOT, "include", "mi355_mp.h")).read()
+    assert int(re.search(r"#define MP_ABI_VERSION (\d+)", hdr).group(1)) == _lib.ABI_VERSION == lib.mp_abi_version()
+    entry = open(os.path.join(ROOT, "__graft_entry__.py")).read()
+    assert "_lib.ABI_VERSION" in entry and "mp_abi_version() == 6" not in entry
 
 
 def test_library_is_bound_to_its_sources(lib, monkeypatch):
