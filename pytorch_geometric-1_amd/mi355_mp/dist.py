@@ -835,6 +835,10 @@ class HaloCover:
         del s_rank, d_rank
         # grouped by owner, each group in edge order (per-owner counts known: no sort)
         ord_p = torch.cat([_nonzero_n(p_own == q, nP_l[q]) for q in range(world)]) if world else p_own
+        # the push edges in the order they go out (plan positions), and their counts
+        # per owner both ways (GatHaloCover's alpha travels back along them)
+        self.push_pos = idx_push[ord_p]
+        self.push_edges_to, self.push_edges_from = list(nP_l), list(snP)
         req = S.new_empty(sum(snS))
         _a2a(req, S.contiguous(), snS, nS_l, group)
         lo = plan.lo
@@ -1726,7 +1730,7 @@ class ShardedGraph:
         weighted sum of a row run over the same edges in the same (global)
         order as on one GPU: no extra collective, alpha bit-equal on rows no
         merge-path task splits.  return_alpha: (global edge ids, alpha [m, H])
-        of this rank's in-edges (the pull form).  dropout: the fused attention
+        of this rank's in-edges (pull or cover).  dropout: the fused attention
         dropout, its keep mask keyed on the GLOBAL edge ids -- the single-GPU
         layer's mask (over the cover too).
         local_gat(graph, edge_index, xw_local, att, H, C, slope, bias,
@@ -1735,14 +1739,17 @@ class ShardedGraph:
         dropout key (default: drawn from the device's generator)."""
         from .gat_cover import cover_ok
         gc = getattr(self, "gat_cover", None)
-        if gc is not None and not return_alpha and local_gat is None:
+        if gc is not None and local_gat is None:
             if not xw_own.is_cuda:
-                if not dropout:
+                if not dropout and not return_alpha:
                     return _host("gat_cover_forward")(gc, xw_own, att, heads, out_channels, negative_slope, bias), None
             elif cover_ok(heads, out_channels):
                 from .gat_cover import gat_cover_propagate
-                return gat_cover_propagate(gc, xw_own, att, heads, out_channels, negative_slope, bias, dropout,
-                                           seed), None
+                res = gat_cover_propagate(gc, xw_own, att, heads, out_channels, negative_slope, bias, dropout, seed,
+                                          return_alpha)
+                if return_alpha:
+                    return res[0], (self.fwd.edge_gid, res[1])
+                return res, None
         if local_gat is None:
             from . import ops
             local_gat = ops.gat_propagate
@@ -1759,9 +1766,9 @@ class ShardedGraph:
         (mi355_mp.gat_cover.GatHaloCover: a remote source row is pulled, or its
         owner pushes its online-softmax piece of the destination row -- 0.57x
         the pull rows on the config-2 graph) instead of the pull exchange.
-        Attention dropout runs over the cover too (keys: global edge ids);
-        return_alpha keeps the pull form; heads of any width (C % 4 == 0,
-        GATConv pads to it) take the cover.  Collective, once (every rank of the group)."""
+        Attention dropout (keys: global edge ids) and return_alpha run over the
+        cover too; heads of any width (C % 4 == 0, GATConv pads to it) take the
+        cover.  Collective, once (every rank of the group)."""
         from .gat_cover import GatHaloCover
         if self.bwd is not None:
             raise ValueError("mi355_mp.dist: enable_gat_halo_cover needs a graph made by for_gat / "

@@ -57,8 +57,14 @@ sent with them (HaloCover(edge_ids=True)).  A piece keeps the undropped
 softmax statistics and the dropped weights on its sum, so the merge rule is
 unchanged; the pulled rows are plain copies (no attention edge, no mask);
 a pusher's share of d a_dst comes node-wise from its pieces' (out2, s2)
-whatever the head width.  return_alpha takes the pull form (the alpha of a
-pushed edge lives on its pusher).
+whatever the head width.
+
+return_alpha: the alpha of every in-edge of the rank's rows, in the plan's
+local edge order, from the MERGED row statistics: the local piece's edges
+directly; for a pushed edge the destination's merged (max, denominator) go
+back to the pusher (one all_to_all of H pairs per piece), which evaluates the
+edge's alpha with the a_dst it received and returns it (one all_to_all of H
+floats per push edge).
 """
 import torch
 
@@ -116,9 +122,14 @@ class GatHaloCover:
         src, dst = lei[0].clone(), lei[1]
         src[hc.pull_pos] = hc.pull_halo
         loc = torch.sort(torch.cat([hc.int_pos, hc.pull_pos])).values
+        self.loc_pos = loc                                     # plan positions of the local piece's edges
         self.loc_src, self.loc_dst = src[loc].contiguous(), dst[loc].contiguous()
         self.loc_gid = plan.edge_gid[loc].contiguous()        # attention-dropout keys
         self.push_gid = hc.push_gid
+        # return_alpha: the push edges' plan positions in the order they went out, and
+        # the per-owner push-edge counts both ways
+        self.push_pos = hc.push_pos
+        self.push_edges_to, self.push_edges_from = hc.push_edges_to, hc.push_edges_from
         self.n_interior = int(hc.int_pos.numel())
         # received pieces -> own destination (the merge list)
         self.part_row = (hc.push_halo - n_own).contiguous()
@@ -168,12 +179,12 @@ class GatHaloCover:
                 "send_rows": self.n_send, "local_piece_edges": int(self.loc_src.numel())}
 
     # ---------------------------------------------------------- device (HIP)
-    def forward_device(self, xw_own, att_c, H, C, slope, bias, train, exchange=True, drop=None):
+    def forward_device(self, xw_own, att_c, H, C, slope, bias, train, exchange=True, drop=None, keep=False):
         """The step on the fused kernels.  Returns (out [n_own, H*C] with bias,
         saved) -- saved holds what backward_device needs when train.
         exchange=False: the compute alone (no collective; the receive buffers
         hold zeros), for decompose().  drop = (seed, p): attention dropout
-        (training form)."""
+        (training form).  keep: return saved outside training too (alpha)."""
         from . import _lib
         lib = _lib.load()
         g_loc, g_send, g_merge, _, g_push = self.graphs()
@@ -304,7 +315,7 @@ class GatHaloCover:
                                                      _lib.ptr(bias),
                                                      out.data_ptr(), F, stats.data_ptr(), _lib.ptr(agg2),
                                                      _lib.ptr(s2), st), "mp_gat_merge_partials_f32")
-        saved = (xl, a_src, a_dst, stats, agg2, s2, send_st, send2, send_s2, drop) if train else None
+        saved = (xl, a_src, a_dst, stats, agg2, s2, send_st, send2, send_s2, drop, send_adst) if (train or keep) else None
         return out, saved
 
     def decompose(self, xw_own, att, H, C, slope, bias, reps=10, barrier=None):
@@ -353,13 +364,51 @@ class GatHaloCover:
         res.update(hidden_fraction(res, staged=xw_own.is_cuda and tdist.get_backend(grp) == "gloo"))
         return res
 
+    def alpha(self, saved, H, slope):
+        """alpha [m, H] of this rank's in-edges, in the plan's local edge order
+        (GATConv's return_attention_weights: the undropped softmax), from the
+        forward's node scores and merged row statistics (saved of
+        forward_device).  Collective over the group (two all_to_alls)."""
+        from . import _lib
+        lib = _lib.load()
+        xl, a_src, a_dst, stats, _, _, _, _, _, _, send_adst = saved
+        dev = xl.device
+        st = _lib.stream_ptr(dev)
+        E_l = int(self.plan.local_edge_index.shape[1])
+        alpha = torch.zeros((E_l, H), dtype=torch.float32, device=dev)
+        n_loc = int(self.loc_src.numel())
+        if n_loc:
+            a_loc = torch.empty((n_loc, H), dtype=torch.float32, device=dev)
+            _lib.check(lib.mp_gat_alpha_f32(self.loc_src.data_ptr(), self.loc_dst.data_ptr(), n_loc, H,
+                                            a_src.data_ptr(), a_dst.data_ptr(), float(slope), stats.data_ptr(),
+                                            a_loc.data_ptr(), st), "mp_gat_alpha_f32 (local piece)")
+            alpha[self.loc_pos] = a_loc
+        # the merged (max, denominator) of each pushed destination back to its pusher
+        rev_st = torch.zeros((self.n_halo, H, 2), dtype=torch.float32, device=dev)
+        if self.part_row.numel():
+            rev_st[self.part_row] = stats[self.part_dst]
+        back_st = torch.zeros((self.n_send, H, 2), dtype=torch.float32, device=dev)
+        _a2a(back_st, rev_st, self.send_counts, self.recv_counts, self.group)
+        # the pusher evaluates its push edges' alpha, which return to the destination's owner
+        E_push = int(self.push_src.numel())
+        a_push = torch.empty((E_push, H), dtype=torch.float32, device=dev)
+        if E_push:
+            _lib.check(lib.mp_gat_alpha_f32(self.push_src.data_ptr(), self.push_dst.data_ptr(), E_push, H,
+                                            a_src.data_ptr(), send_adst.data_ptr(), float(slope), back_st.data_ptr(),
+                                            a_push.data_ptr(), st), "mp_gat_alpha_f32 (pushed pieces)")
+        got = torch.empty((sum(self.push_edges_to), H), dtype=torch.float32, device=dev)
+        _a2a(got, a_push, self.push_edges_to, self.push_edges_from, self.group)
+        if got.shape[0]:
+            alpha[self.push_pos] = got
+        return alpha
+
     def backward_device(self, g, out, bias, att_c, H, C, slope, saved, want_att, want_bias):
         """d xw_own, d att (or None), d bias (or None) of forward_device (see the
         module docstring for the split)."""
         from . import _lib, ops
         lib = _lib.load()
         g_loc, _, g_merge, g_copy_t, g_push = self.graphs()
-        xl, a_src, a_dst, stats, agg2, s2, send_st, send2, send_s2, drop = saved
+        xl, a_src, a_dst, stats, agg2, s2, send_st, send2, send_s2, drop, _ = saved
         seed, p_drop = (0, 0.0) if drop is None else (int(drop[0]), float(drop[1]))
         dev = g.device
         st = _lib.stream_ptr(dev)
@@ -507,9 +556,11 @@ class GatHaloCover:
 
 class _GatCoverFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, xw_own, att, bias, cover, H, C, slope, drop):
+    def forward(ctx, xw_own, att, bias, cover, H, C, slope, drop, holder):
         att_c = att.reshape(H, 2 * C).contiguous().to(torch.float32)
         out, saved = cover.forward_device(xw_own.contiguous(), att_c, H, C, slope, bias, True, drop=drop)
+        if holder is not None:           # return_alpha: the caller evaluates alpha from them
+            holder["saved"] = saved
         ctx.cover, ctx.H, ctx.C, ctx.slope = cover, H, C, slope
         ctx.saved = saved
         ctx.save_for_backward(out, bias, att_c)
@@ -526,16 +577,17 @@ class _GatCoverFn(torch.autograd.Function):
         ctx.saved = None
         if gatt is not None:
             gatt = gatt.view(1, ctx.H, 2 * ctx.C)
-        return gx, gatt, gb, None, None, None, None, None
+        return gx, gatt, gb, None, None, None, None, None, None
 
 
 def gat_cover_propagate(cover, xw_own, att, heads, out_channels, negative_slope=0.2, bias=None, dropout=0.0,
-                        seed=None):
+                        seed=None, return_alpha=False):
     """This rank's rows of the fused GATConv aggregation over the cover (+ bias)
     on the HIP path with its native backward; a host tensor raises.
     dropout > 0: GATConv's training-mode attention dropout, its keep mask keyed
     on the global edge ids (seed from the device's generator unless given):
-    the single-GPU layer's mask."""
+    the single-GPU layer's mask.  return_alpha: (out, alpha [m, H] of this
+    rank's in-edges in the plan's local edge order) (GatHaloCover.alpha)."""
     H, C = int(heads), int(out_channels)
     if xw_own.shape[0] != cover.n_own:
         raise ValueError("mi355_mp.gat_cover: xw_own has %d rows, this rank owns %d" % (xw_own.shape[0], cover.n_own))
@@ -556,6 +608,13 @@ def gat_cover_propagate(cover, xw_own, att, heads, out_channels, negative_slope=
     needs = torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in (xw_own, att, bias))
     if not needs:
         att_c = att.reshape(H, 2 * C).contiguous().to(torch.float32)
-        out, _ = cover.forward_device(xw_own.contiguous(), att_c, H, C, float(negative_slope), bias, False, drop=drop)
+        out, saved = cover.forward_device(xw_own.contiguous(), att_c, H, C, float(negative_slope), bias, False,
+                                          drop=drop, keep=return_alpha)
+    else:
+        holder = {} if return_alpha else None
+        out = _GatCoverFn.apply(xw_own, att, bias, cover, H, C, float(negative_slope), drop, holder)
+        saved = holder["saved"] if return_alpha else None
+    if not return_alpha:
         return out
-    return _GatCoverFn.apply(xw_own, att, bias, cover, H, C, float(negative_slope), drop)
+    with torch.no_grad():
+        return out, cover.alpha(saved, H, float(negative_slope))
