@@ -1,4 +1,5 @@
-// EXPERIMENT (not part of libmi355_mp): a hand-written f32
+// EXPERIMENT of round 4 (superseded: the kernel now ships in csrc/mp_gemm.hip as
+// mp_gemm_rows_f32, GATConv's row-exact x @ W): a hand-written f32
 // MFMA GEMM for the layers' feature transform x @ W (GCNConv /
 // GATConv [U5, U6] `torch.matmul(x, self.weight)`) at the configs' shape:
 // C[M, 256] = A[M, 256] @ B[256, 256] (B = W or W^T), fp32, on gfx950's f32-input
