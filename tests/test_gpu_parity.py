@@ -742,6 +742,19 @@ def test_torch_scatter_out_autograd():
     out = base0.clone()
     TS.scatter_add(src0, idx, 0, out=out)
     assert torch.allclose(out, base0.index_add(0, idx, src0), rtol=1e-5, atol=1e-5)
+    # an element-wise index along the last dim (torch_scatter README shape), out= with grad
+    s2 = torch.randn(6, 40, generator=g).to(DEV)
+    i2 = torch.randint(0, 9, (6, 40), generator=g).to(DEV)
+    o2 = torch.randn(6, 9, generator=g).to(DEV)
+    g2 = torch.randn(6, 9, generator=g).to(DEV)
+    src, base = s2.clone().requires_grad_(True), o2.clone().requires_grad_(True)
+    y = TS.scatter_add(src, i2, -1, out=base * 1.0)
+    (y * g2).sum().backward()
+    src_r, base_r = s2.clone().requires_grad_(True), o2.clone().requires_grad_(True)
+    y_r = (base_r * 1.0).scatter_add_(-1, i2, src_r)
+    (y_r * g2).sum().backward()
+    assert torch.allclose(y.detach(), y_r.detach(), rtol=1e-5, atol=1e-5)
+    assert torch.allclose(src.grad, src_r.grad) and torch.allclose(base.grad, base_r.grad)
 
 
 @pytest.mark.parametrize("K,N", [(256, 256), (24, 64), (1433, 16), (50, 1024), (256, 128)])
