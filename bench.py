@@ -1045,9 +1045,9 @@ def link_model(mine, rank, n_tiles, fused=False, boundary_per_tile=True, pack_pe
 
 # rank 0's halo rows in under the hybrid cover: the exchange volume
 # --emulate-peers moves -- config 2 (profiles/r03_halo_cover_p{2,4,8}.jsonl) and
-# config 5 (profiles/r06_bench_products_gloo{4,8}_rehearsal.json)
+# config 5 (profiles/r06_bench_products_gloo{2,4,8}_rehearsal.json)
 EMULATED_COVER_ROWS = {"rmat21": {2: 288_668, 4: 346_920, 8: 313_427},
-                       "products": {4: 619_964, 8: 570_164}}
+                       "products": {2: 508_972, 4: 619_964, 8: 570_164}}
 
 
 def rccl_contention(sg, P, bias, reps=10, rounds=3, workload="rmat21"):

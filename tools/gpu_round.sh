@@ -10,7 +10,7 @@
 #   rccl      one RCCL rank, --sharded --emulate-peers 8,4,2 (RCCL beside the aggregation),
 #             rocprofv3 kernel trace of the same command -> $R_bench_sharded_rccl_one_rank.json,
 #             $R_rccl_kernel_trace/ (+ tools/kernel_overlap.py summary)
-#   rccl_products  the same for config 5 (P = 8, 4) -> $R_bench_sharded_rccl_one_rank_products.json
+#   rccl_products  the same for config 5 (P = 8, 4, 2) -> $R_bench_sharded_rccl_one_rank_products.json
 #   gloo2     bench.py --gpus 2, gloo ranks sharing the GPU (--verify) -> $R_bench_rmat21_gloo2_rehearsal.json
 #   gloo8 / gloo4  bench.py --gpus 8 / 4 as gloo ranks sharing the GPU (per-rank compute_in_turn:
 #             each rank's compute with the GPU to itself) -> $R_bench_rmat21_gloo{8,4}_rehearsal.json;
@@ -47,7 +47,7 @@ for s in ${STEPS:-tests bench}; do
     rccl) run rccl 500 bash -c "python bench.py --sharded --emulate-peers 8,4,2 --steps 10 --warmup 3 --verify > $O/${R}_bench_sharded_rccl_one_rank.json 2> $O/${R}_bench_sharded_rccl_one_rank.err"
           run rccl_trace 500 rocprofv3 --kernel-trace --stats -d $O/${R}_rccl_kt -o kt --output-format csv -- python3 bench.py --sharded --emulate-peers 8,4,2 --steps 5 --warmup 2 --no-cpu-baseline --no-ref-paths --no-build-split
           python3 tools/kernel_overlap.py $O/${R}_rccl_kt > $O/${R}_rccl_kernel_overlap.json; cat $O/${R}_rccl_kernel_overlap.json | head -40 ;;
-    rccl_products) run rccl_products 500 bash -c "python bench.py --workload products --sharded --emulate-peers 8,4 --steps 10 --warmup 3 --verify > $O/${R}_bench_sharded_rccl_one_rank_products.json 2> $O/${R}_bench_sharded_rccl_one_rank_products.err" ;;
+    rccl_products) run rccl_products 500 bash -c "python bench.py --workload products --sharded --emulate-peers 8,4,2 --steps 10 --warmup 3 --verify > $O/${R}_bench_sharded_rccl_one_rank_products.json 2> $O/${R}_bench_sharded_rccl_one_rank_products.err" ;;
     gloo2) run gloo2 600 bash -c "MP_BENCH_BACKEND=gloo python bench.py --gpus 2 --steps 3 --warmup 1 --verify > $O/${R}_bench_rmat21_gloo2_rehearsal.json 2> $O/${R}_bench_rmat21_gloo2_rehearsal.err"; cut -c1-300 $O/${R}_bench_rmat21_gloo2_rehearsal.json ;;
     gloo8) run gloo8 1100 bash -c "GPU_MAX_HW_QUEUES=1 MP_BENCH_BACKEND=gloo python bench.py --gpus 8 --steps 3 --warmup 1 > $O/${R}_bench_rmat21_gloo8_rehearsal.json 2> $O/${R}_bench_rmat21_gloo8_rehearsal.err"; cut -c1-300 $O/${R}_bench_rmat21_gloo8_rehearsal.json ;;
     gloo4) run gloo4 900 bash -c "GPU_MAX_HW_QUEUES=1 MP_BENCH_BACKEND=gloo python bench.py --gpus 4 --steps 3 --warmup 1 > $O/${R}_bench_rmat21_gloo4_rehearsal.json 2> $O/${R}_bench_rmat21_gloo4_rehearsal.err"; cut -c1-300 $O/${R}_bench_rmat21_gloo4_rehearsal.json ;;
