@@ -1256,6 +1256,11 @@ def gemm_rows(x, w, force_generic=False):
     x has -- a shard's rows equal the single-GPU rows.  No autograd."""
     lib = _lib.load()
     _lib.require_device(x)
+    if x.dim() != 2 or w.dim() != 2 or x.shape[1] != w.shape[0]:
+        raise ValueError("gemm_rows: x [M, K] and w [K, N] (got %s and %s)" % (tuple(x.shape), tuple(w.shape)))
+    if x.dtype != torch.float32 or w.dtype != torch.float32 or w.device != x.device:
+        raise TypeError("gemm_rows: fp32 x and w on one device (got %s / %s on %s / %s)"
+                        % (x.dtype, w.dtype, x.device, w.device))
     x = x if (x.stride(1) == 1 and x.stride(0) >= x.shape[1]) else x.contiguous()
     w = w.contiguous()
     M, K = x.shape

@@ -784,6 +784,11 @@ def test_gemm_rows_row_exact(K, N):
     y.backward(gy)
     assert torch.allclose(xr.grad, gy @ w.t(), rtol=1e-5, atol=1e-5)
     assert torch.allclose(wr.grad, x[:500].t() @ gy, rtol=1e-4, atol=1e-4)
+    # mismatched operands are refused before any launch
+    with pytest.raises(ValueError):
+        ops.gemm_rows(x, w[:-1])
+    with pytest.raises(TypeError):
+        ops.gemm_rows(x.double(), w)
 
 
 @pytest.mark.parametrize("scale", [1e2, 1e4])
