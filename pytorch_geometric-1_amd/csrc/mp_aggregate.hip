@@ -245,10 +245,21 @@ struct SumRed {
     float v[VEC];
   };
   float acc[VEC];
+  // this lane's bias features, read once per task: a load per row would be
+  // waited for at every row end, and the wait (vmcnt retires in order) also
+  // drains every gather issued before it -- the next rows' prefetched batch.
+  // Measured +19 % on a short-row pass (4.4 edges a row, tools/exp_interior.py).
+  float bv[VEC];
   int h = 0;  // unused (GAT only)
 
   __device__ SumRed() {}
-  __device__ SumRed(const AggArgs&, int, bool) {}
+  __device__ SumRed(const AggArgs& p, int f, bool act) {
+    if (p.bias && act) {
+      Frag<VEC> b = load_frag<VEC>(p.bias + f);
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) bv[k] = b.v[k];
+    }
+  }
 
   __device__ __forceinline__ void begin(const AggArgs& p, int64_t row, bool owned, int f, bool act) {
 #pragma unroll
@@ -300,9 +311,8 @@ struct SumRed {
 #pragma unroll
     for (int k = 0; k < VEC; ++k) o.v[k] = MEAN ? __fdiv_rn(acc[k], c) : acc[k];
     if (p.bias) {
-      Frag<VEC> b = load_frag<VEC>(p.bias + f);
 #pragma unroll
-      for (int k = 0; k < VEC; ++k) o.v[k] = __fadd_rn(o.v[k], __fmul_rn(b.v[k], bs));
+      for (int k = 0; k < VEC; ++k) o.v[k] = __fadd_rn(o.v[k], __fmul_rn(bv[k], bs));
     }
     store_out<VEC>(p.out + row * p.ldo + f, o);
   }
@@ -313,9 +323,8 @@ struct SumRed {
 #pragma unroll
     for (int k = 0; k < VEC; ++k) o.v[k] = MEAN ? __fdiv_rn(acc[k], c) : acc[k];
     if (p.bias && with_bias) {
-      Frag<VEC> b = load_frag<VEC>(p.bias + f);
 #pragma unroll
-      for (int k = 0; k < VEC; ++k) o.v[k] = __fadd_rn(o.v[k], b.v[k]);
+      for (int k = 0; k < VEC; ++k) o.v[k] = __fadd_rn(o.v[k], bv[k]);
     }
     store_out<VEC>(p.out + row * p.ldo + f, o);
   }
