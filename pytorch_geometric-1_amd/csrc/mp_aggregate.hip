@@ -245,20 +245,37 @@ struct SumRed {
     float v[VEC];
   };
   float acc[VEC];
-  // this lane's bias features, read once per task: a load per row would be
-  // waited for at every row end, and the wait (vmcnt retires in order) also
-  // drains every gather issued before it -- the next rows' prefetched batch.
-  // Measured +19 % on a short-row pass (4.4 edges a row, tools/exp_interior.py).
+  // the bias features of this lane, read once per task (preload_bias) by the
+  // short-row passes of mp_aggregate_tiles_f32 (k_agg_flat XM != 0)
   float bv[VEC];
+  bool pre = false;
   int h = 0;  // unused (GAT only)
 
   __device__ SumRed() {}
-  __device__ SumRed(const AggArgs& p, int f, bool act) {
+  __device__ SumRed(const AggArgs&, int, bool) {}
+
+  // A bias load per row is waited for at the row's end, and the wait (vmcnt
+  // retires in order) also drains every gather issued before it -- the next
+  // rows' prefetched batch.  On the sharded step's short rows (4.4 edges a row)
+  // that cost the interior pass 19 % (tools/exp_interior.py: 0.287 -> 0.245
+  // ms); on the one-GPU kernel's long rows the per-row load measured faster
+  // (1-3 %), so only the tile launches take it once per task.
+  __device__ __forceinline__ void preload_bias(const AggArgs& p, int f, bool act) {
     if (p.bias && act) {
       Frag<VEC> b = load_frag<VEC>(p.bias + f);
 #pragma unroll
       for (int k = 0; k < VEC; ++k) bv[k] = b.v[k];
     }
+    pre = true;
+  }
+  __device__ __forceinline__ Frag<VEC> bias_of(const AggArgs& p, int f) const {
+    if (pre) {
+      Frag<VEC> b;
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) b.v[k] = bv[k];
+      return b;
+    }
+    return load_frag<VEC>(p.bias + f);
   }
 
   __device__ __forceinline__ void begin(const AggArgs& p, int64_t row, bool owned, int f, bool act) {
@@ -311,8 +328,9 @@ struct SumRed {
 #pragma unroll
     for (int k = 0; k < VEC; ++k) o.v[k] = MEAN ? __fdiv_rn(acc[k], c) : acc[k];
     if (p.bias) {
+      Frag<VEC> b = bias_of(p, f);
 #pragma unroll
-      for (int k = 0; k < VEC; ++k) o.v[k] = __fadd_rn(o.v[k], __fmul_rn(bv[k], bs));
+      for (int k = 0; k < VEC; ++k) o.v[k] = __fadd_rn(o.v[k], __fmul_rn(b.v[k], bs));
     }
     store_out<VEC>(p.out + row * p.ldo + f, o);
   }
@@ -323,8 +341,9 @@ struct SumRed {
 #pragma unroll
     for (int k = 0; k < VEC; ++k) o.v[k] = MEAN ? __fdiv_rn(acc[k], c) : acc[k];
     if (p.bias && with_bias) {
+      Frag<VEC> b = bias_of(p, f);
 #pragma unroll
-      for (int k = 0; k < VEC; ++k) o.v[k] = __fadd_rn(o.v[k], bv[k]);
+      for (int k = 0; k < VEC; ++k) o.v[k] = __fadd_rn(o.v[k], b.v[k]);
     }
     store_out<VEC>(p.out + row * p.ldo + f, o);
   }
@@ -1636,6 +1655,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_flat(AggArgs p) {
   const int64_t e_end = GR::un(p.wave_slot[w + 1]);
 
   Red red(p, f, act);
+  if constexpr (XM != 0) red.preload_bias(p, f, act);  // the tile launches: sum / mean only
   // an owned row opens (rs_ / re_: its slot range); an empty one is skipped
   // (no load of out) under MP_FLAG_SKIP_EMPTY
   auto open_row = [&](int rr, int64_t rs_, int64_t re_) {
