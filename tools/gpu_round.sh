@@ -16,7 +16,7 @@
 #             each rank's compute with the GPU to itself) -> $R_bench_rmat21_gloo{8,4}_rehearsal.json;
 #             one hardware queue per process (GPU_MAX_HW_QUEUES=1): 4 x 4 queues oversubscribe the
 #             GPU's queue slots and stretch a 1 s build to 60 s
-#   products_gloo4 / products_gloo8  config 5 (--workload products) as 4 / 8 gloo ranks sharing the GPU (--verify)
+#   products_gloo2 / products_gloo4 / products_gloo8  config 5 (--workload products) as 4 / 8 gloo ranks sharing the GPU (--verify)
 #   gat_gloo2 the same for --workload gat                -> $R_bench_gat_gloo2_rehearsal.json
 #   gat_drop_gloo2  the same with attention dropout 0.3 over the cover (--verify with the keep mask)
 #   prof      tools/profile.sh (kernel trace + PMC of the default bench); prof_gat / prof_products /
@@ -52,6 +52,7 @@ for s in ${STEPS:-tests bench}; do
     gloo8) run gloo8 1100 bash -c "GPU_MAX_HW_QUEUES=1 MP_BENCH_BACKEND=gloo python bench.py --gpus 8 --steps 3 --warmup 1 > $O/${R}_bench_rmat21_gloo8_rehearsal.json 2> $O/${R}_bench_rmat21_gloo8_rehearsal.err"; cut -c1-300 $O/${R}_bench_rmat21_gloo8_rehearsal.json ;;
     gloo4) run gloo4 900 bash -c "GPU_MAX_HW_QUEUES=1 MP_BENCH_BACKEND=gloo python bench.py --gpus 4 --steps 3 --warmup 1 > $O/${R}_bench_rmat21_gloo4_rehearsal.json 2> $O/${R}_bench_rmat21_gloo4_rehearsal.err"; cut -c1-300 $O/${R}_bench_rmat21_gloo4_rehearsal.json ;;
     products_gloo4) run products_gloo4 1100 bash -c "GPU_MAX_HW_QUEUES=1 MP_BENCH_BACKEND=gloo python bench.py --workload products --gpus 4 --steps 3 --warmup 1 --verify > $O/${R}_bench_products_gloo4_rehearsal.json 2> $O/${R}_bench_products_gloo4_rehearsal.err"; cut -c1-300 $O/${R}_bench_products_gloo4_rehearsal.json ;;
+    products_gloo2) run products_gloo2 900 bash -c "MP_BENCH_BACKEND=gloo python bench.py --workload products --gpus 2 --steps 3 --warmup 1 --verify > $O/${R}_bench_products_gloo2_rehearsal.json 2> $O/${R}_bench_products_gloo2_rehearsal.err"; cut -c1-300 $O/${R}_bench_products_gloo2_rehearsal.json ;;
     products_gloo8) run products_gloo8 1150 bash -c "GPU_MAX_HW_QUEUES=1 MP_BENCH_BACKEND=gloo python bench.py --workload products --gpus 8 --steps 3 --warmup 1 --verify > $O/${R}_bench_products_gloo8_rehearsal.json 2> $O/${R}_bench_products_gloo8_rehearsal.err"; cut -c1-300 $O/${R}_bench_products_gloo8_rehearsal.json ;;
     gat_gloo2) run gat_gloo2 600 bash -c "MP_BENCH_BACKEND=gloo python bench.py --gpus 2 --workload gat --steps 3 --warmup 1 --verify > $O/${R}_bench_gat_gloo2_rehearsal.json 2> $O/${R}_bench_gat_gloo2_rehearsal.err"; cut -c1-300 $O/${R}_bench_gat_gloo2_rehearsal.json ;;
     gat_drop_gloo2) run gat_drop_gloo2 600 bash -c "MP_BENCH_BACKEND=gloo python bench.py --gpus 2 --workload gat --gat-dropout 0.3 --steps 3 --warmup 1 --verify > $O/${R}_bench_gat_dropout_gloo2_rehearsal.json 2> $O/${R}_bench_gat_dropout_gloo2_rehearsal.err"; cut -c1-300 $O/${R}_bench_gat_dropout_gloo2_rehearsal.json ;;
