@@ -56,6 +56,7 @@ for s in ${STEPS:-tests bench}; do
     products_gloo8) run products_gloo8 1150 bash -c "GPU_MAX_HW_QUEUES=1 MP_BENCH_BACKEND=gloo python bench.py --workload products --gpus 8 --steps 3 --warmup 1 --verify > $O/${R}_bench_products_gloo8_rehearsal.json 2> $O/${R}_bench_products_gloo8_rehearsal.err"; cut -c1-300 $O/${R}_bench_products_gloo8_rehearsal.json ;;
     gat_gloo2) run gat_gloo2 600 bash -c "MP_BENCH_BACKEND=gloo python bench.py --gpus 2 --workload gat --steps 3 --warmup 1 --verify > $O/${R}_bench_gat_gloo2_rehearsal.json 2> $O/${R}_bench_gat_gloo2_rehearsal.err"; cut -c1-300 $O/${R}_bench_gat_gloo2_rehearsal.json ;;
     gat_drop_gloo2) run gat_drop_gloo2 600 bash -c "MP_BENCH_BACKEND=gloo python bench.py --gpus 2 --workload gat --gat-dropout 0.3 --steps 3 --warmup 1 --verify > $O/${R}_bench_gat_dropout_gloo2_rehearsal.json 2> $O/${R}_bench_gat_dropout_gloo2_rehearsal.err"; cut -c1-300 $O/${R}_bench_gat_dropout_gloo2_rehearsal.json ;;
+    gat_drop_gloo4) run gat_drop_gloo4 900 bash -c "GPU_MAX_HW_QUEUES=1 MP_BENCH_BACKEND=gloo python bench.py --gpus 4 --workload gat --gat-dropout 0.3 --steps 3 --warmup 1 --verify > $O/${R}_bench_gat_dropout_gloo4_rehearsal.json 2> $O/${R}_bench_gat_dropout_gloo4_rehearsal.err"; cut -c1-300 $O/${R}_bench_gat_dropout_gloo4_rehearsal.json ;;
     diag) run diag 500 bash -c "python tools/gat_shard_diag.py > $O/${R}_gat_shard_diag.jsonl 2> $O/${R}_gat_shard_diag.err"; cat $O/${R}_gat_shard_diag.jsonl ;;
     prof) PROF_OUT=$O/${R}_prof run prof 1100 bash tools/profile.sh ;;
     prof_gat) PROF_OUT=$O/${R}_prof_gat NO_CALIB=1 BENCH_ARGS="--workload gat" run prof_gat 1100 bash tools/profile.sh ;;
