@@ -3060,3 +3060,47 @@ def test_fuzz_torch_scatter_api(shape, dim, elementwise, dtype, reduce, extra, u
         if use_out:
             terms = terms + base.abs()
         assert bool(((got - want).abs() <= 1e-5 * terms.clamp(min=1.0)).all()), (got, want)
+
+
+@pytest.mark.parametrize("reduce", ["sum", "mean"])
+def test_aggregate_tiles_bias_forms(reduce):
+    """mp_aggregate_tiles_f32's compile-time instances against _aggregate's
+    arithmetic on the same values, bit for bit: the per-row bias flags of the
+    sharded interior pass (XM 1: the bias read once per task, DESIGN Appendix
+    A), and (sum) the boundary pass's skipped rows on top of out with the halo
+    rows tile-major (XM 2) -- with hub rows cut across tasks, whose fix-up
+    reads the bias per row, and rows without edges."""
+    from mi355_mp import _lib, ops
+    from mi355_mp.graph import Graph
+    g = torch.Generator().manual_seed(11)
+    n, n_x, F = 3000, 2000, 256
+    dst = torch.cat([torch.randint(0, n - 500, (20000,), generator=g),       # rows >= n - 500 stay empty
+                     torch.full((5000,), 7), torch.full((3000,), 1234)])     # two hub rows
+    src = torch.randint(0, n_x, (dst.numel(),), generator=g)
+    gr = Graph(torch.stack([src, dst]).to(DEV), n, n_x, chunk=16)
+    assert gr.dst.n_split > 0
+    w = gr.dst.to_csr_order(torch.rand(dst.numel(), generator=g).to(DEV))
+    x = torch.randn(n_x, F, generator=g).to(DEV)
+    bias = torch.randn(F, generator=g).to(DEV)
+    flags = torch.randint(0, 2, (n,), generator=g, dtype=torch.int32).to(DEV)
+    with_b = ops._aggregate(gr.dst, "other", x, w, reduce, 0, bias)[0]
+    without = ops._aggregate(gr.dst, "other", x, w, reduce, 0, None)[0]
+    want = torch.where(flags.bool()[:, None], with_b, without)
+    out = torch.full((n, F), float("nan"), device=DEV)
+    ops.aggregate_tiles(gr.dst, "other", x, w, F, out, reduce, 0, bias, bias_rows=flags)
+    assert torch.equal(out, want)
+    if reduce != "sum":
+        return
+    # boundary form: out holds the interior part; rows with edges add theirs in
+    # order, then the bias; rows without edges are left as they are
+    o0 = torch.randn(n, F, generator=g).to(DEV)
+    ref = ops._aggregate(gr.dst, "other", x, w, "sum", _lib.MP_FLAG_INIT_FROM_OUT, bias, out=o0.clone())[0]
+    rp = gr.dst.rowptr
+    has = (rp[1:] > rp[:-1])[:, None]
+    want = torch.where(has, ref, o0)
+    width = 64
+    xt = x.view(n_x, F // width, width).transpose(0, 1).contiguous()     # [T, rows, width]
+    out = o0.clone()
+    ops.aggregate_tiles(gr.dst, "other", xt, w, F, out, "sum", _lib.MP_FLAG_INIT_FROM_OUT | _lib.MP_FLAG_SKIP_EMPTY,
+                        bias, x_tiles=(width, n_x * width))
+    assert torch.equal(out, want)
